@@ -1,0 +1,552 @@
+// K5+K6+K7: fused in-batch scores, logQ correction and softmax cross-entropy
+// (reduction SUM) with its gradient, on bf16 MFMA (v_mfma_f32_32x32x16_bf16)
+// with fp32 accumulation.  The [rows, cols] score matrix never leaves
+// registers.
+//
+// Reference chain (/root/reference):
+//   TwoTowerModel.call        S = Q C^T                  two_tower_model.py:92
+//   LogQCorrection.__call__   S' = S - log p[cand]       logq_correction.py:66-71
+//   eye labels + CE(from_logits, SUM)                    two_tower_model.py:119-122,
+//                                                        runner.py:78-83
+//   loss = sum_i [lse_i(S'_i.) - S'_ii];  dS = softmax(S') - I
+//   dQ = dS C,  dC = dS^T Q
+//
+// Two streaming passes, each "flash"-structured over the other operand:
+//   rows pass (F): per query row i, online softmax over all candidate columns
+//     accumulating O_i = sum_j exp(S'_ij - m_i) c_j -> lse_i and
+//     dq_i = O_i / l_i - c_pos(i)   (the forward IS attention with K = V = C).
+//   cols pass (G): per candidate column j, with lse known,
+//     dc_j = sum_i exp(S'_ij - lse_i) q_i - q_pos(j); the -logq_j shift is
+//     applied as the exact factor exp(-logq_j) on the column sum.
+// 4 B^2 E flops each (S recompute + P.V), i.e. 8 B^2 E per train step.
+//
+// Wave layout (32x32x16 bf16 MFMA, 64-wide wave): a wave owns 32 stationary
+// rows whose bf16 fragments stay in VGPRs for the whole pass (B operand).
+// Streamed rows arrive in 64-row tiles through double-buffered LDS
+// (XOR-swizzled so every ds_read_b128 fragment read is bank-conflict free):
+//   S^T tile [32 streamed x 32 stationary] = A(streamed rows) . B(stationary)
+// so each lane holds 16 scores of ONE stationary row; the per-row bias
+// (-logq_j for F, -lse_i for G) is loaded as the accumulator's initial value.
+// The S^T accumulator is exactly the B operand of the next MFMA
+// (O^T += X^T . P^T) after a bf16 pack, so P never touches LDS; the streamed
+// operand's transposed image X^T is prepared once in HBM with the MFMA's
+// k-permutation baked in (16-byte fragment reads).
+// The stationary extent is split into 128-row workgroups and the streamed
+// extent into S splits (flash-decoding) so that >= 256 workgroups fill the
+// 256 CUs; tiny combine kernels merge the splits.
+#include <cmath>
+
+#include "tt_common.h"
+
+namespace tt {
+namespace {
+
+constexpr int kWavesPerWG = 4;
+constexpr int kThreads = kWavesPerWG * kWave;
+constexpr int kRowsPerWave = 32;
+constexpr int kRowsPerWG = kWavesPerWG * kRowsPerWave;  // stationary rows per WG
+constexpr int kTile = 64;                                // streamed rows per LDS tile
+constexpr int kMaxSplit = 16;
+constexpr float kLog2e = 1.4426950408889634f;
+
+template <int D>
+struct Geo {
+  static constexpr int KS = D / 16;           // MFMA k-steps over the embedding
+  static constexpr int DT = D / 32;           // 32-row output tiles of O^T
+  static constexpr int CH = D / 8;            // 16-byte chunks per bf16 row
+  static constexpr int A_BYTES = kTile * D * 2;   // streamed rows, row-major
+  static constexpr int T_BYTES = D * kTile * 2;   // transposed image [D][64]
+  static constexpr int BIAS_BYTES = kTile * 4;
+  static constexpr int BUF_BYTES = A_BYTES + T_BYTES + BIAS_BYTES;
+  static constexpr int A_CHUNKS_PER_THREAD = kTile * CH / kThreads;  // D/32
+  static constexpr int T_CHUNKS_PER_THREAD = D * 8 / kThreads;       // D/32
+};
+
+// Swizzled byte offset of 16-B chunk `ch` of row `row` in the [64][D] image.
+template <int D>
+__device__ __forceinline__ int a_off(int row, int ch) {
+  constexpr int CH = D / 8;
+  const int swz = (row * CH / 16) % CH;
+  return row * (CH * 16) + ((ch ^ swz) << 4);
+}
+// Swizzled byte offset of 16-B chunk `ch` (0..7) of row `e` in the [D][64] image.
+__device__ __forceinline__ int t_off(int e, int ch) { return e * 128 + ((ch ^ ((e >> 1) & 7)) << 4); }
+
+// Position of streamed row offset o (0..15) inside its 16-row group of the
+// transposed image: MFMA k element j of lane half h is row 8(j>>2)+4h+(j&3).
+__device__ __forceinline__ int perm16(int o) {
+  const int a = o >> 3, h = (o >> 2) & 1, b = o & 3;
+  return 8 * h + 4 * a + b;
+}
+
+// ---------------------------------------------------------------------------
+// Prep: fp32 [n, ld] -> bf16 row-major [n_pad, D] (zero padded) and optionally
+// the permuted transposed image [D, n_pad].  One block = 64 rows.
+template <int D>
+__global__ void __launch_bounds__(256) prep_kernel(const float* __restrict__ src, int64_t ld, int64_t n,
+                                                   int dim, int64_t n_pad, __bf16* __restrict__ dst,
+                                                   __bf16* __restrict__ dstT) {
+  __shared__ float tile[64][D + 1];
+  const int64_t r0 = blockIdx.x * 64ll;
+  for (int i = threadIdx.x; i < 64 * D; i += 256) {
+    const int r = i / D, e = i % D;
+    const int64_t gr = r0 + r;
+    tile[r][e] = (gr < n && e < dim) ? src[gr * ld + e] : 0.0f;
+  }
+  __syncthreads();
+  // row-major: each thread packs 8 consecutive elements (16 B).
+  for (int i = threadIdx.x; i < 64 * D / 8; i += 256) {
+    const int r = i / (D / 8), c8 = (i % (D / 8)) * 8;
+    u32x4 v;
+    v.x = pack_bf16x2(tile[r][c8 + 0], tile[r][c8 + 1]);
+    v.y = pack_bf16x2(tile[r][c8 + 2], tile[r][c8 + 3]);
+    v.z = pack_bf16x2(tile[r][c8 + 4], tile[r][c8 + 5]);
+    v.w = pack_bf16x2(tile[r][c8 + 6], tile[r][c8 + 7]);
+    *reinterpret_cast<u32x4*>(dst + (r0 + r) * D + c8) = v;
+  }
+  if (dstT) {
+    // transposed: image row e holds the 64 rows of this block, permuted per 16.
+    for (int i = threadIdx.x; i < D * 8; i += 256) {
+      const int e = i / 8, p8 = (i % 8) * 8;  // positions p8..p8+7 within the 64
+      float x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int p = p8 + j;
+        const int g = p >> 4, pp = p & 15;
+        // inverse of perm16: position pp holds row offset o with perm16(o) == pp
+        const int h = pp >> 3, a = (pp >> 2) & 1, b = pp & 3;
+        const int o = 8 * a + 4 * h + b;
+        x[j] = tile[16 * g + o][e];
+      }
+      u32x4 v;
+      v.x = pack_bf16x2(x[0], x[1]);
+      v.y = pack_bf16x2(x[2], x[3]);
+      v.z = pack_bf16x2(x[4], x[5]);
+      v.w = pack_bf16x2(x[6], x[7]);
+      *reinterpret_cast<u32x4*>(dstT + static_cast<int64_t>(e) * n_pad + r0 + p8) = v;
+    }
+  }
+}
+
+// bias[i] = sign * v[i] (v may be NULL -> 0) for i < n; pad value beyond.
+__global__ void bias_kernel(const float* __restrict__ v, int64_t n, int64_t n_pad, float sign, float pad,
+                            float* __restrict__ out) {
+  const int64_t i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= n_pad) return;
+  out[i] = (i < n) ? (v ? sign * v[i] : 0.0f) : pad;
+}
+
+struct PassArgs {
+  const __bf16* stat;     // [n_stat_pad, D] stationary rows (B operand)
+  const __bf16* strm;     // [n_strm_pad, D] streamed rows (A operand of S)
+  const __bf16* strmT;    // [D, n_strm_pad] permuted transposed image
+  const float* bias;      // [n_strm_pad] accumulator init per streamed row
+  int64_t n_stat_pad;
+  int64_t n_strm_pad;
+  int64_t per_split;      // streamed rows per split (multiple of kTile)
+  float* part_m;          // [S, n_stat_pad]   (rows pass)
+  float* part_l;          // [S, n_stat_pad]   (rows pass)
+  float* part_o;          // [S, n_stat_pad, D]
+};
+
+// MODE 0: rows pass (online softmax).  MODE 1: cols pass (lse known).
+template <int D, int MODE>
+__global__ void __launch_bounds__(kThreads) inbatch_pass_kernel(const PassArgs a) {
+  using G = Geo<D>;
+  __shared__ __attribute__((aligned(16))) char smem[2 * G::BUF_BYTES];
+  const int tid = threadIdx.x;
+  const int wave = tid / kWave;
+  const int lane = lane_id();
+  const int h = lane >> 5;
+  const int l32 = lane & 31;
+  const int64_t stat_row = static_cast<int64_t>(blockIdx.x) * kRowsPerWG + wave * kRowsPerWave + l32;
+  const int split = blockIdx.y;
+  const int64_t s_begin = split * a.per_split;
+  int64_t s_end = s_begin + a.per_split;
+  if (s_end > a.n_strm_pad) s_end = a.n_strm_pad;
+  const int ntiles = s_begin < s_end ? static_cast<int>((s_end - s_begin) / kTile) : 0;
+
+  // Stationary fragments: B[k = 16s + 8h + j][col = l32].
+  bf16x8 bfrag[G::KS];
+#pragma unroll
+  for (int s = 0; s < G::KS; ++s)
+    bfrag[s] = *reinterpret_cast<const bf16x8*>(a.stat + stat_row * D + 16 * s + 8 * h);
+
+  f32x16 o[G::DT];
+#pragma unroll
+  for (int dt = 0; dt < G::DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[dt][r] = 0.0f;
+  float m_run = -1.0e30f;
+  float l_run = 0.0f;
+
+  u32x4 ra[G::A_CHUNKS_PER_THREAD];
+  u32x4 rt[G::T_CHUNKS_PER_THREAD];
+  float rb = 0.0f;
+  auto gload = [&](int64_t base) {
+#pragma unroll
+    for (int i = 0; i < G::A_CHUNKS_PER_THREAD; ++i) {
+      const int c = tid + kThreads * i;
+      const int row = c / G::CH, ch = c % G::CH;
+      ra[i] = *reinterpret_cast<const u32x4*>(a.strm + (base + row) * D + ch * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < G::T_CHUNKS_PER_THREAD; ++i) {
+      const int c = tid + kThreads * i;
+      const int e = c / 8, ch = c % 8;
+      rt[i] = *reinterpret_cast<const u32x4*>(a.strmT + static_cast<int64_t>(e) * a.n_strm_pad + base + ch * 8);
+    }
+    if (tid < kTile) rb = a.bias[base + tid];
+  };
+  auto lstore = [&](int buf) {
+    char* B = smem + buf * G::BUF_BYTES;
+#pragma unroll
+    for (int i = 0; i < G::A_CHUNKS_PER_THREAD; ++i) {
+      const int c = tid + kThreads * i;
+      const int row = c / G::CH, ch = c % G::CH;
+      *reinterpret_cast<u32x4*>(B + a_off<D>(row, ch)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < G::T_CHUNKS_PER_THREAD; ++i) {
+      const int c = tid + kThreads * i;
+      const int e = c / 8, ch = c % 8;
+      *reinterpret_cast<u32x4*>(B + G::A_BYTES + t_off(e, ch)) = rt[i];
+    }
+    if (tid < kTile) reinterpret_cast<float*>(B + G::A_BYTES + G::T_BYTES)[tid] = rb;
+  };
+
+  if (ntiles > 0) {
+    gload(s_begin);
+    lstore(0);
+  }
+  __syncthreads();
+
+  for (int tile = 0; tile < ntiles; ++tile) {
+    const int cur = tile & 1;
+    const bool more = tile + 1 < ntiles;
+    if (more) gload(s_begin + static_cast<int64_t>(tile + 1) * kTile);
+    const char* B = smem + cur * G::BUF_BYTES;
+    const float* bias = reinterpret_cast<const float*>(B + G::A_BYTES + G::T_BYTES);
+
+    // S^T (+ bias) for the two 32-row sub-tiles.
+    f32x16 sacc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(bias + 32 * t + 8 * r4 + 4 * h);
+        sacc[t][4 * r4 + 0] = b4[0];
+        sacc[t][4 * r4 + 1] = b4[1];
+        sacc[t][4 * r4 + 2] = b4[2];
+        sacc[t][4 * r4 + 3] = b4[3];
+      }
+#pragma unroll
+      for (int s = 0; s < G::KS; ++s) {
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(B + a_off<D>(32 * t + l32, 2 * s + h));
+        sacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfrag[s], sacc[t], 0, 0, 0);
+      }
+    }
+
+    float p[2][16];
+    if constexpr (MODE == 0) {
+      float mx = -1.0e30f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[t][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+      const float m_new = fmaxf(m_run, mx);
+      if (__any(m_new > m_run)) {
+        const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * kLog2e);
+        l_run *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < G::DT; ++dt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+        m_run = m_new;
+      }
+      const float mb = m_run * kLog2e;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          p[t][r] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[t][r], kLog2e, -mb));
+          l_run += p[t][r];
+        }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) p[t][r] = __builtin_amdgcn_exp2f(sacc[t][r] * kLog2e);
+    }
+
+    // P^T fragments (B operand, k = streamed row) and O^T += X^T . P^T.
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        u32x4 pk;
+        pk.x = pack_bf16x2(p[t][8 * s2 + 0], p[t][8 * s2 + 1]);
+        pk.y = pack_bf16x2(p[t][8 * s2 + 2], p[t][8 * s2 + 3]);
+        pk.z = pack_bf16x2(p[t][8 * s2 + 4], p[t][8 * s2 + 5]);
+        pk.w = pack_bf16x2(p[t][8 * s2 + 6], p[t][8 * s2 + 7]);
+        const bf16x8 pf = __builtin_bit_cast(bf16x8, pk);
+#pragma unroll
+        for (int dt = 0; dt < G::DT; ++dt) {
+          const int e = 32 * dt + l32;
+          const bf16x8 tf = *reinterpret_cast<const bf16x8*>(B + G::A_BYTES + t_off(e, 4 * t + 2 * s2 + h));
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tf, pf, o[dt], 0, 0, 0);
+        }
+      }
+    }
+
+    if (more) lstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // Partials: lane (l32, h) holds O^T[e = 32dt + 8r4 + 4h + 0..3][stat_row].
+  const int64_t prow = static_cast<int64_t>(split) * a.n_stat_pad + stat_row;
+  if constexpr (MODE == 0) {
+    const float l_tot = l_run + __shfl_xor(l_run, 32, kWave);
+    if (h == 0) {
+      a.part_m[prow] = m_run;
+      a.part_l[prow] = l_tot;
+    }
+  }
+  float* po = a.part_o + prow * D;
+#pragma unroll
+  for (int dt = 0; dt < G::DT; ++dt)
+#pragma unroll
+    for (int r4 = 0; r4 < 4; ++r4) {
+      f32x4 v;
+      v[0] = o[dt][4 * r4 + 0];
+      v[1] = o[dt][4 * r4 + 1];
+      v[2] = o[dt][4 * r4 + 2];
+      v[3] = o[dt][4 * r4 + 3];
+      *reinterpret_cast<f32x4*>(po + 32 * dt + 8 * r4 + 4 * h) = v;
+    }
+}
+
+// Rows combine: one wave per row.  lse, row loss, dq.
+__global__ void __launch_bounds__(256) combine_rows_kernel(
+    const float* __restrict__ part_m, const float* __restrict__ part_l, const float* __restrict__ part_o,
+    int nsplit, int64_t n_stat_pad, int D, const float* __restrict__ q, int64_t ldq, const float* __restrict__ c,
+    int64_t ldc, const float* __restrict__ logq, int64_t n_rows, int dim, int64_t pos_offset,
+    float* __restrict__ lse_out, float* __restrict__ loss_out, float* __restrict__ dq) {
+  const int64_t i = blockIdx.x * 4ll + threadIdx.x / kWave;
+  if (i >= n_rows) return;
+  const int lane = lane_id();
+  float M = -1.0e30f;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, part_m[s * n_stat_pad + i]);
+  float L = 0.0f;
+  for (int s = 0; s < nsplit; ++s) L += part_l[s * n_stat_pad + i] * expf(part_m[s * n_stat_pad + i] - M);
+  const float lse = M + logf(L);
+  const int64_t pos = i + pos_offset;
+  float dot = 0.0f;
+  for (int e = lane; e < dim; e += kWave) {
+    float oe = 0.0f;
+    for (int s = 0; s < nsplit; ++s)
+      oe += part_o[(s * n_stat_pad + i) * D + e] * expf(part_m[s * n_stat_pad + i] - M);
+    const float ce = c[pos * ldc + e];
+    if (dq) dq[i * dim + e] = oe / L - ce;
+    dot = __builtin_fmaf(q[i * ldq + e], ce, dot);
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) dot += __shfl_xor(dot, m, kWave);
+  if (lane == 0) {
+    const float pos_logit = dot - (logq ? logq[pos] : 0.0f);
+    lse_out[i] = lse;
+    loss_out[i] = lse - pos_logit;
+  }
+}
+
+// Cols combine: dc_j = exp(-logq_j) * sum_s O_s[j] - q_pos(j).
+__global__ void __launch_bounds__(256) combine_cols_kernel(const float* __restrict__ part_o, int nsplit,
+                                                           int64_t n_stat_pad, int D, const float* __restrict__ q,
+                                                           int64_t ldq, const float* __restrict__ logq,
+                                                           int64_t n_cols, int dim, int64_t pos_offset,
+                                                           float* __restrict__ dc) {
+  const int64_t j = blockIdx.x * 4ll + threadIdx.x / kWave;
+  if (j >= n_cols) return;
+  const int lane = lane_id();
+  const float scale = logq ? expf(-logq[j]) : 1.0f;
+  const int64_t pos = j + pos_offset;
+  for (int e = lane; e < dim; e += kWave) {
+    float oe = 0.0f;
+    for (int s = 0; s < nsplit; ++s) oe += part_o[(s * n_stat_pad + j) * D + e];
+    dc[j * dim + e] = oe * scale - q[pos * ldq + e];
+  }
+}
+
+int pick_dpad(int dim) {
+  if (dim <= 32) return 32;
+  if (dim <= 64) return 64;
+  if (dim <= 128) return 128;
+  return 0;
+}
+
+int pick_split(int64_t n_stat_pad, int64_t n_strm_pad) {
+  const int64_t wgs = n_stat_pad / kRowsPerWG;
+  int64_t s = ceil_div(256, wgs);
+  const int64_t tiles = n_strm_pad / kTile;
+  if (s > tiles) s = tiles;
+  if (s > kMaxSplit) s = kMaxSplit;
+  if (s < 1) s = 1;
+  return static_cast<int>(s);
+}
+
+struct Plan {
+  int D;
+  int64_t stat_pad, strm_pad;
+  int split;
+  int64_t per_split;
+};
+
+Plan make_plan(int64_t n_stat, int64_t n_strm, int dim) {
+  Plan p;
+  p.D = pick_dpad(dim);
+  p.stat_pad = round_up(n_stat > 0 ? n_stat : 1, kRowsPerWG);
+  p.strm_pad = round_up(n_strm > 0 ? n_strm : 1, kTile);
+  p.split = pick_split(p.stat_pad, p.strm_pad);
+  p.per_split = round_up(ceil_div(p.strm_pad, p.split), kTile);
+  return p;
+}
+
+struct PassWs {
+  __bf16* stat;
+  __bf16* strm;
+  __bf16* strmT;
+  float* bias;
+  float* part_m;
+  float* part_l;
+  float* part_o;
+};
+
+PassWs carve_pass(Carver& cv, const Plan& p) {
+  PassWs w;
+  w.stat = cv.take<__bf16>(p.stat_pad * p.D);
+  w.strm = cv.take<__bf16>(p.strm_pad * p.D);
+  w.strmT = cv.take<__bf16>(p.strm_pad * p.D);
+  w.bias = cv.take<float>(p.strm_pad);
+  w.part_m = cv.take<float>(int64_t(p.split) * p.stat_pad);
+  w.part_l = cv.take<float>(int64_t(p.split) * p.stat_pad);
+  w.part_o = cv.take<float>(int64_t(p.split) * p.stat_pad * p.D);
+  return w;
+}
+
+size_t pass_bytes(int64_t n_stat, int64_t n_strm, int dim) {
+  Carver cv(nullptr, 0);
+  carve_pass(cv, make_plan(n_stat, n_strm, dim));
+  return cv.used();
+}
+
+template <int D>
+int launch_prep(const float* src, int64_t ld, int64_t n, int dim, int64_t n_pad, __bf16* dst, __bf16* dstT,
+                hipStream_t st) {
+  hipLaunchKernelGGL(prep_kernel<D>, dim3(n_pad / 64), dim3(256), 0, st, src, ld, n, dim, n_pad, dst, dstT);
+  TT_CHECK_LAUNCH();
+  return TT_OK;
+}
+
+int prep(int D, const float* src, int64_t ld, int64_t n, int dim, int64_t n_pad, __bf16* dst, __bf16* dstT,
+         hipStream_t st) {
+  switch (D) {
+    case 32: return launch_prep<32>(src, ld, n, dim, n_pad, dst, dstT, st);
+    case 64: return launch_prep<64>(src, ld, n, dim, n_pad, dst, dstT, st);
+    default: return launch_prep<128>(src, ld, n, dim, n_pad, dst, dstT, st);
+  }
+}
+
+template <int MODE>
+int launch_pass(const Plan& p, const PassArgs& a, hipStream_t st) {
+  dim3 grid(static_cast<unsigned>(p.stat_pad / kRowsPerWG), static_cast<unsigned>(p.split));
+  switch (p.D) {
+    case 32: hipLaunchKernelGGL((inbatch_pass_kernel<32, MODE>), grid, dim3(kThreads), 0, st, a); break;
+    case 64: hipLaunchKernelGGL((inbatch_pass_kernel<64, MODE>), grid, dim3(kThreads), 0, st, a); break;
+    default: hipLaunchKernelGGL((inbatch_pass_kernel<128, MODE>), grid, dim3(kThreads), 0, st, a); break;
+  }
+  TT_CHECK_LAUNCH();
+  return TT_OK;
+}
+
+int check_common(const float* q, int64_t ldq, int64_t n_rows, const float* c, int64_t ldc, int64_t n_cols,
+                 int32_t dim) {
+  TT_REQUIRE(q && c, "inbatch: NULL q/c");
+  TT_REQUIRE(n_rows >= 1 && n_cols >= 1, "inbatch: empty batch");
+  TT_REQUIRE(n_rows < (1ll << 30) && n_cols < (1ll << 30), "inbatch: batch too large");
+  TT_REQUIRE(dim >= 1, "inbatch: dim must be >= 1");
+  if (pick_dpad(dim) == 0) return fail(TT_ERR_UNSUPPORTED, "inbatch: dim=%d > 128 not supported", dim);
+  TT_REQUIRE(ldq >= dim && ldc >= dim, "inbatch: leading dimension smaller than dim");
+  return TT_OK;
+}
+
+}  // namespace
+}  // namespace tt
+
+using namespace tt;
+
+extern "C" size_t tt_inbatch_workspace_size(int64_t n_rows, int64_t n_cols, int32_t dim) {
+  if (n_rows < 1 || n_cols < 1 || pick_dpad(dim) == 0) return 0;
+  const size_t a = pass_bytes(n_rows, n_cols, dim);
+  const size_t b = pass_bytes(n_cols, n_rows, dim);
+  return a > b ? a : b;
+}
+
+extern "C" int tt_inbatch_xent_rows(const float* q, int64_t ldq, int64_t n_rows, const float* c, int64_t ldc,
+                                    int64_t n_cols, int32_t dim, const float* logq, int64_t pos_offset,
+                                    float* lse, float* row_loss, float* dq, void* workspace,
+                                    size_t workspace_bytes, tt_stream_t stream) {
+  clear_error();
+  int rc = check_common(q, ldq, n_rows, c, ldc, n_cols, dim);
+  if (rc) return rc;
+  TT_REQUIRE(lse && row_loss, "tt_inbatch_xent_rows: NULL lse/row_loss");
+  TT_REQUIRE(pos_offset >= 0 && n_rows + pos_offset <= n_cols,
+             "tt_inbatch_xent_rows: positives [pos_offset, pos_offset+n_rows) exceed n_cols");
+  const Plan p = make_plan(n_rows, n_cols, dim);
+  Carver cv(workspace, workspace_bytes);
+  PassWs w = carve_pass(cv, p);
+  if (!workspace || cv.used() > workspace_bytes)
+    return fail(TT_ERR_WORKSPACE, "tt_inbatch_xent_rows: workspace %zu < required %zu", workspace_bytes, cv.used());
+  hipStream_t st = to_stream(stream);
+  if ((rc = prep(p.D, q, ldq, n_rows, dim, p.stat_pad, w.stat, nullptr, st))) return rc;
+  if ((rc = prep(p.D, c, ldc, n_cols, dim, p.strm_pad, w.strm, w.strmT, st))) return rc;
+  hipLaunchKernelGGL(bias_kernel, dim3(ceil_div(p.strm_pad, 256)), dim3(256), 0, st, logq, n_cols, p.strm_pad,
+                     -1.0f, -INFINITY, w.bias);
+  TT_CHECK_LAUNCH();
+  PassArgs a{w.stat, w.strm, w.strmT, w.bias, p.stat_pad, p.strm_pad, p.per_split, w.part_m, w.part_l, w.part_o};
+  if ((rc = launch_pass<0>(p, a, st))) return rc;
+  hipLaunchKernelGGL(combine_rows_kernel, dim3(ceil_div(n_rows, 4)), dim3(256), 0, st, w.part_m, w.part_l,
+                     w.part_o, p.split, p.stat_pad, p.D, q, ldq, c, ldc, logq, n_rows, dim, pos_offset, lse,
+                     row_loss, dq);
+  TT_CHECK_LAUNCH();
+  return TT_OK;
+}
+
+extern "C" int tt_inbatch_xent_cols(const float* q, int64_t ldq, int64_t n_rows, const float* lse, const float* c,
+                                    int64_t ldc, int64_t n_cols, int32_t dim, const float* logq,
+                                    int64_t pos_offset, float* dc, void* workspace, size_t workspace_bytes,
+                                    tt_stream_t stream) {
+  clear_error();
+  int rc = check_common(q, ldq, n_rows, c, ldc, n_cols, dim);
+  if (rc) return rc;
+  TT_REQUIRE(lse && dc, "tt_inbatch_xent_cols: NULL lse/dc");
+  TT_REQUIRE(pos_offset >= 0 && n_cols + pos_offset <= n_rows,
+             "tt_inbatch_xent_cols: positives [pos_offset, pos_offset+n_cols) exceed n_rows");
+  const Plan p = make_plan(n_cols, n_rows, dim);  // stationary = columns, streamed = rows
+  Carver cv(workspace, workspace_bytes);
+  PassWs w = carve_pass(cv, p);
+  if (!workspace || cv.used() > workspace_bytes)
+    return fail(TT_ERR_WORKSPACE, "tt_inbatch_xent_cols: workspace %zu < required %zu", workspace_bytes, cv.used());
+  hipStream_t st = to_stream(stream);
+  if ((rc = prep(p.D, c, ldc, n_cols, dim, p.stat_pad, w.stat, nullptr, st))) return rc;
+  if ((rc = prep(p.D, q, ldq, n_rows, dim, p.strm_pad, w.strm, w.strmT, st))) return rc;
+  hipLaunchKernelGGL(bias_kernel, dim3(ceil_div(p.strm_pad, 256)), dim3(256), 0, st, lse, n_rows, p.strm_pad,
+                     -1.0f, -INFINITY, w.bias);
+  TT_CHECK_LAUNCH();
+  PassArgs a{w.stat, w.strm, w.strmT, w.bias, p.stat_pad, p.strm_pad, p.per_split, nullptr, nullptr, w.part_o};
+  if ((rc = launch_pass<1>(p, a, st))) return rc;
+  hipLaunchKernelGGL(combine_cols_kernel, dim3(ceil_div(n_cols, 4)), dim3(256), 0, st, w.part_o, p.split,
+                     p.stat_pad, p.D, q, ldq, logq, n_cols, dim, pos_offset, dc);
+  TT_CHECK_LAUNCH();
+  return TT_OK;
+}

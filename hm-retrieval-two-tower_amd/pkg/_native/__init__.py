@@ -1,0 +1,150 @@
+"""ctypes binding of libtt.so, the gfx950 C ABI declared in include/tt.h.
+
+The library is built in-tree (``make -C hm-retrieval-two-tower_amd/csrc``) and
+loaded from this directory.  There is no fallback: if the library is missing
+or cannot be loaded, :func:`lib` raises, and every op that needs it fails
+loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from ctypes import POINTER, c_char_p, c_float, c_int32, c_int64, c_size_t, c_void_p
+
+__all__ = [
+    "LIB_PATH",
+    "TTError",
+    "GatherSegment",
+    "SparseTable",
+    "MAX_SEGMENTS",
+    "MAX_SOURCES",
+    "lib",
+    "check",
+    "EXPORTED_SYMBOLS",
+]
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtt.so")
+MAX_SEGMENTS = 32
+MAX_SOURCES = 4
+
+TT_OK = 0
+TT_ERR_BAD_ARG = 1
+TT_ERR_HIP = 2
+TT_ERR_UNSUPPORTED = 3
+TT_ERR_WORKSPACE = 4
+
+
+class TTError(RuntimeError):
+    """A libtt entry point returned a non-zero status."""
+
+    def __init__(self, code: int, message: str):
+        super().__init__(f"libtt error {code}: {message}")
+        self.code = code
+
+
+class GatherSegment(ctypes.Structure):
+    _fields_ = [
+        ("table", c_void_p),
+        ("ids", c_void_p),
+        ("num_rows", c_int64),
+        ("dim", c_int32),
+        ("col_offset", c_int32),
+    ]
+
+
+class SparseTable(ctypes.Structure):
+    _fields_ = [
+        ("table", c_void_p),
+        ("slot0", c_void_p),
+        ("slot1", c_void_p),
+        ("num_rows", c_int64),
+        ("dim", c_int32),
+        ("num_sources", c_int32),
+        ("ids", c_void_p * MAX_SOURCES),
+        ("grad_col_offset", c_int32 * MAX_SOURCES),
+    ]
+
+
+# name -> (restype, argtypes); mirrors include/tt.h one to one.
+_PROTOS = {
+    "tt_version": (c_char_p, []),
+    "tt_last_error": (c_char_p, []),
+    "tt_gather_grouped": (c_int32, [POINTER(GatherSegment), c_int32, c_int64, c_void_p, c_int64, c_void_p]),
+    "tt_sparse_workspace_size": (c_size_t, [POINTER(SparseTable), c_int32, c_int64]),
+    "tt_sparse_adagrad": (
+        c_int32,
+        [POINTER(SparseTable), c_int32, c_int64, c_void_p, c_int64, c_float, c_float, c_void_p, c_size_t, c_void_p],
+    ),
+    "tt_sparse_adam": (
+        c_int32,
+        [POINTER(SparseTable), c_int32, c_int64, c_void_p, c_int64, c_float, c_float, c_float, c_float, c_int64,
+         c_void_p, c_size_t, c_void_p],
+    ),
+    "tt_dedup_workspace_size": (c_size_t, [c_int64, c_int32]),
+    "tt_dedup_sum": (
+        c_int32,
+        [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+         c_void_p],
+    ),
+    "tt_dense_adagrad": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p]),
+    "tt_dense_adam": (
+        c_int32,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_float, c_int64, c_void_p],
+    ),
+    "tt_inbatch_workspace_size": (c_size_t, [c_int64, c_int64, c_int32]),
+    "tt_inbatch_xent_rows": (
+        c_int32,
+        [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int64, c_void_p, c_void_p,
+         c_void_p, c_void_p, c_size_t, c_void_p],
+    ),
+    "tt_inbatch_xent_cols": (
+        c_int32,
+        [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int64, c_void_p,
+         c_void_p, c_size_t, c_void_p],
+    ),
+    "tt_bruteforce_index_bytes": (c_size_t, [c_int64, c_int32]),
+    "tt_bruteforce_build": (c_int32, [c_void_p, c_int64, c_int64, c_int32, c_void_p, c_size_t, c_void_p]),
+    "tt_bruteforce_workspace_size": (c_size_t, [c_int64, c_int64, c_int32, c_int32]),
+    "tt_bruteforce_search": (
+        c_int32,
+        [c_void_p, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int64, c_int64, c_int32, c_int64, c_void_p,
+         c_void_p, c_void_p, c_size_t, c_void_p],
+    ),
+    "tt_topk_merge": (c_int32, [c_void_p, c_void_p, c_int32, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
+    "tt_recall_hits": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, POINTER(c_int32), c_int32, c_void_p, c_void_p]),
+}
+
+EXPORTED_SYMBOLS = tuple(_PROTOS.keys())
+
+_lock = threading.Lock()
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return libtt.so; raises if it is missing or broken."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"libtt.so not found at {LIB_PATH}; build it with "
+                "`make -C hm-retrieval-two-tower_amd/csrc` (or __graft_entry__.build())"
+            )
+        handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, (restype, argtypes) in _PROTOS.items():
+            fn = getattr(handle, name)
+            fn.restype = restype
+            fn.argtypes = argtypes
+        _lib = handle
+        return _lib
+
+
+def check(rc: int) -> None:
+    """Raise TTError for a non-zero libtt status."""
+    if rc != TT_OK:
+        msg = lib().tt_last_error()
+        raise TTError(rc, msg.decode() if msg else "")

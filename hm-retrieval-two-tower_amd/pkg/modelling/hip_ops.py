@@ -1,0 +1,321 @@
+"""Torch-tensor wrappers over the libtt C ABI (include/tt.h).
+
+PyTorch is plumbing here: it owns device memory and the current HIP stream.
+Every function checks shapes/dtypes/devices on the host, passes raw device
+pointers plus torch's current stream to libtt, and raises on error.  There is
+no CPU or eager fallback: a CPU tensor or a missing libtt.so is an error.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from pkg import _native
+from pkg._native import GatherSegment, SparseTable, check, lib
+
+__all__ = [
+    "gather_grouped",
+    "sparse_adagrad",
+    "sparse_adam",
+    "dedup_sum",
+    "dense_adagrad",
+    "dense_adam",
+    "inbatch_rows",
+    "inbatch_cols",
+    "bruteforce_build",
+    "bruteforce_search",
+    "topk_merge",
+    "recall_hits",
+    "Workspace",
+]
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _req(t: torch.Tensor, name: str, dtype: torch.dtype, ndim: Optional[int] = None) -> None:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if t.device.type != "cuda":
+        raise ValueError(f"{name} must live on the GPU (got {t.device}); libtt has no CPU path")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if ndim is not None and t.dim() != ndim:
+        raise ValueError(f"{name} must be {ndim}-D, got shape {tuple(t.shape)}")
+
+
+def _row_major(t: torch.Tensor, name: str) -> int:
+    """Leading dimension of a 2-D tensor with unit column stride."""
+    if t.dim() != 2 or (t.stride(1) != 1 and t.shape[1] > 1):
+        raise ValueError(f"{name} must be 2-D with unit column stride")
+    return max(t.stride(0), t.shape[1])
+
+
+class Workspace:
+    """Grow-only device scratch buffers, one per (device, tag).
+
+    Buffers are reused across calls on the same stream; allocate (warm) them
+    before capturing a hipGraph so replays never allocate.
+    """
+
+    _bufs: Dict[Tuple[int, str], torch.Tensor] = {}
+
+    @classmethod
+    def get(cls, nbytes: int, device: torch.device, tag: str) -> torch.Tensor:
+        key = (device.index if device.index is not None else torch.cuda.current_device(), tag)
+        buf = cls._bufs.get(key)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+            cls._bufs[key] = buf
+        return buf
+
+    @classmethod
+    def clear(cls) -> None:
+        cls._bufs.clear()
+
+
+# --------------------------------------------------------------------------
+# K2+K3 gather
+def gather_grouped(
+    segments: Sequence[Tuple[torch.Tensor, Optional[torch.Tensor], int]],
+    batch: int,
+    out: torch.Tensor,
+) -> torch.Tensor:
+    """segments: (table [V,D] or numeric values [B], ids [B] int32 or None, col_offset)."""
+    _req(out, "out", torch.float32, 2)
+    ld = _row_major(out, "out")
+    if len(segments) > _native.MAX_SEGMENTS:
+        raise ValueError(f"at most {_native.MAX_SEGMENTS} segments per launch")
+    arr = (GatherSegment * len(segments))()
+    for i, (table, ids, off) in enumerate(segments):
+        _req(table, f"table[{i}]", torch.float32)
+        if not table.is_contiguous():
+            raise ValueError(f"table[{i}] must be contiguous")
+        if ids is not None:
+            _req(ids, f"ids[{i}]", torch.int32)
+            if ids.numel() != batch or not ids.is_contiguous():
+                raise ValueError(f"ids[{i}] must be a contiguous [{batch}] int32 tensor")
+            dim = table.shape[1]
+            rows = table.shape[0]
+        else:
+            if table.numel() != batch:
+                raise ValueError(f"numeric column {i} must have {batch} values")
+            dim, rows = 1, batch
+        arr[i].table = table.data_ptr()
+        arr[i].ids = ids.data_ptr() if ids is not None else None
+        arr[i].num_rows = rows
+        arr[i].dim = dim
+        arr[i].col_offset = off
+    check(lib().tt_gather_grouped(arr, len(segments), batch, out.data_ptr(), ld, _stream()))
+    return out
+
+
+# --------------------------------------------------------------------------
+# K8+K9 sparse optimizer steps
+def _sparse_tables(tables: Sequence[dict], batch: int, adam: bool):
+    arr = (SparseTable * len(tables))()
+    for i, t in enumerate(tables):
+        table, slot0 = t["table"], t["slot0"]
+        _req(table, f"table[{i}]", torch.float32, 2)
+        _req(slot0, f"slot0[{i}]", torch.float32, 2)
+        if not (table.is_contiguous() and slot0.is_contiguous()) or slot0.shape != table.shape:
+            raise ValueError(f"table/slot0[{i}] must be contiguous and of equal shape")
+        if adam:
+            slot1 = t["slot1"]
+            _req(slot1, f"slot1[{i}]", torch.float32, 2)
+            if not slot1.is_contiguous() or slot1.shape != table.shape:
+                raise ValueError(f"slot1[{i}] must be contiguous with the table's shape")
+        ids: List[torch.Tensor] = t["ids"]
+        offs: List[int] = t["grad_col_offset"]
+        if not (1 <= len(ids) <= _native.MAX_SOURCES) or len(ids) != len(offs):
+            raise ValueError(f"table[{i}]: 1..{_native.MAX_SOURCES} (ids, col_offset) sources required")
+        arr[i].table = table.data_ptr()
+        arr[i].slot0 = slot0.data_ptr()
+        arr[i].slot1 = t["slot1"].data_ptr() if adam else None
+        arr[i].num_rows = table.shape[0]
+        arr[i].dim = table.shape[1]
+        arr[i].num_sources = len(ids)
+        for s, (x, o) in enumerate(zip(ids, offs)):
+            _req(x, f"ids[{i}][{s}]", torch.int32)
+            if x.numel() != batch or not x.is_contiguous():
+                raise ValueError(f"ids[{i}][{s}] must be contiguous [{batch}] int32")
+            arr[i].ids[s] = x.data_ptr()
+            arr[i].grad_col_offset[s] = o
+    return arr
+
+
+def sparse_adagrad(tables: Sequence[dict], batch: int, grad: torch.Tensor, lr: float, epsilon: float) -> None:
+    """tables: dicts with table, slot0 (accumulator), ids [list], grad_col_offset [list]."""
+    _req(grad, "grad", torch.float32, 2)
+    ld = _row_major(grad, "grad")
+    arr = _sparse_tables(tables, batch, adam=False)
+    L = lib()
+    need = L.tt_sparse_workspace_size(arr, len(tables), batch)
+    ws = Workspace.get(need, grad.device, "sparse")
+    check(L.tt_sparse_adagrad(arr, len(tables), batch, grad.data_ptr(), ld, lr, epsilon, ws.data_ptr(), ws.numel(),
+                              _stream()))
+
+
+def sparse_adam(tables: Sequence[dict], batch: int, grad: torch.Tensor, lr: float, beta1: float, beta2: float,
+                epsilon: float, step: int) -> None:
+    _req(grad, "grad", torch.float32, 2)
+    ld = _row_major(grad, "grad")
+    arr = _sparse_tables(tables, batch, adam=True)
+    L = lib()
+    need = L.tt_sparse_workspace_size(arr, len(tables), batch)
+    ws = Workspace.get(need, grad.device, "sparse")
+    check(L.tt_sparse_adam(arr, len(tables), batch, grad.data_ptr(), ld, lr, beta1, beta2, epsilon, step,
+                           ws.data_ptr(), ws.numel(), _stream()))
+
+
+def dedup_sum(ids: torch.Tensor, grad: torch.Tensor, num_rows: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Distinct ids (ascending) and per-id gradient sums (K8)."""
+    _req(ids, "ids", torch.int32, 1)
+    _req(grad, "grad", torch.float32, 2)
+    ld = _row_major(grad, "grad")
+    n, dim = ids.numel(), grad.shape[1]
+    if grad.shape[0] != n:
+        raise ValueError("grad must have one row per id")
+    L = lib()
+    ws = Workspace.get(L.tt_dedup_workspace_size(n, dim), grad.device, "dedup")
+    uniq = torch.empty(n, dtype=torch.int32, device=grad.device)
+    summed = torch.empty(n, dim, dtype=torch.float32, device=grad.device)
+    count = torch.empty(1, dtype=torch.int32, device=grad.device)
+    check(L.tt_dedup_sum(ids.data_ptr(), n, num_rows, grad.data_ptr(), ld, dim, uniq.data_ptr(), summed.data_ptr(),
+                         count.data_ptr(), ws.data_ptr(), ws.numel(), _stream()))
+    u = int(count.item())
+    return uniq[:u], summed[:u]
+
+
+def dense_adagrad(param: torch.Tensor, accum: torch.Tensor, grad: torch.Tensor, lr: float, epsilon: float) -> None:
+    for t, n in ((param, "param"), (accum, "accum"), (grad, "grad")):
+        _req(t, n, torch.float32)
+        if not t.is_contiguous() or t.numel() != param.numel():
+            raise ValueError(f"{n} must be contiguous with param's numel")
+    check(lib().tt_dense_adagrad(param.data_ptr(), accum.data_ptr(), grad.data_ptr(), param.numel(), lr, epsilon,
+                                 _stream()))
+
+
+def dense_adam(param, m, v, grad, lr, beta1, beta2, epsilon, step) -> None:
+    for t, n in ((param, "param"), (m, "m"), (v, "v"), (grad, "grad")):
+        _req(t, n, torch.float32)
+        if not t.is_contiguous() or t.numel() != param.numel():
+            raise ValueError(f"{n} must be contiguous with param's numel")
+    check(lib().tt_dense_adam(param.data_ptr(), m.data_ptr(), v.data_ptr(), grad.data_ptr(), param.numel(), lr,
+                              beta1, beta2, epsilon, step, _stream()))
+
+
+# --------------------------------------------------------------------------
+# K5+K6+K7 fused in-batch softmax cross-entropy
+def _opt_ptr(t: Optional[torch.Tensor], name: str, n: int) -> Optional[int]:
+    if t is None:
+        return None
+    _req(t, name, torch.float32, 1)
+    if t.numel() != n or not t.is_contiguous():
+        raise ValueError(f"{name} must be a contiguous [{n}] float32 tensor")
+    return t.data_ptr()
+
+
+def inbatch_rows(q: torch.Tensor, c: torch.Tensor, logq: Optional[torch.Tensor], pos_offset: int = 0,
+                 want_dq: bool = True):
+    """Row pass: (lse [R], row_loss [R], dq [R,E] or None)."""
+    _req(q, "q", torch.float32, 2)
+    _req(c, "c", torch.float32, 2)
+    ldq, ldc = _row_major(q, "q"), _row_major(c, "c")
+    R, E = q.shape
+    C = c.shape[0]
+    if c.shape[1] != E:
+        raise ValueError("q and c must share the embedding size")
+    L = lib()
+    ws = Workspace.get(L.tt_inbatch_workspace_size(R, C, E), q.device, "inbatch")
+    lse = torch.empty(R, dtype=torch.float32, device=q.device)
+    row_loss = torch.empty(R, dtype=torch.float32, device=q.device)
+    dq = torch.empty(R, E, dtype=torch.float32, device=q.device) if want_dq else None
+    check(L.tt_inbatch_xent_rows(q.data_ptr(), ldq, R, c.data_ptr(), ldc, C, E, _opt_ptr(logq, "logq", C),
+                                 pos_offset, lse.data_ptr(), row_loss.data_ptr(),
+                                 dq.data_ptr() if dq is not None else None, ws.data_ptr(), ws.numel(), _stream()))
+    return lse, row_loss, dq
+
+
+def inbatch_cols(q: torch.Tensor, lse: torch.Tensor, c: torch.Tensor, logq: Optional[torch.Tensor],
+                 pos_offset: int = 0) -> torch.Tensor:
+    """Column pass: dc [C,E]."""
+    _req(q, "q", torch.float32, 2)
+    _req(c, "c", torch.float32, 2)
+    ldq, ldc = _row_major(q, "q"), _row_major(c, "c")
+    R, E = q.shape
+    C = c.shape[0]
+    L = lib()
+    ws = Workspace.get(L.tt_inbatch_workspace_size(R, C, E), q.device, "inbatch")
+    dc = torch.empty(C, E, dtype=torch.float32, device=q.device)
+    check(L.tt_inbatch_xent_cols(q.data_ptr(), ldq, R, _opt_ptr(lse, "lse", R), c.data_ptr(), ldc, C, E,
+                                 _opt_ptr(logq, "logq", C), pos_offset, dc.data_ptr(), ws.data_ptr(), ws.numel(),
+                                 _stream()))
+    return dc
+
+
+# --------------------------------------------------------------------------
+# K11+K12 brute-force index
+def bruteforce_build(cand: torch.Tensor) -> torch.Tensor:
+    _req(cand, "cand", torch.float32, 2)
+    ld = _row_major(cand, "cand")
+    n, d = cand.shape
+    L = lib()
+    nbytes = L.tt_bruteforce_index_bytes(n, d)
+    if nbytes == 0:
+        raise ValueError(f"unsupported index shape {tuple(cand.shape)}")
+    index = torch.empty(nbytes, dtype=torch.uint8, device=cand.device)
+    check(L.tt_bruteforce_build(cand.data_ptr(), ld, n, d, index.data_ptr(), nbytes, _stream()))
+    return index
+
+
+def bruteforce_search(index: torch.Tensor, cand: torch.Tensor, queries: torch.Tensor, k: int,
+                      index_offset: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+    _req(index, "index", torch.uint8, 1)
+    _req(cand, "cand", torch.float32, 2)
+    _req(queries, "queries", torch.float32, 2)
+    ldc, ldq = _row_major(cand, "cand"), _row_major(queries, "queries")
+    n, d = cand.shape
+    nq = queries.shape[0]
+    if queries.shape[1] != d:
+        raise ValueError("queries and candidates must share the embedding size")
+    if k > n:
+        raise ValueError(f"k={k} exceeds the number of candidates {n}")
+    L = lib()
+    ws = Workspace.get(L.tt_bruteforce_workspace_size(max(nq, 1), n, d, k), queries.device, "bruteforce")
+    out_s = torch.empty(nq, k, dtype=torch.float32, device=queries.device)
+    out_i = torch.empty(nq, k, dtype=torch.int32, device=queries.device)
+    check(L.tt_bruteforce_search(index.data_ptr(), cand.data_ptr(), ldc, n, d, queries.data_ptr(), ldq, nq, k,
+                                 index_offset, out_s.data_ptr(), out_i.data_ptr(), ws.data_ptr(), ws.numel(),
+                                 _stream()))
+    return out_s, out_i
+
+
+def topk_merge(scores: torch.Tensor, idx: torch.Tensor, k_out: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """scores/idx: [L, Q, k_in] sorted per list -> global [Q, k_out]."""
+    _req(scores, "scores", torch.float32, 3)
+    _req(idx, "idx", torch.int32, 3)
+    if not (scores.is_contiguous() and idx.is_contiguous()) or scores.shape != idx.shape:
+        raise ValueError("scores/idx must be contiguous and of equal shape")
+    Ln, Q, k_in = scores.shape
+    out_s = torch.empty(Q, k_out, dtype=torch.float32, device=scores.device)
+    out_i = torch.empty(Q, k_out, dtype=torch.int32, device=scores.device)
+    check(lib().tt_topk_merge(scores.data_ptr(), idx.data_ptr(), Ln, Q, k_in, k_out, out_s.data_ptr(),
+                              out_i.data_ptr(), _stream()))
+    return out_s, out_i
+
+
+def recall_hits(true_ids: torch.Tensor, cand_ids: torch.Tensor, ks: Sequence[int], hits: torch.Tensor) -> None:
+    """hits [len(ks)] int64 += #{b: true_ids[b] in cand_ids[b,:k]} (every match counts)."""
+    _req(true_ids, "true_ids", torch.int32, 1)
+    _req(cand_ids, "cand_ids", torch.int32, 2)
+    _req(hits, "hits", torch.int64, 1)
+    B, K = cand_ids.shape
+    if true_ids.numel() != B or not cand_ids.is_contiguous() or not true_ids.is_contiguous():
+        raise ValueError("true_ids [B] and cand_ids [B,K] must be contiguous")
+    ks_arr = (ctypes.c_int32 * len(ks))(*[int(k) for k in ks])
+    check(lib().tt_recall_hits(true_ids.data_ptr(), cand_ids.data_ptr(), B, K, ks_arr, len(ks), hits.data_ptr(),
+                               _stream()))

@@ -1,0 +1,210 @@
+/*
+ * tt.h — C ABI of libtt.so, the MI355X (gfx950) hot path of the two-tower
+ * retrieval trainer and brute-force index.
+ *
+ * Every entry point is stream-ordered and asynchronous: it validates its
+ * arguments on the host, enqueues HIP kernels on `stream` and returns.  No
+ * entry point allocates device memory or synchronises; scratch comes from a
+ * caller-owned workspace whose size is given by the matching *_workspace_size
+ * query.  All pointers are device pointers unless stated otherwise; all
+ * matrices are row-major with an explicit leading dimension (in elements).
+ *
+ * Return value: TT_OK (0) or a TT_ERR_* code; tt_last_error() returns a
+ * thread-local message describing the last failure on the calling thread.
+ *
+ * Reference interfaces each entry point replaces are cited as
+ * /root/reference/<file>:<line> (SelvinSelbaraju/hm-retrieval-two-tower).
+ * The reference has no FFI: its "operator API" is the Keras layer/model
+ * classes, so the citations name the TF op call sites.
+ */
+#ifndef TT_H_
+#define TT_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* tt_stream_t; /* a hipStream_t; NULL selects the null stream */
+
+enum {
+  TT_OK = 0,
+  TT_ERR_BAD_ARG = 1,     /* invalid shape / pointer / parameter            */
+  TT_ERR_HIP = 2,         /* a HIP runtime call failed                      */
+  TT_ERR_UNSUPPORTED = 3, /* valid request this build does not implement    */
+  TT_ERR_WORKSPACE = 4    /* workspace missing or smaller than required     */
+};
+
+/* Library version string, e.g. "tt 0.1.0 gfx950". */
+const char* tt_version(void);
+/* Thread-local description of the last error ("" if none). */
+const char* tt_last_error(void);
+
+/* ------------------------------------------------------------------------ *
+ * K2+K3  Grouped embedding gather + concat.
+ * Replaces InputLayer.call  (pkg/modelling/layers/input_layer.py:45-69):
+ * numeric features copied first, then per categorical feature
+ * Embedding(table)[ids] (input_layer.py:37-41,67), concatenated on the last
+ * axis (input_layer.py:68).  One launch for all features; each segment
+ * writes straight into its column range of `out`.
+ * Out-of-range ids produce zero rows (TF GPU gather semantics).
+ * ------------------------------------------------------------------------ */
+#define TT_MAX_SEGMENTS 32
+
+typedef struct {
+  const float* table;   /* [num_rows, dim] fp32, or [batch] values if ids==NULL */
+  const int32_t* ids;   /* [batch] row ids; NULL = numeric pass-through column  */
+  int64_t num_rows;     /* rows of `table` (ignored for numeric columns)        */
+  int32_t dim;          /* embedding size (1 for numeric columns)               */
+  int32_t col_offset;   /* first column of this segment in `out`                */
+} tt_gather_segment;
+
+int tt_gather_grouped(const tt_gather_segment* segs, int32_t num_segs,
+                      int64_t batch, float* out, int64_t out_stride,
+                      tt_stream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * K8+K9  Sparse optimizer step on embedding tables.
+ * Replaces the legacy Keras optimizer's sparse path reached from
+ * TwoTowerModel.train_step -> optimizer.minimize
+ * (pkg/modelling/models/two_tower_model.py:124, optimizer_factory.py:15-18):
+ * _deduplicate_indexed_slices (Unique + UnsortedSegmentSum, duplicates summed
+ * in batch order) followed by ResourceSparseApplyAdagradV2 /
+ * the legacy Adam sparse update.
+ *
+ * A table may be looked up by several features of one batch (the reference's
+ * duplicated `product_type_name`, main.py:57-68 with input_layer.py:31,66-67):
+ * list each lookup as a source; the index list is the concatenation of the
+ * sources' ids in source order and duplicates are summed in that order.
+ * ------------------------------------------------------------------------ */
+#define TT_MAX_SOURCES 4
+
+typedef struct {
+  float* table;        /* [num_rows, dim] parameters, updated in place          */
+  float* slot0;        /* Adagrad accumulator / Adam first moment [num_rows,dim] */
+  float* slot1;        /* Adam second moment, NULL for Adagrad                  */
+  int64_t num_rows;
+  int32_t dim;
+  int32_t num_sources; /* 1..TT_MAX_SOURCES                                     */
+  const int32_t* ids[TT_MAX_SOURCES];      /* [batch] row ids per source         */
+  int32_t grad_col_offset[TT_MAX_SOURCES]; /* column of the source's slice in grad */
+} tt_sparse_table;
+
+size_t tt_sparse_workspace_size(const tt_sparse_table* tables, int32_t num_tables,
+                                int64_t batch);
+
+/* acc += g*g ; w -= lr*g / (sqrt(acc) + epsilon) on every touched row, g the
+ * duplicate-summed gradient (TF ResourceSparseApplyAdagradV2 CPU kernel). */
+int tt_sparse_adagrad(const tt_sparse_table* tables, int32_t num_tables,
+                      int64_t batch, const float* grad, int64_t grad_stride,
+                      float lr, float epsilon, void* workspace,
+                      size_t workspace_bytes, tt_stream_t stream);
+
+/* Legacy Keras Adam sparse path: m,v decayed over the WHOLE slot, the scaled
+ * duplicate-summed gradient scatter-added, then the WHOLE table updated with
+ * lr_t = lr*sqrt(1-beta2^step)/(1-beta1^step) (step is 1-based). */
+int tt_sparse_adam(const tt_sparse_table* tables, int32_t num_tables,
+                   int64_t batch, const float* grad, int64_t grad_stride,
+                   float lr, float beta1, float beta2, float epsilon,
+                   int64_t step, void* workspace, size_t workspace_bytes,
+                   tt_stream_t stream);
+
+/* Dedup only (K8), for parity checks: writes the U distinct ids of
+ * ids[0..n) in ascending order, the per-id gradient sums [U, dim] (rows of
+ * `grad` summed in index order) and U (device int32).  Capacity n rows. */
+size_t tt_dedup_workspace_size(int64_t n, int32_t dim);
+int tt_dedup_sum(const int32_t* ids, int64_t n, int64_t num_rows,
+                 const float* grad, int64_t grad_stride, int32_t dim,
+                 int32_t* unique_ids, float* summed, int32_t* num_unique,
+                 void* workspace, size_t workspace_bytes, tt_stream_t stream);
+
+/* K10  Dense optimizer steps on a flat parameter buffer (tower MLP weights).
+ * ResourceApplyAdagradV2 / ResourceApplyAdam (optimizer_factory.py:15-18). */
+int tt_dense_adagrad(float* param, float* accum, const float* grad, int64_t n,
+                     float lr, float epsilon, tt_stream_t stream);
+int tt_dense_adam(float* param, float* m, float* v, const float* grad,
+                  int64_t n, float lr, float beta1, float beta2, float epsilon,
+                  int64_t step, tt_stream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * K5+K6+K7  Fused in-batch scores, logQ correction and softmax
+ * cross-entropy (reduction SUM) with its gradient.
+ * Replaces TwoTowerModel.call's matmul (two_tower_model.py:92),
+ * LogQCorrection.__call__ (logq_correction.py:66-71), the eye-label
+ * CategoricalCrossentropy(from_logits, SUM) (two_tower_model.py:119-122,
+ * runner.py:78-83) and the tape gradient of that chain.
+ *
+ *   S'[i][j] = q_i . c_j - logq[j]
+ *   loss_i   = logsumexp_j S'[i][j] - S'[i][pos(i)]
+ *   dq_i     = sum_j softmax_j(S'[i]) c_j - c_pos(i)
+ *   dc_j     = sum_i softmax(S'[i])_j q_i - q_pos^-1(j)
+ *
+ * bf16 MFMA operands, fp32 accumulation, fp32 outputs; the [rows, cols]
+ * score matrix is never materialised.  Rows and columns are given
+ * separately so a rank can score its local rows against all-gathered
+ * columns (global in-batch negatives): the positive column of local row i
+ * is i + pos_offset, the positive row of local column j is j + pos_offset.
+ * ------------------------------------------------------------------------ */
+size_t tt_inbatch_workspace_size(int64_t n_rows, int64_t n_cols, int32_t dim);
+
+/* Row pass: lse[i], row_loss[i] = lse[i] - S'[i][i+pos_offset], and (if dq
+ * != NULL) dq [n_rows, dim] (ld = dim). */
+int tt_inbatch_xent_rows(const float* q, int64_t ldq, int64_t n_rows,
+                         const float* c, int64_t ldc, int64_t n_cols,
+                         int32_t dim, const float* logq, int64_t pos_offset,
+                         float* lse, float* row_loss, float* dq,
+                         void* workspace, size_t workspace_bytes,
+                         tt_stream_t stream);
+
+/* Column pass: dc [n_cols, dim] (ld = dim) from all rows' q and lse. */
+int tt_inbatch_xent_cols(const float* q, int64_t ldq, int64_t n_rows,
+                         const float* lse, const float* c, int64_t ldc,
+                         int64_t n_cols, int32_t dim, const float* logq,
+                         int64_t pos_offset, float* dc, void* workspace,
+                         size_t workspace_bytes, tt_stream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * K11+K12  Brute-force scoring with fused top-K.
+ * Replaces BruteForceIndex.call (pkg/modelling/indices/brute_force.py:76-81):
+ * matmul(queries, candidates^T) then tf.math.top_k(k) (sorted descending,
+ * ties -> lower index).  bf16 MFMA screening against a certified error bound
+ * keeps a per-query shortlist; the shortlist is rescored in fp32 as a
+ * k-ordered fmaf chain and the exact top-k returned.  Indices are
+ * candidate positions + index_offset (the global offset of a shard).
+ * ------------------------------------------------------------------------ */
+/* Bytes of a prepared candidate image (bf16 copy + norms). */
+size_t tt_bruteforce_index_bytes(int64_t n_cand, int32_t dim);
+int tt_bruteforce_build(const float* cand, int64_t ldc, int64_t n_cand,
+                        int32_t dim, void* index, size_t index_bytes,
+                        tt_stream_t stream);
+size_t tt_bruteforce_workspace_size(int64_t n_queries, int64_t n_cand,
+                                    int32_t dim, int32_t k);
+int tt_bruteforce_search(const void* index, const float* cand, int64_t ldc,
+                         int64_t n_cand, int32_t dim, const float* queries,
+                         int64_t ldq, int64_t n_queries, int32_t k,
+                         int64_t index_offset, float* out_scores,
+                         int32_t* out_idx, void* workspace,
+                         size_t workspace_bytes, tt_stream_t stream);
+
+/* Merge `num_lists` per-shard sorted top-k_in lists laid out
+ * [num_lists][n_queries][k_in] into the global top-k_out with the same
+ * order (score descending, index ascending on ties). */
+int tt_topk_merge(const float* scores, const int32_t* idx, int32_t num_lists,
+                  int64_t n_queries, int32_t k_in, int32_t k_out,
+                  float* out_scores, int32_t* out_idx, tt_stream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * K14  Recall hits (IndexRecall.__call__, metrics/index_recall.py:52-58):
+ * hits[t] += #{b : true_ids[b] in cand_ids[b, 0:ks[t]]}.  hits is int64
+ * [num_ks], accumulated (not overwritten).
+ * ------------------------------------------------------------------------ */
+int tt_recall_hits(const int32_t* true_ids, const int32_t* cand_ids,
+                   int64_t batch, int32_t k_total, const int32_t* ks_host,
+                   int32_t num_ks, int64_t* hits, tt_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TT_H_ */

@@ -1,0 +1,1 @@
+"""CPU restatement of the reference hot path (test infrastructure only)."""

@@ -1,0 +1,361 @@
+"""CPU restatement of the reference hot path — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module, and only as the checker / reported CPU baseline.  The
+product (hm-retrieval-two-tower_amd/pkg) never imports it.
+
+Every function restates SelvinSelbaraju/hm-retrieval-two-tower (cited as
+/root/reference/<file>:<line>) on numpy / plain C.  The reference itself
+cannot run here (TensorFlow is not installed), so parity is
+pinned by the golden values of the reference's own tests
+(tests/golden/reference_tests.json, checked by tests/test_oracle.py) and,
+for the paths no reference test covers (gather, dedup + Adagrad, in-batch
+loss and gradients, top-k tie breaking), by this restatement alone
+("parity unpinned by the reference").
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from ctypes import POINTER, c_float, c_int, c_int32, c_int64, c_void_p
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "_build", "libtt_oracle.so")
+_lib = None
+
+# Keras legacy Adagrad defaults (tf.keras.optimizers.legacy.Adagrad).
+ADAGRAD_INITIAL_ACCUMULATOR = 0.1
+ADAGRAD_EPSILON = 1e-7
+# GPU dedup chunk (csrc/tt_sparse.hip kChunk).
+GPU_DEDUP_CHUNK = 32
+
+
+def build() -> str:
+    """Compile the C restatement (make -C oracle) if needed; returns the .so path."""
+    if not os.path.exists(_SO):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _SO
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_SO)
+        L.oracle_bruteforce_topk.restype = c_int
+        L.oracle_bruteforce_topk.argtypes = [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64, c_int, c_int,
+                                             c_void_p, c_void_p, c_int]
+        L.oracle_scores.restype = None
+        L.oracle_scores.argtypes = [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p]
+        L.oracle_dedup_sum.restype = c_int
+        L.oracle_dedup_sum.argtypes = [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p]
+        L.oracle_sparse_adagrad_apply.restype = None
+        L.oracle_sparse_adagrad_apply.argtypes = [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_float,
+                                                  c_float]
+        _lib = L
+    return _lib
+
+
+def _f32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def _i32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+# ---------------------------------------------------------------------------
+# a1: vocab / StringLookup (features.py:106-127, input_layer.py:33-36)
+def vocab_from_values(values: Sequence, max_vocab_size: Optional[int] = None) -> np.ndarray:
+    """value_counts() order (count desc, first-seen on ties), head(max), str()."""
+    import pandas as pd
+
+    vc = pd.Series(list(values)).value_counts()
+    idx = list(vc.head(max_vocab_size).index) if max_vocab_size else list(vc.index)
+    return np.array([str(x) for x in idx])
+
+
+def string_lookup(vocab: Sequence[str], values: Sequence) -> np.ndarray:
+    """StringLookup(num_oov_indices=1): vocab[i] -> i+1, anything else -> 0."""
+    table = {v: i + 1 for i, v in enumerate(vocab)}
+    return np.array([table.get(str(v) if not isinstance(v, bytes) else v.decode(), 0) for v in values],
+                    dtype=np.int32)
+
+
+# ---------------------------------------------------------------------------
+# a2: InputLayer.call (input_layer.py:45-69)
+def gather_concat(numeric: Sequence[np.ndarray], tables: Sequence[np.ndarray], ids: Sequence[np.ndarray]) -> np.ndarray:
+    """Numeric columns first, then table[ids] per categorical feature, concat."""
+    cols: List[np.ndarray] = [np.asarray(v, np.float32).reshape(-1, 1) for v in numeric]
+    for t, i in zip(tables, ids):
+        i = np.asarray(i, np.int64).reshape(-1)
+        valid = (i >= 0) & (i < t.shape[0])
+        g = np.zeros((i.size, t.shape[1]), np.float32)
+        g[valid] = t[i[valid]]
+        cols.append(g)
+    return np.concatenate(cols, axis=1) if cols else np.zeros((0, 0), np.float32)
+
+
+# ---------------------------------------------------------------------------
+# a7: LogQCorrection (logq_correction.py:32-42, 66-71); prob table etl/runner.py:75-78
+def logq_from_lookup(candidate_ids: Sequence, lookup: Dict[str, float]) -> np.ndarray:
+    """log(p[id]) in fp32 with the StaticHashTable default 1.0 (-> 0)."""
+    p = np.array([lookup.get(str(x) if not isinstance(x, bytes) else x.decode(), 1.0) for x in candidate_ids],
+                 dtype=np.float32)
+    return np.log(p).astype(np.float32)
+
+
+def logq_correction(logits: np.ndarray, candidate_ids: Sequence, lookup: Dict[str, float]) -> np.ndarray:
+    """logits [B,B] - log p[candidate_ids]^T broadcast over rows."""
+    return (np.asarray(logits, np.float32) - logq_from_lookup(candidate_ids, lookup)[None, :]).astype(np.float32)
+
+
+def prob_lookup_from_values(values: Sequence) -> Dict[str, float]:
+    """etl/runner.py:75-78: p = value_counts / len(train), keys str(id)."""
+    import pandas as pd
+
+    s = pd.Series(list(values))
+    probs = s.value_counts() / len(s)
+    return {str(probs.index[i]): float(probs.iloc[i]) for i in range(len(probs))}
+
+
+# ---------------------------------------------------------------------------
+# a5: Tower.call (tower.py:41-49, 51-75): Dense(relu)* then Dense(E, relu)
+def tower_forward(x: np.ndarray, layers: Sequence[Tuple[np.ndarray, np.ndarray]], dtype=np.float64) -> np.ndarray:
+    h = np.asarray(x, dtype)
+    for w, b in layers:
+        h = np.maximum(h @ np.asarray(w, dtype) + np.asarray(b, dtype), 0)
+    return h
+
+
+# ---------------------------------------------------------------------------
+# a6-a8: scores, logQ, CE(from_logits, SUM) with eye labels and its gradient
+# (two_tower_model.py:92, 113-124; runner.py:78-83)
+def inbatch_softmax_xent(q: np.ndarray, c: np.ndarray, logq: Optional[np.ndarray] = None, pos_offset: int = 0,
+                         dtype=np.float64):
+    """Returns dict(loss, row_loss, lse, dq, dc) for local rows q [R,E] against
+    columns c [C,E]; the positive of row i is column i + pos_offset.  dc is
+    the column gradient of THIS row block (sum over blocks = full dc)."""
+    q = np.asarray(q, dtype)
+    c = np.asarray(c, dtype)
+    R = q.shape[0]
+    S = q @ c.T
+    if logq is not None:
+        S = S - np.asarray(logq, dtype)[None, :]
+    m = S.max(axis=1)
+    e = np.exp(S - m[:, None])
+    lse = m + np.log(e.sum(axis=1))
+    rows = np.arange(R)
+    pos = rows + pos_offset
+    row_loss = lse - S[rows, pos]
+    P = e / e.sum(axis=1, keepdims=True)
+    P[rows, pos] -= 1.0
+    return {
+        "loss": row_loss.sum(),
+        "row_loss": row_loss,
+        "lse": lse,
+        "dq": P @ c,
+        "dc": P.T @ q,
+    }
+
+
+# ---------------------------------------------------------------------------
+# a3/a4: dedup + sparse Adagrad (legacy Keras optimizer; see tt_oracle.c)
+def dedup_sum(ids: np.ndarray, grad: np.ndarray, chunk: int = 0) -> Tuple[np.ndarray, np.ndarray]:
+    ids = _i32(ids).reshape(-1)
+    grad = _f32(grad)
+    n, dim = grad.shape
+    uniq = np.empty(max(n, 1), np.int32)
+    sums = np.empty((max(n, 1), dim), np.float32)
+    u = lib().oracle_dedup_sum(ids.ctypes.data, n, grad.ctypes.data, grad.strides[0] // 4, dim, chunk,
+                               uniq.ctypes.data, sums.ctypes.data)
+    return uniq[:u].copy(), sums[:u].copy()
+
+
+def sparse_adagrad(table: np.ndarray, accum: np.ndarray, ids: np.ndarray, grad: np.ndarray, lr: float,
+                   eps: float = ADAGRAD_EPSILON, chunk: int = GPU_DEDUP_CHUNK) -> None:
+    """In place: dedup (ids out of [0, rows) skipped) then Adagrad per distinct row."""
+    ids = _i32(ids).reshape(-1)
+    valid = (ids >= 0) & (ids < table.shape[0])
+    uniq, sums = dedup_sum(ids[valid], _f32(grad)[valid], chunk)
+    assert table.dtype == np.float32 and accum.dtype == np.float32 and table.flags.c_contiguous
+    lib().oracle_sparse_adagrad_apply(table.ctypes.data, accum.ctypes.data, table.shape[1], uniq.ctypes.data,
+                                      sums.ctypes.data, len(uniq), lr, eps)
+
+
+def dense_adagrad(param: np.ndarray, accum: np.ndarray, grad: np.ndarray, lr: float,
+                  eps: float = ADAGRAD_EPSILON) -> None:
+    """ResourceApplyAdagradV2: accum += g^2; var -= g*lr / (sqrt(accum) + eps) (fp32, in place)."""
+    g = _f32(grad)
+    lr = np.float32(lr)
+    eps = np.float32(eps)
+    accum += g * g
+    param -= (g * lr) / (np.sqrt(accum) + eps)
+
+
+def dense_adam(param, m, v, grad, lr, beta1, beta2, eps, step) -> None:
+    """ResourceApplyAdam (fp32, in place)."""
+    f = np.float32
+    g = _f32(grad)
+    b1p = f(np.power(f(beta1), f(step)))
+    b2p = f(np.power(f(beta2), f(step)))
+    alpha = f((f(lr) * np.sqrt(f(1) - b2p)) / (f(1) - b1p))
+    m += (g - m) * (f(1) - f(beta1))
+    v += (g * g - v) * (f(1) - f(beta2))
+    param -= (m * alpha) / (np.sqrt(v) + f(eps))
+
+
+def sparse_adam(table, m, v, ids, grad, lr, beta1, beta2, eps, step, chunk: int = GPU_DEDUP_CHUNK) -> None:
+    """Legacy Adam._resource_apply_sparse after dedup (fp32, in place)."""
+    f = np.float32
+    ids = _i32(ids).reshape(-1)
+    valid = (ids >= 0) & (ids < table.shape[0])
+    uniq, sums = dedup_sum(ids[valid], _f32(grad)[valid], chunk)
+    b1p = f(np.power(f(beta1), f(step)))
+    b2p = f(np.power(f(beta2), f(step)))
+    lr_t = f(f(lr) * (np.sqrt(f(1) - b2p) / (f(1) - b1p)))
+    m *= f(beta1)
+    v *= f(beta2)
+    m[uniq] += sums * (f(1) - f(beta1))
+    v[uniq] += (sums * sums) * (f(1) - f(beta2))
+    table -= (lr_t * m) / (np.sqrt(v) + f(eps))
+
+
+# ---------------------------------------------------------------------------
+# a10: BruteForceIndex.call (brute_force.py:75-83)
+def bruteforce_topk(q: np.ndarray, c: np.ndarray, k: int, threads: int = 0) -> Tuple[np.ndarray, np.ndarray, int]:
+    """Exact fp32 fmaf-chain scores, top-k (score desc, index asc).  Returns
+    (scores [Q,k], indices [Q,k] int32, threads used)."""
+    q = _f32(q)
+    c = _f32(c)
+    nq, d = q.shape
+    n = c.shape[0]
+    if k > n:
+        raise ValueError(f"k={k} > number of candidates {n}")
+    out_s = np.empty((nq, k), np.float32)
+    out_i = np.empty((nq, k), np.int32)
+    used = lib().oracle_bruteforce_topk(q.ctypes.data, d, nq, c.ctypes.data, d, n, d, k, out_s.ctypes.data,
+                                        out_i.ctypes.data, threads)
+    return out_s, out_i, used
+
+
+def fmaf_scores(q: np.ndarray, c: np.ndarray) -> np.ndarray:
+    q = _f32(q)
+    c = _f32(c)
+    out = np.empty((q.shape[0], c.shape[0]), np.float32)
+    lib().oracle_scores(q.ctypes.data, q.shape[1], q.shape[0], c.ctypes.data, c.shape[1], c.shape[0], q.shape[1],
+                        out.ctypes.data)
+    return out
+
+
+def topk_merge(scores: np.ndarray, idx: np.ndarray, k: int) -> Tuple[np.ndarray, np.ndarray]:
+    """[L,Q,k_in] sorted lists -> global top-k with the top_k order."""
+    L, Q, kin = scores.shape
+    s = np.transpose(scores, (1, 0, 2)).reshape(Q, L * kin)
+    i = np.transpose(idx, (1, 0, 2)).reshape(Q, L * kin)
+    order = np.lexsort((i, -s.astype(np.float64)), axis=1)[:, :k]
+    return np.take_along_axis(s, order, 1), np.take_along_axis(i, order, 1)
+
+
+# ---------------------------------------------------------------------------
+# StaticIndex.call (static_index.py:37-55) and IndexRecall (index_recall.py:22-59)
+def static_index(candidates: Sequence, k: int, batch: int) -> np.ndarray:
+    row = np.asarray(list(candidates)[:k])
+    return np.tile(row[None, :], (batch, 1))
+
+
+class RecallAccumulator:
+    """hits[k] += sum(equal(true, cands[:, :k])) (int32); metric = hits/seen (float64)."""
+
+    def __init__(self, ks: Sequence[int]):
+        self.ks = list(ks)
+        self.hits = {k: 0 for k in self.ks}
+        self.seen = 0
+        self.metric: Dict[int, float] = {}
+
+    def update(self, true_ids: Sequence, candidates: np.ndarray) -> Dict[int, float]:
+        t = np.asarray(list(true_ids)).reshape(-1, 1)
+        self.seen += t.shape[0]
+        for k in self.ks:
+            self.hits[k] += int(np.sum(t == candidates[:, :k]))
+            self.metric[k] = np.float64(self.hits[k]) / np.float64(self.seen)
+        return self.metric
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline: one full train step (TwoTowerModel.train_step,
+# two_tower_model.py:94-130, with legacy Adagrad) in numpy fp32.
+def glorot_uniform(rng: np.random.Generator, fan_in: int, fan_out: int) -> np.ndarray:
+    lim = np.sqrt(6.0 / (fan_in + fan_out))
+    return rng.uniform(-lim, lim, size=(fan_in, fan_out)).astype(np.float32)
+
+
+class CpuTwoTower:
+    """fp32 numpy train step: gather -> towers -> scores/logQ/CE-SUM -> grads ->
+    dense Adagrad (MLP) + dedup + sparse Adagrad (tables)."""
+
+    def __init__(self, q_tables: List[np.ndarray], c_tables: List[np.ndarray], q_layers, c_layers, lr: float):
+        self.q_tables, self.c_tables = q_tables, c_tables
+        self.q_layers = [[w.copy(), b.copy()] for w, b in q_layers]
+        self.c_layers = [[w.copy(), b.copy()] for w, b in c_layers]
+        self.lr = lr
+        acc = ADAGRAD_INITIAL_ACCUMULATOR
+        self.q_acc = [np.full_like(t, acc) for t in q_tables]
+        self.c_acc = [np.full_like(t, acc) for t in c_tables]
+        self.ql_acc = [[np.full_like(w, acc), np.full_like(b, acc)] for w, b in self.q_layers]
+        self.cl_acc = [[np.full_like(w, acc), np.full_like(b, acc)] for w, b in self.c_layers]
+
+    @staticmethod
+    def _tower(x, layers):
+        acts = [x]
+        for w, b in layers:
+            acts.append(np.maximum(acts[-1] @ w + b, 0).astype(np.float32))
+        return acts
+
+    @staticmethod
+    def _tower_bwd(acts, layers, g):
+        grads = []
+        for li in range(len(layers) - 1, -1, -1):
+            w, _ = layers[li]
+            g = g * (acts[li + 1] > 0)
+            grads.append((acts[li].T @ g, g.sum(0)))
+            g = g @ w.T
+        return grads[::-1], g
+
+    def step(self, q_ids: List[np.ndarray], c_ids: List[np.ndarray], logq: Optional[np.ndarray]) -> float:
+        xq = gather_concat([], self.q_tables, q_ids)
+        xc = gather_concat([], self.c_tables, c_ids)
+        qa = self._tower(xq, self.q_layers)
+        ca = self._tower(xc, self.c_layers)
+        Q, C = qa[-1], ca[-1]
+        S = Q @ C.T
+        if logq is not None:
+            S -= logq[None, :]
+        m = S.max(1, keepdims=True)
+        e = np.exp(S - m)
+        z = e.sum(1, keepdims=True)
+        B = S.shape[0]
+        loss = float(np.sum(np.log(z[:, 0]) + m[:, 0] - S[np.arange(B), np.arange(B)]))
+        P = e / z
+        P[np.arange(B), np.arange(B)] -= 1.0
+        dQ = P @ C
+        dC = P.T @ Q
+        gq, dxq = self._tower_bwd(qa, self.q_layers, dQ)
+        gc, dxc = self._tower_bwd(ca, self.c_layers, dC)
+        for layers, accs, grads in ((self.q_layers, self.ql_acc, gq), (self.c_layers, self.cl_acc, gc)):
+            for (w, b), (aw, ab), (dw, db) in zip(layers, accs, grads):
+                dense_adagrad(w, aw, dw, self.lr)
+                dense_adagrad(b, ab, db, self.lr)
+        off = 0
+        for t, a, i in zip(self.q_tables, self.q_acc, q_ids):
+            sparse_adagrad(t, a, i, dxq[:, off:off + t.shape[1]], self.lr)
+            off += t.shape[1]
+        off = 0
+        for t, a, i in zip(self.c_tables, self.c_acc, c_ids):
+            sparse_adagrad(t, a, i, dxc[:, off:off + t.shape[1]], self.lr)
+            off += t.shape[1]
+        return loss

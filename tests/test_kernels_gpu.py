@@ -1,0 +1,251 @@
+"""Parity of every libtt entry point against the CPU restatement (oracle/).
+
+Tolerances:
+  gather, dedup, Adagrad, top-k indices + scores, merge, recall: bit-exact.
+  in-batch softmax CE (bf16 MFMA operands, fp32 accumulate) vs fp64 oracle:
+    loss rel 2e-3; ||dq - ref|| / ||ref|| and ||dc - ref|| / ||ref|| <= 1e-2.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle
+from pkg.modelling import hip_ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(x, dev, dtype=None):
+    return torch.as_tensor(np.ascontiguousarray(x), device=dev, dtype=dtype)
+
+
+def zipf_ids(rng, n, vocab, a=1.1):
+    r = rng.zipf(a, size=n) - 1
+    return (r % vocab).astype(np.int32)
+
+
+# --------------------------------------------------------------------------- gather
+def test_gather_grouped_bitexact(cuda):
+    rng = np.random.default_rng(0)
+    B = 1000
+    dims = [128, 2, 128, 16, 4, 8, 32, 4, 16, 4, 1, 3]
+    tables = [rng.standard_normal((rng.integers(1, 3000), d)).astype(np.float32) for d in dims]
+    ids = [rng.integers(-2, t.shape[0] + 2, size=B).astype(np.int32) for t in tables]  # includes OOB
+    numeric = [rng.standard_normal(B).astype(np.float32)]
+    ref = oracle.gather_concat(numeric, tables, ids)
+    W = ref.shape[1]
+    out = torch.full((B, W + 3), float("nan"), device=cuda)  # padded row stride
+    segs = [(_t(numeric[0], cuda), None, 0)]
+    off = 1
+    for t, i in zip(tables, ids):
+        segs.append((_t(t, cuda), _t(i, cuda), off))
+        off += t.shape[1]
+    hip_ops.gather_grouped(segs, B, out)
+    got = out[:, :W].cpu().numpy()
+    assert np.array_equal(got, ref)
+
+
+# --------------------------------------------------------------------------- dedup / adagrad
+@pytest.mark.parametrize("n,vocab,dim", [(1, 5, 4), (777, 50, 16), (16384, 105542, 128), (4096, 3, 2)])
+def test_dedup_sum_bitexact(cuda, n, vocab, dim):
+    rng = np.random.default_rng(n)
+    ids = zipf_ids(rng, n, vocab)
+    grad = rng.standard_normal((n, dim)).astype(np.float32)
+    u_ref, s_ref = oracle.dedup_sum(ids, grad, chunk=oracle.GPU_DEDUP_CHUNK)
+    u, s = hip_ops.dedup_sum(_t(ids, cuda), _t(grad, cuda), vocab)
+    assert np.array_equal(u.cpu().numpy(), u_ref)
+    assert np.array_equal(s.cpu().numpy(), s_ref)
+    # TF order (one sequential sum per id) agrees to within the fp32
+    # summation bound: |chunked - sequential| <= 2 * n_id * 2^-24 * sum|g|
+    _, s_tf = oracle.dedup_sum(ids, grad, chunk=0)
+    _, s_abs = oracle.dedup_sum(ids, np.abs(grad), chunk=0)
+    counts = np.bincount(ids)[u_ref].astype(np.float64)[:, None]
+    bound = 2.0 * counts * 2.0 ** -24 * s_abs
+    assert np.all(np.abs(s.cpu().numpy().astype(np.float64) - s_tf) <= bound + 1e-30)
+
+
+def test_sparse_adagrad_bitexact_multi_source(cuda):
+    rng = np.random.default_rng(1)
+    B = 4096
+    vocab = [1000, 131, 2000000]
+    dims = [64, 4, 128]
+    tabs = [rng.uniform(-0.05, 0.05, (v + 1, d)).astype(np.float32) for v, d in zip(vocab, dims)]
+    accs = [np.full_like(t, 0.1) for t in tabs]
+    ids = [zipf_ids(rng, B, v + 1) for v in vocab] + [zipf_ids(rng, B, vocab[1] + 1)]
+    W = sum(dims) + dims[1]
+    grad = rng.standard_normal((B, W)).astype(np.float32)
+    lr, eps = 0.05, 1e-7
+    dt = [_t(t, cuda) for t in tabs]
+    da = [_t(a, cuda) for a in accs]
+    di = [_t(i, cuda) for i in ids]
+    # table 1 is looked up twice (the reference's duplicated product_type_name)
+    specs = [
+        dict(table=dt[0], slot0=da[0], ids=[di[0]], grad_col_offset=[0]),
+        dict(table=dt[1], slot0=da[1], ids=[di[1], di[3]], grad_col_offset=[64, 64 + 4 + 128]),
+        dict(table=dt[2], slot0=da[2], ids=[di[2]], grad_col_offset=[68]),
+    ]
+    hip_ops.sparse_adagrad(specs, B, _t(grad, cuda), lr, eps)
+    oracle.sparse_adagrad(tabs[0], accs[0], ids[0], grad[:, 0:64], lr, eps)
+    both_ids = np.concatenate([ids[1], ids[3]])
+    both_g = np.concatenate([grad[:, 64:68], grad[:, 196:200]])
+    oracle.sparse_adagrad(tabs[1], accs[1], both_ids, both_g, lr, eps)
+    oracle.sparse_adagrad(tabs[2], accs[2], ids[2], grad[:, 68:196], lr, eps)
+    for i in range(3):
+        assert np.array_equal(dt[i].cpu().numpy(), tabs[i]), f"table {i}"
+        assert np.array_equal(da[i].cpu().numpy(), accs[i]), f"accum {i}"
+
+
+def test_dense_adagrad_and_adam_bitexact(cuda):
+    rng = np.random.default_rng(2)
+    n = 100003
+    p = rng.standard_normal(n).astype(np.float32)
+    a = np.full(n, 0.1, np.float32)
+    g = rng.standard_normal(n).astype(np.float32)
+    tp, ta = _t(p, cuda), _t(a, cuda)
+    hip_ops.dense_adagrad(tp, ta, _t(g, cuda), 0.05, 1e-7)
+    oracle.dense_adagrad(p, a, g, 0.05)
+    assert np.array_equal(tp.cpu().numpy(), p) and np.array_equal(ta.cpu().numpy(), a)
+    m = np.zeros(n, np.float32)
+    v = np.zeros(n, np.float32)
+    tp, tm, tv = _t(p, cuda), _t(m, cuda), _t(v, cuda)
+    for step in (1, 2, 3):
+        hip_ops.dense_adam(tp, tm, tv, _t(g, cuda), 1e-3, 0.9, 0.999, 1e-7, step)
+        oracle.dense_adam(p, m, v, g, 1e-3, 0.9, 0.999, 1e-7, step)
+    np.testing.assert_allclose(tp.cpu().numpy(), p, rtol=2e-6, atol=1e-7)
+
+
+def test_sparse_adam_matches_oracle(cuda):
+    rng = np.random.default_rng(3)
+    B, V, D = 2048, 500, 16
+    t = rng.uniform(-0.05, 0.05, (V, D)).astype(np.float32)
+    m = np.zeros_like(t)
+    v = np.zeros_like(t)
+    tt, tm, tv = _t(t, cuda), _t(m, cuda), _t(v, cuda)
+    for step in (1, 2):
+        ids = zipf_ids(rng, B, V)
+        g = rng.standard_normal((B, D)).astype(np.float32)
+        hip_ops.sparse_adam([dict(table=tt, slot0=tm, slot1=tv, ids=[_t(ids, cuda)], grad_col_offset=[0])], B,
+                            _t(g, cuda), 1e-3, 0.9, 0.999, 1e-7, step)
+        oracle.sparse_adam(t, m, v, ids, g, 1e-3, 0.9, 0.999, 1e-7, step)
+    np.testing.assert_allclose(tt.cpu().numpy(), t, rtol=2e-6, atol=1e-7)
+    np.testing.assert_allclose(tm.cpu().numpy(), m, rtol=2e-6, atol=1e-7)
+
+
+# --------------------------------------------------------------------------- in-batch CE
+def _rel(a, b):
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+@pytest.mark.parametrize("B,E,use_logq,scale", [(64, 16, False, 1.0), (300, 64, True, 0.5), (1024, 128, True, 0.3),
+                                                (2048, 128, True, 1.0), (129, 100, False, 0.2)])
+def test_inbatch_softmax_xent(cuda, B, E, use_logq, scale):
+    rng = np.random.default_rng(B + E)
+    q = np.maximum(rng.standard_normal((B, E)) * scale, 0).astype(np.float32)
+    c = np.maximum(rng.standard_normal((B, E)) * scale, 0).astype(np.float32)
+    logq = np.log(rng.uniform(1e-6, 1e-2, B)).astype(np.float32) if use_logq else None
+    ref = oracle.inbatch_softmax_xent(q, c, logq)
+    tq, tc = _t(q, cuda), _t(c, cuda)
+    tl = _t(logq, cuda) if use_logq else None
+    lse, row_loss, dq = hip_ops.inbatch_rows(tq, tc, tl)
+    dc = hip_ops.inbatch_cols(tq, lse, tc, tl)
+    loss = float(row_loss.double().sum())
+    assert abs(loss - ref["loss"]) <= 2e-3 * abs(ref["loss"])
+    np.testing.assert_allclose(lse.cpu().numpy(), ref["lse"], rtol=2e-3, atol=2e-3)
+    assert _rel(dq.cpu().numpy(), ref["dq"]) <= 1e-2
+    assert _rel(dc.cpu().numpy(), ref["dc"]) <= 1e-2
+
+
+def test_inbatch_row_blocks_with_offset(cuda):
+    """Rows of rank r scored against all-gathered columns (global negatives)."""
+    rng = np.random.default_rng(7)
+    B, E, G = 512, 64, 4
+    q = np.maximum(rng.standard_normal((B, E)) * 0.4, 0).astype(np.float32)
+    c = np.maximum(rng.standard_normal((B, E)) * 0.4, 0).astype(np.float32)
+    logq = np.log(rng.uniform(1e-5, 1e-2, B)).astype(np.float32)
+    ref = oracle.inbatch_softmax_xent(q, c, logq)
+    tq, tc, tl = _t(q, cuda), _t(c, cuda), _t(logq, cuda)
+    lse_full, _, _ = hip_ops.inbatch_rows(tq, tc, tl)
+    b = B // G
+    for r in range(G):
+        lse, rl, dq = hip_ops.inbatch_rows(tq[r * b:(r + 1) * b], tc, tl, pos_offset=r * b)
+        dc = hip_ops.inbatch_cols(tq, lse_full, tc[r * b:(r + 1) * b], tl[r * b:(r + 1) * b], pos_offset=r * b)
+        np.testing.assert_allclose(rl.cpu().numpy(), ref["row_loss"][r * b:(r + 1) * b], rtol=2e-3, atol=2e-3)
+        assert _rel(dq.cpu().numpy(), ref["dq"][r * b:(r + 1) * b]) <= 1e-2
+        assert _rel(dc.cpu().numpy(), ref["dc"][r * b:(r + 1) * b]) <= 1e-2
+
+
+# --------------------------------------------------------------------------- brute force
+def _search(cuda, c, q, k, offset=0):
+    tc = _t(c, cuda)
+    idx = hip_ops.bruteforce_build(tc)
+    s, i = hip_ops.bruteforce_search(idx, tc, _t(q, cuda), k, offset)
+    return s.cpu().numpy(), i.cpu().numpy()
+
+
+@pytest.mark.parametrize("N,Q,E,k", [(5000, 700, 128, 100), (3000, 300, 64, 1000), (777, 65, 16, 1),
+                                     (2048, 256, 128, 10), (300, 33, 100, 300)])
+def test_bruteforce_topk_bitexact(cuda, N, Q, E, k):
+    rng = np.random.default_rng(N + k)
+    c = np.maximum(rng.standard_normal((N, E)), 0).astype(np.float32)
+    q = np.maximum(rng.standard_normal((Q, E)), 0).astype(np.float32)
+    q[::17] = 0.0  # all-zero queries: every score ties at 0 -> lowest indices
+    s, i = _search(cuda, c, q, k)
+    rs, ri, _ = oracle.bruteforce_topk(q, c, k)
+    assert np.array_equal(i, ri)
+    assert np.array_equal(s, rs)
+
+
+def test_bruteforce_massive_ties_fallback(cuda):
+    """2000 identical candidates: the screen cannot separate them, the exact
+    fallback must still return the lowest indices in order."""
+    rng = np.random.default_rng(11)
+    E = 128
+    base = np.maximum(rng.standard_normal(E), 0).astype(np.float32)
+    c = np.maximum(rng.standard_normal((3000, E)) * 0.1, 0).astype(np.float32)
+    c[500:2500] = base * 3.0
+    q = np.maximum(rng.standard_normal((40, E)), 0).astype(np.float32)
+    q[5] = base
+    s, i = _search(cuda, c, q, 100)
+    rs, ri, _ = oracle.bruteforce_topk(q, c, 100)
+    assert np.array_equal(i, ri)
+    assert np.array_equal(s, rs)
+
+
+def test_bruteforce_index_offset_and_k_errors(cuda):
+    rng = np.random.default_rng(5)
+    c = rng.standard_normal((100, 32)).astype(np.float32)
+    q = rng.standard_normal((10, 32)).astype(np.float32)
+    s, i = _search(cuda, c, q, 5, offset=1000)
+    rs, ri, _ = oracle.bruteforce_topk(q, c, 5)
+    assert np.array_equal(i, ri + 1000)
+    with pytest.raises(ValueError):
+        _search(cuda, c, q, 101)
+
+
+def test_topk_merge_bitexact(cuda):
+    rng = np.random.default_rng(9)
+    Ls, Q, k = 8, 300, 50
+    s = np.round(rng.standard_normal((Ls, Q, k)), 1).astype(np.float32)  # many ties
+    idx = np.empty((Ls, Q, k), np.int32)
+    for l in range(Ls):
+        idx[l] = rng.permutation(1000)[:k][None, :] + 1000 * l
+    order = np.lexsort((idx, -s.astype(np.float64)), axis=2)
+    s = np.take_along_axis(s, order, 2)
+    idx = np.take_along_axis(idx, order, 2)
+    rs, ri = oracle.topk_merge(s, idx, k)
+    gs, gi = hip_ops.topk_merge(_t(s, cuda), _t(idx, cuda), k)
+    assert np.array_equal(gi.cpu().numpy(), ri)
+    assert np.array_equal(gs.cpu().numpy(), rs)
+
+
+def test_recall_hits(cuda):
+    rng = np.random.default_rng(4)
+    B, K = 1000, 100
+    cand = rng.integers(0, 300, size=(B, K)).astype(np.int32)
+    true = rng.integers(0, 300, size=B).astype(np.int32)
+    ks = [1, 10, 100]
+    acc = oracle.RecallAccumulator(ks)
+    acc.update(true, cand)
+    hits = torch.zeros(3, dtype=torch.int64, device=cuda)
+    hip_ops.recall_hits(_t(true, cuda), _t(cand, cuda), ks, hits)
+    assert hits.cpu().tolist() == [acc.hits[k] for k in ks]
