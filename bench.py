@@ -1,0 +1,383 @@
+#!/usr/bin/env python3
+"""Benchmark: positive pairs/s of the two-tower train step (+ index QPS).
+
+Workload at N=1 (BASELINE.json configs[2], "C3"): the reference's main.py
+schema (customer_id 128, fashion_news_frequency 2, postal_code 128 /
+article_id 128, product_type_name 16+4 (declared twice, table of 4 used
+twice), colour 8, department 32, index 4, section 16, garment 4) with H&M
+vocabulary sizes, towers [256] -> 128, logQ-corrected in-batch softmax,
+legacy Adagrad lr 0.05, batch 16384.  Synthetic ids: articles Zipf(1.1)
+over a random permutation, customers Zipf(0.6), per-entity attributes fixed;
+random-init weights (no dataset/checkpoint download).  A step is one full
+train_step (gather, towers, fused in-batch CE fwd+bwd, MLP backward, dense
++ sparse Adagrad), replayed as a hipGraph; inputs are resident in HBM.
+
+N>1 (torchrun, one process per GPU, RCCL): weak scaling, each rank runs the
+same C3 step on its own batch of 16384 with per-replica in-batch negatives
+(the reference's train_step under data parallelism); dense gradients are
+all-reduced and sparse (id, gradient) rows all-gathered so every replica
+applies the identical global update.  value = total pairs / max-over-ranks
+time.
+
+The JSON line also carries the roofline of the dominant kernel (the fused
+in-batch rows pass, bf16 MFMA), the index QPS of BASELINE configs[3] at a
+bounded query count on this GPU, and the CPU baseline (oracle/ numpy fp32
+restatement of the same step on a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "hm-retrieval-two-tower_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+# H&M cardinalities (public dataset).
+HM_VOCAB = {
+    "customer_id": 1371980,
+    "fashion_news_frequency": 4,
+    "postal_code": 352899,
+    "article_id": 105542,
+    "product_type_name": 131,
+    "colour_group_name": 50,
+    "department_name": 250,
+    "index_name": 10,
+    "section_name": 56,
+    "garment_group_name": 21,
+}
+MI355X_HBM_PEAK_GBS = 8000.0      # spec, MI355X_MICROARCH.md
+MI355X_BF16_DENSE_TFLOPS = 2500.0  # spec dense (no sparsity)
+
+
+def main_schema(emb_big: int = 128, joint: int = 128, hidden=(256,)):
+    """The reference main.py schema (main.py:32-111) with synthetic H&M vocabs."""
+    from pkg import dtypes
+    from pkg.schema.features import Feature, FeatureFamily
+    from pkg.schema.model_config import ModelConfig
+    from pkg.schema.schema import Schema
+    from pkg.schema.training_config import TrainingConfig
+
+    Q, C = FeatureFamily.QUERY, FeatureFamily.CANDIDATE
+    spec = [
+        ("customer_id", Q, emb_big), ("fashion_news_frequency", Q, 2), ("postal_code", Q, emb_big),
+        ("article_id", C, emb_big), ("product_type_name", C, 16), ("product_type_name", C, 4),
+        ("colour_group_name", C, 8), ("department_name", C, 32), ("index_name", C, 4),
+        ("section_name", C, 16), ("garment_group_name", C, 4),
+    ]
+    feats = []
+    for name, fam, d in spec:
+        f = Feature(name, dtypes.string, fam, embedding_size=d)
+        f.vocab = np.arange(HM_VOCAB[name]).astype(str)  # rows 1..V, 0 = OOV
+        f.is_built = True
+        feats.append(f)
+    tc = TrainingConfig(train_batch_size=16384, test_batch_size=2048, optimizer_name="adagrad",
+                        optimizer_kwargs={"learning_rate": 0.05})
+    mc = ModelConfig(joint_embedding_size=joint, ks=[10, 100, 1000], query_tower_units=list(hidden),
+                     candidate_tower_units=list(hidden))
+    return Schema(feats, tc, mc)
+
+
+def zipf_probs(n: int, a: float) -> np.ndarray:
+    p = np.arange(1, n + 1, dtype=np.float64) ** (-a)
+    return p / p.sum()
+
+
+class SyntheticHM:
+    """Device-resident synthetic batches with H&M shapes (seeded)."""
+
+    def __init__(self, device, seed: int = 0):
+        rng = np.random.default_rng(seed)
+        self.device = device
+        V = HM_VOCAB
+        self.art_perm = rng.permutation(V["article_id"]) + 1
+        self.cust_perm = rng.permutation(V["customer_id"]) + 1
+        self.art_p = zipf_probs(V["article_id"], 1.1)
+        self.cust_cdf = torch.as_tensor(np.cumsum(zipf_probs(V["customer_id"], 0.6)), device=device)
+        self.art_cdf = torch.as_tensor(np.cumsum(self.art_p), device=device)
+        self.cust_attr = {k: torch.as_tensor(rng.integers(1, V[k] + 1, V["customer_id"] + 1), device=device,
+                                             dtype=torch.int32)
+                          for k in ("fashion_news_frequency", "postal_code")}
+        self.art_attr = {k: torch.as_tensor(rng.integers(1, V[k] + 1, V["article_id"] + 1), device=device,
+                                            dtype=torch.int32)
+                         for k in ("product_type_name", "colour_group_name", "department_name", "index_name",
+                                   "section_name", "garment_group_name")}
+        self.art_perm_t = torch.as_tensor(self.art_perm, device=device, dtype=torch.int32)
+        self.cust_perm_t = torch.as_tensor(self.cust_perm, device=device, dtype=torch.int32)
+        self.gen = torch.Generator(device=device)
+        self.gen.manual_seed(seed + 1)
+
+    def prob_lookup(self):
+        """candidate_prob_lookup: article row -> p (str keys, as the ETL writes)."""
+        return {str(int(r) - 1): float(p) for r, p in zip(self.art_perm, self.art_p)}
+
+    def batch(self, B: int):
+        u = torch.rand(B, generator=self.gen, device=self.device, dtype=torch.float64)
+        ar = torch.searchsorted(self.art_cdf, u).clamp_(max=self.art_cdf.numel() - 1)
+        art = self.art_perm_t[ar]
+        u = torch.rand(B, generator=self.gen, device=self.device, dtype=torch.float64)
+        cr = torch.searchsorted(self.cust_cdf, u).clamp_(max=self.cust_cdf.numel() - 1)
+        cust = self.cust_perm_t[cr]
+        out = {"customer_id": cust, "article_id": art}
+        for k, t in self.cust_attr.items():
+            out[k] = t[cust.long()]
+        for k, t in self.art_attr.items():
+            out[k] = t[art.long()]
+        return {k: v.to(torch.int32).contiguous() for k, v in out.items()}
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def time_train(args, device, ws, rank):
+    from pkg.modelling.models.two_tower_model import GraphedTrainStep, TwoTowerModel
+    from pkg.modelling.optimizer_factory import OptimizerFactory
+    from pkg.modelling.distributed import DataParallelTrainStep
+
+    schema = main_schema()
+    data = SyntheticHM(device, seed=1234 + rank)
+    schema.set_candidate_prob_lookup(data.prob_lookup())
+    model = TwoTowerModel.create_from_schema(schema, "article_id", device=device, seed=0)
+    model.compile(optimizer=OptimizerFactory.get_optimizer("adagrad", {"learning_rate": 0.05}))
+    B = args.batch
+    pool = [data.batch(B) for _ in range(4)]
+    torch.cuda.synchronize()
+    if ws > 1:
+        step = DataParallelTrainStep(model, pool[0])
+    else:
+        step = GraphedTrainStep(model, pool[0], warmup=2)
+    for i in range(args.warmup):
+        step(pool[i % len(pool)])
+    torch.cuda.synchronize()
+    if ws > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = None
+    for i in range(args.steps):
+        out = step(pool[i % len(pool)])
+    torch.cuda.synchronize()
+    if ws > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([dt], device=device, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+    loss = float(out["loss"].item())
+    return model, data, dt, loss
+
+
+def time_inbatch_kernel(model, data, device, B: int, reps: int = 20):
+    """Dominant kernel of the step: the fused rows pass (S = Q C^T, logQ,
+    online softmax, P.C) on the step's own embeddings.  Timed with HIP events
+    on the launching (current) stream over `reps` back-to-back launches."""
+    from pkg.modelling import hip_ops
+
+    batch = data.batch(B)
+    with torch.no_grad():
+        q = model.query_tower.call({f.name: batch[f.name] for f in model.query_features})
+        c = model.candidate_tower.call({f.name: batch[f.name] for f in model.candidate_features})
+        logq = model.candidate_logq(batch)
+    E = q.shape[1]
+    for _ in range(3):
+        hip_ops.inbatch_rows(q, c, logq)
+    stream = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        hip_ops.inbatch_rows(q, c, logq)
+    e1.record(stream)
+    e1.synchronize()
+    ms_rows = e0.elapsed_time(e1) / reps
+    lse, _, _ = hip_ops.inbatch_rows(q, c, logq)
+    e0.record(stream)
+    for _ in range(reps):
+        hip_ops.inbatch_cols(q, lse, c, logq)
+    e1.record(stream)
+    e1.synchronize()
+    ms_cols = e0.elapsed_time(e1) / reps
+    flops = 4.0 * B * B * E  # S (2 B^2 E) + P.C (2 B^2 E) per pass
+    return flops, ms_rows, ms_cols
+
+
+def time_index(device, n_queries: int, n_cand: int, k: int, E: int = 128, check: int = 512):
+    """BASELINE configs[3] shape: relu(N(0,1)) candidates [105542,128], queries
+    relu(N(0,1)) with 1% all-zero rows, top-100, one GPU (bounded query count)."""
+    from pkg.modelling import hip_ops
+
+    g = torch.Generator(device=device)
+    g.manual_seed(1)
+    C = torch.relu(torch.randn(n_cand, E, generator=g, device=device))
+    g.manual_seed(2)
+    Q = torch.relu(torch.randn(n_queries, E, generator=g, device=device))
+    Q[::100] = 0.0
+    image = hip_ops.bruteforce_build(C)
+    hip_ops.bruteforce_search(image, C, Q[:4096], k)  # warm (workspace)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    s, i = hip_ops.bruteforce_search(image, C, Q, k)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    res = {"queries": n_queries, "candidates": n_cand, "k": k, "dim": E, "seconds": dt,
+           "qps": n_queries / dt, "tflops_scoring": 2.0 * n_queries * n_cand * E / dt / 1e12}
+    if check:
+        try:
+            from oracle import oracle
+
+            sel = np.linspace(0, n_queries - 1, check).astype(np.int64)
+            _, ri, _ = oracle.bruteforce_topk(Q[sel].cpu().numpy(), C.cpu().numpy(), k)
+            gi = i[sel].cpu().numpy()
+            res["exact_match_rows"] = int((gi == ri).all(axis=1).sum())
+            res["checked_rows"] = int(check)
+            res["recall_at_100_vs_exact"] = float(np.mean([len(set(a) & set(b)) / k for a, b in zip(gi, ri)]))
+        except Exception as e:  # the check is informative only
+            res["check_error"] = repr(e)
+    return res
+
+
+def cpu_baseline(seconds_budget: float = 20.0):
+    """oracle.CpuTwoTower (numpy fp32 restatement of the same train step) on
+    host cores, same schema and batch, timed over whole steps until ~budget."""
+    from oracle import oracle
+
+    try:
+        from threadpoolctl import threadpool_info
+
+        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:
+        threads = 1
+    schema = main_schema()
+    rng = np.random.default_rng(0)
+    V = HM_VOCAB
+
+    def tables(feats):
+        seen, out = {}, []
+        for f in feats:
+            if f.name not in seen:
+                seen[f.name] = rng.uniform(-0.05, 0.05, (V[f.name] + 1, f.embedding_size)).astype(np.float32)
+        # duplicated name: the last declaration's table, looked up per declaration
+        last = {f.name: f for f in feats}
+        for f in feats:
+            if seen[f.name].shape[1] != last[f.name].embedding_size:
+                seen[f.name] = rng.uniform(-0.05, 0.05, (V[f.name] + 1, last[f.name].embedding_size)).astype(
+                    np.float32)
+            out.append(seen[f.name])
+        return out
+
+    qt, ct = tables(schema.query_features), tables(schema.candidate_features)
+
+    def layers(din):
+        return [(oracle.glorot_uniform(rng, din, 256), np.zeros(256, np.float32)),
+                (oracle.glorot_uniform(rng, 256, 128), np.zeros(128, np.float32))]
+
+    wq = sum(t.shape[1] for t in qt)
+    wc = sum(t.shape[1] for t in ct)
+    # identical tables for repeated names -> share objects
+    m = oracle.CpuTwoTower(qt, ct, layers(wq), layers(wc), 0.05)
+    B = 16384
+    p = zipf_probs(V["article_id"], 1.1)
+    logq_rows = np.log(p).astype(np.float32)
+
+    def batch():
+        art = rng.choice(V["article_id"], size=B, p=p).astype(np.int32)
+        cust = (rng.zipf(1.6, size=B) % V["customer_id"]).astype(np.int32)
+        q_ids = [cust + 1, rng.integers(1, 5, B).astype(np.int32), rng.integers(1, V["postal_code"], B).astype(np.int32)]
+        c_ids = [art + 1] + [rng.integers(1, V[f.name] + 1, B).astype(np.int32) for f in schema.candidate_features[1:]]
+        return q_ids, c_ids, logq_rows[art]
+
+    steps, t_total = 0, 0.0
+    while t_total < seconds_budget and steps < 50:
+        q_ids, c_ids, lq = batch()
+        t0 = time.perf_counter()
+        m.step(q_ids, c_ids, lq)
+        t_total += time.perf_counter() - t0
+        steps += 1
+    return {"value": steps * B / t_total, "unit": "positive pairs/s", "cores": int(threads), "kind": "port",
+            "sample": f"{steps} full C3 train steps (B=16384, main.py schema, H&M vocab) of the numpy fp32 "
+                      f"restatement oracle/oracle.py:CpuTwoTower, {t_total:.1f}s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=16384)
+    ap.add_argument("--index-queries", type=int, default=262144)
+    ap.add_argument("--no-index", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    args = ap.parse_args()
+
+    ws, rank, local = dist_env()
+    if ws > 1:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", torch.cuda.current_device())
+
+    model, data, dt, loss = time_train(args, device, ws, rank)
+    B = args.batch
+    pairs = ws * B * args.steps
+    value = pairs / dt
+    ms_per_step = dt / args.steps * 1e3
+
+    flops, ms_rows, ms_cols = time_inbatch_kernel(model, data, device, B)
+    achieved = flops / (ms_rows * 1e-3) / 1e12
+    result = {
+        "metric": "positive pairs/sec (train) + index QPS @ Recall@100, 1/2/4/8 MI355X",
+        "value": value,
+        "unit": "positive pairs/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (H&M-shaped ids, Zipf; random-init weights)",
+        "config": {
+            "workload": "C3: main.py schema @ emb 128, towers [256]->128, logQ in-batch softmax, Adagrad, batch 16384"
+                        + (" per replica, per-replica in-batch negatives" if ws > 1 else ""),
+            "global_batch": ws * B,
+            "parallelism": f"dp{ws}",
+        },
+        "final_loss": loss,
+        "roofline": {
+            "kernel": "inbatch_pass_kernel<128,0> (fused rows pass: S=QC^T-logq, online softmax, P.C)",
+            "bound": "mfma",
+            "achieved": achieved,
+            "peak": MI355X_BF16_DENSE_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved / MI355X_BF16_DENSE_TFLOPS,
+            "traffic": None,
+            "ms_per_launch_rows_op": ms_rows,
+            "ms_per_launch_cols_op": ms_cols,
+            "algorithmic_flops_per_launch": flops,
+        },
+    }
+    if rank == 0 and ws == 1 and not args.no_index:
+        result["index"] = time_index(device, args.index_queries, HM_VOCAB["article_id"], 100)
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if ws > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,66 @@
+"""In-batch softmax cross-entropy with eye labels, fused on the GPU.
+
+Replaces, in one autograd node, the reference's chain
+  TwoTowerModel.call matmul          (two_tower_model.py:92)
+  LogQCorrection                     (two_tower_model.py:113-116)
+  labels = eye(B); CategoricalCrossentropy(from_logits=True, reduction=SUM)
+                                     (two_tower_model.py:119-122, runner.py:78-83)
+The forward runs both libtt passes (rows: lse, row loss, dQ; cols: dC) and
+keeps dQ, dC for the backward, which only scales them by the incoming
+gradient.  The [B, B] score matrix never exists.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from pkg.modelling import hip_ops
+
+__all__ = ["InBatchSoftmaxCrossEntropy", "inbatch_softmax_xent"]
+
+
+class _InBatchXent(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, c, logq, scale):
+        lse, row_loss, dq = hip_ops.inbatch_rows(q, c, logq, want_dq=True)
+        dc = hip_ops.inbatch_cols(q, lse, c, logq)
+        ctx.scale = scale
+        ctx.save_for_backward(dq, dc)
+        return row_loss.sum() * scale
+
+    @staticmethod
+    def backward(ctx, g):
+        dq, dc = ctx.saved_tensors
+        s = g * ctx.scale
+        return dq * s, dc * s, None, None
+
+
+def inbatch_softmax_xent(q: torch.Tensor, c: torch.Tensor, logq: Optional[torch.Tensor] = None,
+                         reduction: str = "sum") -> torch.Tensor:
+    """Loss of query rows q [B,E] against candidates c [B,E] (positive of row
+    i is column i), logq [B] the per-candidate log sampling probability."""
+    if reduction not in ("sum", "sum_over_batch_size", "mean"):
+        raise ValueError(f"unsupported reduction {reduction}")
+    scale = 1.0 if reduction == "sum" else 1.0 / q.shape[0]
+    if not q.requires_grad and not c.requires_grad:
+        lse, row_loss, _ = hip_ops.inbatch_rows(q, c, logq, want_dq=False)
+        return row_loss.sum() * scale
+    return _InBatchXent.apply(q, c, logq, scale)
+
+
+class InBatchSoftmaxCrossEntropy:
+    """Stand-in for tf.keras.losses.CategoricalCrossentropy(from_logits=True,
+    reduction=SUM) as compiled by the reference runner (runner.py:78-83)."""
+
+    def __init__(self, from_logits: bool = True, reduction: str = "sum"):
+        if not from_logits:
+            raise ValueError("the in-batch loss is defined on logits (from_logits=True)")
+        self.reduction = str(reduction).lower().split(".")[-1]
+
+    def __call__(self, q, c, logq=None):
+        return inbatch_softmax_xent(q, c, logq, self.reduction)
+
+
+# Name the reference compiles with.
+CategoricalCrossentropy = InBatchSoftmaxCrossEntropy

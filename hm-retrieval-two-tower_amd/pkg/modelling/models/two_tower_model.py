@@ -1,0 +1,246 @@
+"""TwoTowerModel (mirror of /root/reference/pkg/modelling/models/two_tower_model.py:12-205).
+
+train_step (two_tower_model.py:94-130) on MI355X:
+  1. query / candidate InputLayer gathers        tt_gather_grouped (1 launch per tower)
+  2. tower MLPs                                   torch addmm + relu (hipBLASLt)
+  3. scores + logQ + eye-label CE-SUM + dQ/dC     tt_inbatch_xent_rows / _cols (fused, bf16 MFMA)
+  4. MLP backward                                 torch autograd (hipBLASLt)
+  5. optimizer                                    tt_dense_adagrad + tt_sparse_adagrad (dedup in-kernel)
+Every launch is stream-ordered with no host synchronisation, so the whole step
+can be captured once and replayed as a hipGraph (GraphedTrainStep).
+"""
+from __future__ import annotations
+
+import logging
+import os
+from typing import Any, Dict, Iterable, List, Optional
+
+import numpy as np
+import torch
+
+from pkg.schema.features import Feature
+from pkg.schema.schema import Schema
+from pkg.modelling.device import default_device, make_generator
+from pkg.modelling.layers.logq_correction import LogQCorrection
+from pkg.modelling.losses import InBatchSoftmaxCrossEntropy
+from pkg.modelling.models.abstract_keras_model import AbstractKerasModel, TensorSpec
+from pkg.modelling.models.tower import Tower
+
+logger = logging.getLogger(__name__)
+
+__all__ = ["TwoTowerModel", "GraphedTrainStep", "LOGQ_KEY"]
+
+# Optional batch entry carrying per-example log p(candidate) computed from raw
+# ids at encoding time (exact even for ids outside a truncated vocab).
+LOGQ_KEY = "__logq__"
+
+
+class TwoTowerModel(AbstractKerasModel):
+    """
+    Two Tower Model class.
+
+    Parameters
+    ----------
+    query_features: List[Feature]
+        Features for the query tower.
+    candidate_features: List[Feature]
+        Features for the candidate tower.
+    candidate_id_col: str
+        The column containing the candidate_id.
+    joint_embedding_size: int
+        Joint embedding size which gets dot product.
+    query_tower_units: Optional[List[int]]
+        Hidden units for the query tower.
+    candidate_tower_units: Optional[List[int]]
+        Hidden units for the candidate tower.
+    candidate_prob_lookup: Optional[Dict[str, float]]
+        If provided, logQ correction is applied before the loss.
+    """
+
+    def __init__(self, query_features: List[Feature], candidate_features: List[Feature], candidate_id_col: str,
+                 joint_embedding_size: int, query_tower_units: Optional[List[int]] = None,
+                 candidate_tower_units: Optional[List[int]] = None,
+                 candidate_prob_lookup: Optional[Dict[str, float]] = None,
+                 device: Optional[torch.device] = None, seed: Optional[int] = None):
+        self.query_features = query_features
+        self.candidate_features = candidate_features
+        if candidate_id_col not in [f.name for f in candidate_features]:
+            raise ValueError(f"candidate_id_col {candidate_id_col} not a candidate feature")
+        self.candidate_id_col = candidate_id_col
+        self.device = device if device is not None else default_device()
+        gen = make_generator(seed)
+        self.query_tower = Tower(query_features, joint_embedding_size, query_tower_units, self.device, gen)
+        self.candidate_tower = Tower(candidate_features, joint_embedding_size, candidate_tower_units, self.device, gen)
+        self.logq_correction = LogQCorrection(candidate_prob_lookup) if candidate_prob_lookup else None
+        self._logq_rows: Optional[torch.Tensor] = None
+        self.optimizer = None
+        self.loss = InBatchSoftmaxCrossEntropy()
+        self.initialise_model()
+
+    @property
+    def towers(self) -> List[Tower]:
+        return [self.query_tower, self.candidate_tower]
+
+    # ------------------------------------------------------------------
+    def _split(self, x: Dict[str, Any]):
+        q = {f.name: x[f.name] for f in self.query_features}
+        c = {f.name: x[f.name] for f in self.candidate_features}
+        return q, c
+
+    def call(self, x: Dict[str, Any], training: bool = True) -> torch.Tensor:
+        """[Q, C] scores of every query against every candidate of the batch
+        (two_tower_model.py:65-92); materialised, for inspection / small B."""
+        q, c = self._split(x)
+        with torch.set_grad_enabled(training and torch.is_grad_enabled()):
+            return torch.matmul(self.query_tower.call(q), self.candidate_tower.call(c).t())
+
+    def candidate_logq(self, x: Dict[str, Any]) -> Optional[torch.Tensor]:
+        """Per-example log p(candidate) [B] for the logQ correction, or None."""
+        if self.logq_correction is None:
+            return None
+        if LOGQ_KEY in x:
+            v = x[LOGQ_KEY]
+            v = v if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v, np.float32))
+            return v.reshape(-1).to(device=self.device, dtype=torch.float32).contiguous()
+        if self._logq_rows is None:
+            feat = next(f for f in self.candidate_features if f.name == self.candidate_id_col)
+            self._logq_rows = self.logq_correction.row_table(feat, self.device)
+        ids = x[self.candidate_id_col]
+        ids = ids if isinstance(ids, torch.Tensor) else torch.as_tensor(np.asarray(ids))
+        return self._logq_rows.index_select(0, ids.reshape(-1).to(self.device, torch.int64))
+
+    def compute_loss(self, x: Dict[str, Any], training: bool = True) -> torch.Tensor:
+        q, c = self._split(x)
+        with torch.set_grad_enabled(training):
+            qe = self.query_tower.call(q)
+            ce = self.candidate_tower.call(c)
+            return self.loss(qe, ce, self.candidate_logq(x))
+
+    def compile(self, loss=None, optimizer=None, **kwargs) -> None:
+        """Keras-style compile: the loss must be the in-batch softmax CE
+        (CategoricalCrossentropy(from_logits=True, reduction=SUM) in the
+        reference, runner.py:78-83)."""
+        if loss is not None:
+            if not isinstance(loss, InBatchSoftmaxCrossEntropy):
+                raise TypeError("loss must be pkg.modelling.losses.CategoricalCrossentropy(from_logits=True, ...)")
+            self.loss = loss
+        if optimizer is not None:
+            self.optimizer = optimizer
+
+    def train_step(self, data: Dict[str, Any]) -> Dict[str, torch.Tensor]:
+        """One optimisation step on a batch of positive pairs; returns the
+        (device) loss without synchronising."""
+        if self.optimizer is None:
+            raise RuntimeError("call compile(optimizer=...) before training")
+        loss = self.compute_loss(data, training=True)
+        for t in self.towers:
+            t.dense.flat.grad = None
+        loss.backward()
+        self.optimizer.apply_gradients(self.towers)
+        return {"loss": loss.detach()}
+
+    def fit(self, dataset: Iterable[Dict[str, Any]], epochs: int = 1, callbacks=None,
+            use_graph: bool = False) -> Dict[str, List[float]]:
+        """Train for `epochs` passes; returns {"loss": [mean batch loss per epoch]}
+        (Keras' loss metric is the running mean over the epoch's batches)."""
+        history: Dict[str, List[float]] = {"loss": []}
+        graphed: Optional[GraphedTrainStep] = None
+        for epoch in range(epochs):
+            total = torch.zeros((), dtype=torch.float64, device=self.device)
+            n = 0
+            for batch in dataset:
+                bs = next(iter(batch.values())).shape[0]
+                if use_graph and graphed is None:
+                    # the single warm-up step IS this batch's optimisation step
+                    graphed = GraphedTrainStep(self, batch, warmup=1)
+                    out = graphed.warmup_out
+                elif use_graph and bs == graphed.batch_size:
+                    out = graphed(batch)
+                else:  # eager (also the partial last batch of a graphed epoch)
+                    out = self.train_step(batch)
+                total += out["loss"].double()
+                n += 1
+            mean = float(total.item()) / max(n, 1)
+            history["loss"].append(mean)
+            logger.info(f"epoch {epoch + 1}/{epochs}: loss {mean:.6f} over {n} batches")
+            for cb in callbacks or []:
+                if callable(cb):
+                    cb(epoch, {"loss": mean})
+        return history
+
+    @classmethod
+    def create_from_schema(cls, schema: Schema, candidate_id_col: str, **kwargs) -> "TwoTowerModel":
+        """Instance from a Schema (two_tower_model.py:132-158)."""
+        return TwoTowerModel(
+            query_features=schema.query_features,
+            candidate_features=schema.candidate_features,
+            candidate_id_col=candidate_id_col,
+            joint_embedding_size=schema.model_config.joint_embedding_size,
+            query_tower_units=schema.model_config.query_tower_units,
+            candidate_tower_units=schema.model_config.candidate_tower_units,
+            candidate_prob_lookup=schema.training_config.candidate_prob_lookup,
+            **kwargs,
+        )
+
+    def get_input_signature(self) -> Dict[str, TensorSpec]:
+        return {f.name: TensorSpec((None, 1), f.dtype, f.name) for f in self.candidate_features + self.query_features}
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        sd = {f"query_tower.{k}": v for k, v in self.query_tower.state_dict().items()}
+        sd.update({f"candidate_tower.{k}": v for k, v in self.candidate_tower.state_dict().items()})
+        return sd
+
+    def save(self, model_path: str) -> None:
+        """Save the two-tower model and each tower separately in the
+        two_tower / query_tower / candidate_tower entries of the model
+        directory (two_tower_model.py:176-205), as weights-only checkpoints."""
+        base = os.path.dirname(model_path)
+        os.makedirs(base or ".", exist_ok=True)
+        for name, obj in (("two_tower", self), ("query_tower", self.query_tower),
+                          ("candidate_tower", self.candidate_tower)):
+            path = os.path.join(base, name + ".pt")
+            logging.info(f"Saving {name} at path: {path}")
+            torch.save(obj.state_dict(), path)
+
+
+class GraphedTrainStep:
+    """Capture TwoTowerModel.train_step once as a hipGraph and replay it.
+
+    The batch is copied into static device buffers before each replay; all
+    libtt launches, the hipBLASLt GEMMs and the optimizer kernels replay with
+    no Python or launch overhead.  Warm-up steps (run eagerly on a side stream
+    before capture) are real optimisation steps on the example batch.
+    Requires an optimizer whose kernels do not depend on the host step count
+    (Adagrad)."""
+
+    def __init__(self, model: TwoTowerModel, example_batch: Dict[str, Any], warmup: int = 2):
+        from pkg.modelling.optimizer_factory import Adagrad
+
+        if not isinstance(model.optimizer, Adagrad):
+            raise ValueError("graph capture needs the Adagrad optimizer (Adam's coefficients depend on the step)")
+        self.model = model
+        self.static = {k: self._to_dev(v, model.device).clone() for k, v in example_batch.items()}
+        self.batch_size = next(iter(self.static.values())).shape[0]
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(max(warmup, 1)):
+                out = model.train_step(self.static)
+            self.warmup_out = {k: v.clone() for k, v in out.items()}
+        torch.cuda.current_stream().wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = model.train_step(self.static)
+
+    @staticmethod
+    def _to_dev(v, device):
+        t = v if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v))
+        return t.to(device)
+
+    def __call__(self, batch: Optional[Dict[str, Any]] = None) -> Dict[str, torch.Tensor]:
+        if batch is not None:
+            for k, v in batch.items():
+                self.static[k].copy_(self._to_dev(v, self.model.device).reshape(self.static[k].shape),
+                                     non_blocking=True)
+        self.graph.replay()
+        return self.out

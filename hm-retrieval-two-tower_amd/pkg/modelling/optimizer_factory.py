@@ -1,0 +1,139 @@
+"""Optimizers with tf.keras.optimizers.legacy semantics, applied by libtt.
+
+Mirror of /root/reference/pkg/modelling/optimizer_factory.py:8-57 (same names,
+same required kwargs and error messages).  The update rules are the legacy
+Keras / TF kernels the reference reaches:
+  Adagrad (initial_accumulator_value=0.1, epsilon=1e-7):
+    dense  ResourceApplyAdagradV2        -> tt_dense_adagrad (one launch per tower)
+    sparse dedup + ResourceSparseApplyAdagradV2 -> tt_sparse_adagrad
+  Adam (beta_1=0.9, beta_2=0.999, epsilon=1e-7):
+    dense  ResourceApplyAdam             -> tt_dense_adam
+    sparse legacy _resource_apply_sparse (decays the WHOLE m/v slots, then a
+           dense var update)              -> tt_sparse_adam
+Slots are created on first use, as Keras creates them on the first
+apply_gradients.
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, List
+import logging
+
+import torch
+
+from pkg.modelling import hip_ops
+
+logger = logging.getLogger(__name__)
+
+__all__ = ["OptimizerFactory", "Adagrad", "Adam"]
+
+
+class _Optimizer:
+    def __init__(self, learning_rate: float = 0.001, name: str = "", **kwargs):
+        self.learning_rate = float(learning_rate)
+        self.name = name
+        self.iterations = 0
+        self._slots: Dict[int, List[torch.Tensor]] = {}
+        if kwargs:
+            unknown = set(kwargs) - {"clipnorm", "clipvalue", "global_clipnorm", "decay"}
+            if unknown:
+                raise TypeError(f"Unexpected keyword argument(s) passed to optimizer: {sorted(unknown)}")
+            if any(kwargs.get(k) for k in ("clipnorm", "clipvalue", "global_clipnorm", "decay")):
+                raise NotImplementedError("gradient clipping / decay are not supported")
+
+    def _slot(self, param: torch.Tensor, n: int, init: float) -> List[torch.Tensor]:
+        key = id(param)
+        s = self._slots.get(key)
+        if s is None or s[0].shape != param.shape:
+            s = [torch.full_like(param, init, requires_grad=False) for _ in range(n)]
+            self._slots[key] = s
+        return s
+
+    def apply_gradients(self, towers) -> None:
+        """Dense step on each tower's flat MLP buffer, sparse step on its tables."""
+        self._apply(towers)
+        self.iterations += 1
+
+    minimize = apply_gradients
+
+
+class Adagrad(_Optimizer):
+    def __init__(self, learning_rate: float = 0.001, initial_accumulator_value: float = 0.1, epsilon: float = 1e-7,
+                 name: str = "Adagrad", **kwargs):
+        super().__init__(learning_rate, name, **kwargs)
+        if initial_accumulator_value < 0.0:
+            raise ValueError(f"initial_accumulator_value must be non-negative: {initial_accumulator_value}")
+        self.initial_accumulator_value = float(initial_accumulator_value)
+        self.epsilon = float(epsilon)
+
+    def _apply(self, towers) -> None:
+        lr, eps, init = self.learning_rate, self.epsilon, self.initial_accumulator_value
+        for tower in towers:
+            flat = tower.dense.flat
+            if flat.grad is not None:
+                (acc,) = self._slot(flat, 1, init)
+                hip_ops.dense_adagrad(flat.data, acc, flat.grad, lr, eps)
+            layer = tower.input_layer
+            if layer.last_grad is None or not layer.embedding_layers:
+                continue
+            specs = []
+            for src in layer.sparse_sources():
+                t = src["table"]
+                (acc,) = self._slot(t.weight, 1, init)
+                specs.append(dict(table=t.weight, slot0=acc, ids=src["ids"], grad_col_offset=src["grad_col_offset"]))
+            hip_ops.sparse_adagrad(specs, layer.last_grad.shape[0], layer.last_grad, lr, eps)
+
+
+class Adam(_Optimizer):
+    def __init__(self, learning_rate: float = 0.001, beta_1: float = 0.9, beta_2: float = 0.999,
+                 epsilon: float = 1e-7, amsgrad: bool = False, name: str = "Adam", **kwargs):
+        super().__init__(learning_rate, name, **kwargs)
+        if amsgrad:
+            raise NotImplementedError("amsgrad is not supported")
+        self.beta_1, self.beta_2, self.epsilon = float(beta_1), float(beta_2), float(epsilon)
+
+    def _apply(self, towers) -> None:
+        step = self.iterations + 1
+        lr, b1, b2, eps = self.learning_rate, self.beta_1, self.beta_2, self.epsilon
+        for tower in towers:
+            flat = tower.dense.flat
+            if flat.grad is not None:
+                m, v = self._slot(flat, 2, 0.0)
+                hip_ops.dense_adam(flat.data, m, v, flat.grad, lr, b1, b2, eps, step)
+            layer = tower.input_layer
+            if layer.last_grad is None or not layer.embedding_layers:
+                continue
+            specs = []
+            for src in layer.sparse_sources():
+                t = src["table"]
+                m, v = self._slot(t.weight, 2, 0.0)
+                specs.append(dict(table=t.weight, slot0=m, slot1=v, ids=src["ids"],
+                                  grad_col_offset=src["grad_col_offset"]))
+            hip_ops.sparse_adam(specs, layer.last_grad.shape[0], layer.last_grad, lr, b1, b2, eps, step)
+
+
+class OptimizerFactory:
+    """
+    Fetch a supported optimizer instance using config.
+    Some kwargs are required.
+    """
+
+    _supported_optimizers = {
+        "adam": Adam,
+        "adagrad": Adagrad,
+    }
+
+    _required_kwargs = ["learning_rate"]
+
+    @classmethod
+    def get_optimizer(cls, optimizer_name: str, optimizer_kwargs: Dict[str, Any]) -> _Optimizer:
+        if optimizer_name not in cls._supported_optimizers:
+            raise ValueError(
+                "name must be one of "
+                f"{list(cls._supported_optimizers.keys())}, "
+                f"got {optimizer_name}"
+            )
+        for kwarg in cls._required_kwargs:
+            if kwarg not in optimizer_kwargs:
+                raise ValueError(f"kwarg {kwarg} not found in kwargs: {optimizer_kwargs}")
+        logger.info(f"Creating {optimizer_name} obj with kwargs: {optimizer_kwargs}")
+        return cls._supported_optimizers[optimizer_name](**optimizer_kwargs)
