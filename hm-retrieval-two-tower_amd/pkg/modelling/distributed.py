@@ -30,7 +30,20 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-__all__ = ["IndexOps", "ShardedBruteForceIndex", "DataParallelTrainStep", "shard_range"]
+__all__ = ["IndexOps", "ShardedBruteForceIndex", "DataParallelTrainStep", "shard_range", "all_gather_cat"]
+
+
+def all_gather_cat(t: torch.Tensor, group=None) -> torch.Tensor:
+    """Rank-ordered concatenation along a new leading dim [world, *t.shape]
+    (all_gather_into_tensor on RCCL; list all_gather elsewhere, e.g. gloo)."""
+    world = dist.get_world_size(group)
+    t = t.contiguous()
+    out = torch.empty((world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(out, t, group=group)
+    else:
+        dist.all_gather(list(out.unbind(0)), t, group=group)
+    return out
 
 
 def shard_range(n: int, world: int, rank: int) -> Tuple[int, int]:
@@ -96,10 +109,8 @@ class ShardedBruteForceIndex:
         """Global (scores [Q,k], indices [Q,k]) on every rank."""
         k = k or self.k
         s, i = self.ops.search(self.image, self.cand, query_embeddings.contiguous(), k, self.offset)
-        all_s = torch.empty((self.world,) + tuple(s.shape), dtype=s.dtype, device=s.device)
-        all_i = torch.empty((self.world,) + tuple(i.shape), dtype=i.dtype, device=i.device)
-        dist.all_gather_into_tensor(all_s, s.contiguous(), group=self.group)
-        dist.all_gather_into_tensor(all_i, i.contiguous(), group=self.group)
+        all_s = all_gather_cat(s, self.group)
+        all_i = all_gather_cat(i, self.group)
         return self.ops.merge(all_s, all_i, k)
 
     def __call__(self, queries: Dict[str, Any]):
@@ -140,11 +151,9 @@ class DataParallelTrainStep:
             return
         B = layer.last_grad.shape[0]
         ids = torch.stack([c[1] for c in calls], 1).contiguous()  # [B, n_lookups]
-        all_ids = torch.empty((self.world * B, ids.shape[1]), dtype=ids.dtype, device=ids.device)
-        dist.all_gather_into_tensor(all_ids, ids, group=self.group)
+        all_ids = all_gather_cat(ids, self.group).reshape(self.world * B, ids.shape[1])
         g = layer.last_grad.contiguous()
-        all_g = torch.empty((self.world * B, g.shape[1]), dtype=g.dtype, device=g.device)
-        dist.all_gather_into_tensor(all_g, g, group=self.group)
+        all_g = all_gather_cat(g, self.group).reshape(self.world * B, g.shape[1])
         layer._last_calls = [(name, all_ids[:, j].contiguous(), off) for j, (name, _, off) in enumerate(calls)]
         layer.last_grad = all_g
 

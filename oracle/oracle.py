@@ -350,12 +350,17 @@ class CpuTwoTower:
             for (w, b), (aw, ab), (dw, db) in zip(layers, accs, grads):
                 dense_adagrad(w, aw, dw, self.lr)
                 dense_adagrad(b, ab, db, self.lr)
-        off = 0
-        for t, a, i in zip(self.q_tables, self.q_acc, q_ids):
-            sparse_adagrad(t, a, i, dxq[:, off:off + t.shape[1]], self.lr)
-            off += t.shape[1]
-        off = 0
-        for t, a, i in zip(self.c_tables, self.c_acc, c_ids):
-            sparse_adagrad(t, a, i, dxc[:, off:off + t.shape[1]], self.lr)
-            off += t.shape[1]
+        # A table looked up by several features gets ONE update from the
+        # concatenation of its lookups (TF aggregates the IndexedSlices of a
+        # variable used twice before the sparse apply).
+        for tables, accs, ids, dx in ((self.q_tables, self.q_acc, q_ids, dxq), (self.c_tables, self.c_acc, c_ids, dxc)):
+            groups = {}
+            off = 0
+            for t, a, i in zip(tables, accs, ids):
+                g = groups.setdefault(id(t), [t, a, [], []])
+                g[2].append(np.asarray(i, np.int32).reshape(-1))
+                g[3].append(dx[:, off:off + t.shape[1]])
+                off += t.shape[1]
+            for t, a, il, gl in groups.values():
+                sparse_adagrad(t, a, np.concatenate(il), np.concatenate(gl), self.lr)
         return loss

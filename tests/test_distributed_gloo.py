@@ -1,0 +1,131 @@
+"""CPU, world_size 2 over gloo: the multi-GPU orchestration of
+pkg.modelling.distributed with the kernels replaced by the CPU restatement
+(injected `ops`; the product's defaults are the libtt kernels)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _oracle_ops():
+    from oracle import oracle
+    from pkg.modelling.distributed import IndexOps
+
+    def search(img, cand, q, k, off):
+        s, i, _ = oracle.bruteforce_topk(q.numpy(), cand.numpy(), k)
+        return torch.from_numpy(s), torch.from_numpy(i + off)
+
+    def merge(s, i, k):
+        ms, mi = oracle.topk_merge(s.numpy(), i.numpy(), k)
+        return torch.from_numpy(np.ascontiguousarray(ms)), torch.from_numpy(np.ascontiguousarray(mi))
+
+    return IndexOps(build=lambda c: None, search=search, merge=merge)
+
+
+def _index_worker(rank, world, port, q, c, k, out):
+    _init(rank, world, port)
+    from pkg.modelling.distributed import ShardedBruteForceIndex, shard_range
+
+    b, e = shard_range(c.shape[0], world, rank)
+    idx = ShardedBruteForceIndex(k, None, torch.from_numpy(c[b:e]), b, ops=_oracle_ops())
+    s, i = idx.search(torch.from_numpy(q))
+    out[rank] = (s.numpy(), i.numpy(), idx.num_candidates)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_index_equals_unsharded(world):
+    from oracle import oracle
+
+    rng = np.random.default_rng(0)
+    c = np.maximum(rng.standard_normal((301, 16)), 0).astype(np.float32)
+    c[100:140] = c[99]  # cross-shard ties must resolve by global index
+    q = np.maximum(rng.standard_normal((20, 16)), 0).astype(np.float32)
+    q[3] = 0.0
+    k = 25
+    out = mp.Manager().dict()
+    mp.spawn(_index_worker, args=(world, _free_port(), q, c, k, out), nprocs=world, join=True)
+    rs, ri, _ = oracle.bruteforce_topk(q, c, k)
+    for r in range(world):
+        s, i, n = out[r]
+        assert n == 301
+        assert np.array_equal(i, ri) and np.array_equal(s, rs)
+
+
+class _Dense:
+    def __init__(self, g):
+        self.flat = torch.zeros(g.numel(), requires_grad=True)
+        self.flat.grad = g.clone()
+
+
+class _Layer:
+    def __init__(self, calls, grad):
+        self._last_calls = calls
+        self.last_grad = grad
+
+
+class _Tower:
+    def __init__(self, g, calls, grad):
+        self.dense = _Dense(g)
+        self.input_layer = _Layer(calls, grad)
+
+
+class _Model:
+    def __init__(self, towers):
+        self.towers = towers
+
+
+def _dp_worker(rank, world, port, out):
+    _init(rank, world, port)
+    from pkg.modelling.distributed import DataParallelTrainStep
+
+    B = 4
+    towers = []
+    for t in range(2):
+        g = torch.arange(5, dtype=torch.float32) * (rank + 1) + t
+        ids = [("a", torch.arange(B, dtype=torch.int32) + 10 * rank, 0),
+               ("p", torch.full((B,), 7 + rank, dtype=torch.int32), 3),
+               ("p", torch.full((B,), 100 + rank, dtype=torch.int32), 5)]
+        grad = torch.full((B, 6), float(rank + 10 * t))
+        towers.append(_Tower(g, ids, grad))
+    step = DataParallelTrainStep(_Model(towers))
+    step.allreduce_dense()
+    for tw in towers:
+        step.gather_sparse(tw.input_layer)
+    out[rank] = [(tw.dense.flat.grad.numpy().copy(), [(n, i.numpy().copy(), o) for n, i, o in tw.input_layer._last_calls],
+                  tw.input_layer.last_grad.numpy().copy()) for tw in towers]
+    dist.destroy_process_group()
+
+
+def test_dp_collectives_sum_dense_and_concat_sparse_rank_major():
+    world = 2
+    out = mp.Manager().dict()
+    mp.spawn(_dp_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    for r in range(world):
+        for t, (g, calls, grad) in enumerate(out[r]):
+            assert np.array_equal(g, np.arange(5) * 3 + 2 * t)  # (1 + 2) * arange + t + t
+            names = [c[0] for c in calls]
+            assert names == ["a", "p", "p"]
+            assert calls[0][1].tolist() == [0, 1, 2, 3, 10, 11, 12, 13]
+            assert calls[1][1].tolist() == [7] * 4 + [8] * 4
+            assert calls[2][1].tolist() == [100] * 4 + [101] * 4
+            assert [c[2] for c in calls] == [0, 3, 5]
+            assert grad.shape == (8, 6) and grad[0, 0] == 10 * t and grad[4, 0] == 1 + 10 * t

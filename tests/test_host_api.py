@@ -1,0 +1,181 @@
+"""CPU: host-side logic of the reference-API mirror (no GPU compute).
+
+Mirrors the reference's constructor validation (features.py:55-80,
+two_tower_model.py:47-50, optimizer_factory.py:43-53), vocab building, the
+StaticIndex/IndexRecall golden (tests/test_recall.py) through our classes,
+the LogQCorrection golden (tests/test_layers.py) through our layer, and the
+date_filter golden (tests/test_transformations.py).
+"""
+import json
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from pkg import dtypes
+from pkg.etl.transformations import date_filter
+from pkg.modelling.indices.static_index import StaticIndex
+from pkg.modelling.layers.logq_correction import LogQCorrection
+from pkg.modelling.metrics.index_recall import IndexRecall
+from pkg.modelling.optimizer_factory import Adagrad, Adam, OptimizerFactory
+from pkg.modelling.dataset import EncodedDataset, encode_dataframe
+from pkg.schema.features import Feature, FeatureFamily
+from pkg.schema.model_config import ModelConfig
+from pkg.schema.schema import Schema
+from pkg.schema.training_config import TrainingConfig
+from pkg.utils.settings import Settings
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_tests.json")))
+
+
+def test_feature_validation_mirrors_reference():
+    with pytest.raises(TypeError):
+        Feature("x", "int64", FeatureFamily.QUERY)
+    with pytest.raises(ValueError):
+        Feature("x", dtypes.string, "query")
+    with pytest.raises(TypeError):
+        Feature("x", dtypes.float32, FeatureFamily.QUERY, embedding_size=4)
+    with pytest.raises(TypeError):
+        Feature("x", dtypes.string, FeatureFamily.QUERY, embedding_size=4, max_vocab_size=2.5)
+    f = Feature("x", "tf.string", FeatureFamily.QUERY, embedding_size=4)
+    assert f.dtype == dtypes.string and not f.is_built
+    n = Feature("p", dtypes.float32, FeatureFamily.QUERY, vocab=["a"])
+    assert n.vocab is None and n.is_built
+
+
+def test_vocab_from_dataframe_and_string_lookup():
+    df = pd.DataFrame({"x": ["b", "a", "b", "c", "a", "b"]})
+    f = Feature("x", dtypes.string, FeatureFamily.QUERY, embedding_size=4, max_vocab_size=2)
+    f.set_vocab_from_dataframe(df)
+    assert f.vocab.tolist() == ["b", "a"] and f.num_rows == 3
+    assert f.encode(["a", b"b", "zz"]).tolist() == [2, 1, 0]
+    with pytest.raises(ValueError):
+        f.set_vocab_from_dataframe(pd.DataFrame({"y": [1]}))
+
+
+def test_schema_split_build_save_load(tmp_path):
+    feats = [Feature("q", dtypes.string, FeatureFamily.QUERY, embedding_size=4),
+             Feature("c", dtypes.string, FeatureFamily.CANDIDATE, embedding_size=4, vocab=["u", "v"])]
+    s = Schema(feats, TrainingConfig(8, 8, "adagrad", {"learning_rate": 0.1}), ModelConfig(4, [1, 2]))
+    assert [f.name for f in s.query_features] == ["q"] and [f.name for f in s.candidate_features] == ["c"]
+    s.build_features_from_dataframe(pd.DataFrame({"q": ["z", "z", "y"], "c": ["u", "u", "u"]}))
+    assert s.query_features[0].vocab.tolist() == ["z", "y"]
+    assert s.candidate_features[0].vocab.tolist() == ["u", "v"]  # given vocab kept
+    s.set_candidate_prob_lookup({"u": 1.0})
+    p = tmp_path / "sub" / "schema.pkl"
+    s.save(str(p))
+    t = Schema.load_from_filepath(str(p))
+    assert t.training_config.candidate_prob_lookup == {"u": 1.0}
+    assert t.query_features[0].encode(["y"]).tolist() == [2]
+
+
+def test_optimizer_factory_errors_and_types():
+    with pytest.raises(ValueError, match="name must be one of"):
+        OptimizerFactory.get_optimizer("sgd", {"learning_rate": 0.1})
+    with pytest.raises(ValueError, match="kwarg learning_rate not found"):
+        OptimizerFactory.get_optimizer("adam", {})
+    a = OptimizerFactory.get_optimizer("adagrad", {"learning_rate": 0.05})
+    assert isinstance(a, Adagrad) and a.initial_accumulator_value == 0.1 and a.epsilon == 1e-7
+    assert isinstance(OptimizerFactory.get_optimizer("adam", {"learning_rate": 1e-3}), Adam)
+
+
+def test_two_tower_candidate_id_col_validation():
+    from pkg.modelling.models.two_tower_model import TwoTowerModel
+
+    q = Feature("q", dtypes.string, FeatureFamily.QUERY, embedding_size=4, vocab=["a"])
+    c = Feature("c", dtypes.string, FeatureFamily.CANDIDATE, embedding_size=4, vocab=["b"])
+    with pytest.raises(ValueError, match="not a candidate feature"):
+        TwoTowerModel([q], [c], "q", 8, device=torch.device("cpu"))
+
+
+def test_input_layer_duplicate_name_semantics():
+    """main.py declares product_type_name twice (16 and 4): the dict keeps the
+    last table (input_layer.py:31) and it is looked up twice (:66-67)."""
+    from pkg.modelling.layers.input_layer import InputLayer
+
+    v = ["x", "y"]
+    feats = [Feature("a", dtypes.string, FeatureFamily.CANDIDATE, embedding_size=8, vocab=v),
+             Feature("p", dtypes.string, FeatureFamily.CANDIDATE, embedding_size=16, vocab=v),
+             Feature("p", dtypes.string, FeatureFamily.CANDIDATE, embedding_size=4, vocab=v),
+             Feature("n", dtypes.float32, FeatureFamily.CANDIDATE)]
+    layer = InputLayer(feats, device=torch.device("cpu"))
+    assert list(layer.embedding_layers) == ["a", "p"]
+    assert layer.embedding_layers["p"].dim == 4
+    assert layer.output_dim == 1 + 8 + 4 + 4
+    assert layer.column_offsets() == [1, 9, 13]
+
+
+def test_main_schema_widths_match_survey():
+    import bench
+
+    s = bench.main_schema()
+    from pkg.modelling.layers.input_layer import InputLayer
+
+    assert InputLayer(s.query_features, device=torch.device("cpu")).output_dim == 258
+    assert InputLayer(s.candidate_features, device=torch.device("cpu")).output_dim == 200
+
+
+def test_static_index_recall_golden_host_path():
+    g = GOLD["recall"]
+    feats = [Feature("query_id", dtypes.string, FeatureFamily.QUERY, embedding_size=2)]
+    idx = StaticIndex(k=g["k"], input_features=feats, candidates=np.array(g["static_candidates"]).reshape(1, -1))
+    metric = IndexRecall(idx, ks=g["ks"])
+    t = g["true_candidate_ids"]
+    for s in range(0, len(t), g["batch_size"]):
+        part = t[s:s + g["batch_size"]]
+        metric({"query_id": np.array([[b"q"]] * len(part))}, np.array(part, dtype=object))
+    for k, v in g["expected"].items():
+        assert metric.metric[int(k)] == np.float64(v)
+
+
+def test_logq_correction_golden():
+    g = GOLD["logq"]
+    layer = LogQCorrection(g["candidate_prob_lookup"])
+    out = layer(torch.tensor(g["logits"]), g["candidate_ids"]).numpy()
+    exp = np.asarray(g["expected"], np.float32)
+    assert np.array_equal(np.round(out, 5), np.round(exp, 5))
+
+
+def test_date_filter_golden():
+    g = GOLD["date_filter"]
+    df = pd.DataFrame({"date_col": g["date_col"]})
+    for (lo, hi), (mn, mx) in zip(g["ranges"], g["expected_min_max"]):
+        out = date_filter(df, "t", "date_col", (lo, hi))
+        assert (out["date_col"].min(), out["date_col"].max()) == (mn, mx)
+
+
+def test_encoded_dataset_batches_partial_last_and_shards(tmp_path):
+    f = Feature("x", dtypes.string, FeatureFamily.QUERY, embedding_size=2, vocab=["a", "b"])
+    n = Feature("v", dtypes.float32, FeatureFamily.QUERY)
+    df = pd.DataFrame({"x": ["a", "b", "c", "a", "b"], "v": [1.0, 2.0, 3.0, 4.0, 5.0]})
+    cols = encode_dataframe(df, [f, n])
+    ds = EncodedDataset(cols, batch_size=2, device=torch.device("cpu"))
+    bs = list(ds)
+    assert [b["x"].tolist() for b in bs] == [[1, 2], [0, 1], [2]]
+    ds.save(str(tmp_path), max_rows=3)
+    back = EncodedDataset.load(str(tmp_path), batch_size=4, device=torch.device("cpu"))
+    assert [b["v"].tolist() for b in back] == [[1.0, 2.0, 3.0, 4.0], [5.0]]
+    sh = EncodedDataset(cols, batch_size=5, shuffle_size=5, seed=1, device=torch.device("cpu"))
+    assert sorted(next(iter(sh))["v"].tolist()) == [1.0, 2.0, 3.0, 4.0, 5.0]
+
+
+def test_settings_fields_match_reference():
+    import dataclasses
+
+    names = [f.name for f in dataclasses.fields(Settings)]
+    assert names[:3] == ["raw_data_filepath", "articles_data_filepath", "customers_data_filepath"]
+    assert names[-2:] == ["tensorboard_logs_dir", "max_tfrecord_rows"]
+    assert len(names) == 19
+
+
+def test_hip_ops_reject_cpu_tensors():
+    """No CPU fallback: every op refuses host tensors."""
+    from pkg.modelling import hip_ops
+
+    q = torch.zeros(4, 8)
+    with pytest.raises(ValueError, match="GPU"):
+        hip_ops.inbatch_rows(q, q, None)
+    with pytest.raises(ValueError, match="GPU"):
+        hip_ops.gather_grouped([(torch.zeros(3, 2), torch.zeros(4, dtype=torch.int32), 0)], 4, torch.zeros(4, 2))
