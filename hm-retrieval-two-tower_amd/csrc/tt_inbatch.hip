@@ -136,6 +136,16 @@ __global__ void bias_kernel(const float* __restrict__ v, int64_t n, int64_t n_pa
   out[i] = (i < n) ? (v ? sign * v[i] : 0.0f) : pad;
 }
 
+// bias1[i] = -logq[i] (0 if logq NULL) for i < n, -inf for n <= i < n_pad;
+// bias2[i] = -inf for n <= i < n_pad (its [0, n) is written by combine_rows).
+__global__ void dual_bias_kernel(const float* __restrict__ logq, int64_t n, int64_t n_pad, float* __restrict__ bias1,
+                                 float* __restrict__ bias2) {
+  const int64_t i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= n_pad) return;
+  bias1[i] = (i < n) ? (logq ? -logq[i] : 0.0f) : -INFINITY;
+  if (i >= n) bias2[i] = -INFINITY;
+}
+
 struct PassArgs {
   const __bf16* stat;     // [n_stat_pad, D] stationary rows (B operand)
   const __bf16* strm;     // [n_strm_pad, D] streamed rows (A operand of S)
@@ -332,7 +342,8 @@ __global__ void __launch_bounds__(256) combine_rows_kernel(
     const float* __restrict__ part_m, const float* __restrict__ part_l, const float* __restrict__ part_o,
     int nsplit, int64_t n_stat_pad, int D, const float* __restrict__ q, int64_t ldq, const float* __restrict__ c,
     int64_t ldc, const float* __restrict__ logq, int64_t n_rows, int dim, int64_t pos_offset,
-    float* __restrict__ lse_out, float* __restrict__ loss_out, float* __restrict__ dq) {
+    float* __restrict__ lse_out, float* __restrict__ loss_out, float* __restrict__ dq,
+    float* __restrict__ neg_lse_bias) {
   const int64_t i = blockIdx.x * 4ll + threadIdx.x / kWave;
   if (i >= n_rows) return;
   const int lane = lane_id();
@@ -357,6 +368,7 @@ __global__ void __launch_bounds__(256) combine_rows_kernel(
     const float pos_logit = dot - (logq ? logq[pos] : 0.0f);
     lse_out[i] = lse;
     loss_out[i] = lse - pos_logit;
+    if (neg_lse_bias) neg_lse_bias[i] = -lse;
   }
 }
 
@@ -517,7 +529,7 @@ extern "C" int tt_inbatch_xent_rows(const float* q, int64_t ldq, int64_t n_rows,
   if ((rc = launch_pass<0>(p, a, st))) return rc;
   hipLaunchKernelGGL(combine_rows_kernel, dim3(ceil_div(n_rows, 4)), dim3(256), 0, st, w.part_m, w.part_l,
                      w.part_o, p.split, p.stat_pad, p.D, q, ldq, c, ldc, logq, n_rows, dim, pos_offset, lse,
-                     row_loss, dq);
+                     row_loss, dq, nullptr);
   TT_CHECK_LAUNCH();
   return TT_OK;
 }
@@ -547,6 +559,88 @@ extern "C" int tt_inbatch_xent_cols(const float* q, int64_t ldq, int64_t n_rows,
   if ((rc = launch_pass<1>(p, a, st))) return rc;
   hipLaunchKernelGGL(combine_cols_kernel, dim3(ceil_div(n_cols, 4)), dim3(256), 0, st, w.part_o, p.split,
                      p.stat_pad, p.D, q, ldq, logq, n_cols, dim, pos_offset, dc);
+  TT_CHECK_LAUNCH();
+  return TT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Single-device fused loss: rows and cols passes share one bf16 preparation of
+// q and c (row-major + transposed images), the cols pass's -lse bias is
+// written by the rows combine.  7 launches in total.
+namespace tt {
+namespace {
+struct FusedWs {
+  __bf16 *qb, *qbT, *cb, *cbT;
+  float *bias_logq, *bias_lse;
+  float *part_m, *part_l, *part_o_rows, *part_o_cols;
+};
+struct FusedPlan {
+  int D;
+  int64_t n_pad;
+  int split;
+  int64_t per_split;
+};
+FusedPlan fused_plan(int64_t n, int dim) {
+  FusedPlan p;
+  p.D = pick_dpad(dim);
+  p.n_pad = round_up(n > 0 ? n : 1, kRowsPerWG);  // multiple of both 128 and 64
+  p.split = pick_split(p.n_pad, p.n_pad);
+  p.per_split = round_up(ceil_div(p.n_pad, p.split), kTile);
+  return p;
+}
+FusedWs carve_fused(Carver& cv, const FusedPlan& p) {
+  FusedWs w;
+  w.qb = cv.take<__bf16>(p.n_pad * p.D);
+  w.qbT = cv.take<__bf16>(p.n_pad * p.D);
+  w.cb = cv.take<__bf16>(p.n_pad * p.D);
+  w.cbT = cv.take<__bf16>(p.n_pad * p.D);
+  w.bias_logq = cv.take<float>(p.n_pad);
+  w.bias_lse = cv.take<float>(p.n_pad);
+  w.part_m = cv.take<float>(int64_t(p.split) * p.n_pad);
+  w.part_l = cv.take<float>(int64_t(p.split) * p.n_pad);
+  w.part_o_rows = cv.take<float>(int64_t(p.split) * p.n_pad * p.D);
+  w.part_o_cols = cv.take<float>(int64_t(p.split) * p.n_pad * p.D);
+  return w;
+}
+}  // namespace
+}  // namespace tt
+
+extern "C" size_t tt_inbatch_fused_workspace_size(int64_t n, int32_t dim) {
+  if (n < 1 || pick_dpad(dim) == 0) return 0;
+  Carver cv(nullptr, 0);
+  carve_fused(cv, fused_plan(n, dim));
+  return cv.used();
+}
+
+extern "C" int tt_inbatch_softmax_xent(const float* q, int64_t ldq, const float* c, int64_t ldc, int64_t n,
+                                       int32_t dim, const float* logq, float* lse, float* row_loss, float* dq,
+                                       float* dc, void* workspace, size_t workspace_bytes, tt_stream_t stream) {
+  clear_error();
+  int rc = check_common(q, ldq, n, c, ldc, n, dim);
+  if (rc) return rc;
+  TT_REQUIRE(lse && row_loss && dq && dc, "tt_inbatch_softmax_xent: NULL output");
+  const FusedPlan p = fused_plan(n, dim);
+  Carver cv(workspace, workspace_bytes);
+  FusedWs w = carve_fused(cv, p);
+  if (!workspace || cv.used() > workspace_bytes)
+    return fail(TT_ERR_WORKSPACE, "tt_inbatch_softmax_xent: workspace %zu < required %zu", workspace_bytes,
+                cv.used());
+  hipStream_t st = to_stream(stream);
+  if ((rc = prep(p.D, q, ldq, n, dim, p.n_pad, w.qb, w.qbT, st))) return rc;
+  if ((rc = prep(p.D, c, ldc, n, dim, p.n_pad, w.cb, w.cbT, st))) return rc;
+  hipLaunchKernelGGL(dual_bias_kernel, dim3(ceil_div(p.n_pad, 256)), dim3(256), 0, st, logq, n, p.n_pad, w.bias_logq,
+                     w.bias_lse);
+  TT_CHECK_LAUNCH();
+  const Plan pl{p.D, p.n_pad, p.n_pad, p.split, p.per_split};
+  PassArgs ar{w.qb, w.cb, w.cbT, w.bias_logq, p.n_pad, p.n_pad, p.per_split, w.part_m, w.part_l, w.part_o_rows};
+  if ((rc = launch_pass<0>(pl, ar, st))) return rc;
+  hipLaunchKernelGGL(combine_rows_kernel, dim3(ceil_div(n, 4)), dim3(256), 0, st, w.part_m, w.part_l, w.part_o_rows,
+                     p.split, p.n_pad, p.D, q, ldq, c, ldc, logq, n, dim, (int64_t)0, lse, row_loss, dq, w.bias_lse);
+  TT_CHECK_LAUNCH();
+  PassArgs ac{w.cb, w.qb, w.qbT, w.bias_lse, p.n_pad, p.n_pad, p.per_split, nullptr, nullptr, w.part_o_cols};
+  if ((rc = launch_pass<1>(pl, ac, st))) return rc;
+  hipLaunchKernelGGL(combine_cols_kernel, dim3(ceil_div(n, 4)), dim3(256), 0, st, w.part_o_cols, p.split, p.n_pad,
+                     p.D, q, ldq, logq, n, dim, (int64_t)0, dc);
   TT_CHECK_LAUNCH();
   return TT_OK;
 }

@@ -9,26 +9,31 @@
 //   0), then ResourceSparseApplyAdagradV2 per distinct row:
 //       acc += g*g;  w -= lr*g / (sqrt(acc) + eps)
 //
-// MI355X design:
-//  1. sort   — one 1024-thread workgroup per table: stable LSD radix sort of
-//     (id, position) with 8-bit digits (ceil(bits(num_rows)/8) passes).  Each
-//     wave owns a contiguous slice and ranks its elements with 8 ballots per
-//     64-element group (wave-private LDS digit counters), so the sort is
-//     stable and deterministic.  Then segment heads, per-id chunk layout.
-//  2. chunk_sum — one (sub-)wave per chunk of <= kChunk consecutive rows of a
-//     segment: sequential fp32 sum in position order, lanes over columns, so
-//     every global read is a coalesced row slice.  Zipf heavy hitters (ids
-//     repeated thousands of times in one batch) are split into chunks that run
-//     in parallel instead of one long serial chain.
-//  3. apply — one (sub-)wave per distinct id: chunk partials summed in chunk
-//     order (bitwise reproducible; identical to TF's flat order whenever an id
-//     occurs <= kChunk times in the batch, within 1e-6 rel otherwise), then the
-//     optimizer update of that row.  HBM-bound: per distinct row
-//     param r/w + slot r/w = 16*dim bytes.
+// MI355X design (every stage uses the whole GPU):
+//  1. keys   — one launch over all tables' lookups builds 32-bit keys
+//     (table index | row id) and values (lookup index); each table's region is
+//     padded to a multiple of kBlock with an "invalid" id that sorts last.
+//  2. sort   — one stable LSD radix sort of all tables' (key, value) pairs
+//     (rocPRIM onesweep, only the key bits in use), so each table's lookups
+//     come out grouped by row id in increasing batch position.
+//  3. blocks — one (sub-)wave per kBlock consecutive sorted lookups of a
+//     table, lanes over embedding columns (coalesced row reads): sequential
+//     fp32 sums of each segment piece; a segment that starts and ends inside
+//     the block is applied immediately, the pieces of longer segments (Zipf
+//     heavy hitters repeated thousands of times) are written out.
+//  4. join   — the block where a long segment starts adds the pieces of the
+//     following blocks in order and applies the update.
+// Summation order = per table, sorted lookups cut into aligned blocks of
+// kBlock; each piece summed sequentially from 0, pieces added in order from 0.
+// This equals TF's flat order whenever an id occurs within one block and is
+// bitwise reproducible always; oracle/tt_oracle.c restates the same order.
 // All arithmetic goes through ieee_op<> (one correctly rounded IEEE operation
 // each; the file is built with -ffp-contract=off and HIP's default correctly
 // rounded fp32 divide/sqrt) so results match the CPU restatement bit for bit.
 // (HIP's __fsqrt_rn maps to the approximate native sqrt on this toolchain.)
+#include <algorithm>
+#include <rocprim/device/device_radix_sort.hpp>
+
 #include "tt_common.h"
 
 namespace tt {
@@ -42,105 +47,281 @@ __device__ __forceinline__ float ieee_op(float a, float b) {
   return a / b;
 }
 
-constexpr int kSortThreads = 1024;
-constexpr int kSortWaves = kSortThreads / kWave;
-constexpr int kChunk = 32;
+constexpr int kBlock = 32;            // sorted lookups per block (summation granule)
 constexpr int kTablesPerLaunch = 16;
-constexpr int kApplyThreads = 256;
+constexpr int kThreads = 256;
+constexpr int kPFJoin = 32;           // pieces loaded per batch in join
+constexpr int64_t kMaxLookups = int64_t(1) << 24;
 
-// Per-table workspace layout (device and host agree on it).
-struct TableWs {
-  uint32_t* keys0;
-  uint32_t* vals0;
-  uint32_t* keys1;
-  uint32_t* vals1;
-  int32_t* uniq;      // [n+1] distinct ids, ascending
-  int32_t* seg;       // [n+1] segment starts (seg[U] = n)
-  int32_t* cbase;     // [n+1] first chunk of each distinct id (cbase[U] = #chunks)
-  int32_t* cseg;      // [max_chunks] owning distinct id of each chunk
-  int32_t* counts;    // [0] = U, [1] = #chunks
-  float* partial;     // [max_chunks, dim] chunk sums
-};
-
-__host__ __device__ inline int64_t max_chunks(int64_t n) { return n + (n + kChunk - 1) / kChunk + 1; }
-
-__host__ __device__ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
-
-__host__ __device__ inline size_t table_ws_bytes(int64_t n, int32_t dim) {
-  size_t b = 0;
-  b += 4 * align256(sizeof(uint32_t) * n);
-  b += 3 * align256(sizeof(int32_t) * (n + 1));
-  b += align256(sizeof(int32_t) * max_chunks(n));
-  b += align256(sizeof(int32_t) * 4);
-  b += align256(sizeof(float) * max_chunks(n) * dim);
-  return b;
-}
-
-__host__ __device__ inline TableWs carve_table(char* base, int64_t n, int32_t dim) {
-  TableWs w;
-  size_t o = 0;
-  auto take = [&](size_t bytes) { char* p = base + o; o += align256(bytes); return p; };
-  w.keys0 = reinterpret_cast<uint32_t*>(take(sizeof(uint32_t) * n));
-  w.vals0 = reinterpret_cast<uint32_t*>(take(sizeof(uint32_t) * n));
-  w.keys1 = reinterpret_cast<uint32_t*>(take(sizeof(uint32_t) * n));
-  w.vals1 = reinterpret_cast<uint32_t*>(take(sizeof(uint32_t) * n));
-  w.uniq = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * (n + 1)));
-  w.seg = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * (n + 1)));
-  w.cbase = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * (n + 1)));
-  w.cseg = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * max_chunks(n)));
-  w.counts = reinterpret_cast<int32_t*>(take(sizeof(int32_t) * 4));
-  w.partial = reinterpret_cast<float*>(take(sizeof(float) * max_chunks(n) * dim));
-  return w;
-}
-
-struct TableJob {
-  char* ws;
+struct TableDesc {
   const int32_t* ids[TT_MAX_SOURCES];
   int32_t goff[TT_MAX_SOURCES];
   float* table;
   float* slot0;
   float* slot1;
   int64_t num_rows;
-  int32_t n;          // num_sources * batch
   int32_t dim;
   int32_t num_sources;
-  int32_t passes;     // radix passes
-  int32_t lanes_per_slot;  // P: lanes per chunk/id slot (pow2 <= 64)
-  int32_t wave_begin_chunk; // first global wave of this table in chunk_sum
-  int32_t wave_begin_apply; // first global wave of this table in apply
+  int32_t n;           // valid lookups = num_sources * batch
+  int32_t base;        // first sorted index of this table's region
+  int32_t n_pad;       // region size, multiple of kBlock
+  int32_t lanes;       // P: lanes per block slot (pow2 <= 64)
+  int32_t wave_begin;  // first global wave of this table in the block kernels
+  int64_t piece_off;   // first float of this table's pieces [blocks][2][dim]
 };
 
-struct JobList {
-  TableJob job[kTablesPerLaunch];
-  int32_t num_jobs;
+struct Job {
+  TableDesc t[kTablesPerLaunch];
+  int32_t num;
+  int32_t id_bits;
   int64_t batch;
   const float* grad;
   int64_t grad_stride;
+  uint32_t* keys_in;
+  uint32_t* vals_in;
+  const uint32_t* keys;  // sorted
+  const uint32_t* vals;  // sorted
+  float* pieces;
+  float* dense_out;      // kWriteSum: per-sorted-index segment sums [total][dim_max]
+  int32_t dense_dim;
 };
 
-__device__ __forceinline__ uint64_t lanemask_lt() {
-  const int l = lane_id();
-  return (l == 0) ? 0ull : (~0ull >> (64 - l));
+enum ApplyOp { kWriteSum = 0, kAdagrad = 1, kAdamScatter = 2 };
+
+struct ApplyParams {
+  float lr;
+  float eps;
+  float one_minus_beta1;
+  float one_minus_beta2;
+};
+
+__device__ __forceinline__ int table_of_wave(const Job& j, int gw) {
+  int t = 0;
+#pragma unroll 1
+  for (int i = 1; i < j.num; ++i)
+    if (gw >= j.t[i].wave_begin) t = i;
+  return t;
 }
 
-// Lanes (among `active`) holding the same 8-bit digit as this lane.
-__device__ __forceinline__ uint64_t match_digit(unsigned d, uint64_t active) {
-  uint64_t peers = active;
-#pragma unroll
-  for (int b = 0; b < 8; ++b) {
-    const bool bit = (d >> b) & 1u;
-    const uint64_t m = __ballot(bit);
-    peers &= bit ? m : ~m;
+// 1. keys / values of every lookup (+ padding) of every table.
+__global__ void __launch_bounds__(kThreads) build_keys_kernel(const Job j, int total) {
+  const int i = blockIdx.x * kThreads + threadIdx.x;
+  if (i >= total) return;
+  int t = 0;
+#pragma unroll 1
+  for (int k = 1; k < j.num; ++k)
+    if (i >= j.t[k].base) t = k;
+  const TableDesc& T = j.t[t];
+  const int loc = i - T.base;
+  const uint32_t invalid = (1u << j.id_bits) - 1u;
+  uint32_t id = invalid, val = 0xFFFFFFFFu;
+  if (loc < T.n) {
+    const int s = static_cast<int>(loc / j.batch);
+    const int32_t r = T.ids[s][loc - s * j.batch];
+    id = (r >= 0 && r < T.num_rows) ? static_cast<uint32_t>(r) : invalid;
+    val = static_cast<uint32_t>(loc);
   }
-  return peers;
+  j.keys_in[i] = (static_cast<uint32_t>(t) << j.id_bits) | id;
+  j.vals_in[i] = val;
 }
 
-// Exclusive scan of one int per thread over the 1024-thread block; returns
-// the prefix, writes the block total to *total.  Uses LDS scratch[>=16].
-__device__ int block_exclusive_scan(int v, int* scratch, int* total) {
+// The optimizer update of one distinct row, split into a load phase and a
+// compute/store phase so that a lane can have every row of its block in
+// flight at once (the applies are independent, the latency is not).
+struct RowState {
+  float x0, x1;
+};
+
+template <int OP>
+__device__ __forceinline__ RowState load_row(const TableDesc& T, int64_t o) {
+  RowState r{0.0f, 0.0f};
+  if (OP == kAdagrad) {
+    r.x0 = T.slot0[o];
+    r.x1 = T.table[o];
+  } else if (OP == kAdamScatter) {
+    r.x0 = T.slot0[o];
+    r.x1 = T.slot1[o];
+  }
+  return r;
+}
+
+template <int OP>
+__device__ __forceinline__ void store_row(const TableDesc& T, const ApplyParams& ap, int64_t o, RowState r, float g) {
+  if (OP == kAdagrad) {
+    const float a = ieee_op<'+'>(r.x0, ieee_op<'*'>(g, g));
+    T.slot0[o] = a;
+    T.table[o] = ieee_op<'-'>(r.x1, ieee_op<'/'>(ieee_op<'*'>(ap.lr, g), ieee_op<'+'>(sqrtf(a), ap.eps)));
+  } else if (OP == kAdamScatter) {  // scatter-add of the scaled distinct-id gradient into the decayed slots
+    T.slot0[o] = ieee_op<'+'>(r.x0, ieee_op<'*'>(g, ap.one_minus_beta1));
+    T.slot1[o] = ieee_op<'+'>(r.x1, ieee_op<'*'>(ieee_op<'*'>(g, g), ap.one_minus_beta2));
+  }
+}
+
+template <int OP>
+__device__ __forceinline__ void apply_row(const Job& j, const TableDesc& T, const ApplyParams& ap, uint32_t key,
+                                          int seg_start_sorted, int col, float g) {
+  const uint32_t id = key & ((1u << j.id_bits) - 1u);
+  if (OP == kWriteSum) {
+    j.dense_out[static_cast<int64_t>(seg_start_sorted) * j.dense_dim + col] = g;
+    return;
+  }
+  if (id >= static_cast<uint32_t>(T.num_rows)) return;  // invalid / padding
+  const int64_t o = static_cast<int64_t>(id) * T.dim + col;
+  store_row<OP>(T, ap, o, load_row<OP>(T, o), g);
+}
+
+// 3. per block of kBlock sorted lookups: piece sums; complete segments applied.
+template <int OP>
+__global__ void __launch_bounds__(kThreads) block_sum_kernel(const Job j, const ApplyParams ap) {
+  const int gw = blockIdx.x * (kThreads / kWave) + threadIdx.x / kWave;
+  const int t = table_of_wave(j, gw);
+  const TableDesc& T = j.t[t];
+  const int P = T.lanes;
   const int lane = lane_id();
-  const int w = threadIdx.x / kWave;
-  int x = v;
+  const int blk = (gw - T.wave_begin) * (kWave / P) + lane / P;
+  const int nblk = T.n_pad / kBlock;
+  if (blk >= nblk) return;
+  const int b0 = T.base + blk * kBlock;   // first sorted index of the block
+  const int tend = T.base + T.n_pad;      // end of the table's region
+  const uint32_t id_mask = (1u << j.id_bits) - 1u;
+  uint32_t key[kBlock], off[kBlock];
+#pragma unroll
+  for (int r = 0; r < kBlock; ++r) {
+    key[r] = j.keys[b0 + r];
+    off[r] = j.vals[b0 + r];
+  }
+  const uint32_t kprev = blk > 0 ? j.keys[b0 - 1] : ~0u;
+  const uint32_t knext = b0 + kBlock < tend ? j.keys[b0 + kBlock] : ~0u;
+  // grad offsets (validated to fit 32 bits) and the segment structure; both are
+  // the same for every column this lane visits.
+  uint32_t ends = 0, apply = 0;
+#pragma unroll
+  for (int r = 0; r < kBlock; ++r) {
+    if (off[r] != 0xFFFFFFFFu) {
+      const uint32_t s = off[r] / static_cast<uint32_t>(j.batch);
+      const uint32_t b = off[r] - s * static_cast<uint32_t>(j.batch);
+      off[r] = b * static_cast<uint32_t>(j.grad_stride) + static_cast<uint32_t>(T.goff[s]);
+    }
+    if (r == kBlock - 1 || key[r + 1] != key[r]) ends |= 1u << r;
+  }
+  const bool head_cont = key[0] == kprev;
+  const bool tail_cont = key[kBlock - 1] == knext;
+  {
+    int seg_begin = 0;
+#pragma unroll
+    for (int r = 0; r < kBlock; ++r) {
+      if (ends >> r & 1u) {
+        const bool piece = (seg_begin == 0 && head_cont) || (r == kBlock - 1 && tail_cont);
+        const bool valid = OP == kWriteSum || (key[r] & id_mask) < static_cast<uint32_t>(T.num_rows);
+        if (!piece && valid) apply |= 1u << r;
+        seg_begin = r + 1;
+      }
+    }
+  }
+  float* pc = j.pieces + T.piece_off + static_cast<int64_t>(blk) * 2 * T.dim;
+  for (int col = lane % P; col < T.dim; col += P) {
+    float v[kBlock];
+#pragma unroll
+    for (int r = 0; r < kBlock; ++r) v[r] = off[r] != 0xFFFFFFFFu ? j.grad[off[r] + col] : 0.0f;
+    // segment sums, left in v[r] at each segment's last row
+    float acc = 0.0f;
+    int seg_begin = 0;
+#pragma unroll
+    for (int r = 0; r < kBlock; ++r) {
+      acc = ieee_op<'+'>(acc, v[r]);
+      v[r] = acc;
+      if (ends >> r & 1u) {
+        if (seg_begin == 0 && head_cont) pc[col] = acc;                    // piece of an earlier segment
+        else if (r == kBlock - 1 && tail_cont) pc[T.dim + col] = acc;      // first piece of a continuing one
+        acc = 0.0f;
+        seg_begin = r + 1;
+      }
+    }
+    if (OP == kWriteSum) {
+      int sb = 0;
+#pragma unroll
+      for (int r = 0; r < kBlock; ++r) {
+        if (apply >> r & 1u) j.dense_out[static_cast<int64_t>(b0 + sb) * j.dense_dim + col] = ieee_op<'+'>(0.0f, v[r]);
+        if (ends >> r & 1u) sb = r + 1;
+      }
+    } else {
+      RowState st[kBlock];
+#pragma unroll
+      for (int r = 0; r < kBlock; ++r)
+        if (apply >> r & 1u) st[r] = load_row<OP>(T, static_cast<int64_t>(key[r] & id_mask) * T.dim + col);
+#pragma unroll
+      for (int r = 0; r < kBlock; ++r)
+        if (apply >> r & 1u)
+          store_row<OP>(T, ap, static_cast<int64_t>(key[r] & id_mask) * T.dim + col, st[r], ieee_op<'+'>(0.0f, v[r]));
+    }
+  }
+}
+
+// 4. segments spanning blocks: the block where one starts adds the pieces.
+template <int OP>
+__global__ void __launch_bounds__(kThreads) join_kernel(const Job j, const ApplyParams ap) {
+  const int gw = blockIdx.x * (kThreads / kWave) + threadIdx.x / kWave;
+  const int t = table_of_wave(j, gw);
+  const TableDesc& T = j.t[t];
+  const int P = T.lanes;
+  const int lane = lane_id();
+  const int blk = (gw - T.wave_begin) * (kWave / P) + lane / P;
+  const int nblk = T.n_pad / kBlock;
+  if (blk >= nblk) return;
+  const int b0 = T.base + blk * kBlock;
+  const int tend = T.base + T.n_pad;
+  uint32_t key[kBlock];
+#pragma unroll
+  for (int r = 0; r < kBlock; ++r) key[r] = j.keys[b0 + r];
+  const uint32_t klast = key[kBlock - 1];
+  const bool tail_cont = (b0 + kBlock < tend) && j.keys[b0 + kBlock] == klast;
+  if (!tail_cont) return;
+  // the continuing segment must START in this block
+  int seg_start = kBlock - 1;
+#pragma unroll
+  for (int r = kBlock - 2; r >= 0; --r)
+    if (key[r] == klast && seg_start == r + 1) seg_start = r;
+  if (seg_start == 0 && blk > 0 && j.keys[b0 - 1] == klast) return;  // began in an earlier block
+  // end of the segment: first sorted index in (b0+kBlock, tend) with a larger key
+  int lo = b0 + kBlock, hi = tend;  // keys[lo] == klast, answer in (lo, hi]
+  while (hi - lo > 1) {
+    const int mid = lo + (hi - lo) / 2;
+    if (j.keys[mid] == klast) lo = mid; else hi = mid;
+  }
+  const int last = (lo - T.base) / kBlock;  // last block holding the segment
+  const float* pcs = j.pieces + T.piece_off;
+  for (int col = lane % P; col < T.dim; col += P) {
+    float g = ieee_op<'+'>(0.0f, pcs[static_cast<int64_t>(blk) * 2 * T.dim + T.dim + col]);
+    for (int bb = blk + 1; bb <= last; bb += kPFJoin) {
+      float v[kPFJoin];
+#pragma unroll
+      for (int q = 0; q < kPFJoin; ++q)
+        v[q] = (bb + q <= last) ? pcs[static_cast<int64_t>(bb + q) * 2 * T.dim + col] : 0.0f;
+#pragma unroll
+      for (int q = 0; q < kPFJoin; ++q)
+        if (bb + q <= last) g = ieee_op<'+'>(g, v[q]);
+    }
+    apply_row<OP>(j, T, ap, klast, b0 + seg_start, col, g);
+  }
+}
+
+// kWriteSum only: compact the per-sorted-index sums into [U, dim] in id order.
+__global__ void __launch_bounds__(1024) compact_kernel(const Job j, int32_t* out_uniq, float* out_sum,
+                                                       int32_t* out_count) {
+  const TableDesc& T = j.t[0];
+  __shared__ int scratch[17];
+  const int n = T.n_pad;
+  const uint32_t mask = (1u << j.id_bits) - 1u;
+  const int per = (n + 1023) / 1024;
+  const int r0 = threadIdx.x * per, r1 = min(r0 + per, n);
+  int heads = 0;
+  for (int i = r0; i < r1; ++i) {
+    const uint32_t k = j.keys[i];
+    if ((k & mask) < static_cast<uint32_t>(T.num_rows) && (i == 0 || j.keys[i - 1] != k)) ++heads;
+  }
+  // block exclusive scan
+  const int lane = lane_id(), w = threadIdx.x / kWave;
+  int x = heads;
 #pragma unroll
   for (int off = 1; off < kWave; off <<= 1) {
     const int y = __shfl_up(x, off, kWave);
@@ -150,244 +331,193 @@ __device__ int block_exclusive_scan(int v, int* scratch, int* total) {
   __syncthreads();
   if (threadIdx.x == 0) {
     int run = 0;
-    for (int i = 0; i < kSortWaves; ++i) {
-      const int t = scratch[i];
+    for (int i = 0; i < 16; ++i) {
+      const int tt = scratch[i];
       scratch[i] = run;
-      run += t;
+      run += tt;
     }
-    scratch[kSortWaves] = run;
+    scratch[16] = run;
   }
   __syncthreads();
-  const int r = scratch[w] + x - v;
-  *total = scratch[kSortWaves];
-  __syncthreads();
-  return r;
-}
-
-__global__ void __launch_bounds__(kSortThreads) sort_segments_kernel(const JobList jl) {
-  const TableJob& J = jl.job[blockIdx.x];
-  const int64_t n = J.n;
-  TableWs W = carve_table(J.ws, n, J.dim);
-  __shared__ unsigned cnt[kSortWaves][256];
-  __shared__ unsigned digit_base[256];
-  __shared__ int scratch[kSortWaves + 1];
-
-  // Step 0: keys = ids (out-of-range -> num_rows, sorted last and skipped),
-  // vals = position in the concatenated source list.
-  const uint32_t invalid_key = static_cast<uint32_t>(J.num_rows);
-  for (int64_t p = threadIdx.x; p < n; p += kSortThreads) {
-    const int s = static_cast<int>(p / jl.batch);
-    const int64_t b = p - static_cast<int64_t>(s) * jl.batch;
-    const int32_t id = J.ids[s][b];
-    W.keys0[p] = (id >= 0 && id < J.num_rows) ? static_cast<uint32_t>(id) : invalid_key;
-    W.vals0[p] = static_cast<uint32_t>(p);
-  }
-  __syncthreads();
-
-  const int w = threadIdx.x / kWave;
-  const int lane = lane_id();
-  const int64_t chunk = ((n + kSortWaves - 1) / kSortWaves + kWave - 1) / kWave * kWave;
-  const int64_t beg = w * chunk;
-  const int64_t end = (beg + chunk < n) ? beg + chunk : n;
-
-  uint32_t* sk = W.keys0;
-  uint32_t* sv = W.vals0;
-  uint32_t* dk = W.keys1;
-  uint32_t* dv = W.vals1;
-  for (int pass = 0; pass < J.passes; ++pass) {
-    const int shift = 8 * pass;
-    for (int i = threadIdx.x; i < kSortWaves * 256; i += kSortThreads) (&cnt[0][0])[i] = 0;
-    __syncthreads();
-    // Count digits per wave slice.
-    for (int64_t g = beg; g < end; g += kWave) {
-      const int64_t p = g + lane;
-      const bool valid = p < end;
-      const unsigned d = valid ? ((sk[p] >> shift) & 255u) : 0u;
-      const uint64_t act = __ballot(valid);
-      const uint64_t peers = match_digit(d, act);
-      if (valid && (__ffsll(static_cast<long long>(peers)) - 1) == lane)
-        cnt[w][d] += static_cast<unsigned>(__popcll(peers));
-    }
-    __syncthreads();
-    if (threadIdx.x < 256) {
-      const int d = threadIdx.x;
-      unsigned run = 0;
-      for (int ww = 0; ww < kSortWaves; ++ww) {
-        const unsigned c = cnt[ww][d];
-        cnt[ww][d] = run;
-        run += c;
-      }
-      digit_base[d] = run;
-    }
-    __syncthreads();
-    if (threadIdx.x < kWave) {  // exclusive scan of the 256 digit totals
-      unsigned v0 = digit_base[4 * lane + 0], v1 = digit_base[4 * lane + 1];
-      unsigned v2 = digit_base[4 * lane + 2], v3 = digit_base[4 * lane + 3];
-      unsigned s = v0 + v1 + v2 + v3, x = s;
-#pragma unroll
-      for (int off = 1; off < kWave; off <<= 1) {
-        const unsigned y = __shfl_up(x, off, kWave);
-        if (lane >= off) x += y;
-      }
-      unsigned e = x - s;
-      digit_base[4 * lane + 0] = e;
-      digit_base[4 * lane + 1] = e + v0;
-      digit_base[4 * lane + 2] = e + v0 + v1;
-      digit_base[4 * lane + 3] = e + v0 + v1 + v2;
-    }
-    __syncthreads();
-    // Stable scatter.
-    for (int64_t g = beg; g < end; g += kWave) {
-      const int64_t p = g + lane;
-      const bool valid = p < end;
-      const uint32_t k = valid ? sk[p] : 0u;
-      const uint32_t v = valid ? sv[p] : 0u;
-      const unsigned d = (k >> shift) & 255u;
-      const uint64_t act = __ballot(valid);
-      const uint64_t peers = match_digit(d, act);
-      const unsigned base = cnt[w][d];
-      __builtin_amdgcn_wave_barrier();
-      if (valid) {
-        const unsigned pos = digit_base[d] + base + static_cast<unsigned>(__popcll(peers & lanemask_lt()));
-        dk[pos] = k;
-        dv[pos] = v;
-        if ((__ffsll(static_cast<long long>(peers)) - 1) == lane)
-          cnt[w][d] = base + static_cast<unsigned>(__popcll(peers));
-      }
-      __builtin_amdgcn_wave_barrier();
-    }
-    __syncthreads();
-    uint32_t* t0 = sk; sk = dk; dk = t0;
-    uint32_t* t1 = sv; sv = dv; dv = t1;
-  }
-
-  // Segment heads -> distinct ids and segment starts.
-  const int64_t per = (n + kSortThreads - 1) / kSortThreads;
-  const int64_t r0 = threadIdx.x * per;
-  const int64_t r1 = (r0 + per < n) ? r0 + per : n;
-  int heads = 0;
-  for (int64_t i = r0; i < r1; ++i) heads += (i == 0 || sk[i] != sk[i - 1]) ? 1 : 0;
-  int total_u = 0;
-  int u = block_exclusive_scan(heads, scratch, &total_u);
-  for (int64_t i = r0; i < r1; ++i) {
-    if (i == 0 || sk[i] != sk[i - 1]) {
-      W.uniq[u] = static_cast<int32_t>(sk[i]);
-      W.seg[u] = static_cast<int32_t>(i);
+  int u = scratch[w] + x - heads;
+  for (int i = r0; i < r1; ++i) {
+    const uint32_t k = j.keys[i];
+    if ((k & mask) < static_cast<uint32_t>(T.num_rows) && (i == 0 || j.keys[i - 1] != k)) {
+      out_uniq[u] = static_cast<int32_t>(k & mask);
+      for (int c = 0; c < T.dim; ++c) out_sum[static_cast<int64_t>(u) * T.dim + c] = j.dense_out[static_cast<int64_t>(i) * j.dense_dim + c];
       ++u;
     }
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    W.seg[total_u] = static_cast<int32_t>(n);
-    W.counts[0] = total_u;
-  }
-  __syncthreads();
-  // Chunk layout: ceil(len / kChunk) chunks per distinct id.
-  const int64_t uper = (total_u + kSortThreads - 1) / kSortThreads;
-  const int64_t u0 = threadIdx.x * uper;
-  const int64_t u1 = (u0 + uper < total_u) ? u0 + uper : total_u;
-  int nch = 0;
-  for (int64_t q = u0; q < u1; ++q) nch += (W.seg[q + 1] - W.seg[q] + kChunk - 1) / kChunk;
-  int total_c = 0;
-  int c = block_exclusive_scan(nch, scratch, &total_c);
-  for (int64_t q = u0; q < u1; ++q) {
-    W.cbase[q] = c;
-    const int k = (W.seg[q + 1] - W.seg[q] + kChunk - 1) / kChunk;
-    for (int j = 0; j < k; ++j) W.cseg[c + j] = static_cast<int32_t>(q);
-    c += k;
-  }
-  if (threadIdx.x == 0) {
-    W.cbase[total_u] = total_c;
-    W.counts[1] = total_c;
-  }
+  if (threadIdx.x == 0) *out_count = scratch[16];
 }
 
-// The sorted (id, position) arrays live in buffer 0 or 1 by pass parity.
-__device__ __forceinline__ const uint32_t* sorted_vals(const TableWs& W, int passes) {
-  return (passes & 1) ? W.vals1 : W.vals0;
+int bits_for(int64_t x) {  // bits needed to represent values in [0, x]
+  int b = 1;
+  while ((int64_t(1) << b) <= x) ++b;
+  return b;
 }
 
-__device__ __forceinline__ int find_job(const JobList& jl, int gw, bool apply) {
-  int t = 0;
-#pragma unroll 1
-  for (int i = 1; i < jl.num_jobs; ++i) {
-    const int b = apply ? jl.job[i].wave_begin_apply : jl.job[i].wave_begin_chunk;
-    if (gw >= b) t = i;
-  }
-  return t;
+int lanes_per_slot(int dim) {
+  int p = 1;
+  while (p < dim && p < kWave) p <<= 1;
+  return p;
 }
 
-__global__ void __launch_bounds__(kApplyThreads) chunk_sum_kernel(const JobList jl) {
-  const int gw = blockIdx.x * (kApplyThreads / kWave) + threadIdx.x / kWave;
-  const int t = find_job(jl, gw, false);
-  const TableJob& J = jl.job[t];
-  const TableWs W = carve_table(J.ws, J.n, J.dim);
-  const int P = J.lanes_per_slot;
-  const int lane = lane_id();
-  const int c = (gw - J.wave_begin_chunk) * (kWave / P) + lane / P;
-  if (c >= W.counts[1]) return;
-  const int col0 = lane % P;
-  const int q = W.cseg[c];
-  const int r0 = W.seg[q] + (c - W.cbase[q]) * kChunk;
-  const int r1 = min(r0 + kChunk, W.seg[q + 1]);
-  const uint32_t* sv = sorted_vals(W, J.passes);
-  for (int col = col0; col < J.dim; col += P) {
-    float acc = 0.0f;
-    for (int r = r0; r < r1; ++r) {
-      const uint32_t p = sv[r];
-      const int s = static_cast<int>(p / static_cast<uint32_t>(jl.batch));
-      const int64_t b = static_cast<int64_t>(p) - static_cast<int64_t>(s) * jl.batch;
-      acc = ieee_op<'+'>(acc, jl.grad[b * jl.grad_stride + J.goff[s] + col]);
-    }
-    W.partial[static_cast<int64_t>(c) * J.dim + col] = acc;
-  }
-}
-
-enum ApplyOp { kWriteSum = 0, kAdagrad = 1, kAdamScatter = 2 };
-
-struct ApplyParams {
-  float lr;
-  float eps;
-  float one_minus_beta1;
-  float one_minus_beta2;
-  int32_t* out_uniq;   // kWriteSum
-  float* out_sum;      // kWriteSum
-  int32_t* out_count;  // kWriteSum
+// Host-side plan of one launch group (<= kTablesPerLaunch tables).
+struct Plan {
+  Job job;
+  int total;          // sorted elements
+  int waves;          // block-kernel waves
+  int64_t piece_floats;
+  size_t sort_bytes;
+  int end_bit;
 };
 
+int make_plan(const tt_sparse_table* tables, int cnt, int64_t batch, Plan* p) {
+  Job& j = p->job;
+  j = Job{};
+  j.num = cnt;
+  j.batch = batch;
+  int64_t max_rows = 1;
+  for (int i = 0; i < cnt; ++i) max_rows = std::max<int64_t>(max_rows, tables[i].num_rows);
+  j.id_bits = bits_for(max_rows);  // (1<<id_bits)-1 >= max_rows: never a valid row
+  const int table_bits = bits_for(std::max(cnt - 1, 1));
+  p->end_bit = j.id_bits + table_bits;
+  if (p->end_bit > 32) return fail(TT_ERR_UNSUPPORTED, "sparse: %d tables x %lld rows exceed 32-bit keys", cnt,
+                                   static_cast<long long>(max_rows));
+  int base = 0, waves = 0;
+  int64_t poff = 0;
+  for (int i = 0; i < cnt; ++i) {
+    const tt_sparse_table& s = tables[i];
+    TableDesc& T = j.t[i];
+    for (int q = 0; q < TT_MAX_SOURCES; ++q) {
+      T.ids[q] = (q < s.num_sources) ? s.ids[q] : nullptr;
+      T.goff[q] = (q < s.num_sources) ? s.grad_col_offset[q] : 0;
+    }
+    T.table = s.table;
+    T.slot0 = s.slot0;
+    T.slot1 = s.slot1;
+    T.num_rows = s.num_rows;
+    T.dim = s.dim;
+    T.num_sources = s.num_sources;
+    T.n = static_cast<int32_t>(s.num_sources * batch);
+    T.base = base;
+    T.n_pad = static_cast<int32_t>(round_up(std::max<int64_t>(T.n, 1), kBlock));
+    T.lanes = lanes_per_slot(s.dim);
+    T.wave_begin = waves;
+    T.piece_off = poff;
+    base += T.n_pad;
+    const int nblk = T.n_pad / kBlock;
+    waves += static_cast<int>(ceil_div(nblk, kWave / T.lanes));
+    poff += static_cast<int64_t>(nblk) * 2 * s.dim;
+  }
+  p->total = base;
+  p->waves = waves;
+  p->piece_floats = poff;
+  size_t sb = 0;
+  uint32_t* np = nullptr;
+  hipError_t e = rocprim::radix_sort_pairs(nullptr, sb, np, np, np, np, static_cast<unsigned>(base), 0, p->end_bit,
+                                           nullptr, false);
+  // rocPRIM picks its config from the device; on a host without one (size
+  // queries only) use a bound: a key/value ping-pong copy plus 4 MiB.
+  p->sort_bytes = (e == hipSuccess) ? sb : static_cast<size_t>(base) * 8 + (size_t(4) << 20);
+  return TT_OK;
+}
+
+// Workspace carve for one plan (also used for the size query with base=null).
+struct PlanWs {
+  uint32_t *keys_in, *vals_in, *keys, *vals;
+  float* pieces;
+  float* dense_out;
+  void* sort_tmp;
+};
+PlanWs carve_plan(Carver& cv, const Plan& p, int dense_dim) {
+  PlanWs w;
+  w.keys_in = cv.take<uint32_t>(p.total);
+  w.vals_in = cv.take<uint32_t>(p.total);
+  w.keys = cv.take<uint32_t>(p.total);
+  w.vals = cv.take<uint32_t>(p.total);
+  w.pieces = cv.take<float>(std::max<int64_t>(p.piece_floats, 1));
+  w.dense_out = dense_dim > 0 ? cv.take<float>(static_cast<int64_t>(p.total) * dense_dim) : nullptr;
+  w.sort_tmp = cv.take<char>(static_cast<int64_t>(p.sort_bytes) + 256);
+  return w;
+}
+
+int validate_tables(const tt_sparse_table* tables, int32_t num_tables, int64_t batch, bool adam) {
+  TT_REQUIRE(tables != nullptr && num_tables >= 1, "sparse: no tables");
+  TT_REQUIRE(batch >= 0, "sparse: negative batch");
+  int64_t total = 0;
+  for (int i = 0; i < num_tables; ++i) {
+    const tt_sparse_table& t = tables[i];
+    TT_REQUIRE(t.table && t.slot0, "sparse: table %d has NULL parameter/slot pointer", i);
+    TT_REQUIRE(!adam || t.slot1, "sparse: table %d needs slot1 for Adam", i);
+    TT_REQUIRE(t.num_rows >= 1 && t.num_rows < (int64_t(1) << 30), "sparse: table %d num_rows out of range", i);
+    TT_REQUIRE(t.dim >= 1 && t.dim <= 4096, "sparse: table %d dim=%d out of range", i, t.dim);
+    TT_REQUIRE(t.num_sources >= 1 && t.num_sources <= TT_MAX_SOURCES, "sparse: table %d num_sources=%d", i,
+               t.num_sources);
+    for (int s = 0; s < t.num_sources; ++s) TT_REQUIRE(t.ids[s] || batch == 0, "sparse: table %d source %d ids NULL", i, s);
+    total += t.num_sources * batch;
+  }
+  TT_REQUIRE(total < kMaxLookups, "sparse: %lld lookups in one call (max %lld)", static_cast<long long>(total),
+             static_cast<long long>(kMaxLookups));
+  return TT_OK;
+}
+
+size_t tables_ws_bytes(const tt_sparse_table* tables, int32_t num_tables, int64_t batch, int dense_dim) {
+  size_t total = 0;
+  for (int first = 0; first < num_tables; first += kTablesPerLaunch) {
+    const int cnt = std::min(num_tables - first, kTablesPerLaunch);
+    Plan p;
+    if (make_plan(tables + first, cnt, batch, &p)) return 0;
+    Carver cv(nullptr, 0);
+    carve_plan(cv, p, dense_dim);
+    total = std::max(total, cv.used());
+  }
+  return total;
+}
+
 template <int OP>
-__global__ void __launch_bounds__(kApplyThreads) apply_kernel(const JobList jl, const ApplyParams ap) {
-  const int gw = blockIdx.x * (kApplyThreads / kWave) + threadIdx.x / kWave;
-  const int t = find_job(jl, gw, true);
-  const TableJob& J = jl.job[t];
-  const TableWs W = carve_table(J.ws, J.n, J.dim);
-  const int P = J.lanes_per_slot;
-  const int lane = lane_id();
-  const int q = (gw - J.wave_begin_apply) * (kWave / P) + lane / P;
-  const int U = W.counts[0];
-  if (OP == kWriteSum && gw == 0 && lane == 0) *ap.out_count = U;
-  if (q >= U) return;
-  const int32_t row = W.uniq[q];
-  if (OP == kWriteSum && lane % P == 0) ap.out_uniq[q] = row;
-  if (OP != kWriteSum && (row < 0 || row >= J.num_rows)) return;  // out-of-range ids
-  const int c0 = W.cbase[q];
-  const int c1 = W.cbase[q + 1];
-  for (int col = lane % P; col < J.dim; col += P) {
-    float g = 0.0f;
-    for (int c = c0; c < c1; ++c) g = ieee_op<'+'>(g, W.partial[static_cast<int64_t>(c) * J.dim + col]);
+int run_sparse(const tt_sparse_table* tables, int32_t num_tables, int64_t batch, const float* grad,
+               int64_t grad_stride, const ApplyParams& ap, void* workspace, size_t ws_bytes, hipStream_t st,
+               int32_t* out_uniq = nullptr, float* out_sum = nullptr, int32_t* out_count = nullptr) {
+  TT_REQUIRE(grad_stride >= 0 && batch * grad_stride < (int64_t(1) << 31),
+             "sparse: grad buffer of %lld x %lld floats exceeds 2^31 elements", static_cast<long long>(batch),
+             static_cast<long long>(grad_stride));
+  for (int first = 0; first < num_tables; first += kTablesPerLaunch) {
+    const int cnt = std::min(num_tables - first, kTablesPerLaunch);
+    Plan p;
+    int rc = make_plan(tables + first, cnt, batch, &p);
+    if (rc) return rc;
+    Carver cv(workspace, ws_bytes);
+    const int dense_dim = (OP == kWriteSum) ? tables[first].dim : 0;
+    PlanWs w = carve_plan(cv, p, dense_dim);
+    if (cv.used() > ws_bytes) return fail(TT_ERR_WORKSPACE, "sparse: workspace %zu < required %zu", ws_bytes, cv.used());
+    Job& j = p.job;
+    j.grad = grad;
+    j.grad_stride = grad_stride;
+    j.keys_in = w.keys_in;
+    j.vals_in = w.vals_in;
+    j.keys = w.keys;
+    j.vals = w.vals;
+    j.pieces = w.pieces;
+    j.dense_out = w.dense_out;
+    j.dense_dim = dense_dim;
+    hipLaunchKernelGGL(build_keys_kernel, dim3(ceil_div(p.total, kThreads)), dim3(kThreads), 0, st, j, p.total);
+    TT_CHECK_LAUNCH();
+    size_t sb = p.sort_bytes;
+    TT_CHECK_HIP(rocprim::radix_sort_pairs(w.sort_tmp, sb, w.keys_in, w.keys, w.vals_in, w.vals,
+                                           static_cast<unsigned>(p.total), 0, p.end_bit, st, false));
+    const int blocks = static_cast<int>(ceil_div(p.waves, kThreads / kWave));
+    hipLaunchKernelGGL(block_sum_kernel<OP>, dim3(blocks), dim3(kThreads), 0, st, j, ap);
+    TT_CHECK_LAUNCH();
+    hipLaunchKernelGGL(join_kernel<OP>, dim3(blocks), dim3(kThreads), 0, st, j, ap);
+    TT_CHECK_LAUNCH();
     if (OP == kWriteSum) {
-      ap.out_sum[static_cast<int64_t>(q) * J.dim + col] = g;
-    } else if (OP == kAdagrad) {
-      const int64_t o = static_cast<int64_t>(row) * J.dim + col;
-      const float a = ieee_op<'+'>(J.slot0[o], ieee_op<'*'>(g, g));
-      J.slot0[o] = a;
-      J.table[o] = ieee_op<'-'>(J.table[o], ieee_op<'/'>(ieee_op<'*'>(ap.lr, g), ieee_op<'+'>(sqrtf(a), ap.eps)));
-    } else {  // Adam: scatter-add of the scaled distinct-id gradient into the decayed slots
-      const int64_t o = static_cast<int64_t>(row) * J.dim + col;
-      J.slot0[o] = ieee_op<'+'>(J.slot0[o], ieee_op<'*'>(g, ap.one_minus_beta1));
-      J.slot1[o] = ieee_op<'+'>(J.slot1[o], ieee_op<'*'>(ieee_op<'*'>(g, g), ap.one_minus_beta2));
+      hipLaunchKernelGGL(compact_kernel, dim3(1), dim3(1024), 0, st, j, out_uniq, out_sum, out_count);
+      TT_CHECK_LAUNCH();
     }
   }
+  return TT_OK;
 }
 
 // Dense elementwise passes (grid-stride).
@@ -428,91 +558,6 @@ __global__ void dense_adam_kernel(float* p, float* m, float* v, const float* g, 
   }
 }
 
-int bits_for(int64_t x) {  // bits needed to represent values in [0, x]
-  int b = 1;
-  while ((int64_t(1) << b) <= x) ++b;
-  return b;
-}
-
-int lanes_per_slot(int dim) {
-  int p = 1;
-  while (p < dim && p < kWave) p <<= 1;
-  return p;
-}
-
-size_t tables_ws_bytes(const tt_sparse_table* tables, int32_t num_tables, int64_t batch) {
-  size_t b = 0;
-  for (int i = 0; i < num_tables; ++i)
-    b += align256(table_ws_bytes(tables[i].num_sources * batch, tables[i].dim));
-  return b;
-}
-
-int validate_tables(const tt_sparse_table* tables, int32_t num_tables, int64_t batch, bool adam) {
-  TT_REQUIRE(tables != nullptr && num_tables >= 1, "sparse: no tables");
-  TT_REQUIRE(batch >= 0, "sparse: negative batch");
-  for (int i = 0; i < num_tables; ++i) {
-    const tt_sparse_table& t = tables[i];
-    TT_REQUIRE(t.table && t.slot0, "sparse: table %d has NULL parameter/slot pointer", i);
-    TT_REQUIRE(!adam || t.slot1, "sparse: table %d needs slot1 for Adam", i);
-    TT_REQUIRE(t.num_rows >= 1 && t.num_rows < (int64_t(1) << 31) - 1, "sparse: table %d num_rows out of range", i);
-    TT_REQUIRE(t.dim >= 1 && t.dim <= 4096, "sparse: table %d dim=%d out of range", i, t.dim);
-    TT_REQUIRE(t.num_sources >= 1 && t.num_sources <= TT_MAX_SOURCES, "sparse: table %d num_sources=%d", i, t.num_sources);
-    TT_REQUIRE(t.num_sources * batch <= 65536 * 4, "sparse: table %d has %lld lookups (max %d)", i,
-               static_cast<long long>(t.num_sources * batch), 65536 * 4);
-    for (int s = 0; s < t.num_sources; ++s) TT_REQUIRE(t.ids[s] || batch == 0, "sparse: table %d source %d ids NULL", i, s);
-  }
-  return TT_OK;
-}
-
-// Runs sort -> chunk_sum -> apply<OP> over all tables, kTablesPerLaunch at a time.
-template <int OP>
-int run_sparse(const tt_sparse_table* tables, int32_t num_tables, int64_t batch, const float* grad,
-               int64_t grad_stride, const ApplyParams& ap, void* workspace, hipStream_t st) {
-  char* ws = static_cast<char*>(workspace);
-  for (int first = 0; first < num_tables; first += kTablesPerLaunch) {
-    const int cnt = (num_tables - first < kTablesPerLaunch) ? num_tables - first : kTablesPerLaunch;
-    JobList jl{};
-    jl.num_jobs = cnt;
-    jl.batch = batch;
-    jl.grad = grad;
-    jl.grad_stride = grad_stride;
-    int waves_c = 0, waves_a = 0;
-    for (int i = 0; i < cnt; ++i) {
-      const tt_sparse_table& t = tables[first + i];
-      TableJob& J = jl.job[i];
-      const int64_t n = t.num_sources * batch;
-      J.ws = ws;
-      ws += align256(table_ws_bytes(n, t.dim));
-      for (int s = 0; s < TT_MAX_SOURCES; ++s) {
-        J.ids[s] = (s < t.num_sources) ? t.ids[s] : nullptr;
-        J.goff[s] = (s < t.num_sources) ? t.grad_col_offset[s] : 0;
-      }
-      J.table = t.table;
-      J.slot0 = t.slot0;
-      J.slot1 = t.slot1;
-      J.num_rows = t.num_rows;
-      J.n = static_cast<int32_t>(n);
-      J.dim = t.dim;
-      J.num_sources = t.num_sources;
-      J.passes = (bits_for(t.num_rows) + 7) / 8;
-      J.lanes_per_slot = lanes_per_slot(t.dim);
-      J.wave_begin_chunk = waves_c;
-      J.wave_begin_apply = waves_a;
-      const int spw = kWave / J.lanes_per_slot;
-      waves_c += static_cast<int>(ceil_div(max_chunks(n), spw));
-      waves_a += static_cast<int>(ceil_div(n + 1, spw));
-    }
-    hipLaunchKernelGGL(sort_segments_kernel, dim3(cnt), dim3(kSortThreads), 0, st, jl);
-    TT_CHECK_LAUNCH();
-    const int wpb = kApplyThreads / kWave;
-    hipLaunchKernelGGL(chunk_sum_kernel, dim3(ceil_div(waves_c, wpb)), dim3(kApplyThreads), 0, st, jl);
-    TT_CHECK_LAUNCH();
-    hipLaunchKernelGGL(apply_kernel<OP>, dim3(ceil_div(waves_a, wpb)), dim3(kApplyThreads), 0, st, jl, ap);
-    TT_CHECK_LAUNCH();
-  }
-  return TT_OK;
-}
-
 dim3 stride_grid(int64_t n) {
   int64_t b = ceil_div(n, 256);
   if (b > 8192) b = 8192;
@@ -527,7 +572,7 @@ using namespace tt;
 
 extern "C" size_t tt_sparse_workspace_size(const tt_sparse_table* tables, int32_t num_tables, int64_t batch) {
   if (!tables || num_tables < 1 || batch < 0) return 0;
-  return tables_ws_bytes(tables, num_tables, batch);
+  return tables_ws_bytes(tables, num_tables, batch, 0);
 }
 
 extern "C" int tt_sparse_adagrad(const tt_sparse_table* tables, int32_t num_tables, int64_t batch,
@@ -538,13 +583,14 @@ extern "C" int tt_sparse_adagrad(const tt_sparse_table* tables, int32_t num_tabl
   if (rc) return rc;
   if (batch == 0) return TT_OK;
   TT_REQUIRE(grad != nullptr, "tt_sparse_adagrad: grad is NULL");
-  const size_t need = tables_ws_bytes(tables, num_tables, batch);
+  const size_t need = tables_ws_bytes(tables, num_tables, batch, 0);
   if (!workspace || workspace_bytes < need)
     return fail(TT_ERR_WORKSPACE, "tt_sparse_adagrad: workspace %zu < required %zu", workspace_bytes, need);
   ApplyParams ap{};
   ap.lr = lr;
   ap.eps = epsilon;
-  return run_sparse<kAdagrad>(tables, num_tables, batch, grad, grad_stride, ap, workspace, to_stream(stream));
+  return run_sparse<kAdagrad>(tables, num_tables, batch, grad, grad_stride, ap, workspace, workspace_bytes,
+                              to_stream(stream));
 }
 
 extern "C" int tt_sparse_adam(const tt_sparse_table* tables, int32_t num_tables, int64_t batch,
@@ -556,7 +602,7 @@ extern "C" int tt_sparse_adam(const tt_sparse_table* tables, int32_t num_tables,
   if (rc) return rc;
   TT_REQUIRE(step >= 1, "tt_sparse_adam: step must be >= 1");
   TT_REQUIRE(batch == 0 || grad != nullptr, "tt_sparse_adam: grad is NULL");
-  const size_t need = tables_ws_bytes(tables, num_tables, batch);
+  const size_t need = tables_ws_bytes(tables, num_tables, batch, 0);
   if (batch > 0 && (!workspace || workspace_bytes < need))
     return fail(TT_ERR_WORKSPACE, "tt_sparse_adam: workspace %zu < required %zu", workspace_bytes, need);
   hipStream_t st = to_stream(stream);
@@ -574,7 +620,7 @@ extern "C" int tt_sparse_adam(const tt_sparse_table* tables, int32_t num_tables,
     ApplyParams ap{};
     ap.one_minus_beta1 = 1.0f - b1;
     ap.one_minus_beta2 = 1.0f - b2;
-    rc = run_sparse<kAdamScatter>(tables, num_tables, batch, grad, grad_stride, ap, workspace, st);
+    rc = run_sparse<kAdamScatter>(tables, num_tables, batch, grad, grad_stride, ap, workspace, workspace_bytes, st);
     if (rc) return rc;
   }
   for (int i = 0; i < num_tables; ++i) {
@@ -587,8 +633,12 @@ extern "C" int tt_sparse_adam(const tt_sparse_table* tables, int32_t num_tables,
 }
 
 extern "C" size_t tt_dedup_workspace_size(int64_t n, int32_t dim) {
-  if (n < 0 || dim < 1) return 0;
-  return align256(table_ws_bytes(n, dim));
+  if (n < 1 || dim < 1) return 0;
+  tt_sparse_table t{};
+  t.num_rows = (int64_t(1) << 30) - 1;  // worst case key bits
+  t.dim = dim;
+  t.num_sources = 1;
+  return tables_ws_bytes(&t, 1, n, dim);
 }
 
 extern "C" int tt_dedup_sum(const int32_t* ids, int64_t n, int64_t num_rows, const float* grad,
@@ -596,7 +646,7 @@ extern "C" int tt_dedup_sum(const int32_t* ids, int64_t n, int64_t num_rows, con
                             int32_t* num_unique, void* workspace, size_t workspace_bytes, tt_stream_t stream) {
   clear_error();
   TT_REQUIRE(ids && grad && unique_ids && summed && num_unique, "tt_dedup_sum: NULL pointer");
-  TT_REQUIRE(n >= 1 && n <= 65536 * 4, "tt_dedup_sum: n=%lld out of range", static_cast<long long>(n));
+  TT_REQUIRE(n >= 1 && n < kMaxLookups, "tt_dedup_sum: n=%lld out of range", static_cast<long long>(n));
   tt_sparse_table t{};
   t.table = summed;  // not written by kWriteSum
   t.slot0 = summed;
@@ -607,14 +657,12 @@ extern "C" int tt_dedup_sum(const int32_t* ids, int64_t n, int64_t num_rows, con
   t.grad_col_offset[0] = 0;
   int rc = validate_tables(&t, 1, n, false);
   if (rc) return rc;
-  const size_t need = tables_ws_bytes(&t, 1, n);
+  const size_t need = tables_ws_bytes(&t, 1, n, dim);
   if (!workspace || workspace_bytes < need)
     return fail(TT_ERR_WORKSPACE, "tt_dedup_sum: workspace %zu < required %zu", workspace_bytes, need);
   ApplyParams ap{};
-  ap.out_uniq = unique_ids;
-  ap.out_sum = summed;
-  ap.out_count = num_unique;
-  return run_sparse<kWriteSum>(&t, 1, n, grad, grad_stride, ap, workspace, to_stream(stream));
+  return run_sparse<kWriteSum>(&t, 1, n, grad, grad_stride, ap, workspace, workspace_bytes, to_stream(stream),
+                               unique_ids, summed, num_unique);
 }
 
 extern "C" int tt_dense_adagrad(float* param, float* accum, const float* grad, int64_t n, float lr,

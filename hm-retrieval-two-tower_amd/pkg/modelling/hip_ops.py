@@ -24,6 +24,7 @@ __all__ = [
     "dense_adam",
     "inbatch_rows",
     "inbatch_cols",
+    "inbatch_fused",
     "bruteforce_build",
     "bruteforce_search",
     "topk_merge",
@@ -255,6 +256,27 @@ def inbatch_cols(q: torch.Tensor, lse: torch.Tensor, c: torch.Tensor, logq: Opti
                                  _opt_ptr(logq, "logq", C), pos_offset, dc.data_ptr(), ws.data_ptr(), ws.numel(),
                                  _stream()))
     return dc
+
+
+def inbatch_fused(q: torch.Tensor, c: torch.Tensor, logq: Optional[torch.Tensor]):
+    """Single-device loss + gradients (both passes, shared bf16 prep):
+    (lse [B], row_loss [B], dq [B,E], dc [B,E])."""
+    _req(q, "q", torch.float32, 2)
+    _req(c, "c", torch.float32, 2)
+    ldq, ldc = _row_major(q, "q"), _row_major(c, "c")
+    B, E = q.shape
+    if tuple(c.shape) != (B, E):
+        raise ValueError("q and c must both be [B, E]")
+    L = lib()
+    ws = Workspace.get(L.tt_inbatch_fused_workspace_size(B, E), q.device, "inbatch_fused")
+    lse = torch.empty(B, dtype=torch.float32, device=q.device)
+    row_loss = torch.empty(B, dtype=torch.float32, device=q.device)
+    dq = torch.empty(B, E, dtype=torch.float32, device=q.device)
+    dc = torch.empty(B, E, dtype=torch.float32, device=q.device)
+    check(L.tt_inbatch_softmax_xent(q.data_ptr(), ldq, c.data_ptr(), ldc, B, E, _opt_ptr(logq, "logq", B),
+                                    lse.data_ptr(), row_loss.data_ptr(), dq.data_ptr(), dc.data_ptr(), ws.data_ptr(),
+                                    ws.numel(), _stream()))
+    return lse, row_loss, dq, dc
 
 
 # --------------------------------------------------------------------------

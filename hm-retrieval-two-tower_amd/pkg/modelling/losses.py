@@ -23,8 +23,7 @@ __all__ = ["InBatchSoftmaxCrossEntropy", "inbatch_softmax_xent"]
 class _InBatchXent(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, c, logq, scale):
-        lse, row_loss, dq = hip_ops.inbatch_rows(q, c, logq, want_dq=True)
-        dc = hip_ops.inbatch_cols(q, lse, c, logq)
+        lse, row_loss, dq, dc = hip_ops.inbatch_fused(q, c, logq)
         ctx.scale = scale
         ctx.save_for_backward(dq, dc)
         return row_loss.sum() * scale

@@ -206,12 +206,13 @@ class TwoTowerModel(AbstractKerasModel):
 class GraphedTrainStep:
     """Capture TwoTowerModel.train_step once as a hipGraph and replay it.
 
-    The batch is copied into static device buffers before each replay; all
-    libtt launches, the hipBLASLt GEMMs and the optimizer kernels replay with
-    no Python or launch overhead.  Warm-up steps (run eagerly on a side stream
-    before capture) are real optimisation steps on the example batch.
-    Requires an optimizer whose kernels do not depend on the host step count
-    (Adagrad)."""
+    The batch lives in two static device buffers (int32 ids [K, B], float32
+    values [F, B]); a replay is one D2D copy per buffer (or none, for
+    `replay()`), then the whole step — gathers, hipBLASLt GEMMs, the fused
+    loss kernels and the optimizer kernels — with no Python or launch
+    overhead.  Warm-up steps (run eagerly on a side stream before capture)
+    are real optimisation steps on the example batch.  Requires an optimizer
+    whose kernels do not depend on the host step count (Adagrad)."""
 
     def __init__(self, model: TwoTowerModel, example_batch: Dict[str, Any], warmup: int = 2):
         from pkg.modelling.optimizer_factory import Adagrad
@@ -219,8 +220,16 @@ class GraphedTrainStep:
         if not isinstance(model.optimizer, Adagrad):
             raise ValueError("graph capture needs the Adagrad optimizer (Adam's coefficients depend on the step)")
         self.model = model
-        self.static = {k: self._to_dev(v, model.device).clone() for k, v in example_batch.items()}
-        self.batch_size = next(iter(self.static.values())).shape[0]
+        ex = {k: self._to_dev(v, model.device).reshape(-1) for k, v in example_batch.items()}
+        self.int_keys = sorted(k for k, v in ex.items() if v.dtype != torch.float32)
+        self.float_keys = sorted(k for k, v in ex.items() if v.dtype == torch.float32)
+        self.batch_size = next(iter(ex.values())).shape[0]
+        B = self.batch_size
+        self._ibuf = torch.empty(max(len(self.int_keys), 1), B, dtype=torch.int32, device=model.device)
+        self._fbuf = torch.empty(max(len(self.float_keys), 1), B, dtype=torch.float32, device=model.device)
+        self.static = {k: self._ibuf[i] for i, k in enumerate(self.int_keys)}
+        self.static.update({k: self._fbuf[i] for i, k in enumerate(self.float_keys)})
+        self.load(ex)
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -237,10 +246,27 @@ class GraphedTrainStep:
         t = v if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v))
         return t.to(device)
 
-    def __call__(self, batch: Optional[Dict[str, Any]] = None) -> Dict[str, torch.Tensor]:
-        if batch is not None:
-            for k, v in batch.items():
-                self.static[k].copy_(self._to_dev(v, self.model.device).reshape(self.static[k].shape),
-                                     non_blocking=True)
+    def pack(self, batch: Dict[str, Any]):
+        """Device buffers laid out like the static batch (copy with one D2D each)."""
+        ib = torch.stack([self._to_dev(batch[k], self.model.device).reshape(-1).to(torch.int32)
+                          for k in self.int_keys]) if self.int_keys else self._ibuf.clone()
+        fb = torch.stack([self._to_dev(batch[k], self.model.device).reshape(-1).to(torch.float32)
+                          for k in self.float_keys]) if self.float_keys else self._fbuf.clone()
+        return ib.contiguous(), fb.contiguous()
+
+    def load(self, batch: Dict[str, Any]) -> None:
+        for k, v in batch.items():
+            self.static[k].copy_(self._to_dev(v, self.model.device).reshape(-1), non_blocking=True)
+
+    def replay(self) -> Dict[str, torch.Tensor]:
         self.graph.replay()
         return self.out
+
+    def __call__(self, batch: Optional[Dict[str, Any]] = None, packed=None) -> Dict[str, torch.Tensor]:
+        if packed is not None:
+            self._ibuf.copy_(packed[0], non_blocking=True)
+            if self.float_keys:
+                self._fbuf.copy_(packed[1], non_blocking=True)
+        elif batch is not None:
+            self.load(batch)
+        return self.replay()

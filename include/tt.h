@@ -165,6 +165,16 @@ int tt_inbatch_xent_cols(const float* q, int64_t ldq, int64_t n_rows,
                          int64_t pos_offset, float* dc, void* workspace,
                          size_t workspace_bytes, tt_stream_t stream);
 
+/* Single-device form of the two passes above (rows = cols = the batch,
+ * positive of row i is column i): one shared bf16 preparation of q and c,
+ * outputs lse, row_loss [n], dq, dc [n, dim] (ld = dim). */
+size_t tt_inbatch_fused_workspace_size(int64_t n, int32_t dim);
+int tt_inbatch_softmax_xent(const float* q, int64_t ldq, const float* c,
+                            int64_t ldc, int64_t n, int32_t dim,
+                            const float* logq, float* lse, float* row_loss,
+                            float* dq, float* dc, void* workspace,
+                            size_t workspace_bytes, tt_stream_t stream);
+
 /* ------------------------------------------------------------------------ *
  * K11+K12  Brute-force scoring with fused top-K.
  * Replaces BruteForceIndex.call (pkg/modelling/indices/brute_force.py:76-81):

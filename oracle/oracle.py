@@ -30,7 +30,7 @@ _lib = None
 # Keras legacy Adagrad defaults (tf.keras.optimizers.legacy.Adagrad).
 ADAGRAD_INITIAL_ACCUMULATOR = 0.1
 ADAGRAD_EPSILON = 1e-7
-# GPU dedup chunk (csrc/tt_sparse.hip kChunk).
+# GPU summation block (csrc/tt_sparse.hip kBlock).
 GPU_DEDUP_CHUNK = 32
 
 

@@ -124,8 +124,10 @@ static int cmp_idpos(const void* x, const void* y) {
 /* Distinct ids (ascending) and per-id gradient sums.
  * chunk == 0: TF order — one sequential sum 0 + g_p1 + g_p2 + ... over the
  *             id's positions in increasing order (UnsortedSegmentSum CPU).
- * chunk  > 0: the GPU's order — sequential sums over consecutive runs of
- *             `chunk` positions, the run sums added in order starting from 0.
+ * chunk  > 0: the GPU's order — the lookups sorted by (id, position) are cut
+ *             into aligned blocks of `chunk`; each segment's piece in a block
+ *             is summed sequentially from 0 and the pieces are added in order
+ *             starting from 0 (csrc/tt_sparse.hip, block_sum/join kernels).
  * grad row of position p is grad + p*ld.  Returns U. */
 int oracle_dedup_sum(const int32_t* ids, int64_t n, const float* grad, int64_t ld, int dim, int chunk,
                      int32_t* uniq, float* sums) {
@@ -148,12 +150,14 @@ int oracle_dedup_sum(const int32_t* ids, int64_t n, const float* grad, int64_t l
       for (int64_t r = i; r < j; ++r)
         for (int e = 0; e < dim; ++e) out[e] = out[e] + grad[(int64_t)v[r].pos * ld + e];
     } else {
-      for (int64_t r0 = i; r0 < j; r0 += chunk) {
+      for (int64_t r0 = i; r0 < j;) {
+        int64_t r1 = (r0 / chunk + 1) * chunk;
+        if (r1 > j) r1 = j;
         for (int e = 0; e < dim; ++e) part[e] = 0.0f;
-        int64_t r1 = r0 + chunk < j ? r0 + chunk : j;
         for (int64_t r = r0; r < r1; ++r)
           for (int e = 0; e < dim; ++e) part[e] = part[e] + grad[(int64_t)v[r].pos * ld + e];
         for (int e = 0; e < dim; ++e) out[e] = out[e] + part[e];
+        r0 = r1;
       }
     }
     ++u;
