@@ -8,30 +8,51 @@
 //   s = fmaf(q[D-1], c[D-1], ... fmaf(q[0], c[0], 0))
 // and the returned scores are those fp32 values.
 //
+// Screening bound.  A bf16 MFMA score s~ differs from the exact chain s by at
+// most M_q = eps * |q| * max_c |c| with eps = 2^-8 + 2^-14 (bf16 rounding of
+// both operands 2^-8 + 2^-18, fp32 accumulation of 128 products and the exact
+// chain's own rounding each below 2^-16).  If tau is a lower bound of the
+// K-th largest screened score, every member of the exact top-K has
+// s~ >= tau - 2 M_q, so "s~ > next_down(tau - 2 M_q)" loses nothing.
+//
 // Design (MI355X):
-//  screen   — one workgroup = 8 waves x 32 queries; the queries' bf16
-//             fragments stay in VGPRs (B operand), candidates stream through
-//             double-buffered, XOR-swizzled LDS tiles of 64 rows and are scored
-//             with v_mfma_f32_32x32x16_bf16 (S^T tile: each lane holds 16
-//             candidates of one query).  Per register a single v_cmp against
-//             the query's running threshold and a wave-uniform branch filter
-//             the tile; survivors are appended to a per-query HBM shortlist.
-//             When a shortlist fills, the wave compacts it: the K-th best
-//             screened (score, index) key is found by a 64-step bitwise search
-//             and everything that provably cannot reach the exact top-K is
-//             dropped.  Screened scores err from the exact chain by at most
-//             M_q = eps * |q| * max_c |c| (eps = 2^-7 covers bf16 rounding of
-//             both operands and fp32 accumulation twice over); the threshold
-//             is thr = s_K - 2 M_q and a later candidate survives iff s > thr.
-//  finalize — one wave per query: the surviving shortlist is rescored with
-//             the exact fp32 fmaf chain (row gathers of the fp32 candidates),
-//             the exact top-K selected by the same bitwise search on
-//             (score, ~index) keys and ranked.  A query whose shortlist cannot
-//             be compacted below capacity (massive near-ties) falls back to an
-//             exact fp32 scan with the same machinery and margin 0.
+//  screen (k <= 128, the bins path) — one workgroup = 8 waves x 32 queries;
+//    the queries' bf16 fragments stay in VGPRs (B operand), 64-candidate
+//    bf16 tiles stream through double-buffered, XOR-swizzled LDS with global
+//    loads issued two tiles ahead, and are scored with
+//    v_mfma_f32_32x32x16_bf16 (S^T: each lane holds 16 candidates of one
+//    query).  Per register: one v_max into a per-lane "bin" (64 bins per lane,
+//    128 per query, each the running maximum over a fixed residue class of
+//    candidates) and one v_cmp against the query's threshold; survivors are
+//    appended to a lane-private HBM shortlist (no atomics, no cross-lane
+//    work).  At geometrically spaced tiles the lanes refresh their
+//    threshold in parallel from the bins: the K-th largest of 128 bin maxima
+//    (distinct candidates) is a lower bound of the K-th screened score.
+//    Small query batches split the candidates over up to 8 workgroups per
+//    query block (split = blockIdx % S keeps a split on fixed XCDs, so its
+//    slice stays in that L2); splits share thresholds through a per-query
+//    atomicMax.
+//  screen (k > 128, the compaction path) — per-query wave shortlists compacted
+//    by a bitwise K-th search when they fill.
+//  finalize — one wave per query: shortlist entries above the final
+//    threshold are gathered into LDS, cut by a coarse K-th search,
+//    rescored with the exact fp32 fmaf chain, the exact top-K is selected on
+//    (score, -index) and ranked with an LDS bitonic sort.  A query whose
+//    shortlist cannot be bounded (massive near-ties) is answered by an exact
+//    fp32 scan with the same machinery.
 #include <cmath>
 
 #include "tt_common.h"
+
+// Probe hooks for tools/index_probe.hip (never defined in the library build):
+//   TT_INDEX_STATS    count inserts / compactions / overflows
+//   TT_INDEX_NOINSERT screening threshold pinned above every score
+#ifdef TT_INDEX_STATS
+__device__ unsigned long long g_index_stats[4];
+#define TT_STAT(i, v) atomicAdd(&g_index_stats[i], static_cast<unsigned long long>(v))
+#else
+#define TT_STAT(i, v) ((void)0)
+#endif
 
 namespace tt {
 namespace {
@@ -41,9 +62,19 @@ constexpr int kScreenThreads = kScreenWaves * kWave;
 constexpr int kQPerWave = 32;
 constexpr int kQPerWG = kScreenWaves * kQPerWave;  // 256 queries
 constexpr int kCTile = 64;                         // candidates per LDS tile
-constexpr float kScreenEps = 0.0078125f;           // 2^-7
-constexpr int64_t kQueryChunk = 131072;            // queries per screening pass
-constexpr int kFinalWaves = 4;
+constexpr int kBins = 64;                          // per lane (128 per query)
+constexpr int kBinsMaxK = 2 * kBins;               // bins path serves k <= 128
+#ifndef TT_LANE_CAP
+#define TT_LANE_CAP 1024
+#endif
+constexpr int kLaneCap = TT_LANE_CAP;              // entries per (query, split, lane half)
+constexpr int kMaxSplits = 8;
+constexpr float kScreenEps = 0.00396728515625f;    // 2^-8 + 2^-14
+constexpr int64_t kMaxChunk = 65536;               // queries per screening pass
+#ifndef TT_SHORTLIST_BUDGET
+#define TT_SHORTLIST_BUDGET (size_t(1) << 30)
+#endif
+constexpr size_t kShortlistBudget = TT_SHORTLIST_BUDGET;  // bytes of shortlists per pass
 
 struct IndexHeader {
   int64_t n;
@@ -68,6 +99,12 @@ inline int cap_for_k(int k) {
   return c;
 }
 
+inline int next_pow2(int x) {
+  int p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
 size_t index_bytes(int64_t n, int dim) {
   const int D = pick_dpad(dim);
   const int64_t n_pad = round_up(n, kCTile);
@@ -83,31 +120,40 @@ __device__ __forceinline__ const float* index_bias(const void* idx, int64_t n_pa
 
 // ---- build ----------------------------------------------------------------
 // Row-major bf16 image (zero padded to n_pad rows, D columns), bias (0 / -inf
-// for padding rows) and max row norm.
-__global__ void build_kernel(const float* __restrict__ cand, int64_t ldc, int64_t n, int dim, int64_t n_pad, int D,
-                             void* index) {
+// for padding rows) and max row norm (one atomic per workgroup of 64 rows).
+constexpr int kBuildRowsPerWave = 16;
+__global__ void __launch_bounds__(256) build_kernel(const float* __restrict__ cand, int64_t ldc, int64_t n, int dim,
+                                                    int64_t n_pad, int D, void* index) {
+  __shared__ float wmax[4];
   IndexHeader* hdr = static_cast<IndexHeader*>(index);
   __bf16* rows = reinterpret_cast<__bf16*>(static_cast<char*>(index) + 64);
   float* bias = reinterpret_cast<float*>(static_cast<char*>(index) + 64 + n_pad * D * 2);
-  const int64_t r = blockIdx.x * 4ll + threadIdx.x / kWave;  // one wave per row
-  if (r >= n_pad) return;
+  const int wave = threadIdx.x / kWave;
   const int lane = lane_id();
-  float ss = 0.0f;
-  for (int e2 = lane; e2 < D / 2; e2 += kWave) {
-    const int e = 2 * e2;
-    const float x0 = (r < n && e < dim) ? cand[r * ldc + e] : 0.0f;
-    const float x1 = (r < n && e + 1 < dim) ? cand[r * ldc + e + 1] : 0.0f;
-    ss = __builtin_fmaf(x0, x0, __builtin_fmaf(x1, x1, ss));
-    reinterpret_cast<unsigned*>(rows + r * D)[e2] = pack_bf16x2(x0, x1);
-  }
+  float mx = 0.0f;
+  for (int i = 0; i < kBuildRowsPerWave; ++i) {
+    const int64_t r = (blockIdx.x * 4ll + wave) * kBuildRowsPerWave + i;
+    if (r >= n_pad) break;
+    float ss = 0.0f;
+    for (int e2 = lane; e2 < D / 2; e2 += kWave) {
+      const int e = 2 * e2;
+      const float x0 = (r < n && e < dim) ? cand[r * ldc + e] : 0.0f;
+      const float x1 = (r < n && e + 1 < dim) ? cand[r * ldc + e + 1] : 0.0f;
+      ss = __builtin_fmaf(x0, x0, __builtin_fmaf(x1, x1, ss));
+      reinterpret_cast<unsigned*>(rows + r * D)[e2] = pack_bf16x2(x0, x1);
+    }
 #pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) ss += __shfl_xor(ss, m, kWave);
-  if (lane == 0) {
-    bias[r] = (r < n) ? 0.0f : -INFINITY;
-    // round the norm up by a few ulps so the bound stays an upper bound
-    const float nr = sqrtf(ss) * (1.0f + 1e-6f);
-    atomicMax(&hdr->maxnorm_bits, __float_as_uint(nr));
-    if (r == 0) {
+    for (int m = 32; m >= 1; m >>= 1) ss += __shfl_xor(ss, m, kWave);
+    if (lane == 0) bias[r] = (r < n) ? 0.0f : -INFINITY;
+    if (r < n) mx = fmaxf(mx, sqrtf(ss));
+  }
+  if (lane == 0) wmax[wave] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float m = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+    // round the norm up so the bound stays an upper bound
+    atomicMax(&hdr->maxnorm_bits, __float_as_uint(m * (1.0f + 1e-5f)));
+    if (blockIdx.x == 0) {
       hdr->n = n;
       hdr->n_pad = n_pad;
       hdr->dim = dim;
@@ -124,43 +170,31 @@ __global__ void query_prep_kernel(const float* __restrict__ q, int64_t ldq, int6
   if (r >= nq_pad) return;
   const int lane = lane_id();
   float ss = 0.0f;
+  bool nz = false;
   for (int e2 = lane; e2 < D / 2; e2 += kWave) {
     const int e = 2 * e2;
     const float x0 = (r < nq && e < dim) ? q[r * ldq + e] : 0.0f;
     const float x1 = (r < nq && e + 1 < dim) ? q[r * ldq + e + 1] : 0.0f;
     ss = __builtin_fmaf(x0, x0, __builtin_fmaf(x1, x1, ss));
+    nz = nz || x0 != 0.0f || x1 != 0.0f;
     reinterpret_cast<unsigned*>(qb + r * D)[e2] = pack_bf16x2(x0, x1);
   }
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) ss += __shfl_xor(ss, m, kWave);
+  const bool nonzero = __ballot(nz) != 0;
   if (lane == 0) {
     const float maxc = __uint_as_float(static_cast<const IndexHeader*>(index)->maxnorm_bits);
-    const float qn = sqrtf(ss) * (1.0f + 1e-6f);
+    const float qn = sqrtf(ss) * (1.0f + 1e-5f);
     // 2 * eps * |q| * max|c|, rounded up; tiny absolute floor for subnormals.
-    margin2[r] = (r < nq) ? (2.0f * kScreenEps * qn * maxc) * (1.0f + 1e-5f) + 1e-30f : 0.0f;
+    // A zero query scores exactly +0 against every candidate in both paths, so
+    // its margin is 0 and ties resolve by index.
+    margin2[r] = (r < nq && nonzero) ? (2.0f * kScreenEps * qn * maxc) * (1.0f + 1e-5f) + 1e-30f : 0.0f;
   }
 }
 
 __device__ __forceinline__ unsigned long long make_key(float s, unsigned idx) {
   return (static_cast<unsigned long long>(float_order_key(s)) << 32) |
          static_cast<unsigned long long>(0xFFFFFFFFu - idx);
-}
-
-// Largest key v such that at least K of the wave's keys are >= v, i.e. the
-// K-th largest key (keys are distinct).  Keys of empty slots are 0.
-template <int NPL>
-__device__ unsigned long long kth_largest(const unsigned long long (&key)[NPL], int K) {
-  unsigned long long res = 0;
-#pragma unroll 1
-  for (int bit = 63; bit >= 0; --bit) {
-    const unsigned long long cand = res | (1ull << bit);
-    int c = 0;
-#pragma unroll
-    for (int i = 0; i < NPL; ++i) c += (key[i] >= cand) ? 1 : 0;
-    c = wave_sum_i32(c);
-    if (c >= K) res = cand;
-  }
-  return res;
 }
 
 // Largest float strictly below x (x finite).
@@ -175,10 +209,282 @@ __device__ __forceinline__ uint64_t lanemask_lt64() {
   return (l == 0) ? 0ull : (~0ull >> (64 - l));
 }
 
-// Compacts the shortlist buf[0..n) of one query with the whole wave.
-// Keeps every entry that might still belong to the exact top-K given screened
-// scores within +-M of the exact ones (margin2 = 2M).  Returns the new count
-// and the new strict insert threshold.  n <= 64*NPL.
+// Largest v such that at least K of the wave's keys are >= v (keys distinct:
+// the K-th largest).  Keys of empty slots are 0.
+template <int NPL>
+__device__ unsigned long long kth_largest(const unsigned long long (&key)[NPL], int K) {
+  unsigned long long res = 0;
+#pragma unroll 1
+  for (int bit = 63; bit >= 0; --bit) {
+    const unsigned long long cand = res | (1ull << bit);
+    int c = 0;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) c += __popcll(__ballot(key[i] >= cand));
+    if (c >= K) res = cand;
+  }
+  return res;
+}
+
+// ---- screen, bins path (k <= 128) -------------------------------------------
+struct ScreenArgs {
+  const void* index;
+  const __bf16* qb;      // [nq_pad, D]
+  const float* margin2;  // [nq_pad]
+  int64_t nq;            // real queries in this chunk
+  int64_t n;             // real candidates (rows >= n are zero padding)
+  int64_t n_pad;
+  int k;
+  int S;                 // candidate splits
+  int R;                 // entries per (query, split, half) region
+  uint2* buf;            // [nq_pad][S][2][R] (score bits, candidate)
+  int* count;            // [nq_pad][S][2]; -1 = region overflowed
+  unsigned* thr;         // [nq_pad] order key of a valid strict threshold (0 = none)
+};
+
+// s_waitcnt with only the vector-memory counter constrained (gfx9 encoding).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
+// Keeps the entries of region[0..n) scoring above thr; returns their count.
+__device__ __noinline__ int compact_region(uint2* region, int n, float thr) {
+  int m = 0;
+  for (int j0 = 0; j0 < n; j0 += 16) {
+    uint2 e[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) e[u] = (j0 + u < n) ? region[j0 + u] : make_uint2(0u, 0u);
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (j0 + u < n && __uint_as_float(e[u].x) > thr) region[m++] = e[u];
+  }
+  return m;
+}
+
+constexpr int kStages = 4;     // LDS ring: tile i computed while tiles i+1..i+3 land
+constexpr int kWarmTiles = 64; // bins-only warm-up tiles per split (4096 candidates)
+
+template <int D>
+__global__ void __launch_bounds__(kScreenThreads) screen_bins_kernel(const ScreenArgs a) {
+  constexpr int KS = D / 16, CH = D / 8, RB = D * 2;
+  constexpr int TILE_BYTES = kCTile * RB;                 // 16 KiB at D = 128
+  constexpr int PIECES = TILE_BYTES / 1024;               // 1 KiB LDS-DMA pieces per tile
+  constexpr int PPW = PIECES >= kScreenWaves ? PIECES / kScreenWaves : 1;
+  __shared__ __attribute__((aligned(1024))) char smem[kStages * TILE_BYTES];
+  const int tid = threadIdx.x;
+  const int wave = tid / kWave;
+  const int lane = lane_id();
+  const int h = lane >> 5, l32 = lane & 31;
+  const int split = static_cast<int>(blockIdx.x % a.S);
+  const int64_t qg = static_cast<int64_t>(blockIdx.x / a.S) * kQPerWG + wave * kQPerWave + l32;
+  const int ntiles = static_cast<int>(a.n_pad / kCTile);
+  const int per = (ntiles + a.S - 1) / a.S;
+  const int tb = split * per;
+  const int nt = max(min(ntiles, tb + per) - tb, 0);
+  const __bf16* crow = index_rows(a.index);
+  const bool my_pieces = wave * PPW < PIECES;  // D = 32: waves 4..7 stage nothing
+
+  bf16x8 bfrag[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) bfrag[s] = *reinterpret_cast<const bf16x8*>(a.qb + qg * D + 16 * s + 8 * h);
+  const float m2 = a.margin2[qg];
+  wait_vmcnt<0>();  // ordinary loads retired before the LDS-DMA ring starts
+  const bool live = qg < a.nq;
+  float thr = live ? -INFINITY : INFINITY;  // insertion threshold (strict)
+  float gthr = -INFINITY;                   // best globally valid strict threshold
+  float bins[kBins];
+#pragma unroll
+  for (int i = 0; i < kBins; ++i) bins[i] = -INFINITY;
+  uint2* region = a.buf + ((qg * a.S + split) * 2 + h) * static_cast<int64_t>(a.R);
+  int cnt = 0;
+  bool ovf = false;
+
+  // LDS image of a tile: row-major RB-byte rows, 16-B chunks XOR-swizzled by
+  // row; the swizzle is applied to the per-lane SOURCE address so that every
+  // 1 KiB DMA piece lands lane-linear.
+  auto issue = [&](int tile, int stage) {
+    const int64_t base = static_cast<int64_t>(tile) * kCTile;
+#pragma unroll
+    for (int u = 0; u < PPW; ++u) {
+      const int p = wave * PPW + u;
+      if (p < PIECES) {
+        const int off = p * 1024 + lane * 16;
+        const int row = off / RB, chp = (off % RB) / 16;
+        const int ch = chp ^ ((row * CH / 16) % CH);
+        const __bf16* src = crow + (base + row) * D + ch * 8;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src),
+                                         (__attribute__((address_space(3))) void*)(smem + stage * TILE_BYTES + p * 1024),
+                                         16, 0, 0);
+      }
+    }
+  };
+  // wait until at most `ahead` tiles of this wave's DMA are still in flight
+  auto wait_tiles = [&](int ahead) {
+    if (!my_pieces || ahead <= 0) {
+      wait_vmcnt<0>();
+    } else if (ahead == 1) {
+      wait_vmcnt<PPW>();
+    } else {
+      wait_vmcnt<2 * PPW>();
+    }
+  };
+
+  // Lane-parallel threshold refresh: K-th largest of the pair's 128 bins by a
+  // 16-bit prefix search of their order keys (a lower bound of the K-th).
+  auto refresh = [&](bool warm) {
+    unsigned res = 0;
+#pragma unroll 1
+    for (int bit = 15; bit >= 0; --bit) {
+      const unsigned c = res | (1u << bit);
+      const float f = order_key_float(c << 16);  // smallest float with this key prefix (NaN: none)
+      int n = 0;
+#pragma unroll
+      for (int i = 0; i < kBins; ++i) n += (bins[i] >= f) ? 1 : 0;
+      n += __shfl_xor(n, 32, kWave);
+      if (n >= a.k) res = c;
+    }
+    const float tau = order_key_float(res << 16);
+    // A zero query (m2 == 0, every score exactly 0) relies on a strict local
+    // threshold that is valid only for candidates after the certifying ones;
+    // the warm-up tiles are scanned again, so it skips the warm-up threshold
+    // and restarts its bins.
+    if (warm && m2 == 0.0f) {
+#pragma unroll
+      for (int i = 0; i < kBins; ++i) bins[i] = -INFINITY;
+    } else if (tau > -INFINITY && tau < INFINITY) {
+      const float local = m2 > 0.0f ? next_down(tau - m2) : tau;
+      const float pub = m2 > 0.0f ? local : next_down(tau);
+      gthr = fmaxf(gthr, pub);
+      thr = fmaxf(thr, local);
+    }
+    if (a.S > 1) {
+      unsigned g = float_order_key(gthr);
+      if (h == 0 && live) g = max(g, atomicMax(&a.thr[qg], g));
+      const unsigned g2 = __shfl_xor(g, 32, kWave);
+      gthr = fmaxf(gthr, order_key_float(g2 > g ? g2 : g));
+      thr = fmaxf(thr, gthr);
+    }
+    thr = fmaxf(thr, __shfl_xor(thr, 32, kWave));
+#ifdef TT_INDEX_NOINSERT
+    thr = 3.0e38f;
+#endif
+  };
+
+  // A lane whose region is nearly full drops the entries the globally valid
+  // threshold rules out (the strict local one of a zero-margin query is only
+  // valid for later candidates); if that does not make room the query is
+  // answered by the exact fallback.
+  auto self_compact = [&]() {
+    if (cnt > a.R - 2 * 16) {
+      cnt = compact_region(region, cnt, gthr);
+      TT_STAT(1, 1);
+      if (cnt > a.R - 2 * 16) {
+        ovf = true;
+        thr = INFINITY;
+        TT_STAT(2, 1);
+      }
+    }
+  };
+
+  // Warm-up: the first `pre` tiles of the split are scanned once for the bins
+  // only (no inserts), so the insertion threshold starts near the top few
+  // percent instead of at -inf; then the split is scanned from its start.
+  // Virtual tile v < pre is tile tb + v, v >= pre is tile tb + v - pre.
+  // pre is a multiple of 4 so a tile re-scanned after the warm-up lands in the
+  // same bins (Q = v & 3): every bin stays a maximum over distinct candidates.
+  const int pre = min(kWarmTiles, nt / 4) & ~3;
+  const int nv = pre + nt;
+  auto vtile = [&](int v) { return tb + (v < pre ? v : v - pre); };
+#pragma unroll
+  for (int s = 0; s < kStages - 1; ++s)
+    if (s < nv) issue(vtile(s), s);
+  wait_tiles(min(nv, kStages - 1) - 1);
+  __builtin_amdgcn_s_barrier();
+
+  // One 64-candidate tile from LDS stage v % 4 (Q = v & 3 selects the bins):
+  // both 32-candidate blocks are issued to the MFMA pipe before either is
+  // filtered, so the first block's filter overlaps the second's MFMAs.
+  auto tile_body = [&](int v, const int Q) {
+    if (v + kStages - 1 < nv) issue(vtile(v + kStages - 1), (v + kStages - 1) % kStages);
+    const char* B = smem + (v % kStages) * TILE_BYTES;
+    const int64_t cbase = static_cast<int64_t>(vtile(v)) * kCTile;
+    const bool pad = cbase + kCTile > a.n;  // last tile holds zero padding rows
+    const bool scan = v >= pre;
+    f32x16 acc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      acc[t] = f32x16{};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int row = 32 * t + l32, ch = 2 * s + h;
+        const int swz = (row * CH / 16) % CH;
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(B + row * RB + ((ch ^ swz) << 4));
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfrag[s], acc[t], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if (pad) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (cbase + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h >= a.n) acc[t][r] = -INFINITY;
+      }
+#pragma unroll
+      for (int pr = 0; pr < 8; ++pr) {
+        const float x = acc[t][2 * pr], y = acc[t][2 * pr + 1];
+        const float pm = __builtin_elementwise_maximum(x, y);
+        bins[Q * 16 + t * 8 + pr] = __builtin_elementwise_maximum(bins[Q * 16 + t * 8 + pr], pm);
+        if (scan && pm > thr) {
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const float val = u ? y : x;
+            const int r = 2 * pr + u;
+            if (val > thr) {
+              const unsigned cidx = static_cast<unsigned>(cbase + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h);
+              region[cnt] = make_uint2(__float_as_uint(val), cidx);
+              ++cnt;
+              TT_STAT(0, 1);
+            }
+          }
+        }
+      }
+    }
+    const int j = v + 1 - pre;  // main-scan tiles done
+    const bool due = j == 0 || (j >= 2 && (j & (j - 1)) == 0) || (j > 0 && j % 128 == 0) || j == nt;
+    const bool full = __any(cnt > a.R - 2 * 16);
+    if (due || full) refresh(j == 0);
+    if (full) self_compact();
+    if (v + 1 < nv) wait_tiles(min(v + kStages - 1, nv - 1) - (v + 1));  // tile v+1 landed
+    __builtin_amdgcn_s_barrier();
+  };
+
+  for (int v = 0; v < nv; v += 4) {
+    tile_body(v, 0);
+    if (v + 1 < nv) tile_body(v + 1, 1);
+    if (v + 2 < nv) tile_body(v + 2, 2);
+    if (v + 3 < nv) tile_body(v + 3, 3);
+  }
+  a.count[(qg * a.S + split) * 2 + h] = ovf ? -1 : cnt;
+  if (h == 0 && live && gthr > -INFINITY) atomicMax(&a.thr[qg], float_order_key(gthr));
+}
+
+// ---- screen, compaction path (k > 128) ---------------------------------------
+struct ScreenCArgs {
+  const void* index;
+  const __bf16* qb;
+  const float* margin2;
+  int64_t nq;
+  int64_t n_pad;
+  int k;
+  int cap;
+  uint2* buf;    // [nq_pad][cap]
+  int* count;    // [nq_pad]; -1 = overflow
+};
+
+// Compacts the shortlist buf[0..n) of one query with the whole wave.  Keeps
+// every entry that might still belong to the exact top-K given screened
+// scores within +-M of the exact ones (margin2 = 2M).  n <= 64*NPL.
 template <int NPL>
 __device__ int compact_shortlist(uint2* buf, int n, int K, float margin2, float* thr_out) {
   const int lane = lane_id();
@@ -198,7 +504,7 @@ __device__ int compact_shortlist(uint2* buf, int n, int K, float margin2, float*
   const float sK = order_key_float(static_cast<unsigned>(kk >> 32));
   const unsigned idxK = 0xFFFFFFFFu - static_cast<unsigned>(kk & 0xFFFFFFFFull);
   float thr = sK - margin2;
-  if (margin2 > 0.0f) thr = next_down(thr);  // round the threshold down
+  if (margin2 > 0.0f) thr = next_down(thr);
   int out = 0;
 #pragma unroll
   for (int i = 0; i < NPL; ++i) {
@@ -209,30 +515,17 @@ __device__ int compact_shortlist(uint2* buf, int n, int K, float margin2, float*
     if (keep) buf[out + __popcll(m & lanemask_lt64())] = ent[i];
     out += __popcll(m);
   }
-  __threadfence_block();  // other lanes of this wave re-read the shortlist
+  __threadfence_block();
   *thr_out = thr;
   return out;
 }
 
-struct ScreenArgs {
-  const void* index;
-  const __bf16* qb;      // [nq_pad, D]
-  const float* margin2;  // [nq_pad]
-  int64_t nq;            // real queries in this chunk
-  int64_t n_pad;
-  int k;
-  int cap;
-  uint2* buf;            // [nq_pad, cap]
-  int* count;            // [nq_pad]
-  int* overflow;         // [nq_pad]
-};
-
 template <int D, int NPL>
-__global__ void __launch_bounds__(kScreenThreads) screen_kernel(const ScreenArgs a) {
+__global__ void __launch_bounds__(kScreenThreads) screen_compact_kernel(const ScreenCArgs a) {
   constexpr int KS = D / 16, CH = D / 8;
   constexpr int A_BYTES = kCTile * D * 2;
   constexpr int BUF_BYTES = A_BYTES + kCTile * 4;
-  constexpr int CPT = (kCTile * CH + kScreenThreads - 1) / kScreenThreads;  // chunks per thread
+  constexpr int CPT = (kCTile * CH + kScreenThreads - 1) / kScreenThreads;
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF_BYTES];
   __shared__ int cnt_s[kQPerWG];
   __shared__ float thr_s[kQPerWG];
@@ -240,7 +533,7 @@ __global__ void __launch_bounds__(kScreenThreads) screen_kernel(const ScreenArgs
   const int wave = tid / kWave;
   const int lane = lane_id();
   const int h = lane >> 5, l32 = lane & 31;
-  const int ql = wave * kQPerWave + l32;  // query slot in the WG
+  const int ql = wave * kQPerWave + l32;
   const int64_t qg = static_cast<int64_t>(blockIdx.x) * kQPerWG + ql;
   const __bf16* crow = index_rows(a.index);
   const float* cbias = index_bias(a.index, a.n_pad, D);
@@ -252,7 +545,7 @@ __global__ void __launch_bounds__(kScreenThreads) screen_kernel(const ScreenArgs
   if (tid < kQPerWG) {
     const int64_t q = static_cast<int64_t>(blockIdx.x) * kQPerWG + tid;
     cnt_s[tid] = 0;
-    thr_s[tid] = (q < a.nq) ? -INFINITY : INFINITY;  // padding queries never insert
+    thr_s[tid] = (q < a.nq) ? -INFINITY : INFINITY;
   }
   uint2* mybuf_base = a.buf + (static_cast<int64_t>(blockIdx.x) * kQPerWG + wave * kQPerWave) * a.cap;
   bool ovf = false;
@@ -297,17 +590,16 @@ __global__ void __launch_bounds__(kScreenThreads) screen_kernel(const ScreenArgs
     const char* B = smem + cur * BUF_BYTES;
     const float* bias = reinterpret_cast<const float*>(B + A_BYTES);
 
-    // Make room: a tile adds at most kCTile entries per query.
     const bool need = cnt_s[ql] > a.cap - kCTile;
     uint64_t needm = __ballot(need) & 0xFFFFFFFFull;
-    if (needm) __threadfence_block();  // inserts of earlier tiles visible to the wave
+    if (needm) __threadfence_block();
     while (needm) {
       const int qq = __ffsll(static_cast<long long>(needm)) - 1;
       needm &= needm - 1;
-      const float m2 = __shfl(margin2, qq, kWave);
+      const float mq = __shfl(margin2, qq, kWave);
       float nthr;
       const int nc = compact_shortlist<NPL>(mybuf_base + static_cast<int64_t>(qq) * a.cap,
-                                            cnt_s[wave * kQPerWave + qq], a.k, m2, &nthr);
+                                            cnt_s[wave * kQPerWave + qq], a.k, mq, &nthr);
       if (lane == 0) {
         if (nc > a.cap - kCTile) {  // cannot make room: exact fallback in finalize
           cnt_s[wave * kQPerWave + qq] = 0;
@@ -356,16 +648,39 @@ __global__ void __launch_bounds__(kScreenThreads) screen_kernel(const ScreenArgs
     if (more) lstore(cur ^ 1);
     __syncthreads();
   }
-  if (h == 0) {
-    a.count[qg] = cnt_s[ql];
-    a.overflow[qg] = ovf ? 1 : 0;
-  }
+  if (h == 0) a.count[qg] = ovf ? -1 : cnt_s[ql];
 }
 
+// ---- finalize ------------------------------------------------------------
 // Exact score: k-ordered fmaf chain over the fp32 rows (dim real columns).
-__device__ __forceinline__ float exact_score(const float* __restrict__ qs, const float* __restrict__ c, int dim) {
+// qs is the query row in LDS (broadcast reads); the candidate row is loaded in
+// batches (16 x float4 or 16 scalars in flight) ahead of the dependent chain.
+__device__ __forceinline__ float exact_score(const float* __restrict__ qs, const float* __restrict__ c, int dim,
+                                             bool vec4) {
   float acc = 0.0f;
-  for (int e = 0; e < dim; ++e) acc = __builtin_fmaf(qs[e], c[e], acc);
+  if (vec4) {  // c 16-byte aligned, dim % 4 == 0
+    for (int e0 = 0; e0 < dim; e0 += 64) {
+      f32x4 v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (e0 + 4 * i < dim) v[i] = *reinterpret_cast<const f32x4*>(c + e0 + 4 * i);
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (e0 + 4 * i < dim) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) acc = __builtin_fmaf(qs[e0 + 4 * i + u], v[i][u], acc);
+        }
+    }
+  } else {
+    for (int e0 = 0; e0 < dim; e0 += 16) {
+      float v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = (e0 + i < dim) ? c[e0 + i] : 0.0f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (e0 + i < dim) acc = __builtin_fmaf(qs[e0 + i], v[i], acc);
+    }
+  }
   return acc;
 }
 
@@ -377,102 +692,324 @@ struct FinalArgs {
   int64_t n;
   int dim;
   int k;
-  int cap;
+  int S;     // splits
+  int H;     // regions per split (2 bins path, 1 compaction path)
+  int R;     // entries per region
+  int L;     // LDS list capacity
+  int P;     // bitonic sort size (pow2 >= k)
+  int vec4;  // candidate rows are 16-byte aligned float4 rows
   int64_t nq;
   int64_t index_offset;
   const float* margin2;
-  uint2* buf;
+  const uint2* buf;
   const int* count;
-  const int* overflow;
+  const unsigned* thr;  // null for the compaction path
   float* out_s;
   int32_t* out_i;
 };
 
-template <int NPL>
-__global__ void __launch_bounds__(kFinalWaves * kWave) finalize_kernel(const FinalArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char fsm[];
-  const int wave = threadIdx.x / kWave;
-  const int lane = lane_id();
-  const int64_t q = blockIdx.x * static_cast<int64_t>(kFinalWaves) + wave;
-  if (q >= a.nq) return;
-  float* qs = reinterpret_cast<float*>(fsm) + wave * 128;  // query row (dim <= 128)
-  for (int e = lane; e < a.dim; e += kWave) qs[e] = a.q[q * a.ldq + e];
-  __threadfence_block();
-  uint2* buf = a.buf + q * a.cap;
-  int n = a.count[q];
+// Keeps list entries with sc > thr (in place, whole wave).  Returns the count.
+__device__ __forceinline__ int filter_list(float* sc, unsigned* id, int n, float thr) {
+  int out = 0;
+  for (int j0 = 0; j0 < n; j0 += kWave) {
+    const int j = j0 + lane_id();
+    const float s = j < n ? sc[j] : 0.0f;
+    const unsigned i = j < n ? id[j] : 0u;
+    const bool keep = j < n && s > thr;
+    const uint64_t m = __ballot(keep);
+    __syncthreads();  // all reads of this chunk before any write into it
+    if (keep) {
+      const int p = out + __popcll(m & lanemask_lt64());
+      sc[p] = s;
+      id[p] = i;
+    }
+    out += __popcll(m);
+  }
+  __syncthreads();
+  return out;
+}
 
-  if (a.overflow[q]) {
-    // Exact fallback: scan every candidate with the fp32 chain, keep an exact
-    // shortlist (margin 0: compaction always reduces to exactly K).
-    float thr = -INFINITY;
+// Radix select on the list's score order keys with 8-bit digits and an LDS
+// histogram (one wave): after `passes` digits, `prefix` holds the top
+// 8*passes bits of the K-th largest key, `above` = #keys whose top bits are
+// greater, `at` = #keys sharing the prefix (above < K <= above + at).
+struct Kth {
+  unsigned prefix;
+  int above;
+  int at;
+};
+
+__device__ Kth radix_select(const float* sc, int n, int K, int passes, unsigned* hist) {
+  const int lane = lane_id();
+  unsigned prefix = 0;
+  int above = 0, at = n;
+  for (int d = 0; d < passes; ++d) {
+    const int shift = 24 - 8 * d;
+    const unsigned hi_mask = d == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
+#pragma unroll
+    for (int u = 0; u < 4; ++u) hist[4 * lane + u] = 0;
+    __syncthreads();
+    for (int j = lane; j < n; j += kWave) {
+      const unsigned key = float_order_key(sc[j]);
+      if ((key & hi_mask) == prefix) atomicAdd(&hist[(key >> shift) & 0xFFu], 1u);
+    }
+    __syncthreads();
+    // counts at or above each bin: lane L owns bins 4L..4L+3
+    unsigned h4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) h4[u] = hist[4 * lane + u];
+    const unsigned mine = h4[0] + h4[1] + h4[2] + h4[3];
+    unsigned suffix = mine;  // inclusive suffix sum over lanes >= L
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+      const unsigned o = __shfl_down(suffix, off, kWave);
+      if (lane + off < kWave) suffix += o;
+    }
+    unsigned cum[4];  // keys in bins >= 4L+u (within the prefix)
+    cum[3] = suffix - mine + h4[3];
+    cum[2] = cum[3] + h4[2];
+    cum[1] = cum[2] + h4[1];
+    cum[0] = cum[1] + h4[0];
+    const int need = K - above;
+    int best = -1;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (static_cast<int>(cum[u]) >= need) best = 4 * lane + u;
+    const uint64_t m = __ballot(best >= 0);
+    const int src = 63 - __clzll(m);
+    const int b = __shfl(best, src, kWave);
+    const int u = b & 3;
+    const unsigned cb = __shfl(cum[0], src, kWave), cb1 = __shfl(cum[1], src, kWave),
+                   cb2 = __shfl(cum[2], src, kWave), cb3 = __shfl(cum[3], src, kWave);
+    const unsigned cumb = u == 0 ? cb : u == 1 ? cb1 : u == 2 ? cb2 : cb3;
+    const unsigned hb = hist[b];
+    above += static_cast<int>(cumb - hb);
+    at = static_cast<int>(hb);
+    prefix |= static_cast<unsigned>(b) << shift;
+    __syncthreads();
+  }
+  return Kth{prefix, above, at};
+}
+
+// Screened cut: tau = lower bound of the K-th largest screened score (16-bit
+// key prefix); keeps s > next_down(tau - margin2).  Raises *thr.
+__device__ int coarse_cut(float* sc, unsigned* id, int n, int K, float margin2, float* thr, unsigned* hist) {
+  if (n <= K) return n;
+  const Kth r = radix_select(sc, n, K, 2, hist);
+  const float tau = order_key_float(r.prefix);
+  if (!(tau > -INFINITY)) return n;
+  const float t = next_down(margin2 > 0.0f ? tau - margin2 : tau);
+  if (t <= *thr) return n;
+  *thr = t;
+  return filter_list(sc, id, n, t);
+}
+
+// Exact selection: keeps exactly the K best entries by (score desc, index
+// asc); *thr = the K-th score (later candidates of an in-order scan need a
+// strictly larger score).
+__device__ int exact_select(float* sc, unsigned* id, int n, int K, float* thr, unsigned* hist) {
+  if (n <= K) {
+    *thr = -INFINITY;
+    return n;
+  }
+  const Kth r = radix_select(sc, n, K, 4, hist);
+  const unsigned res = r.prefix;  // exact key of the K-th score
+  const int need = K - r.above;   // ties at the K-th score to keep, lowest indices first
+  unsigned cut = 0xFFFFFFFFu;
+  if (need < r.at) {
+    // need-th smallest index among the ties: largest v with #(idx < v) < need
+    unsigned v = 0;
+#pragma unroll 1
+    for (int bit = 31; bit >= 0; --bit) {
+      const unsigned c = v | (1u << bit);
+      int lt = 0;
+      for (int j0 = 0; j0 < n; j0 += kWave) {
+        const int j = j0 + lane_id();
+        lt += __popcll(__ballot(j < n && float_order_key(sc[j]) == res && id[j] < c));
+      }
+      if (lt < need) v = c;
+    }
+    cut = v;
+  }
+  int out = 0;
+  for (int j0 = 0; j0 < n; j0 += kWave) {
+    const int j = j0 + lane_id();
+    const float s = j < n ? sc[j] : 0.0f;
+    const unsigned i = j < n ? id[j] : 0u;
+    const unsigned key = float_order_key(s);
+    const bool keep = j < n && (key > res || (key == res && i <= cut));
+    const uint64_t m = __ballot(keep);
+    __syncthreads();
+    if (keep) {
+      const int p = out + __popcll(m & lanemask_lt64());
+      sc[p] = s;
+      id[p] = i;
+    }
+    out += __popcll(m);
+  }
+  __syncthreads();
+  *thr = order_key_float(res);
+  return out;
+}
+
+__global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char fsm[];
+  float* qs = reinterpret_cast<float*>(fsm);  // query row (dim <= 128)
+  float* sc = qs + 128;
+  unsigned* id = reinterpret_cast<unsigned*>(sc + a.L);
+  unsigned long long* sk = reinterpret_cast<unsigned long long*>(id + a.L);
+  unsigned* hist = reinterpret_cast<unsigned*>(sk + a.P);  // 256 radix bins
+  const int64_t q = blockIdx.x;
+  const int lane = lane_id();
+  for (int e = lane; e < a.dim; e += kWave) qs[e] = a.q[q * a.ldq + e];
+  const float m2 = a.margin2[q];
+  float thr = (a.thr && a.thr[q]) ? order_key_float(a.thr[q]) : -INFINITY;
+  const int nreg = a.S * a.H;
+  bool ovf = false;
+  for (int r = 0; r < nreg; ++r) ovf = ovf || a.count[q * nreg + r] < 0;
+  __syncthreads();
+
+  int n = 0;
+  if (!ovf) {
+    // Gather the entries above the final threshold; cut whenever the list fills.
+    for (int r = 0; r < nreg && !ovf; ++r) {
+      const int c = a.count[q * nreg + r];
+      const uint2* reg = a.buf + (q * nreg + r) * static_cast<int64_t>(a.R);
+      for (int j0 = 0; j0 < c && !ovf; j0 += 4 * kWave) {
+        uint2 e[4];  // four chunks in flight
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int j = j0 + u * kWave + lane;
+          e[u] = j < c ? reg[j] : make_uint2(0u, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int j = j0 + u * kWave + lane;
+          const float s = __uint_as_float(e[u].x);
+          const bool keep = j < c && s > thr;
+          const uint64_t m = __ballot(keep);
+          if (keep) {
+            const int p = n + __popcll(m & lanemask_lt64());
+            sc[p] = s;
+            id[p] = e[u].y;
+          }
+          n += __popcll(m);
+          if (n > a.L - kWave) {
+            __syncthreads();
+            if (m2 > 0.0f) {
+              n = coarse_cut(sc, id, n, a.k, m2, &thr, hist);
+            } else {  // zero query: screened scores are exact, cut ties by index
+              float t;
+              n = exact_select(sc, id, n, a.k, &t, hist);
+              thr = fmaxf(thr, next_down(t));
+            }
+            if (n > a.L - kWave) {
+              ovf = true;
+              break;
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (!ovf) {
+    n = coarse_cut(sc, id, n, a.k, m2, &thr, hist);
+    ovf = n < a.k;  // cannot happen with a valid screen; answer exactly regardless
+  }
+  if (!ovf) {
+    for (int j = lane; j < n; j += kWave)
+      sc[j] = exact_score(qs, a.cand + static_cast<int64_t>(id[j]) * a.ldc, a.dim, a.vec4 != 0) + 0.0f;
+    __syncthreads();
+  } else {
+    // Exact fallback: scan every candidate with the fp32 chain (in index
+    // order, so a strict threshold at the K-th score is exact).
+    float ethr = -INFINITY;
     n = 0;
     for (int64_t c0 = 0; c0 < a.n; c0 += kWave) {
       const int64_t c = c0 + lane;
       float s = -INFINITY;
-      if (c < a.n) s = exact_score(qs, a.cand + c * a.ldc, a.dim);
-      const bool hit = (c < a.n) && (s + 0.0f > thr);
-      const uint64_t m = __ballot(hit);
-      if (hit) buf[n + __popcll(m & lanemask_lt64())] = make_uint2(__float_as_uint(s + 0.0f), static_cast<unsigned>(c));
+      if (c < a.n) s = exact_score(qs, a.cand + c * a.ldc, a.dim, a.vec4 != 0) + 0.0f;
+      const bool keep = c < a.n && s > ethr;
+      const uint64_t m = __ballot(keep);
+      if (keep) {
+        const int p = n + __popcll(m & lanemask_lt64());
+        sc[p] = s;
+        id[p] = static_cast<unsigned>(c);
+      }
       n += __popcll(m);
-      if (n > a.cap - kWave) {
-        __threadfence_block();
-        n = compact_shortlist<NPL>(buf, n, a.k, 0.0f, &thr);
+      if (n > a.L - kWave) {
+        __syncthreads();
+        n = exact_select(sc, id, n, a.k, &ethr, hist);
       }
     }
-  } else {
-    // Drop what the final screened threshold rules out, then rescore exactly.
-    float thr;
-    n = compact_shortlist<NPL>(buf, n, a.k, a.margin2[q], &thr);
-    for (int j = lane; j < n; j += kWave) {
-      const uint2 e = buf[j];
-      const float s = exact_score(qs, a.cand + static_cast<int64_t>(e.y) * a.ldc, a.dim);
-      buf[j] = make_uint2(__float_as_uint(s + 0.0f), e.y);
-    }
-    __threadfence_block();
+    __syncthreads();
   }
-  // Exact selection of the top-K (distinct keys -> exactly K remain).
-  __threadfence_block();
-  float thr0;
-  n = compact_shortlist<NPL>(buf, n, a.k, 0.0f, &thr0);
-  // Rank the K survivors: rank = #keys greater than own key.
-  for (int j = lane; j < n; j += kWave) {
-    const uint2 e = buf[j];
-    const unsigned long long mine = make_key(__uint_as_float(e.x), e.y);
-    int rank = 0;
-    for (int i = 0; i < n; ++i) {
-      const uint2 o = buf[i];
-      rank += (make_key(__uint_as_float(o.x), o.y) > mine) ? 1 : 0;
-    }
-    if (rank < a.k) {
-      a.out_s[q * a.k + rank] = __uint_as_float(e.x);
-      a.out_i[q * a.k + rank] = static_cast<int32_t>(static_cast<int64_t>(e.y) + a.index_offset);
+  float kth;
+  n = exact_select(sc, id, n, a.k, &kth, hist);
+  // Rank: bitonic sort of (score, -index) keys, descending.
+  for (int j = lane; j < a.P; j += kWave) sk[j] = j < n ? make_key(sc[j], id[j]) : 0ull;
+  for (int size = 2; size <= a.P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      for (int i = lane; i < a.P / 2; i += kWave) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool desc = (lo & size) == 0;
+        const unsigned long long x = sk[lo], y = sk[hi];
+        if ((x < y) == desc) {
+          sk[lo] = y;
+          sk[hi] = x;
+        }
+      }
     }
   }
-}
-
-template <int D, int NPL>
-int launch_screen(const ScreenArgs& sa, int64_t nq_pad, hipStream_t st) {
-  hipLaunchKernelGGL((screen_kernel<D, NPL>), dim3(nq_pad / kQPerWG), dim3(kScreenThreads), 0, st, sa);
-  TT_CHECK_LAUNCH();
-  return TT_OK;
-}
-
-template <int NPL>
-int launch_screen_d(int D, const ScreenArgs& sa, int64_t nq_pad, hipStream_t st) {
-  switch (D) {
-    case 32: return launch_screen<32, NPL>(sa, nq_pad, st);
-    case 64: return launch_screen<64, NPL>(sa, nq_pad, st);
-    default: return launch_screen<128, NPL>(sa, nq_pad, st);
+  __syncthreads();
+  for (int t = lane; t < a.k; t += kWave) {
+    const unsigned long long key = sk[t];
+    a.out_s[q * a.k + t] = order_key_float(static_cast<unsigned>(key >> 32));
+    a.out_i[q * a.k + t] =
+        static_cast<int32_t>(static_cast<int64_t>(0xFFFFFFFFu - static_cast<unsigned>(key)) + a.index_offset);
   }
 }
 
-template <int NPL>
-int launch_final(const FinalArgs& fa, hipStream_t st) {
-  const size_t shm = kFinalWaves * 128 * sizeof(float);
-  hipLaunchKernelGGL(finalize_kernel<NPL>, dim3(ceil_div(fa.nq, kFinalWaves)), dim3(kFinalWaves * kWave), shm, st,
-                     fa);
-  TT_CHECK_LAUNCH();
-  return TT_OK;
+// ---- host plan -------------------------------------------------------------
+struct SearchPlan {
+  bool bins;
+  int S, H, R, L, P;
+  int64_t chunk;
+};
+
+SearchPlan plan_search(int64_t nq, int64_t n_cand, int k) {
+  SearchPlan p{};
+  const int64_t ntiles = ceil_div(n_cand, kCTile);
+  p.P = next_pow2(k < 2 ? 2 : k);
+  p.bins = k <= kBinsMaxK;
+  p.H = p.bins ? 2 : 1;
+  p.R = p.bins ? kLaneCap : cap_for_k(k);
+  p.L = p.bins ? 1024 : (p.R > 2048 ? p.R : 2048);
+  p.S = 1;
+  p.chunk = nq < kMaxChunk ? (nq > 0 ? nq : 1) : kMaxChunk;
+  for (int pass = 0; pass < 3; ++pass) {
+    if (p.bins) {  // enough workgroups for the chip: split the candidates of few query blocks
+      const int64_t qblocks = ceil_div(p.chunk, kQPerWG);
+      p.S = 1;
+      while (p.S < kMaxSplits && qblocks * p.S < 256 && ntiles / (2 * p.S) >= 64) p.S *= 2;
+#ifdef TT_FORCE_SPLITS
+      p.S = TT_FORCE_SPLITS;
+#endif
+    }
+    const size_t per_query = static_cast<size_t>(p.S) * p.H * p.R * sizeof(uint2);
+    int64_t chunk = static_cast<int64_t>(kShortlistBudget / per_query) / kQPerWG * kQPerWG;
+    if (chunk < kQPerWG) chunk = kQPerWG;
+    if (chunk > p.chunk) chunk = p.chunk;
+    p.chunk = chunk;
+  }
+  return p;
+}
+
+size_t final_lds_bytes(const SearchPlan& p) {
+  return 128 * sizeof(float) + static_cast<size_t>(p.L) * 8 + static_cast<size_t>(p.P) * 8 + 256 * sizeof(unsigned);
 }
 
 struct SearchWs {
@@ -480,19 +1017,38 @@ struct SearchWs {
   float* margin2;
   uint2* buf;
   int* count;
-  int* overflow;
+  unsigned* thr;
 };
 
-SearchWs carve_search(Carver& cv, int64_t nq, int D, int cap) {
-  const int64_t chunk = nq < kQueryChunk ? nq : kQueryChunk;
+SearchWs carve_search(Carver& cv, int64_t nq, int D, const SearchPlan& p) {
+  const int64_t chunk = nq < p.chunk ? nq : p.chunk;
   const int64_t nq_pad = round_up(chunk > 0 ? chunk : 1, kQPerWG);
   SearchWs w;
   w.qb = cv.take<__bf16>(nq_pad * D);
   w.margin2 = cv.take<float>(nq_pad);
-  w.buf = cv.take<uint2>(nq_pad * cap);
-  w.count = cv.take<int>(nq_pad);
-  w.overflow = cv.take<int>(nq_pad);
+  w.buf = cv.take<uint2>(nq_pad * p.S * p.H * static_cast<int64_t>(p.R));
+  w.count = cv.take<int>(nq_pad * p.S * p.H);
+  w.thr = cv.take<unsigned>(nq_pad);
   return w;
+}
+
+template <int D>
+int launch_screen(const SearchPlan& p, const ScreenArgs& sa, const ScreenCArgs& ca, int64_t nq_pad, hipStream_t st) {
+  if (p.bins) {
+    hipLaunchKernelGGL(screen_bins_kernel<D>, dim3((nq_pad / kQPerWG) * p.S), dim3(kScreenThreads), 0, st, sa);
+    TT_CHECK_LAUNCH();
+    return TT_OK;
+  }
+  const dim3 grid(nq_pad / kQPerWG), block(kScreenThreads);
+  switch (p.R / kWave) {
+    case 16: hipLaunchKernelGGL((screen_compact_kernel<D, 16>), grid, block, 0, st, ca); break;
+    case 32: hipLaunchKernelGGL((screen_compact_kernel<D, 32>), grid, block, 0, st, ca); break;
+    case 64: hipLaunchKernelGGL((screen_compact_kernel<D, 64>), grid, block, 0, st, ca); break;
+    case 128: hipLaunchKernelGGL((screen_compact_kernel<D, 128>), grid, block, 0, st, ca); break;
+    default: return fail(TT_ERR_UNSUPPORTED, "tt_bruteforce_search: shortlist capacity %d", p.R);
+  }
+  TT_CHECK_LAUNCH();
+  return TT_OK;
 }
 
 }  // namespace
@@ -519,17 +1075,17 @@ extern "C" int tt_bruteforce_build(const float* cand, int64_t ldc, int64_t n_can
   TT_CHECK_HIP(hipMemsetAsync(index, 0, 64, st));
   const int D = pick_dpad(dim);
   const int64_t n_pad = round_up(n_cand, kCTile);
-  hipLaunchKernelGGL(build_kernel, dim3(ceil_div(n_pad, 4)), dim3(256), 0, st, cand, ldc, n_cand, dim, n_pad, D,
-                     index);
+  hipLaunchKernelGGL(build_kernel, dim3(ceil_div(n_pad, 4 * kBuildRowsPerWave)), dim3(256), 0, st, cand, ldc, n_cand,
+                     dim, n_pad, D, index);
   TT_CHECK_LAUNCH();
   return TT_OK;
 }
 
 extern "C" size_t tt_bruteforce_workspace_size(int64_t n_queries, int64_t n_cand, int32_t dim, int32_t k) {
-  (void)n_cand;
-  if (n_queries < 1 || k < 1 || pick_dpad(dim) == 0) return 0;
+  if (n_queries < 1 || n_cand < 1 || k < 1 || pick_dpad(dim) == 0) return 0;
+  const SearchPlan p = plan_search(n_queries, n_cand, k);
   Carver cv(nullptr, 0);
-  carve_search(cv, n_queries, pick_dpad(dim), cap_for_k(k));
+  carve_search(cv, n_queries, pick_dpad(dim), p);
   return cv.used();
 }
 
@@ -544,37 +1100,45 @@ extern "C" int tt_bruteforce_search(const void* index, const float* cand, int64_
   TT_REQUIRE(k >= 1, "tt_bruteforce_search: k must be >= 1");
   TT_REQUIRE(k <= n_cand, "tt_bruteforce_search: k=%d > number of candidates %lld", k,
              static_cast<long long>(n_cand));
-  TT_REQUIRE(k <= 4096, "tt_bruteforce_search: k=%d > 4096", k);
+  TT_REQUIRE(k <= 4000, "tt_bruteforce_search: k=%d > 4000", k);
   TT_REQUIRE(n_queries >= 0, "tt_bruteforce_search: negative n_queries");
   TT_REQUIRE(index_offset >= 0 && index_offset + n_cand < (1ll << 31), "tt_bruteforce_search: index_offset range");
   if (n_queries == 0) return TT_OK;
   TT_REQUIRE(queries && out_scores && out_idx, "tt_bruteforce_search: NULL queries/outputs");
   const int D = pick_dpad(dim);
-  const int cap = cap_for_k(k);
+  const SearchPlan p = plan_search(n_queries, n_cand, k);
   Carver cv(workspace, workspace_bytes);
-  SearchWs w = carve_search(cv, n_queries, D, cap);
+  SearchWs w = carve_search(cv, n_queries, D, p);
   if (!workspace || cv.used() > workspace_bytes)
     return fail(TT_ERR_WORKSPACE, "tt_bruteforce_search: workspace %zu < required %zu", workspace_bytes, cv.used());
   hipStream_t st = to_stream(stream);
   const int64_t n_pad = round_up(n_cand, kCTile);
-  for (int64_t q0 = 0; q0 < n_queries; q0 += kQueryChunk) {
-    const int64_t nq = (n_queries - q0 < kQueryChunk) ? n_queries - q0 : kQueryChunk;
+  const size_t shm = final_lds_bytes(p);
+  if (shm > 65536)
+    TT_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(finalize_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(shm)));
+  const int vec4 = (reinterpret_cast<uintptr_t>(cand) % 16 == 0 && ldc % 4 == 0 && dim % 4 == 0) ? 1 : 0;
+  for (int64_t q0 = 0; q0 < n_queries; q0 += p.chunk) {
+    const int64_t nq = (n_queries - q0 < p.chunk) ? n_queries - q0 : p.chunk;
     const int64_t nq_pad = round_up(nq, kQPerWG);
+    if (p.bins) TT_CHECK_HIP(hipMemsetAsync(w.thr, 0, nq_pad * sizeof(unsigned), st));
     hipLaunchKernelGGL(query_prep_kernel, dim3(ceil_div(nq_pad, 4)), dim3(256), 0, st, queries + q0 * ldq, ldq, nq,
                        dim, nq_pad, D, index, w.qb, w.margin2);
     TT_CHECK_LAUNCH();
-    ScreenArgs sa{index, w.qb, w.margin2, nq, n_pad, k, cap, w.buf, w.count, w.overflow};
-    FinalArgs fa{queries + q0 * ldq, ldq, cand, ldc, n_cand, dim, k, cap, nq, index_offset, w.margin2,
-                 w.buf, w.count, w.overflow, out_scores + q0 * k, out_idx + q0 * k};
+    ScreenArgs sa{index, w.qb, w.margin2, nq, n_cand, n_pad, k, p.S, p.R, w.buf, w.count, w.thr};
+    ScreenCArgs ca{index, w.qb, w.margin2, nq, n_pad, k, p.R, w.buf, w.count};
     int rc;
-    switch (cap / kWave) {
-      case 16: rc = launch_screen_d<16>(D, sa, nq_pad, st); if (!rc) rc = launch_final<16>(fa, st); break;
-      case 32: rc = launch_screen_d<32>(D, sa, nq_pad, st); if (!rc) rc = launch_final<32>(fa, st); break;
-      case 64: rc = launch_screen_d<64>(D, sa, nq_pad, st); if (!rc) rc = launch_final<64>(fa, st); break;
-      case 128: rc = launch_screen_d<128>(D, sa, nq_pad, st); if (!rc) rc = launch_final<128>(fa, st); break;
-      default: return fail(TT_ERR_UNSUPPORTED, "tt_bruteforce_search: shortlist capacity %d", cap);
+    switch (D) {
+      case 32: rc = launch_screen<32>(p, sa, ca, nq_pad, st); break;
+      case 64: rc = launch_screen<64>(p, sa, ca, nq_pad, st); break;
+      default: rc = launch_screen<128>(p, sa, ca, nq_pad, st); break;
     }
     if (rc) return rc;
+    FinalArgs fa{queries + q0 * ldq, ldq, cand, ldc, n_cand, dim, k, p.S, p.H, p.R, p.L, p.P, vec4, nq,
+                 index_offset, w.margin2, w.buf, w.count, p.bins ? w.thr : nullptr, out_scores + q0 * k,
+                 out_idx + q0 * k};
+    hipLaunchKernelGGL(finalize_kernel, dim3(nq), dim3(kWave), shm, st, fa);
+    TT_CHECK_LAUNCH();
   }
   return TT_OK;
 }

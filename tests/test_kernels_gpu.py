@@ -183,12 +183,44 @@ def _search(cuda, c, q, k, offset=0):
 
 
 @pytest.mark.parametrize("N,Q,E,k", [(5000, 700, 128, 100), (3000, 300, 64, 1000), (777, 65, 16, 1),
-                                     (2048, 256, 128, 10), (300, 33, 100, 300)])
+                                     (2048, 256, 128, 10), (300, 33, 100, 300), (40000, 1000, 128, 100),
+                                     (20000, 300, 128, 128), (20000, 300, 128, 129), (500, 44, 16, 20),
+                                     (1800, 130, 32, 64), (4000, 257, 64, 100)])
 def test_bruteforce_topk_bitexact(cuda, N, Q, E, k):
     rng = np.random.default_rng(N + k)
     c = np.maximum(rng.standard_normal((N, E)), 0).astype(np.float32)
     q = np.maximum(rng.standard_normal((Q, E)), 0).astype(np.float32)
     q[::17] = 0.0  # all-zero queries: every score ties at 0 -> lowest indices
+    s, i = _search(cuda, c, q, k)
+    rs, ri, _ = oracle.bruteforce_topk(q, c, k)
+    assert np.array_equal(i, ri)
+    assert np.array_equal(s, rs)
+
+
+def test_bruteforce_signed_split_candidates(cuda):
+    """Signed Gaussian data (negative scores), few queries -> candidate splits
+    sharing thresholds; duplicated candidate rows create exact ties across
+    splits that must resolve to the lower index."""
+    rng = np.random.default_rng(21)
+    N, Q, E, k = 60000, 300, 64, 50
+    c = rng.standard_normal((N, E)).astype(np.float32)
+    c[45000:45040] = c[100:140]  # same rows in a later split
+    q = rng.standard_normal((Q, E)).astype(np.float32)
+    q[7] = c[120] * 4.0
+    s, i = _search(cuda, c, q, k)
+    rs, ri, _ = oracle.bruteforce_topk(q, c, k)
+    assert np.array_equal(i, ri)
+    assert np.array_equal(s, rs)
+
+
+def test_bruteforce_zero_queries_many_splits(cuda):
+    """All-zero queries against a large candidate set split across workgroups:
+    every score ties at 0, the answer is the lowest k indices."""
+    rng = np.random.default_rng(3)
+    N, Q, E, k = 70000, 64, 128, 100
+    c = np.maximum(rng.standard_normal((N, E)), 0).astype(np.float32)
+    q = np.maximum(rng.standard_normal((Q, E)), 0).astype(np.float32)
+    q[::2] = 0.0
     s, i = _search(cuda, c, q, k)
     rs, ri, _ = oracle.bruteforce_topk(q, c, k)
     assert np.array_equal(i, ri)
