@@ -216,6 +216,61 @@ def time_inbatch_kernel(model, data, device, B: int, reps: int = 20):
     return flops, ms_rows, ms_cols
 
 
+def time_gather(model, data, device, B: int, reps: int = 50):
+    """K2+K3 gather of both towers' inputs for one step's batch in one
+    tt_gather_multi launch (as the train step issues it), HIP events on the
+    launching stream.  Algorithmic bytes per launch:
+    per categorical lookup 4 B id + D_f*4 B row read + D_f*4 B output write;
+    per numeric column 4 B read + 4 B write."""
+    from pkg.modelling import hip_ops
+
+    batch = data.batch(B)
+    launches = []
+    nbytes = 0
+    for tower in (model.query_tower, model.candidate_tower):
+        layer = tower.input_layer
+        segs = []
+        for f in layer.numerical_features:
+            v = batch[f.name].reshape(-1).to(torch.float32).contiguous()
+            segs.append((v, None, len(segs)))
+            nbytes += B * 8
+        for f, off in zip(layer.categorical_features, layer.column_offsets()):
+            w = layer.embedding_layers[f.name].weight
+            segs.append((w, batch[f.name].reshape(-1).to(torch.int32).contiguous(), off))
+            nbytes += B * (4 + 8 * w.shape[1])
+        out = torch.empty(B, layer.output_dim, device=device)
+        launches.append((segs, out))
+    with torch.no_grad():
+        for _ in range(3):
+            hip_ops.gather_multi(launches, B)
+        torch.cuda.synchronize()
+        # reps launches captured in a hipGraph: the replay has no host overhead
+        # between launches, so the events see the kernel, not the Python call.
+        graph = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(graph, stream=side):
+                for _ in range(reps):
+                    hip_ops.gather_multi(launches, B)
+        torch.cuda.current_stream().wait_stream(side)
+        graph.replay()
+        torch.cuda.synchronize()
+        stream = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        graph.replay()
+        e1.record(stream)
+        e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps  # one launch: both towers
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    return {"kernel": "gather_grouped_kernel (tt_gather_multi: query + candidate tower inputs, one launch)",
+            "bound": "hbm",
+            "achieved": gbs, "peak": MI355X_HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / MI355X_HBM_PEAK_GBS,
+            "algorithmic_bytes_per_launch": nbytes, "ms_per_launch": ms,
+            "note": "Zipf ids: popular rows hit L2/Infinity Cache, so the algorithmic rate can exceed HBM"}
+
+
 def time_index(device, n_queries: int, n_cand: int, k: int, E: int = 128, check: int = 512):
     """BASELINE configs[3] shape: relu(N(0,1)) candidates [105542,128], queries
     relu(N(0,1)) with 1% all-zero rows, top-100, one GPU (bounded query count)."""
@@ -234,8 +289,12 @@ def time_index(device, n_queries: int, n_cand: int, k: int, E: int = 128, check:
     s, i = hip_ops.bruteforce_search(image, C, Q, k)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    tf = 2.0 * n_queries * n_cand * E / dt / 1e12
     res = {"queries": n_queries, "candidates": n_cand, "k": k, "dim": E, "seconds": dt,
-           "qps": n_queries / dt, "tflops_scoring": 2.0 * n_queries * n_cand * E / dt / 1e12}
+           "qps": n_queries / dt, "tflops_scoring": tf,
+           "roofline": {"bound": "mfma", "achieved": tf, "peak": MI355X_BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
+                        "frac": tf / MI355X_BF16_DENSE_TFLOPS,
+                        "note": "2*Q*N*E scoring flops over the whole search (screen + exact finalize)"}}
     if check:
         try:
             from oracle import oracle
@@ -338,6 +397,7 @@ def main():
     ms_per_step = dt / args.steps * 1e3
 
     flops, ms_rows, ms_cols = time_inbatch_kernel(model, data, device, B)
+    gather = time_gather(model, data, device, B)
     achieved = flops / (ms_rows * 1e-3) / 1e12
     result = {
         "metric": "positive pairs/sec (train) + index QPS @ Recall@100, 1/2/4/8 MI355X",
@@ -360,7 +420,8 @@ def main():
         },
         "final_loss": loss,
         "roofline": {
-            "kernel": "inbatch_pass_kernel<128,0> (fused rows pass: S=QC^T-logq, online softmax, P.C)",
+            "kernel": "tt_inbatch_xent_rows: bf16 prep + inbatch_pass_kernel<128,0> (S=QC^T-logq, online softmax, "
+                      "P.C) + combine_rows_kernel, timed as one op",
             "bound": "mfma",
             "achieved": achieved,
             "peak": MI355X_BF16_DENSE_TFLOPS,
@@ -371,6 +432,7 @@ def main():
             "ms_per_launch_cols_op": ms_cols,
             "algorithmic_flops_per_launch": flops,
         },
+        "gather_roofline": gather,
     }
     if rank == 0 and ws == 1 and not args.no_index:
         result["index"] = time_index(device, args.index_queries, HM_VOCAB["article_id"], 100)

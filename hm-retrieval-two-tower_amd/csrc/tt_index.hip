@@ -57,12 +57,18 @@ __device__ unsigned long long g_index_stats[4];
 namespace tt {
 namespace {
 
-constexpr int kScreenWaves = 8;
+#ifndef TT_SCREEN_WAVES
+#define TT_SCREEN_WAVES 8
+#endif
+constexpr int kScreenWaves = TT_SCREEN_WAVES;
 constexpr int kScreenThreads = kScreenWaves * kWave;
 constexpr int kQPerWave = 32;
 constexpr int kQPerWG = kScreenWaves * kQPerWave;  // 256 queries
 constexpr int kCTile = 64;                         // candidates per LDS tile
-constexpr int kBins = 64;                          // per lane (128 per query)
+#ifndef TT_BINS
+#define TT_BINS 64
+#endif
+constexpr int kBins = TT_BINS;                     // per lane (128 per query)
 constexpr int kBinsMaxK = 2 * kBins;               // bins path serves k <= 128
 #ifndef TT_LANE_CAP
 #define TT_LANE_CAP 1024
@@ -271,7 +277,7 @@ __global__ void __launch_bounds__(kScreenThreads) screen_bins_kernel(const Scree
   constexpr int TILE_BYTES = kCTile * RB;                 // 16 KiB at D = 128
   constexpr int PIECES = TILE_BYTES / 1024;               // 1 KiB LDS-DMA pieces per tile
   constexpr int PPW = PIECES >= kScreenWaves ? PIECES / kScreenWaves : 1;
-  __shared__ __attribute__((aligned(1024))) char smem[kStages * TILE_BYTES];
+  __shared__ __attribute__((aligned(1024))) char smem[kStages * TILE_BYTES];  // tile ring (LDS-DMA)
   const int tid = threadIdx.x;
   const int wave = tid / kWave;
   const int lane = lane_id();
@@ -402,68 +408,139 @@ __global__ void __launch_bounds__(kScreenThreads) screen_bins_kernel(const Scree
   wait_tiles(min(nv, kStages - 1) - 1);
   __builtin_amdgcn_s_barrier();
 
-  // One 64-candidate tile from LDS stage v % 4 (Q = v & 3 selects the bins):
-  // both 32-candidate blocks are issued to the MFMA pipe before either is
-  // filtered, so the first block's filter overlaps the second's MFMAs.
-  auto tile_body = [&](int v, const int Q) {
-    if (v + kStages - 1 < nv) issue(vtile(v + kStages - 1), (v + kStages - 1) % kStages);
-    const char* B = smem + (v % kStages) * TILE_BYTES;
-    const int64_t cbase = static_cast<int64_t>(vtile(v)) * kCTile;
-    const bool pad = cbase + kCTile > a.n;  // last tile holds zero padding rows
-    const bool scan = v >= pre;
-    f32x16 acc[2];
+  // Software pipeline at 32-candidate block granularity: the 8 MFMAs of a
+  // block are issued with the filter of the previous block (bins, threshold
+  // test, inserts) in their issue gaps.
+  // Tile v: [MFMA(v,0) | filter(v-1,1)] then [MFMA(v,1) | filter(v,0)].
+  // Q = v & 3 selects a tile's bins (static under the unroll by 4).
+  constexpr int PPS = 8 / KS;  // filter pairs per MFMA slot
+  f32x16 accf = {};            // block waiting to be filtered: tile v-1, block 1
+  int64_t cbase_f = 0;         // first candidate of that tile
+  bool scan_f = false;
+
+  auto filter_pair = [&](const f32x16& acc, const int Qb, const int t, const int pr, int64_t cbase, float tins) {
+    const float x = acc[2 * pr], y = acc[2 * pr + 1];
+    const float pm = __builtin_elementwise_maximum(x, y);
+    constexpr int NQ = kBins / 16;  // tile parities with their own bins
+    bins[(Qb % NQ) * 16 + t * 8 + pr] = __builtin_elementwise_maximum(bins[(Qb % NQ) * 16 + t * 8 + pr], pm);
+#ifndef TT_PROBE_LIGHT
+    if (pm > tins) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      acc[t] = f32x16{};
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const int row = 32 * t + l32, ch = 2 * s + h;
-        const int swz = (row * CH / 16) % CH;
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(B + row * RB + ((ch ^ swz) << 4));
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfrag[s], acc[t], 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      if (pad) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (cbase + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h >= a.n) acc[t][r] = -INFINITY;
-      }
-#pragma unroll
-      for (int pr = 0; pr < 8; ++pr) {
-        const float x = acc[t][2 * pr], y = acc[t][2 * pr + 1];
-        const float pm = __builtin_elementwise_maximum(x, y);
-        bins[Q * 16 + t * 8 + pr] = __builtin_elementwise_maximum(bins[Q * 16 + t * 8 + pr], pm);
-        if (scan && pm > thr) {
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const float val = u ? y : x;
-            const int r = 2 * pr + u;
-            if (val > thr) {
-              const unsigned cidx = static_cast<unsigned>(cbase + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h);
-              region[cnt] = make_uint2(__float_as_uint(val), cidx);
-              ++cnt;
-              TT_STAT(0, 1);
-            }
-          }
+      for (int u = 0; u < 2; ++u) {
+        const float val = u ? y : x;
+        const int r = 2 * pr + u;
+        if (val > tins) {
+          const unsigned cidx = static_cast<unsigned>(cbase + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h);
+          region[cnt] = make_uint2(__float_as_uint(val), cidx);
+          ++cnt;
+          TT_STAT(0, 1);
         }
       }
     }
-    const int j = v + 1 - pre;  // main-scan tiles done
-    const bool due = j == 0 || (j >= 2 && (j & (j - 1)) == 0) || (j > 0 && j % 128 == 0) || j == nt;
-    const bool full = __any(cnt > a.R - 2 * 16);
-    if (due || full) refresh(j == 0);
+#endif
+  };
+  auto mask_pad = [&](f32x16& acc, const int t, int64_t cbase) {  // zero padding rows of the last tile
+    if (cbase + kCTile > a.n) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (cbase + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h >= a.n) acc[r] = -INFINITY;
+    }
+  };
+  // after the filter of main-scan tile j-1: refresh on a geometric schedule;
+  // j == 1 (pre > 0) is the first refresh after the warm-up tiles.
+  auto after_filter = [&](int j) {
+    const bool warm = pre > 0 && j == 1;
+    const bool due = warm || (j >= 2 && (j & (j - 1)) == 0) || (j > 0 && j % 128 == 0);
+    const bool full = __any(cnt > a.R - 2 * 32);
+    if (due || full) refresh(warm);
     if (full) self_compact();
-    if (v + 1 < nv) wait_tiles(min(v + kStages - 1, nv - 1) - (v + 1));  // tile v+1 landed
-    __builtin_amdgcn_s_barrier();
   };
 
+  auto tile_body = [&](int v, const int Q) {
+    const int Qp = (Q + 3) & 3;
+    if (v + kStages - 1 < nv) issue(vtile(v + kStages - 1), (v + kStages - 1) % kStages);
+#ifdef TT_PROBE_NOLDS
+    const char* B = smem;  // probe: always the same stage (fragments stay cached)
+#else
+    const char* B = smem + (v % kStages) * TILE_BYTES;
+#endif
+    const int64_t cbase = static_cast<int64_t>(vtile(v)) * kCTile;
+    const bool scan = v >= pre;
+    const bool have_prev = v > 0;
+    const float tins_f = scan_f ? thr : INFINITY;
+    if (have_prev) mask_pad(accf, 1, cbase_f);
+    f32x16 acc0 = {}, acc1 = {};
+    auto block0 = [&](const bool with_filter) {  // block 0 of tile v | filter block 1 of tile v-1
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int row = l32, ch = 2 * s + h;
+        const int swz = (row * CH / 16) % CH;
+#ifdef TT_PROBE_REGA
+        const bf16x8 af = bfrag[(s + 1) % KS];  // probe: no LDS reads
+#else
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(B + row * RB + ((ch ^ swz) << 4));
+#endif
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfrag[s], acc0, 0, 0, 0);
+        if (with_filter) {
+#pragma unroll
+          for (int u = 0; u < PPS; ++u) filter_pair(accf, Qp, 1, s * PPS + u, cbase_f, tins_f);
+        }
+      }
+    };
+    if (have_prev) {
+      block0(true);
+      after_filter(v - pre);
+    } else {
+      block0(false);
+    }
+    mask_pad(acc0, 0, cbase);
+    const float tins = scan ? thr : INFINITY;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {  // block 1 of tile v | filter block 0 of tile v
+      const int row = 32 + l32, ch = 2 * s + h;
+      const int swz = (row * CH / 16) % CH;
+#ifdef TT_PROBE_REGA
+      const bf16x8 af = bfrag[(s + 2) % KS];  // probe: no LDS reads
+#else
+      const bf16x8 af = *reinterpret_cast<const bf16x8*>(B + row * RB + ((ch ^ swz) << 4));
+#endif
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfrag[s], acc1, 0, 0, 0);
+#pragma unroll
+      for (int u = 0; u < PPS; ++u) filter_pair(acc0, Q, 0, s * PPS + u, cbase, tins);
+    }
+    accf = acc1;
+    cbase_f = cbase;
+    scan_f = scan;
+#ifndef TT_PROBE_NOBARRIER
+    if (v + 1 < nv) wait_tiles(min(v + kStages - 1, nv - 1) - (v + 1));  // tile v+1 landed
+    __builtin_amdgcn_s_barrier();
+#endif
+  };
+
+#ifdef TT_PROBE_NOUNROLL
+  for (int v = 0; v < nv; ++v) tile_body(v, 0);  // probe: one code copy (bins aliased)
+#else
   for (int v = 0; v < nv; v += 4) {
     tile_body(v, 0);
     if (v + 1 < nv) tile_body(v + 1, 1);
     if (v + 2 < nv) tile_body(v + 2, 2);
     if (v + 3 < nv) tile_body(v + 3, 3);
+  }
+#endif
+  if (nv > 0) {  // drain: filter the last block, final refresh
+    mask_pad(accf, 1, cbase_f);
+    const int Ql = (nv - 1) & 3;
+    const float tins_f = scan_f ? thr : INFINITY;
+#pragma unroll
+    for (int pr = 0; pr < 8; ++pr) {
+      switch (Ql) {  // static bin index per case
+        case 0: filter_pair(accf, 0, 1, pr, cbase_f, tins_f); break;
+        case 1: filter_pair(accf, 1, 1, pr, cbase_f, tins_f); break;
+        case 2: filter_pair(accf, 2, 1, pr, cbase_f, tins_f); break;
+        default: filter_pair(accf, 3, 1, pr, cbase_f, tins_f); break;
+      }
+    }
+    refresh(false);
   }
   a.count[(qg * a.S + split) * 2 + h] = ovf ? -1 : cnt;
   if (h == 0 && live && gthr > -INFINITY) atomicMax(&a.thr[qg], float_order_key(gthr));
@@ -698,6 +775,7 @@ struct FinalArgs {
   int L;     // LDS list capacity
   int P;     // bitonic sort size (pow2 >= k)
   int vec4;  // candidate rows are 16-byte aligned float4 rows
+  int pairs; // entries are (max of candidates c, c+1; c) pairs (bins path)
   int64_t nq;
   int64_t index_offset;
   const float* margin2;
@@ -861,6 +939,9 @@ __global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
   unsigned* hist = reinterpret_cast<unsigned*>(sk + a.P);  // 256 radix bins
   const int64_t q = blockIdx.x;
   const int lane = lane_id();
+#ifdef TT_INDEX_NOINSERT
+  return;  // probe build: the screen inserted nothing
+#endif
   for (int e = lane; e < a.dim; e += kWave) qs[e] = a.q[q * a.ldq + e];
   const float m2 = a.margin2[q];
   float thr = (a.thr && a.thr[q]) ? order_key_float(a.thr[q]) : -INFINITY;
@@ -917,9 +998,31 @@ __global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
     n = coarse_cut(sc, id, n, a.k, m2, &thr, hist);
     ovf = n < a.k;  // cannot happen with a valid screen; answer exactly regardless
   }
+  if (!ovf && a.pairs) {
+    // expand pair entries into their two candidates (c, c + 1), top chunk first
+    if (2 * n > a.L) {
+      ovf = true;
+    } else {
+      for (int j0 = (n - 1) / kWave * kWave; j0 >= 0; j0 -= kWave) {
+        const int j = j0 + lane;
+        const unsigned c = j < n ? id[j] : 0u;
+        __syncthreads();
+        if (j < n) {
+          id[2 * j] = c;
+          id[2 * j + 1] = c + 1;
+        }
+        __syncthreads();
+      }
+      n *= 2;
+    }
+  }
   if (!ovf) {
-    for (int j = lane; j < n; j += kWave)
-      sc[j] = exact_score(qs, a.cand + static_cast<int64_t>(id[j]) * a.ldc, a.dim, a.vec4 != 0) + 0.0f;
+    for (int j = lane; j < n; j += kWave) {
+      const unsigned c = id[j];
+      sc[j] = c < static_cast<uint64_t>(a.n)
+                  ? exact_score(qs, a.cand + static_cast<int64_t>(c) * a.ldc, a.dim, a.vec4 != 0) + 0.0f
+                  : -INFINITY;  // c + 1 past the last candidate
+    }
     __syncthreads();
   } else {
     // Exact fallback: scan every candidate with the fp32 chain (in index
@@ -994,7 +1097,7 @@ SearchPlan plan_search(int64_t nq, int64_t n_cand, int k) {
     if (p.bins) {  // enough workgroups for the chip: split the candidates of few query blocks
       const int64_t qblocks = ceil_div(p.chunk, kQPerWG);
       p.S = 1;
-      while (p.S < kMaxSplits && qblocks * p.S < 256 && ntiles / (2 * p.S) >= 64) p.S *= 2;
+      while (p.S < kMaxSplits && qblocks * p.S * kScreenWaves < 2048 && ntiles / (2 * p.S) >= 64) p.S *= 2;
 #ifdef TT_FORCE_SPLITS
       p.S = TT_FORCE_SPLITS;
 #endif
@@ -1134,7 +1237,7 @@ extern "C" int tt_bruteforce_search(const void* index, const float* cand, int64_
       default: rc = launch_screen<128>(p, sa, ca, nq_pad, st); break;
     }
     if (rc) return rc;
-    FinalArgs fa{queries + q0 * ldq, ldq, cand, ldc, n_cand, dim, k, p.S, p.H, p.R, p.L, p.P, vec4, nq,
+    FinalArgs fa{queries + q0 * ldq, ldq, cand, ldc, n_cand, dim, k, p.S, p.H, p.R, p.L, p.P, vec4, 0, nq,
                  index_offset, w.margin2, w.buf, w.count, p.bins ? w.thr : nullptr, out_scores + q0 * k,
                  out_idx + q0 * k};
     hipLaunchKernelGGL(finalize_kernel, dim3(nq), dim3(kWave), shm, st, fa);

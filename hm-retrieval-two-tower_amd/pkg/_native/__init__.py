@@ -16,6 +16,7 @@ __all__ = [
     "LIB_PATH",
     "TTError",
     "GatherSegment",
+    "GatherCall",
     "SparseTable",
     "MAX_SEGMENTS",
     "MAX_SOURCES",
@@ -53,6 +54,15 @@ class GatherSegment(ctypes.Structure):
     ]
 
 
+class GatherCall(ctypes.Structure):
+    _fields_ = [
+        ("segs", c_void_p),
+        ("num_segs", c_int32),
+        ("out", c_void_p),
+        ("out_stride", c_int64),
+    ]
+
+
 class SparseTable(ctypes.Structure):
     _fields_ = [
         ("table", c_void_p),
@@ -71,6 +81,7 @@ _PROTOS = {
     "tt_version": (c_char_p, []),
     "tt_last_error": (c_char_p, []),
     "tt_gather_grouped": (c_int32, [POINTER(GatherSegment), c_int32, c_int64, c_void_p, c_int64, c_void_p]),
+    "tt_gather_multi": (c_int32, [POINTER(GatherCall), c_int32, c_int64, c_void_p]),
     "tt_sparse_workspace_size": (c_size_t, [POINTER(SparseTable), c_int32, c_int64]),
     "tt_sparse_adagrad": (
         c_int32,

@@ -80,16 +80,7 @@ class Workspace:
 
 # --------------------------------------------------------------------------
 # K2+K3 gather
-def gather_grouped(
-    segments: Sequence[Tuple[torch.Tensor, Optional[torch.Tensor], int]],
-    batch: int,
-    out: torch.Tensor,
-) -> torch.Tensor:
-    """segments: (table [V,D] or numeric values [B], ids [B] int32 or None, col_offset)."""
-    _req(out, "out", torch.float32, 2)
-    ld = _row_major(out, "out")
-    if len(segments) > _native.MAX_SEGMENTS:
-        raise ValueError(f"at most {_native.MAX_SEGMENTS} segments per launch")
+def _gather_segments(segments, batch: int):
     arr = (GatherSegment * len(segments))()
     for i, (table, ids, off) in enumerate(segments):
         _req(table, f"table[{i}]", torch.float32)
@@ -110,12 +101,42 @@ def gather_grouped(
         arr[i].num_rows = rows
         arr[i].dim = dim
         arr[i].col_offset = off
+    return arr
+
+
+def gather_grouped(
+    segments: Sequence[Tuple[torch.Tensor, Optional[torch.Tensor], int]],
+    batch: int,
+    out: torch.Tensor,
+) -> torch.Tensor:
+    """segments: (table [V,D] or numeric values [B], ids [B] int32 or None, col_offset)."""
+    _req(out, "out", torch.float32, 2)
+    ld = _row_major(out, "out")
+    if len(segments) > _native.MAX_SEGMENTS:
+        raise ValueError(f"at most {_native.MAX_SEGMENTS} segments per launch")
+    arr = _gather_segments(segments, batch)
     check(lib().tt_gather_grouped(arr, len(segments), batch, out.data_ptr(), ld, _stream()))
     return out
 
 
-# --------------------------------------------------------------------------
-# K8+K9 sparse optimizer steps
+def gather_multi(calls: Sequence[Tuple[Sequence[Tuple[torch.Tensor, Optional[torch.Tensor], int]], torch.Tensor]],
+                 batch: int) -> None:
+    """Several gather_grouped calls of one batch (e.g. both towers) in one launch."""
+    if sum(len(segs) for segs, _ in calls) > _native.MAX_SEGMENTS:
+        raise ValueError(f"at most {_native.MAX_SEGMENTS} segments per launch")
+    keep = []
+    arr = (_native.GatherCall * len(calls))()
+    for i, (segs, out) in enumerate(calls):
+        _req(out, f"out[{i}]", torch.float32, 2)
+        ld = _row_major(out, f"out[{i}]")
+        sa = _gather_segments(segs, batch)
+        keep.append(sa)
+        arr[i].segs = ctypes.cast(sa, ctypes.c_void_p)
+        arr[i].num_segs = len(segs)
+        arr[i].out = out.data_ptr()
+        arr[i].out_stride = ld
+    check(lib().tt_gather_multi(arr, len(calls), batch, _stream()))
+
 def _sparse_tables(tables: Sequence[dict], batch: int, adam: bool):
     arr = (SparseTable * len(tables))()
     for i, t in enumerate(tables):

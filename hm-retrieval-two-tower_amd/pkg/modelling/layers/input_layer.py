@@ -60,6 +60,25 @@ class _GatherFn(torch.autograd.Function):
         return None, None, None, None
 
 
+class _MultiGatherFn(torch.autograd.Function):
+    """Several InputLayers of one batch gathered by one tt_gather_multi launch."""
+
+    @staticmethod
+    def forward(ctx, layers, seglists, batch, *anchors):
+        outs = [torch.empty(batch, l.row_stride, dtype=torch.float32, device=l.device) for l in layers]
+        hip_ops.gather_multi(list(zip(seglists, outs)), batch)
+        ctx.layers = layers
+        return tuple(o[:, : l.output_dim] for o, l in zip(outs, layers))
+
+    @staticmethod
+    def backward(ctx, *grads):
+        for layer, g in zip(ctx.layers, grads):
+            if g is not None and g.stride(1) != 1:
+                g = g.contiguous()
+            layer.last_grad = g
+        return (None, None, None) + (None,) * len(ctx.layers)
+
+
 class InputLayer:
     """
     Convert a dict of tensors, embed categorical and concat together
@@ -131,8 +150,7 @@ class InputLayer:
             t = t.to(self.device)
         return t.contiguous()
 
-    def __call__(self, x: Dict[str, torch.Tensor]) -> torch.Tensor:
-        """Pass a dict of [B] or [B,1] tensors; returns [B, output_dim] fp32."""
+    def _segments(self, x: Dict[str, torch.Tensor]):
         segments = []
         batch = None
         for f in self.numerical_features:
@@ -153,7 +171,25 @@ class InputLayer:
             raise ValueError("InputLayer called with no features")
         self._last_calls = ids_by_call
         self.last_grad = None
+        return segments, batch
+
+    def __call__(self, x: Dict[str, torch.Tensor]) -> torch.Tensor:
+        """Pass a dict of [B] or [B,1] tensors; returns [B, output_dim] fp32."""
+        segments, batch = self._segments(x)
         return _GatherFn.apply(self._anchor, self, segments, batch)
+
+    @staticmethod
+    def gather_many(layers: Sequence["InputLayer"], xs: Sequence[Dict[str, torch.Tensor]]) -> List[torch.Tensor]:
+        """The outputs of several InputLayers on one batch from ONE gather launch
+        (the query and candidate towers of a train step)."""
+        prepared = [l._segments(x) for l, x in zip(layers, xs)]
+        batches = {b for _, b in prepared}
+        if len(batches) != 1:
+            raise ValueError(f"gather_many needs one batch size, got {sorted(batches)}")
+        if sum(len(segs) for segs, _ in prepared) > hip_ops._native.MAX_SEGMENTS:
+            return [_GatherFn.apply(l._anchor, l, segs, b) for l, (segs, b) in zip(layers, prepared)]
+        return list(_MultiGatherFn.apply(list(layers), [segs for segs, _ in prepared], batches.pop(),
+                                         *[l._anchor for l in layers]))
 
     def sparse_sources(self) -> List[dict]:
         """Per table: its lookups of the last call as (ids, grad column) sources."""

@@ -24,6 +24,7 @@ from pkg.modelling.device import default_device, make_generator
 from pkg.modelling.layers.logq_correction import LogQCorrection
 from pkg.modelling.losses import InBatchSoftmaxCrossEntropy
 from pkg.modelling.models.abstract_keras_model import AbstractKerasModel, TensorSpec
+from pkg.modelling.layers.input_layer import InputLayer
 from pkg.modelling.models.tower import Tower
 
 logger = logging.getLogger(__name__)
@@ -112,8 +113,9 @@ class TwoTowerModel(AbstractKerasModel):
     def compute_loss(self, x: Dict[str, Any], training: bool = True) -> torch.Tensor:
         q, c = self._split(x)
         with torch.set_grad_enabled(training):
-            qe = self.query_tower.call(q)
-            ce = self.candidate_tower.call(c)
+            qi, ci = InputLayer.gather_many([self.query_tower.input_layer, self.candidate_tower.input_layer], [q, c])
+            qe = self.query_tower.dense(qi)
+            ce = self.candidate_tower.dense(ci)
             return self.loss(qe, ce, self.candidate_logq(x))
 
     def compile(self, loss=None, optimizer=None, **kwargs) -> None:

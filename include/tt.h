@@ -65,6 +65,20 @@ int tt_gather_grouped(const tt_gather_segment* segs, int32_t num_segs,
                       int64_t batch, float* out, int64_t out_stride,
                       tt_stream_t stream);
 
+/* Several InputLayer.call's of one batch (e.g. the query and the candidate
+ * tower, two_tower_model.py:65-92) in ONE launch: call i gathers its
+ * `num_segs` segments into its own `out` [batch, out_stride].  At most
+ * TT_MAX_SEGMENTS segments in total. */
+typedef struct {
+  const tt_gather_segment* segs;
+  int32_t num_segs;
+  float* out;
+  int64_t out_stride;
+} tt_gather_call;
+
+int tt_gather_multi(const tt_gather_call* calls, int32_t num_calls,
+                    int64_t batch, tt_stream_t stream);
+
 /* ------------------------------------------------------------------------ *
  * K8+K9  Sparse optimizer step on embedding tables.
  * Replaces the legacy Keras optimizer's sparse path reached from

@@ -45,6 +45,35 @@ def test_gather_grouped_bitexact(cuda):
     assert np.array_equal(got, ref)
 
 
+def test_gather_multi_matches_single(cuda):
+    """Both towers in one tt_gather_multi launch == two tt_gather_grouped calls
+    (misaligned column after a 2-wide segment exercises the split stores)."""
+    g = torch.Generator(device="cpu").manual_seed(4)
+    B = 1000
+    ta = torch.rand(5000, 128, generator=g).to(cuda)
+    tb = torch.rand(7, 2, generator=g).to(cuda)
+    tc = torch.rand(300, 128, generator=g).to(cuda)
+    td = torch.rand(40, 4, generator=g).to(cuda)
+    ids = lambda n: torch.randint(-2, n + 2, (B,), generator=g, dtype=torch.int32).to(cuda)
+    ia, ib, ic, id_ = ids(5000), ids(7), ids(300), ids(40)
+    segs1 = [(ta, ia, 0), (tb, ib, 128), (tc, ic, 130)]
+    segs2 = [(td, id_, 0), (td, id_, 4), (ta, ia, 8)]
+    o1 = torch.full((B, 260), 7.0, device=cuda)
+    o2 = torch.full((B, 136), 7.0, device=cuda)
+    hip_ops.gather_multi([(segs1, o1), (segs2, o2)], B)
+    r1 = torch.full((B, 260), 7.0, device=cuda)
+    r2 = torch.full((B, 136), 7.0, device=cuda)
+    hip_ops.gather_grouped(segs1, B, r1)
+    hip_ops.gather_grouped(segs2, B, r2)
+    assert torch.equal(o1, r1) and torch.equal(o2, r2)
+    ref = torch.zeros(B, 258)
+    for t, i, off in segs1:
+        ii = i.cpu().long()
+        ok = (ii >= 0) & (ii < t.shape[0])
+        ref[ok, off:off + t.shape[1]] = t.cpu()[ii[ok]]
+    assert torch.equal(o1[:, :258].cpu(), ref)
+
+
 # --------------------------------------------------------------------------- dedup / adagrad
 @pytest.mark.parametrize("n,vocab,dim", [(1, 5, 4), (777, 50, 16), (16384, 105542, 128), (4096, 3, 2)])
 def test_dedup_sum_bitexact(cuda, n, vocab, dim):

@@ -23,7 +23,7 @@ __global__ void fill_relu(float* x, int64_t n, unsigned long long seed, int zero
 int main(int argc, char** argv) {
   const int64_t nq = argc > 1 ? atoll(argv[1]) : 65536;
   const int64_t nc = argc > 2 ? atoll(argv[2]) : 105542;
-  const int dim = 128, k = 100;
+  const int dim = 128, k = argc > 3 ? atoi(argv[3]) : 100;
   float *C, *Q, *S;
   int32_t* I;
   hipMalloc(&C, nc * dim * 4);
