@@ -93,7 +93,9 @@ def zipf_probs(n: int, a: float) -> np.ndarray:
 class SyntheticHM:
     """Device-resident synthetic batches with H&M shapes (seeded)."""
 
-    def __init__(self, device, seed: int = 0):
+    def __init__(self, device, seed: int = 0, stream: int = 0):
+        """seed fixes the catalogue (popularity, attributes, logQ); stream picks
+        the sample sequence (one per data-parallel rank)."""
         rng = np.random.default_rng(seed)
         self.device = device
         V = HM_VOCAB
@@ -112,7 +114,7 @@ class SyntheticHM:
         self.art_perm_t = torch.as_tensor(self.art_perm, device=device, dtype=torch.int32)
         self.cust_perm_t = torch.as_tensor(self.cust_perm, device=device, dtype=torch.int32)
         self.gen = torch.Generator(device=device)
-        self.gen.manual_seed(seed + 1)
+        self.gen.manual_seed(seed + 1 + 7919 * stream)
 
     def prob_lookup(self):
         """candidate_prob_lookup: article row -> p (str keys, as the ETL writes)."""
@@ -143,10 +145,10 @@ def dist_env():
 def time_train(args, device, ws, rank):
     from pkg.modelling.models.two_tower_model import GraphedTrainStep, TwoTowerModel
     from pkg.modelling.optimizer_factory import OptimizerFactory
-    from pkg.modelling.distributed import DataParallelTrainStep
+    from pkg.modelling.distributed import ShardedTrainStep
 
     schema = main_schema()
-    data = SyntheticHM(device, seed=1234 + rank)
+    data = SyntheticHM(device, seed=1234, stream=rank)
     schema.set_candidate_prob_lookup(data.prob_lookup())
     model = TwoTowerModel.create_from_schema(schema, "article_id", device=device, seed=0)
     model.compile(optimizer=OptimizerFactory.get_optimizer("adagrad", {"learning_rate": 0.05}))
@@ -154,7 +156,8 @@ def time_train(args, device, ws, rank):
     pool = [data.batch(B) for _ in range(4)]
     torch.cuda.synchronize()
     if ws > 1:
-        step = DataParallelTrainStep(model, pool[0])
+        # large tables (customer, postal, article) row-sharded over the ranks
+        step = ShardedTrainStep(model, shard_min_rows=100_000)
         run = lambda i: step(pool[i % len(pool)])
     else:
         step = GraphedTrainStep(model, pool[0], warmup=2)
@@ -414,7 +417,9 @@ def main():
         "data": "synthetic (H&M-shaped ids, Zipf; random-init weights)",
         "config": {
             "workload": "C3: main.py schema @ emb 128, towers [256]->128, logQ in-batch softmax, Adagrad, batch 16384"
-                        + (" per replica, per-replica in-batch negatives" if ws > 1 else ""),
+                        + (" per replica, per-replica in-batch negatives; customer/postal/article tables row-sharded "
+                           "over the ranks (all_to_all), small tables and MLP replicated (all_reduce)"
+                           if ws > 1 else ""),
             "global_batch": ws * B,
             "parallelism": f"dp{ws}",
         },

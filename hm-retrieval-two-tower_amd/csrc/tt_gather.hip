@@ -144,6 +144,34 @@ int pick_vec(const tt_gather_segment& s, const float* out, int64_t out_stride, i
   return 1;
 }
 
+constexpr int kMaxTagged = 16;
+struct TaggedArgs {
+  const float* table[kMaxTagged];
+  int64_t num_rows[kMaxTagged];
+  int32_t num_tables;
+  int32_t dim;
+  const int32_t* tags;
+  const int32_t* rows;
+  int64_t n;
+  float* out;
+  int64_t out_stride;
+};
+
+// One (sub-)wave of dim/4 lanes per request row, float4 moves.
+__global__ void __launch_bounds__(256) gather_tagged_kernel(const TaggedArgs a) {
+  const int tpr = a.dim / 4;
+  const int rpb = 256 / tpr;
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * rpb + threadIdx.x / tpr;
+  const int lane = threadIdx.x % tpr;
+  if (j >= a.n || threadIdx.x / tpr >= rpb) return;
+  const int t = a.tags[j];
+  const int64_t r = a.rows[j];
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (t >= 0 && t < a.num_tables && r >= 0 && r < a.num_rows[t])
+    v = reinterpret_cast<const float4*>(a.table[t] + r * a.dim)[lane];
+  reinterpret_cast<float4*>(a.out + j * a.out_stride)[lane] = v;
+}
+
 int add_call(GatherArgs& a, int32_t& blocks, const tt_gather_segment* segs, int32_t num_segs, float* out,
              int64_t out_stride) {
   TT_REQUIRE(segs != nullptr, "tt_gather: segs is NULL");
@@ -225,4 +253,37 @@ extern "C" int tt_gather_multi(const tt_gather_call* calls, int32_t num_calls, i
     if (rc) return rc;
   }
   return launch(a, blocks, stream);
+}
+
+extern "C" int tt_gather_tagged(const tt_row_table* tables, int32_t num_tables, int32_t dim, const int32_t* tags,
+                                const int32_t* rows, int64_t n, float* out, int64_t out_stride,
+                                tt_stream_t stream) {
+  using namespace tt;
+  clear_error();
+  TT_REQUIRE(tables && num_tables >= 1 && num_tables <= kMaxTagged, "tt_gather_tagged: 1..%d tables", kMaxTagged);
+  TT_REQUIRE(dim >= 4 && dim % 4 == 0 && dim <= 1024, "tt_gather_tagged: dim=%d must be a multiple of 4 in [4,1024]",
+             dim);
+  TT_REQUIRE(n >= 0, "tt_gather_tagged: negative n");
+  if (n == 0) return TT_OK;
+  TT_REQUIRE(tags && rows && out, "tt_gather_tagged: NULL pointer");
+  TT_REQUIRE(out_stride >= dim && out_stride % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0,
+             "tt_gather_tagged: out must be 16-byte aligned rows");
+  TaggedArgs a{};
+  for (int i = 0; i < num_tables; ++i) {
+    TT_REQUIRE(tables[i].table && reinterpret_cast<uintptr_t>(tables[i].table) % 16 == 0,
+               "tt_gather_tagged: table %d must be 16-byte aligned", i);
+    a.table[i] = tables[i].table;
+    a.num_rows[i] = tables[i].num_rows;
+  }
+  a.num_tables = num_tables;
+  a.dim = dim;
+  a.tags = tags;
+  a.rows = rows;
+  a.n = n;
+  a.out = out;
+  a.out_stride = out_stride;
+  const int rpb = 256 / (dim / 4);
+  hipLaunchKernelGGL(gather_tagged_kernel, dim3(ceil_div(n, rpb)), dim3(256), 0, to_stream(stream), a);
+  TT_CHECK_LAUNCH();
+  return TT_OK;
 }

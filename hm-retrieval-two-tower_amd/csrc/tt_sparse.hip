@@ -86,7 +86,7 @@ struct Job {
   int32_t dense_dim;
 };
 
-enum ApplyOp { kWriteSum = 0, kAdagrad = 1, kAdamScatter = 2 };
+enum ApplyOp { kWriteSum = 0, kAdagrad = 1, kAdamScatter = 2, kScatterSum = 3 };
 
 struct ApplyParams {
   float lr;
@@ -154,6 +154,8 @@ __device__ __forceinline__ void store_row(const TableDesc& T, const ApplyParams&
   } else if (OP == kAdamScatter) {  // scatter-add of the scaled distinct-id gradient into the decayed slots
     T.slot0[o] = ieee_op<'+'>(r.x0, ieee_op<'*'>(g, ap.one_minus_beta1));
     T.slot1[o] = ieee_op<'+'>(r.x1, ieee_op<'*'>(ieee_op<'*'>(g, g), ap.one_minus_beta2));
+  } else if (OP == kScatterSum) {  // dense per-row gradient: each distinct row written once
+    T.table[o] = g;
   }
 }
 
@@ -443,13 +445,14 @@ PlanWs carve_plan(Carver& cv, const Plan& p, int dense_dim) {
   return w;
 }
 
-int validate_tables(const tt_sparse_table* tables, int32_t num_tables, int64_t batch, bool adam) {
+int validate_tables(const tt_sparse_table* tables, int32_t num_tables, int64_t batch, bool adam,
+                    bool need_slot0 = true) {
   TT_REQUIRE(tables != nullptr && num_tables >= 1, "sparse: no tables");
   TT_REQUIRE(batch >= 0, "sparse: negative batch");
   int64_t total = 0;
   for (int i = 0; i < num_tables; ++i) {
     const tt_sparse_table& t = tables[i];
-    TT_REQUIRE(t.table && t.slot0, "sparse: table %d has NULL parameter/slot pointer", i);
+    TT_REQUIRE(t.table && (t.slot0 || !need_slot0), "sparse: table %d has NULL parameter/slot pointer", i);
     TT_REQUIRE(!adam || t.slot1, "sparse: table %d needs slot1 for Adam", i);
     TT_REQUIRE(t.num_rows >= 1 && t.num_rows < (int64_t(1) << 30), "sparse: table %d num_rows out of range", i);
     TT_REQUIRE(t.dim >= 1 && t.dim <= 4096, "sparse: table %d dim=%d out of range", i, t.dim);
@@ -691,4 +694,20 @@ extern "C" int tt_dense_adam(float* param, float* m, float* v, const float* grad
                      alpha, 1.0f - beta1, 1.0f - beta2, epsilon);
   TT_CHECK_LAUNCH();
   return TT_OK;
+}
+
+extern "C" int tt_sparse_scatter_sum(const tt_sparse_table* tables, int32_t num_tables, int64_t batch,
+                                     const float* grad, int64_t grad_stride, void* workspace,
+                                     size_t workspace_bytes, tt_stream_t stream) {
+  clear_error();
+  int rc = validate_tables(tables, num_tables, batch, false, false);
+  if (rc) return rc;
+  if (batch == 0) return TT_OK;
+  TT_REQUIRE(grad != nullptr, "tt_sparse_scatter_sum: grad is NULL");
+  const size_t need = tables_ws_bytes(tables, num_tables, batch, 0);
+  if (!workspace || workspace_bytes < need)
+    return fail(TT_ERR_WORKSPACE, "tt_sparse_scatter_sum: workspace %zu < required %zu", workspace_bytes, need);
+  ApplyParams ap{};
+  return run_sparse<kScatterSum>(tables, num_tables, batch, grad, grad_stride, ap, workspace, workspace_bytes,
+                                 to_stream(stream));
 }

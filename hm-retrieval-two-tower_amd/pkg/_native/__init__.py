@@ -17,6 +17,7 @@ __all__ = [
     "TTError",
     "GatherSegment",
     "GatherCall",
+    "RowTable",
     "SparseTable",
     "MAX_SEGMENTS",
     "MAX_SOURCES",
@@ -63,6 +64,13 @@ class GatherCall(ctypes.Structure):
     ]
 
 
+class RowTable(ctypes.Structure):
+    _fields_ = [
+        ("table", c_void_p),
+        ("num_rows", c_int64),
+    ]
+
+
 class SparseTable(ctypes.Structure):
     _fields_ = [
         ("table", c_void_p),
@@ -82,6 +90,8 @@ _PROTOS = {
     "tt_last_error": (c_char_p, []),
     "tt_gather_grouped": (c_int32, [POINTER(GatherSegment), c_int32, c_int64, c_void_p, c_int64, c_void_p]),
     "tt_gather_multi": (c_int32, [POINTER(GatherCall), c_int32, c_int64, c_void_p]),
+    "tt_gather_tagged": (c_int32, [POINTER(RowTable), c_int32, c_int32, c_void_p, c_void_p, c_int64, c_void_p, c_int64,
+                                   c_void_p]),
     "tt_sparse_workspace_size": (c_size_t, [POINTER(SparseTable), c_int32, c_int64]),
     "tt_sparse_adagrad": (
         c_int32,
@@ -92,6 +102,8 @@ _PROTOS = {
         [POINTER(SparseTable), c_int32, c_int64, c_void_p, c_int64, c_float, c_float, c_float, c_float, c_int64,
          c_void_p, c_size_t, c_void_p],
     ),
+    "tt_sparse_scatter_sum": (
+        c_int32, [POINTER(SparseTable), c_int32, c_int64, c_void_p, c_int64, c_void_p, c_size_t, c_void_p]),
     "tt_dedup_workspace_size": (c_size_t, [c_int64, c_int32]),
     "tt_dedup_sum": (
         c_int32,

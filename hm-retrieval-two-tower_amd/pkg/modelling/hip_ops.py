@@ -137,14 +137,18 @@ def gather_multi(calls: Sequence[Tuple[Sequence[Tuple[torch.Tensor, Optional[tor
         arr[i].out_stride = ld
     check(lib().tt_gather_multi(arr, len(calls), batch, _stream()))
 
-def _sparse_tables(tables: Sequence[dict], batch: int, adam: bool):
+def _sparse_tables(tables: Sequence[dict], batch: int, adam: bool, slots: bool = True):
     arr = (SparseTable * len(tables))()
     for i, t in enumerate(tables):
-        table, slot0 = t["table"], t["slot0"]
+        table = t["table"]
         _req(table, f"table[{i}]", torch.float32, 2)
-        _req(slot0, f"slot0[{i}]", torch.float32, 2)
-        if not (table.is_contiguous() and slot0.is_contiguous()) or slot0.shape != table.shape:
-            raise ValueError(f"table/slot0[{i}] must be contiguous and of equal shape")
+        slot0 = t["slot0"] if slots else None
+        if not table.is_contiguous():
+            raise ValueError(f"table[{i}] must be contiguous")
+        if slots:
+            _req(slot0, f"slot0[{i}]", torch.float32, 2)
+            if not slot0.is_contiguous() or slot0.shape != table.shape:
+                raise ValueError(f"table/slot0[{i}] must be contiguous and of equal shape")
         if adam:
             slot1 = t["slot1"]
             _req(slot1, f"slot1[{i}]", torch.float32, 2)
@@ -155,7 +159,7 @@ def _sparse_tables(tables: Sequence[dict], batch: int, adam: bool):
         if not (1 <= len(ids) <= _native.MAX_SOURCES) or len(ids) != len(offs):
             raise ValueError(f"table[{i}]: 1..{_native.MAX_SOURCES} (ids, col_offset) sources required")
         arr[i].table = table.data_ptr()
-        arr[i].slot0 = slot0.data_ptr()
+        arr[i].slot0 = slot0.data_ptr() if slots else None
         arr[i].slot1 = t["slot1"].data_ptr() if adam else None
         arr[i].num_rows = table.shape[0]
         arr[i].dim = table.shape[1]
@@ -191,6 +195,43 @@ def sparse_adam(tables: Sequence[dict], batch: int, grad: torch.Tensor, lr: floa
     ws = Workspace.get(need, grad.device, "sparse")
     check(L.tt_sparse_adam(arr, len(tables), batch, grad.data_ptr(), ld, lr, beta1, beta2, epsilon, step,
                            ws.data_ptr(), ws.numel(), _stream()))
+
+
+def sparse_scatter_sum(tables: Sequence[dict], batch: int, grad: torch.Tensor) -> None:
+    """tables: dicts with table (zero-filled dense gradient [rows, dim]), ids
+    [list], grad_col_offset [list]; every touched row receives its
+    duplicate-summed gradient (tt_sparse_scatter_sum)."""
+    _req(grad, "grad", torch.float32, 2)
+    ld = _row_major(grad, "grad")
+    arr = _sparse_tables(tables, batch, adam=False, slots=False)
+    L = lib()
+    need = L.tt_sparse_workspace_size(arr, len(tables), batch)
+    ws = Workspace.get(need, grad.device, "sparse")
+    check(L.tt_sparse_scatter_sum(arr, len(tables), batch, grad.data_ptr(), ld, ws.data_ptr(), ws.numel(),
+                                  _stream()))
+
+
+def gather_tagged(tables: Sequence[torch.Tensor], tags: torch.Tensor, rows: torch.Tensor,
+                  out: torch.Tensor) -> torch.Tensor:
+    """out[j] = tables[tags[j]][rows[j]] (zero row when invalid); tables share dim."""
+    _req(tags, "tags", torch.int32, 1)
+    _req(rows, "rows", torch.int32, 1)
+    _req(out, "out", torch.float32, 2)
+    ld = _row_major(out, "out")
+    dim = tables[0].shape[1]
+    arr = (_native.RowTable * len(tables))()
+    for i, t in enumerate(tables):
+        _req(t, f"tables[{i}]", torch.float32, 2)
+        if t.shape[1] != dim or not t.is_contiguous():
+            raise ValueError("tables must be contiguous and share one dim")
+        arr[i].table = t.data_ptr()
+        arr[i].num_rows = t.shape[0]
+    n = tags.numel()
+    if rows.numel() != n or out.shape[0] < n or out.shape[1] < dim:
+        raise ValueError("tags/rows/out sizes disagree")
+    check(lib().tt_gather_tagged(arr, len(tables), dim, tags.data_ptr(), rows.data_ptr(), n, out.data_ptr(), ld,
+                                 _stream()))
+    return out
 
 
 def dedup_sum(ids: torch.Tensor, grad: torch.Tensor, num_rows: int) -> Tuple[torch.Tensor, torch.Tensor]:

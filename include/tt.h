@@ -79,6 +79,19 @@ typedef struct {
 int tt_gather_multi(const tt_gather_call* calls, int32_t num_calls,
                     int64_t batch, tt_stream_t stream);
 
+/* Row-sharded tables (data parallel / SURVEY C5): the owner of a shard
+ * answers row requests from every rank in one launch.  Request j reads row
+ * rows[j] of tables[tags[j]] into out[j, 0:dim] (zeros for an invalid tag or
+ * row).  All tables must share `dim`. */
+typedef struct {
+  const float* table;  /* [num_rows, dim] fp32 */
+  int64_t num_rows;
+} tt_row_table;
+
+int tt_gather_tagged(const tt_row_table* tables, int32_t num_tables, int32_t dim,
+                     const int32_t* tags, const int32_t* rows, int64_t n,
+                     float* out, int64_t out_stride, tt_stream_t stream);
+
 /* ------------------------------------------------------------------------ *
  * K8+K9  Sparse optimizer step on embedding tables.
  * Replaces the legacy Keras optimizer's sparse path reached from
@@ -124,6 +137,16 @@ int tt_sparse_adam(const tt_sparse_table* tables, int32_t num_tables,
                    float lr, float beta1, float beta2, float epsilon,
                    int64_t step, void* workspace, size_t workspace_bytes,
                    tt_stream_t stream);
+
+/* Dense gradient of each table from its lookups: every touched row of
+ * `table` (a zero-filled [num_rows, dim] gradient buffer; slots unused) is
+ * set to its duplicate-summed gradient, in the same summation order as
+ * tt_sparse_adagrad.  Used by data-parallel training to all-reduce the
+ * gradients of small replicated tables. */
+int tt_sparse_scatter_sum(const tt_sparse_table* tables, int32_t num_tables,
+                          int64_t batch, const float* grad, int64_t grad_stride,
+                          void* workspace, size_t workspace_bytes,
+                          tt_stream_t stream);
 
 /* Dedup only (K8), for parity checks: writes the U distinct ids of
  * ids[0..n) in ascending order, the per-id gradient sums [U, dim] (rows of

@@ -129,3 +129,114 @@ def test_dp_collectives_sum_dense_and_concat_sparse_rank_major():
             assert calls[2][1].tolist() == [100] * 4 + [101] * 4
             assert [c[2] for c in calls] == [0, 3, 5]
             assert grad.shape == (8, 6) and grad[0, 0] == 10 * t and grad[4, 0] == 1 + 10 * t
+
+
+# --------------------------------------------------------------------------- row-sharded tables (C5)
+def _cpu_embedding_ops():
+    """CPU restatement of the libtt kernels the sharded path calls (test-only)."""
+    from pkg.modelling.distributed import EmbeddingOps
+
+    def gather_multi(calls, batch):
+        for segs, out in calls:
+            for table, ids, off in segs:
+                if ids is None:
+                    out[:, off] = table
+                    continue
+                d = table.shape[1]
+                ii = ids.long()
+                ok = (ii >= 0) & (ii < table.shape[0])
+                rows = torch.zeros(batch, d)
+                rows[ok] = table[ii[ok]]
+                out[:, off:off + d] = rows
+
+    def gather_tagged(tables, tags, rows, out):
+        out.zero_()
+        for j in range(tags.numel()):
+            t, r = int(tags[j]), int(rows[j])
+            if 0 <= t < len(tables) and 0 <= r < tables[t].shape[0]:
+                out[j, :tables[t].shape[1]] = tables[t][r]
+        return out
+
+    def scatter_sum(specs, batch, grad):
+        for s in specs:
+            tab = s["table"]
+            d = tab.shape[1]
+            acc = torch.zeros_like(tab, dtype=torch.float64)
+            touched = torch.zeros(tab.shape[0], dtype=torch.bool)
+            for ids, off in zip(s["ids"], s["grad_col_offset"]):
+                ii = ids.long()
+                ok = (ii >= 0) & (ii < tab.shape[0])
+                acc.index_add_(0, ii[ok], grad[ok, off:off + d].double())
+                touched[ii[ok]] = True
+            tab[touched] = acc[touched].float()
+
+    def sparse_adagrad(specs, batch, grad, lr, eps):
+        for s in specs:
+            tab, accum = s["table"], s["slot0"]
+            d = tab.shape[1]
+            g = torch.zeros_like(tab, dtype=torch.float64)
+            touched = torch.zeros(tab.shape[0], dtype=torch.bool)
+            for ids, off in zip(s["ids"], s["grad_col_offset"]):
+                ii = ids.long()
+                ok = (ii >= 0) & (ii < tab.shape[0])
+                g.index_add_(0, ii[ok], grad[ok, off:off + d].double())
+                touched[ii[ok]] = True
+            gt = g[touched]
+            a = accum[touched].double() + gt * gt
+            accum[touched] = a.float()
+            tab[touched] = (tab[touched].double() - lr * gt / (a.sqrt() + eps)).float()
+
+    def dense_adagrad(p, acc, g, lr, eps):
+        a = acc.double() + g.double() ** 2
+        acc.copy_(a.float())
+        p.copy_((p.double() - lr * g.double() / (a.sqrt() + eps)).float())
+
+    return EmbeddingOps(gather_multi, gather_tagged, scatter_sum, sparse_adagrad, dense_adagrad)
+
+
+def _sharded_worker(rank, world, port, tables, lookups, grads, out):
+    _init(rank, world, port)
+    from pkg.modelling.distributed import ShardedTables
+
+    st = ShardedTables({k: torch.from_numpy(v) for k, v in tables.items()}, 0.1, ops=_cpu_embedding_ops())
+    lk = [(name, torch.from_numpy(ids[rank])) for name, ids in lookups]
+    got, idx = st.fetch(lk)
+    fwd = [got[i.long()].numpy() for i in idx]
+    # gradient matrix of this rank: one [B, 16 * L] block, lookup l at column 16 l
+    g = torch.from_numpy(grads[rank])
+    st.apply([(g, [(idx[l], 16 * l) for l in range(len(lk))])], lr=0.05, eps=1e-7)
+    out[rank] = (fwd, {k: st.gather_full(k).numpy() for k in tables})
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_tables_match_unsharded_adagrad(world):
+    rng = np.random.default_rng(1)
+    B, D = 40, 16
+    tables = {"cust": rng.uniform(-0.05, 0.05, (97, D)).astype(np.float32),
+              "art": rng.uniform(-0.05, 0.05, (31, D)).astype(np.float32)}
+    # per rank ids (with duplicates, out-of-range ids and one table looked up twice)
+    ids = lambda n: rng.integers(-2, n + 3, (world, B)).astype(np.int32)
+    lookups = [("cust", ids(97)), ("art", ids(31)), ("cust", ids(97))]
+    grads = rng.standard_normal((world, B, 16 * len(lookups))).astype(np.float32)
+    out = mp.Manager().dict()
+    mp.spawn(_sharded_worker, args=(world, _free_port(), tables, lookups, grads, out), nprocs=world, join=True)
+    # reference: unsharded tables, global batch = all ranks' lookups, one Adagrad step
+    ref = {k: v.astype(np.float64) for k, v in tables.items()}
+    acc = {k: np.full_like(v, 0.1) for k, v in ref.items()}
+    gsum = {k: np.zeros_like(v) for k, v in ref.items()}
+    for r in range(world):
+        for l, (name, idsl) in enumerate(lookups):
+            ok = (idsl[r] >= 0) & (idsl[r] < tables[name].shape[0])
+            # forward rows equal the unsharded gather (zeros for invalid ids)
+            exp = np.zeros((B, D), np.float32)
+            exp[ok] = tables[name][idsl[r][ok]]
+            assert np.array_equal(out[r][0][l], exp)
+            np.add.at(gsum[name], idsl[r][ok], grads[r][ok, 16 * l:16 * l + D])
+    for k in ref:
+        touched = np.abs(gsum[k]).sum(1) > 0
+        a = acc[k] + gsum[k] ** 2
+        upd = ref[k] - 0.05 * gsum[k] / (np.sqrt(a) + 1e-7)
+        ref[k] = np.where(touched[:, None], upd, ref[k])
+        for r in range(world):
+            np.testing.assert_allclose(out[r][1][k], ref[k], rtol=0, atol=2e-6)

@@ -238,3 +238,38 @@ def test_modelling_runner_end_to_end(cuda, tmp_path):
     assert os.path.exists(f"{d}/model/two_tower.pt") and os.path.exists(f"{d}/index/i.pt")
     sd = torch.load(f"{d}/model/two_tower.pt", weights_only=True)
     assert "query_tower.dense.flat" in sd
+
+
+def test_sharded_train_step_world1_matches_single_gpu(cuda):
+    """ShardedTrainStep on a 1-rank RCCL group (large tables sharded, small
+    ones replicated with dense all-reduced gradients) is bit-identical to the
+    single-GPU train step: same summation orders, same Adagrad arithmetic."""
+    import socket
+
+    import torch.distributed as dist
+    from pkg.modelling.distributed import ShardedTrainStep
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device(cuda))
+    try:
+        a, b = _small_model(cuda, seed=3), _small_model(cuda, seed=3)
+        step = ShardedTrainStep(a, shard_min_rows=300)
+        assert step.tables is not None and len(step.tables.names) == 2
+        rng = np.random.default_rng(7)
+        for _ in range(3):
+            batch = _batch(cuda, rng, 256)
+            la = step(batch)["loss"]
+            lb = b.train_step(batch)["loss"]
+            assert torch.equal(la, lb)
+        for ta, tb in zip(a.towers, b.towers):
+            assert torch.equal(ta.dense.flat, tb.dense.flat)
+            for name, t in tb.input_layer.embedding_layers.items():
+                mine = ta.input_layer.embedding_layers[name]
+                full = step.tables.gather_full(mine._shard_key) if hasattr(mine, "_shard_key") else mine.weight
+                assert torch.equal(full, t.weight), name
+    finally:
+        dist.destroy_process_group()
