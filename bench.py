@@ -219,6 +219,23 @@ def time_inbatch_kernel(model, data, device, B: int, reps: int = 20):
     return flops, ms_rows, ms_cols
 
 
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
+    summary (profiles/*_pmc_traffic.json: separate FETCH_SIZE / WRITE_SIZE
+    passes, gfx950 FETCH_SIZE doubled); None if no summary is present."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    for k, v in d.items():
+        if kernel in k and isinstance(v, dict):
+            return {"bytes_per_launch": v["hbm_bytes_per_launch"], "source": os.path.relpath(files[-1], ROOT)}
+    return None
+
+
 def time_gather(model, data, device, B: int, reps: int = 50):
     """K2+K3 gather of both towers' inputs for one step's batch in one
     tt_gather_multi launch (as the train step issues it), HIP events on the
@@ -271,6 +288,7 @@ def time_gather(model, data, device, B: int, reps: int = 50):
             "bound": "hbm",
             "achieved": gbs, "peak": MI355X_HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / MI355X_HBM_PEAK_GBS,
             "algorithmic_bytes_per_launch": nbytes, "ms_per_launch": ms,
+            "traffic": pmc_traffic("gather_grouped_kernel"),
             "note": "Zipf ids: popular rows hit L2/Infinity Cache, so the algorithmic rate can exceed HBM"}
 
 
@@ -432,7 +450,7 @@ def main():
             "peak": MI355X_BF16_DENSE_TFLOPS,
             "unit": "TFLOP/s",
             "frac": achieved / MI355X_BF16_DENSE_TFLOPS,
-            "traffic": None,
+            "traffic": pmc_traffic("inbatch_pass_kernel"),
             "ms_per_launch_rows_op": ms_rows,
             "ms_per_launch_cols_op": ms_cols,
             "algorithmic_flops_per_launch": flops,
