@@ -397,9 +397,14 @@ int pick_dpad(int dim) {
   return 0;
 }
 
+#ifndef TT_INBATCH_WG_TARGET
+#define TT_INBATCH_WG_TARGET 256
+#endif
+// Splits of the streamed extent so that the grid has >= TT_INBATCH_WG_TARGET
+// workgroups (several per CU: two waves per SIMD hide each other's softmax).
 int pick_split(int64_t n_stat_pad, int64_t n_strm_pad) {
   const int64_t wgs = n_stat_pad / kRowsPerWG;
-  int64_t s = ceil_div(256, wgs);
+  int64_t s = ceil_div(TT_INBATCH_WG_TARGET, wgs);
   const int64_t tiles = n_strm_pad / kTile;
   if (s > tiles) s = tiles;
   if (s > kMaxSplit) s = kMaxSplit;
