@@ -22,7 +22,7 @@
 //
 // Wave layout (32x32x16 bf16 MFMA, 64-wide wave): a wave owns 32 stationary
 // rows whose bf16 fragments stay in VGPRs for the whole pass (B operand).
-// Streamed rows arrive in 64-row tiles through double-buffered LDS
+// Streamed rows arrive in 64-row tiles through a 4-stage LDS-DMA ring
 // (XOR-swizzled so every ds_read_b128 fragment read is bank-conflict free):
 //   S^T tile [32 streamed x 32 stationary] = A(streamed rows) . B(stationary)
 // so each lane holds 16 scores of ONE stationary row; the per-row bias
@@ -47,6 +47,7 @@ constexpr int kRowsPerWave = 32;
 constexpr int kRowsPerWG = kWavesPerWG * kRowsPerWave;  // stationary rows per WG
 constexpr int kTile = 64;                                // streamed rows per LDS tile
 constexpr int kMaxSplit = 16;
+constexpr int kRingStages = 4;                           // LDS tile ring depth
 constexpr float kLog2e = 1.4426950408889634f;
 
 template <int D>
@@ -56,10 +57,9 @@ struct Geo {
   static constexpr int CH = D / 8;            // 16-byte chunks per bf16 row
   static constexpr int A_BYTES = kTile * D * 2;   // streamed rows, row-major
   static constexpr int T_BYTES = D * kTile * 2;   // transposed image [D][64]
-  static constexpr int BIAS_BYTES = kTile * 4;
-  static constexpr int BUF_BYTES = A_BYTES + T_BYTES + BIAS_BYTES;
-  static constexpr int A_CHUNKS_PER_THREAD = kTile * CH / kThreads;  // D/32
-  static constexpr int T_CHUNKS_PER_THREAD = D * 8 / kThreads;       // D/32
+  static constexpr int STAGE_BYTES = A_BYTES + T_BYTES + kTile * 4;  // + 64 biases
+  static constexpr int LDS_BYTES = kRingStages * STAGE_BYTES;
+  static constexpr int PPW = (A_BYTES / 1024) / 2;  // 1 KiB DMA pieces per wave
 };
 
 // Swizzled byte offset of 16-B chunk `ch` of row `row` in the [64][D] image.
@@ -80,11 +80,12 @@ __device__ __forceinline__ int perm16(int o) {
 }
 
 // ---------------------------------------------------------------------------
-// Prep: fp32 [n, ld] -> bf16 row-major [n_pad, D] (zero padded) and optionally
-// the permuted transposed image [D, n_pad].  One block = 64 rows.
+// Prep: fp32 [n, ld] -> bf16 row-major [n_pad, D] of scale * src (zero padded)
+// and optionally the permuted transposed image [D, n_pad] of src (unscaled).
+// One block = 64 rows.
 template <int D>
 __global__ void __launch_bounds__(256) prep_kernel(const float* __restrict__ src, int64_t ld, int64_t n,
-                                                   int dim, int64_t n_pad, __bf16* __restrict__ dst,
+                                                   int dim, int64_t n_pad, float scale, __bf16* __restrict__ dst,
                                                    __bf16* __restrict__ dstT) {
   __shared__ float tile[64][D + 1];
   const int64_t r0 = blockIdx.x * 64ll;
@@ -98,10 +99,10 @@ __global__ void __launch_bounds__(256) prep_kernel(const float* __restrict__ src
   for (int i = threadIdx.x; i < 64 * D / 8; i += 256) {
     const int r = i / (D / 8), c8 = (i % (D / 8)) * 8;
     u32x4 v;
-    v.x = pack_bf16x2(tile[r][c8 + 0], tile[r][c8 + 1]);
-    v.y = pack_bf16x2(tile[r][c8 + 2], tile[r][c8 + 3]);
-    v.z = pack_bf16x2(tile[r][c8 + 4], tile[r][c8 + 5]);
-    v.w = pack_bf16x2(tile[r][c8 + 6], tile[r][c8 + 7]);
+    v.x = pack_bf16x2(scale * tile[r][c8 + 0], scale * tile[r][c8 + 1]);
+    v.y = pack_bf16x2(scale * tile[r][c8 + 2], scale * tile[r][c8 + 3]);
+    v.z = pack_bf16x2(scale * tile[r][c8 + 4], scale * tile[r][c8 + 5]);
+    v.w = pack_bf16x2(scale * tile[r][c8 + 6], scale * tile[r][c8 + 7]);
     *reinterpret_cast<u32x4*>(dst + (r0 + r) * D + c8) = v;
   }
   if (dstT) {
@@ -136,13 +137,13 @@ __global__ void bias_kernel(const float* __restrict__ v, int64_t n, int64_t n_pa
   out[i] = (i < n) ? (v ? sign * v[i] : 0.0f) : pad;
 }
 
-// bias1[i] = -logq[i] (0 if logq NULL) for i < n, -inf for n <= i < n_pad;
+// bias1[i] = -log2(e) logq[i] (0 if logq NULL) for i < n, -inf for n <= i < n_pad;
 // bias2[i] = -inf for n <= i < n_pad (its [0, n) is written by combine_rows).
 __global__ void dual_bias_kernel(const float* __restrict__ logq, int64_t n, int64_t n_pad, float* __restrict__ bias1,
                                  float* __restrict__ bias2) {
   const int64_t i = blockIdx.x * 256ll + threadIdx.x;
   if (i >= n_pad) return;
-  bias1[i] = (i < n) ? (logq ? -logq[i] : 0.0f) : -INFINITY;
+  bias1[i] = (i < n) ? (logq ? -kLog2e * logq[i] : 0.0f) : -INFINITY;
   if (i >= n) bias2[i] = -INFINITY;
 }
 
@@ -159,13 +160,38 @@ struct PassArgs {
   float* part_o;          // [S, n_stat_pad, D]
 };
 
-// MODE 0: rows pass (online softmax).  MODE 1: cols pass (lse known).
+// ---------------------------------------------------------------------------
+// The pass kernel (MODE 0: rows pass, online softmax; MODE 1: cols pass, lse
+// known), software-pipelined so that the MFMA pipe never waits on the softmax:
+//   iteration t:  [S(t+1) = A(t+1) . B  ||  p(t) = exp2(S(t)), bf16 pack]
+//                 [O^T += X^T(t) . P^T(t) ||  l += sum p(t), max S(t+1)]
+// i.e. the exp/pack work of tile t issues between the score MFMAs of tile
+// t+1, and the row-sum / next max between the P.V MFMAs of tile t.
+// Tiles arrive by LDS-DMA (buffer_load ... lds: zero VGPR staging, the tile
+// offset is a scalar) into a 4-stage ring; one counted vmcnt + one s_barrier
+// per tile.  Waves 0-1 fetch the row-major image, waves 2-3 the transposed
+// one, wave 0 also the 64 biases.
+// Scores are in log2 units: the row-major image of q is prepared scaled by
+// log2(e) and the biases likewise, so p = exp2(s - m) is one subtract + one
+// v_exp per score.  (The row sum stays an fp32 add chain: a v_dot2 over the
+// packed weights miscompiles with this hipcc — it re-reads one source pair.)
+// Rows pass: lazy rescaling — the running max m only moves when a tile's max
+// exceeds it by more than 8 (log2 units), so p <= 2^8 and the 64-register O
+// rescale leaves the steady state (m, l, O stay consistent: lse = m + log l).
+constexpr float kLazyRescale = 8.0f;  // log2 units
+constexpr float kLn2 = 0.6931471805599453f;
+
+template <int N>
+__device__ __forceinline__ void ib_wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
 template <int D, int MODE>
-__global__ void __launch_bounds__(kThreads) inbatch_pass_kernel(const PassArgs a) {
+__global__ void __launch_bounds__(kThreads) inbatch_pipe_kernel(const PassArgs a) {
   using G = Geo<D>;
-  __shared__ __attribute__((aligned(16))) char smem[2 * G::BUF_BYTES];
-  const int tid = threadIdx.x;
-  const int wave = tid / kWave;
+  extern __shared__ __attribute__((aligned(16))) char ring[];
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) / kWave);
   const int lane = lane_id();
   const int h = lane >> 5;
   const int l32 = lane & 31;
@@ -176,11 +202,62 @@ __global__ void __launch_bounds__(kThreads) inbatch_pass_kernel(const PassArgs a
   if (s_end > a.n_strm_pad) s_end = a.n_strm_pad;
   const int ntiles = s_begin < s_end ? static_cast<int>((s_end - s_begin) / kTile) : 0;
 
-  // Stationary fragments: B[k = 16s + 8h + j][col = l32].
   bf16x8 bfrag[G::KS];
 #pragma unroll
   for (int s = 0; s < G::KS; ++s)
     bfrag[s] = *reinterpret_cast<const bf16x8*>(a.stat + stat_row * D + 16 * s + 8 * h);
+
+  // DMA plan of this wave: PPW pieces of the A image (waves 0-1) or of the
+  // T image (waves 2-3); lane offsets are tile-invariant, the tile moves the
+  // scalar offset only.  Swizzle applied on the source so pieces land
+  // lane-linear in the XOR-swizzled layout.
+  const bool is_t = wave >= 2;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      is_t ? (void*)a.strmT : (void*)a.strm, 0, static_cast<int>(a.n_strm_pad * D * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t brsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.bias, 0, static_cast<int>(a.n_strm_pad * 4), 0x00020000);
+  unsigned voff[G::PPW];
+#pragma unroll
+  for (int u = 0; u < G::PPW; ++u) {
+    const int p = (wave & 1) * G::PPW + u;
+    const int off = p * 1024 + lane * 16;
+    if (!is_t) {
+      const int row = off / (D * 2), chp = (off % (D * 2)) / 16;
+      const int ch = chp ^ ((row * G::CH / 16) % G::CH);
+      voff[u] = static_cast<unsigned>(row * D * 2 + ch * 16);
+    } else {
+      const int e = off / 128, chp = (off % 128) / 16;
+      const int ch = chp ^ ((e >> 1) & 7);
+      voff[u] = static_cast<unsigned>(static_cast<int64_t>(e) * a.n_strm_pad * 2 + ch * 16);
+    }
+  }
+  const int dst0 = (is_t ? G::A_BYTES : 0) + (wave & 1) * G::PPW * 1024;
+  auto issue = [&](int tile) {
+    const int64_t row0 = s_begin + static_cast<int64_t>(tile) * kTile;
+    const unsigned soff = static_cast<unsigned>(is_t ? row0 * 2 : row0 * D * 2);
+    char* st = ring + (tile % kRingStages) * G::STAGE_BYTES;
+#pragma unroll
+    for (int u = 0; u < G::PPW; ++u)
+      // (the explicit copy of voff[u] is needed: passing the captured array
+      // element itself drops the kernel's host-side stub with this hipcc)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(st + dst0 + u * 1024),
+                                               16, static_cast<unsigned>(voff[u]), soff, 0, 0);
+    if (wave == 0)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (__attribute__((address_space(3))) void*)(st + G::A_BYTES + G::T_BYTES),
+                                               4, lane * 4, static_cast<unsigned>(row0 * 4), 0, 0);
+  };
+  // Wait until at most `ahead` issued tiles of this wave are still in flight.
+  auto wait_tiles = [&](int ahead) {
+    if (wave == 0) {
+      if (ahead >= 2) ib_wait_vmcnt<2 * (G::PPW + 1)>();
+      else if (ahead == 1) ib_wait_vmcnt<G::PPW + 1>();
+      else ib_wait_vmcnt<0>();
+    } else {
+      if (ahead >= 2) ib_wait_vmcnt<2 * G::PPW>();
+      else if (ahead == 1) ib_wait_vmcnt<G::PPW>();
+      else ib_wait_vmcnt<0>();
+    }
+  };
 
   f32x16 o[G::DT];
 #pragma unroll
@@ -190,58 +267,11 @@ __global__ void __launch_bounds__(kThreads) inbatch_pass_kernel(const PassArgs a
   float m_run = -1.0e30f;
   float l_run = 0.0f;
 
-  u32x4 ra[G::A_CHUNKS_PER_THREAD];
-  u32x4 rt[G::T_CHUNKS_PER_THREAD];
-  float rb = 0.0f;
-  auto gload = [&](int64_t base) {
-#pragma unroll
-    for (int i = 0; i < G::A_CHUNKS_PER_THREAD; ++i) {
-      const int c = tid + kThreads * i;
-      const int row = c / G::CH, ch = c % G::CH;
-      ra[i] = *reinterpret_cast<const u32x4*>(a.strm + (base + row) * D + ch * 8);
-    }
-#pragma unroll
-    for (int i = 0; i < G::T_CHUNKS_PER_THREAD; ++i) {
-      const int c = tid + kThreads * i;
-      const int e = c / 8, ch = c % 8;
-      rt[i] = *reinterpret_cast<const u32x4*>(a.strmT + static_cast<int64_t>(e) * a.n_strm_pad + base + ch * 8);
-    }
-    if (tid < kTile) rb = a.bias[base + tid];
-  };
-  auto lstore = [&](int buf) {
-    char* B = smem + buf * G::BUF_BYTES;
-#pragma unroll
-    for (int i = 0; i < G::A_CHUNKS_PER_THREAD; ++i) {
-      const int c = tid + kThreads * i;
-      const int row = c / G::CH, ch = c % G::CH;
-      *reinterpret_cast<u32x4*>(B + a_off<D>(row, ch)) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < G::T_CHUNKS_PER_THREAD; ++i) {
-      const int c = tid + kThreads * i;
-      const int e = c / 8, ch = c % 8;
-      *reinterpret_cast<u32x4*>(B + G::A_BYTES + t_off(e, ch)) = rt[i];
-    }
-    if (tid < kTile) reinterpret_cast<float*>(B + G::A_BYTES + G::T_BYTES)[tid] = rb;
-  };
-
-  if (ntiles > 0) {
-    gload(s_begin);
-    lstore(0);
-  }
-  __syncthreads();
-
-  for (int tile = 0; tile < ntiles; ++tile) {
-    const int cur = tile & 1;
-    const bool more = tile + 1 < ntiles;
-    if (more) gload(s_begin + static_cast<int64_t>(tile + 1) * kTile);
-    const char* B = smem + cur * G::BUF_BYTES;
+  auto scores = [&](int tile, f32x16* sacc) {
+    const char* B = ring + (tile % kRingStages) * G::STAGE_BYTES;
     const float* bias = reinterpret_cast<const float*>(B + G::A_BYTES + G::T_BYTES);
-
-    // S^T (+ bias) for the two 32-row sub-tiles.
-    f32x16 sacc[2];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r4 = 0; r4 < 4; ++r4) {
         const f32x4 b4 = *reinterpret_cast<const f32x4*>(bias + 32 * t + 8 * r4 + 4 * h);
@@ -251,23 +281,41 @@ __global__ void __launch_bounds__(kThreads) inbatch_pass_kernel(const PassArgs a
         sacc[t][4 * r4 + 3] = b4[3];
       }
 #pragma unroll
-      for (int s = 0; s < G::KS; ++s) {
+    for (int s = 0; s < G::KS; ++s)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
         const bf16x8 af = *reinterpret_cast<const bf16x8*>(B + a_off<D>(32 * t + l32, 2 * s + h));
         sacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfrag[s], sacc[t], 0, 0, 0);
       }
+  };
+  auto tile_max = [&](const f32x16* sacc) {
+    float m0 = sacc[0][0], m1 = sacc[1][0];
+#pragma unroll
+    for (int r = 1; r < 16; r += 2) {
+      m0 = __builtin_elementwise_maximum(__builtin_elementwise_maximum(m0, sacc[0][r]), sacc[0][r + 1 < 16 ? r + 1 : r]);
+      m1 = __builtin_elementwise_maximum(__builtin_elementwise_maximum(m1, sacc[1][r]), sacc[1][r + 1 < 16 ? r + 1 : r]);
     }
+    const float m = __builtin_elementwise_maximum(m0, m1);
+    return __builtin_elementwise_maximum(m, __shfl_xor(m, 32, kWave));
+  };
 
-    float p[2][16];
+  const int pre = ntiles < kRingStages ? ntiles : kRingStages;
+  for (int t = 0; t < pre; ++t) issue(t);
+  f32x16 sa[2], sb[2];
+  float mx = -INFINITY;
+  if (ntiles > 0) {
+    wait_tiles(pre - 1);  // tile 0 landed
+    __builtin_amdgcn_s_barrier();
+    scores(0, sa);
+    if constexpr (MODE == 0) mx = tile_max(sa);
+  }
+
+  // One tile: sc holds S(tile) (log2 units), sn receives S(tile+1).
+  auto step = [&](int tile, f32x16* sc, f32x16* sn) {
     if constexpr (MODE == 0) {
-      float mx = -1.0e30f;
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[t][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
-      const float m_new = fmaxf(m_run, mx);
-      if (__any(m_new > m_run)) {
-        const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * kLog2e);
+      if (__any(mx > m_run + kLazyRescale)) {
+        const float m_new = __builtin_elementwise_maximum(m_run, mx);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
         l_run *= alpha;
 #pragma unroll
         for (int dt = 0; dt < G::DT; ++dt)
@@ -275,51 +323,69 @@ __global__ void __launch_bounds__(kThreads) inbatch_pass_kernel(const PassArgs a
           for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
         m_run = m_new;
       }
-      const float mb = m_run * kLog2e;
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          p[t][r] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[t][r], kLog2e, -mb));
-          l_run += p[t][r];
-        }
-    } else {
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) p[t][r] = __builtin_amdgcn_exp2f(sacc[t][r] * kLog2e);
+    }
+    if (tile == 0 && ntiles > 1) {
+      // tile 1 must be resident before the first look-ahead scores
+      wait_tiles(pre - 2);
+      __builtin_amdgcn_s_barrier();
     }
 
-    // P^T fragments (B operand, k = streamed row) and O^T += X^T . P^T.
+    // Region A: next scores || exp + pack of this tile.  (After the last
+    // tile the look-ahead reads a stale stage: harmless, never used.)
+    scores(tile + 1, sn);
+    const float mb = (MODE == 0) ? m_run : 0.0f;
+    bf16x8 pf[4];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
+        float p[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) p[j] = __builtin_amdgcn_exp2f(sc[t][8 * s2 + j] - mb);
         u32x4 pk;
-        pk.x = pack_bf16x2(p[t][8 * s2 + 0], p[t][8 * s2 + 1]);
-        pk.y = pack_bf16x2(p[t][8 * s2 + 2], p[t][8 * s2 + 3]);
-        pk.z = pack_bf16x2(p[t][8 * s2 + 4], p[t][8 * s2 + 5]);
-        pk.w = pack_bf16x2(p[t][8 * s2 + 6], p[t][8 * s2 + 7]);
-        const bf16x8 pf = __builtin_bit_cast(bf16x8, pk);
+        pk.x = pack_bf16x2(p[0], p[1]);
+        pk.y = pack_bf16x2(p[2], p[3]);
+        pk.z = pack_bf16x2(p[4], p[5]);
+        pk.w = pack_bf16x2(p[6], p[7]);
+        pf[2 * t + s2] = __builtin_bit_cast(bf16x8, pk);
+        if constexpr (MODE == 0) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) l_run += p[j];
+        }
+      }
+
+    // Region B: P.V of this tile || the next tile's max.
+    const char* B = ring + (tile % kRingStages) * G::STAGE_BYTES;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
         for (int dt = 0; dt < G::DT; ++dt) {
           const int e = 32 * dt + l32;
           const bf16x8 tf = *reinterpret_cast<const bf16x8*>(B + G::A_BYTES + t_off(e, 4 * t + 2 * s2 + h));
-          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tf, pf, o[dt], 0, 0, 0);
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tf, pf[2 * t + s2], o[dt], 0, 0, 0);
         }
-      }
-    }
+    if constexpr (MODE == 0) mx = tile_max(sn);
 
-    if (more) lstore(cur ^ 1);
-    __syncthreads();
+    // Ring: tile+2 resident for the next step, this tile's stage free.
+    if (tile + 2 < ntiles) {
+      wait_tiles(tile + 3 < ntiles ? 1 : 0);
+      __builtin_amdgcn_s_barrier();
+      if (tile + kRingStages < ntiles) issue(tile + kRingStages);
+    }
+  };
+  // Unrolled by two so the S(t) / S(t+1) register sets swap roles without copies.
+  for (int tile = 0; tile < ntiles; tile += 2) {
+    step(tile, sa, sb);
+    if (tile + 1 < ntiles) step(tile + 1, sb, sa);
   }
 
-  // Partials: lane (l32, h) holds O^T[e = 32dt + 8r4 + 4h + 0..3][stat_row].
   const int64_t prow = static_cast<int64_t>(split) * a.n_stat_pad + stat_row;
   if constexpr (MODE == 0) {
     const float l_tot = l_run + __shfl_xor(l_run, 32, kWave);
     if (h == 0) {
-      a.part_m[prow] = m_run;
+      a.part_m[prow] = m_run * kLn2;  // natural-log units for the combine
       a.part_l[prow] = l_tot;
     }
   }
@@ -368,7 +434,7 @@ __global__ void __launch_bounds__(256) combine_rows_kernel(
     const float pos_logit = dot - (logq ? logq[pos] : 0.0f);
     lse_out[i] = lse;
     loss_out[i] = lse - pos_logit;
-    if (neg_lse_bias) neg_lse_bias[i] = -lse;
+    if (neg_lse_bias) neg_lse_bias[i] = -kLog2e * lse;
   }
 }
 
@@ -458,32 +524,47 @@ size_t pass_bytes(int64_t n_stat, int64_t n_strm, int dim) {
 }
 
 template <int D>
-int launch_prep(const float* src, int64_t ld, int64_t n, int dim, int64_t n_pad, __bf16* dst, __bf16* dstT,
-                hipStream_t st) {
-  hipLaunchKernelGGL(prep_kernel<D>, dim3(n_pad / 64), dim3(256), 0, st, src, ld, n, dim, n_pad, dst, dstT);
+int launch_prep(const float* src, int64_t ld, int64_t n, int dim, int64_t n_pad, float scale, __bf16* dst,
+                __bf16* dstT, hipStream_t st) {
+  hipLaunchKernelGGL(prep_kernel<D>, dim3(n_pad / 64), dim3(256), 0, st, src, ld, n, dim, n_pad, scale, dst, dstT);
   TT_CHECK_LAUNCH();
   return TT_OK;
 }
 
-int prep(int D, const float* src, int64_t ld, int64_t n, int dim, int64_t n_pad, __bf16* dst, __bf16* dstT,
-         hipStream_t st) {
+// scale applies to the row-major image only (log2(e) for q, 1 for c).
+int prep(int D, const float* src, int64_t ld, int64_t n, int dim, int64_t n_pad, float scale, __bf16* dst,
+         __bf16* dstT, hipStream_t st) {
   switch (D) {
-    case 32: return launch_prep<32>(src, ld, n, dim, n_pad, dst, dstT, st);
-    case 64: return launch_prep<64>(src, ld, n, dim, n_pad, dst, dstT, st);
-    default: return launch_prep<128>(src, ld, n, dim, n_pad, dst, dstT, st);
+    case 32: return launch_prep<32>(src, ld, n, dim, n_pad, scale, dst, dstT, st);
+    case 64: return launch_prep<64>(src, ld, n, dim, n_pad, scale, dst, dstT, st);
+    default: return launch_prep<128>(src, ld, n, dim, n_pad, scale, dst, dstT, st);
   }
+}
+
+template <int D, int MODE>
+int launch_pass_d(dim3 grid, const PassArgs& a, hipStream_t st) {
+  constexpr int shm = Geo<D>::LDS_BYTES;
+  if (shm > 65536) {
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(inbatch_pipe_kernel<D, MODE>),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, shm);
+    TT_CHECK_HIP(attr);
+  }
+  hipLaunchKernelGGL((inbatch_pipe_kernel<D, MODE>), grid, dim3(kThreads), shm, st, a);
+  TT_CHECK_LAUNCH();
+  return TT_OK;
 }
 
 template <int MODE>
 int launch_pass(const Plan& p, const PassArgs& a, hipStream_t st) {
+  // buffer descriptors address the bf16 images with 32-bit byte offsets
+  if (p.strm_pad * p.D * 2 >= (1ll << 31))
+    return fail(TT_ERR_UNSUPPORTED, "inbatch: %lld x %d streamed batch too large", (long long)p.strm_pad, p.D);
   dim3 grid(static_cast<unsigned>(p.stat_pad / kRowsPerWG), static_cast<unsigned>(p.split));
   switch (p.D) {
-    case 32: hipLaunchKernelGGL((inbatch_pass_kernel<32, MODE>), grid, dim3(kThreads), 0, st, a); break;
-    case 64: hipLaunchKernelGGL((inbatch_pass_kernel<64, MODE>), grid, dim3(kThreads), 0, st, a); break;
-    default: hipLaunchKernelGGL((inbatch_pass_kernel<128, MODE>), grid, dim3(kThreads), 0, st, a); break;
+    case 32: return launch_pass_d<32, MODE>(grid, a, st);
+    case 64: return launch_pass_d<64, MODE>(grid, a, st);
+    default: return launch_pass_d<128, MODE>(grid, a, st);
   }
-  TT_CHECK_LAUNCH();
-  return TT_OK;
 }
 
 int check_common(const float* q, int64_t ldq, int64_t n_rows, const float* c, int64_t ldc, int64_t n_cols,
@@ -525,10 +606,10 @@ extern "C" int tt_inbatch_xent_rows(const float* q, int64_t ldq, int64_t n_rows,
   if (!workspace || cv.used() > workspace_bytes)
     return fail(TT_ERR_WORKSPACE, "tt_inbatch_xent_rows: workspace %zu < required %zu", workspace_bytes, cv.used());
   hipStream_t st = to_stream(stream);
-  if ((rc = prep(p.D, q, ldq, n_rows, dim, p.stat_pad, w.stat, nullptr, st))) return rc;
-  if ((rc = prep(p.D, c, ldc, n_cols, dim, p.strm_pad, w.strm, w.strmT, st))) return rc;
+  if ((rc = prep(p.D, q, ldq, n_rows, dim, p.stat_pad, kLog2e, w.stat, nullptr, st))) return rc;
+  if ((rc = prep(p.D, c, ldc, n_cols, dim, p.strm_pad, 1.0f, w.strm, w.strmT, st))) return rc;
   hipLaunchKernelGGL(bias_kernel, dim3(ceil_div(p.strm_pad, 256)), dim3(256), 0, st, logq, n_cols, p.strm_pad,
-                     -1.0f, -INFINITY, w.bias);
+                     -kLog2e, -INFINITY, w.bias);
   TT_CHECK_LAUNCH();
   PassArgs a{w.stat, w.strm, w.strmT, w.bias, p.stat_pad, p.strm_pad, p.per_split, w.part_m, w.part_l, w.part_o};
   if ((rc = launch_pass<0>(p, a, st))) return rc;
@@ -555,10 +636,10 @@ extern "C" int tt_inbatch_xent_cols(const float* q, int64_t ldq, int64_t n_rows,
   if (!workspace || cv.used() > workspace_bytes)
     return fail(TT_ERR_WORKSPACE, "tt_inbatch_xent_cols: workspace %zu < required %zu", workspace_bytes, cv.used());
   hipStream_t st = to_stream(stream);
-  if ((rc = prep(p.D, c, ldc, n_cols, dim, p.stat_pad, w.stat, nullptr, st))) return rc;
-  if ((rc = prep(p.D, q, ldq, n_rows, dim, p.strm_pad, w.strm, w.strmT, st))) return rc;
+  if ((rc = prep(p.D, c, ldc, n_cols, dim, p.stat_pad, 1.0f, w.stat, nullptr, st))) return rc;
+  if ((rc = prep(p.D, q, ldq, n_rows, dim, p.strm_pad, kLog2e, w.strm, w.strmT, st))) return rc;
   hipLaunchKernelGGL(bias_kernel, dim3(ceil_div(p.strm_pad, 256)), dim3(256), 0, st, lse, n_rows, p.strm_pad,
-                     -1.0f, -INFINITY, w.bias);
+                     -kLog2e, -INFINITY, w.bias);
   TT_CHECK_LAUNCH();
   PassArgs a{w.stat, w.strm, w.strmT, w.bias, p.stat_pad, p.strm_pad, p.per_split, nullptr, nullptr, w.part_o};
   if ((rc = launch_pass<1>(p, a, st))) return rc;
@@ -631,8 +712,8 @@ extern "C" int tt_inbatch_softmax_xent(const float* q, int64_t ldq, const float*
     return fail(TT_ERR_WORKSPACE, "tt_inbatch_softmax_xent: workspace %zu < required %zu", workspace_bytes,
                 cv.used());
   hipStream_t st = to_stream(stream);
-  if ((rc = prep(p.D, q, ldq, n, dim, p.n_pad, w.qb, w.qbT, st))) return rc;
-  if ((rc = prep(p.D, c, ldc, n, dim, p.n_pad, w.cb, w.cbT, st))) return rc;
+  if ((rc = prep(p.D, q, ldq, n, dim, p.n_pad, kLog2e, w.qb, w.qbT, st))) return rc;
+  if ((rc = prep(p.D, c, ldc, n, dim, p.n_pad, 1.0f, w.cb, w.cbT, st))) return rc;
   hipLaunchKernelGGL(dual_bias_kernel, dim3(ceil_div(p.n_pad, 256)), dim3(256), 0, st, logq, n, p.n_pad, w.bias_logq,
                      w.bias_lse);
   TT_CHECK_LAUNCH();

@@ -184,6 +184,25 @@ def test_inbatch_softmax_xent(cuda, B, E, use_logq, scale):
     assert _rel(dc.cpu().numpy(), ref["dc"]) <= 1e-2
 
 
+@pytest.mark.parametrize("B,E,use_logq,scale", [(8192, 128, True, 0.3), (4100, 64, True, 0.7), (2500, 32, False, 0.6),
+                                                (1100, 128, True, 0.5), (60, 8, True, 1.0)])
+def test_inbatch_fused_entry(cuda, B, E, use_logq, scale):
+    """tt_inbatch_softmax_xent at sizes whose splits hold many tiles (LDS ring
+    wrap-around), ragged tails (fully padded last tiles) and a -logq spread
+    (~13 log2 units) that moves the lazily rescaled running max."""
+    rng = np.random.default_rng(B * 7 + E)
+    q = np.maximum(rng.standard_normal((B, E)) * scale, 0).astype(np.float32)
+    c = np.maximum(rng.standard_normal((B, E)) * scale, 0).astype(np.float32)
+    logq = np.log(rng.uniform(1e-6, 1e-2, B)).astype(np.float32) if use_logq else None
+    ref = oracle.inbatch_softmax_xent(q, c, logq)
+    lse, row_loss, dq, dc = hip_ops.inbatch_fused(_t(q, cuda), _t(c, cuda), _t(logq, cuda) if use_logq else None)
+    loss = float(row_loss.double().sum())
+    assert abs(loss - ref["loss"]) <= 2e-3 * abs(ref["loss"])
+    np.testing.assert_allclose(lse.cpu().numpy(), ref["lse"], rtol=2e-3, atol=2e-3)
+    assert _rel(dq.cpu().numpy(), ref["dq"]) <= 1e-2
+    assert _rel(dc.cpu().numpy(), ref["dc"]) <= 1e-2
+
+
 def test_inbatch_row_blocks_with_offset(cuda):
     """Rows of rank r scored against all-gathered columns (global negatives)."""
     rng = np.random.default_rng(7)
