@@ -22,19 +22,21 @@
 //
 // Wave layout (32x32x16 bf16 MFMA, 64-wide wave): a wave owns 32 stationary
 // rows whose bf16 fragments stay in VGPRs for the whole pass (B operand).
-// Streamed rows arrive in 64-row tiles through a 4-stage LDS-DMA ring
-// (XOR-swizzled so every ds_read_b128 fragment read is bank-conflict free):
+// Streamed rows arrive in 64-row tiles, by LDS-DMA, into a 4-stage ring of
+// ONE row-major image per tile, read two ways:
 //   S^T tile [32 streamed x 32 stationary] = A(streamed rows) . B(stationary)
-// so each lane holds 16 scores of ONE stationary row; the per-row bias
-// (-logq_j for F, -lse_i for G) is loaded as the accumulator's initial value.
-// The S^T accumulator is exactly the B operand of the next MFMA
-// (O^T += X^T . P^T) after a bf16 pack, so P never touches LDS; the streamed
-// operand's transposed image X^T is prepared once in HBM with the MFMA's
-// k-permutation baked in (16-byte fragment reads).
+//     with row reads (ds_read_b128), so each lane holds 16 scores of ONE
+//     stationary row; the per-row bias (-logq_j for F, -lse_i for G) is the
+//     accumulator's initial value;
+//   O^T [E x 32 stationary] += X^T . P^T, where the S^T accumulator packed to
+//     bf16 IS the B operand P^T (P never touches LDS) and X^T comes from the
+//     same image through the hardware transposing read ds_read_b64_tr_b16.
+// The image's XOR swizzle keeps both kinds of read bank-conflict free.
 // The stationary extent is split into 128-row workgroups and the streamed
 // extent into S splits (flash-decoding) so that >= 256 workgroups fill the
-// 256 CUs; tiny combine kernels merge the splits.
+// 256 CUs; small combine kernels merge the splits.
 #include <cmath>
+#include <type_traits>
 
 #include "tt_common.h"
 
@@ -49,83 +51,52 @@ constexpr int kTile = 64;                                // streamed rows per LD
 constexpr int kMaxSplit = 16;
 constexpr int kRingStages = 4;                           // LDS tile ring depth
 constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLazyRescale = 8.0f / kLog2e;  // 8 in log2 units (natural-log units here)
+
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 template <int D>
 struct Geo {
-  static constexpr int KS = D / 16;           // MFMA k-steps over the embedding
-  static constexpr int DT = D / 32;           // 32-row output tiles of O^T
-  static constexpr int CH = D / 8;            // 16-byte chunks per bf16 row
-  static constexpr int A_BYTES = kTile * D * 2;   // streamed rows, row-major
-  static constexpr int T_BYTES = D * kTile * 2;   // transposed image [D][64]
-  static constexpr int STAGE_BYTES = A_BYTES + T_BYTES + kTile * 4;  // + 64 biases
-  static constexpr int LDS_BYTES = kRingStages * STAGE_BYTES;
-  static constexpr int PPW = (A_BYTES / 1024) / 2;  // 1 KiB DMA pieces per wave
+  static constexpr int KS = D / 16;                        // MFMA k-steps over the embedding
+  static constexpr int DT = D / 32;                        // 32-row output tiles of O^T
+  static constexpr int CH = D / 8;                         // 16-byte chunks per bf16 row
+  static constexpr int A_BYTES = kTile * D * 2;            // one tile image = one ring stage
+  static constexpr int BIAS_OFF = kRingStages * A_BYTES;   // then kRingStages x 64 biases
+  static constexpr int LDS_BYTES = BIAS_OFF + kRingStages * kTile * 4;
+  static constexpr int PPW = A_BYTES / 1024 / kWavesPerWG; // 1 KiB DMA pieces per wave per tile
 };
 
-// Swizzled byte offset of 16-B chunk `ch` of row `row` in the [64][D] image.
+// Byte offset of 16-B chunk ch of tile row `row` (rows of 2D bytes).  The XOR
+// swizzle makes both the 16-lane ds_read_b128 groups of the row reads (rows
+// {0-3,12-15,20-27}, one chunk) and the 32-lane halves of the transposed reads
+// (4 consecutive rows x 4 aligned chunks) hit 64 distinct banks.
 template <int D>
 __device__ __forceinline__ int a_off(int row, int ch) {
-  constexpr int CH = D / 8;
-  const int swz = (row * CH / 16) % CH;
-  return row * (CH * 16) + ((ch ^ swz) << 4);
-}
-// Swizzled byte offset of 16-B chunk `ch` (0..7) of row `e` in the [D][64] image.
-__device__ __forceinline__ int t_off(int e, int ch) { return e * 128 + ((ch ^ ((e >> 1) & 7)) << 4); }
-
-// Position of streamed row offset o (0..15) inside its 16-row group of the
-// transposed image: MFMA k element j of lane half h is row 8(j>>2)+4h+(j&3).
-__device__ __forceinline__ int perm16(int o) {
-  const int a = o >> 3, h = (o >> 2) & 1, b = o & 3;
-  return 8 * h + 4 * a + b;
+  int f;
+  if constexpr (D == 128) f = ((row & 3) << 2) | ((row >> 2) & 3);
+  else if constexpr (D == 64) f = (((row >> 1) & 1) << 2) | ((row >> 2) & 3);
+  else f = (row >> 2) & 3;
+  return row * (D * 2) + ((ch ^ f) << 4);
 }
 
 // ---------------------------------------------------------------------------
-// Prep: fp32 [n, ld] -> bf16 row-major [n_pad, D] of scale * src (zero padded)
-// and optionally the permuted transposed image [D, n_pad] of src (unscaled).
-// One block = 64 rows.
+// Prep: fp32 [n, ld] -> bf16 [n_pad, D] (zero padded).  One block = 64 rows.
 template <int D>
 __global__ void __launch_bounds__(256) prep_kernel(const float* __restrict__ src, int64_t ld, int64_t n,
-                                                   int dim, int64_t n_pad, float scale, __bf16* __restrict__ dst,
-                                                   __bf16* __restrict__ dstT) {
-  __shared__ float tile[64][D + 1];
+                                                   int dim, __bf16* __restrict__ dst) {
   const int64_t r0 = blockIdx.x * 64ll;
-  for (int i = threadIdx.x; i < 64 * D; i += 256) {
-    const int r = i / D, e = i % D;
-    const int64_t gr = r0 + r;
-    tile[r][e] = (gr < n && e < dim) ? src[gr * ld + e] : 0.0f;
-  }
-  __syncthreads();
-  // row-major: each thread packs 8 consecutive elements (16 B).
   for (int i = threadIdx.x; i < 64 * D / 8; i += 256) {
     const int r = i / (D / 8), c8 = (i % (D / 8)) * 8;
-    u32x4 v;
-    v.x = pack_bf16x2(scale * tile[r][c8 + 0], scale * tile[r][c8 + 1]);
-    v.y = pack_bf16x2(scale * tile[r][c8 + 2], scale * tile[r][c8 + 3]);
-    v.z = pack_bf16x2(scale * tile[r][c8 + 4], scale * tile[r][c8 + 5]);
-    v.w = pack_bf16x2(scale * tile[r][c8 + 6], scale * tile[r][c8 + 7]);
-    *reinterpret_cast<u32x4*>(dst + (r0 + r) * D + c8) = v;
-  }
-  if (dstT) {
-    // transposed: image row e holds the 64 rows of this block, permuted per 16.
-    for (int i = threadIdx.x; i < D * 8; i += 256) {
-      const int e = i / 8, p8 = (i % 8) * 8;  // positions p8..p8+7 within the 64
-      float x[8];
+    const int64_t gr = r0 + r;
+    float x[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int p = p8 + j;
-        const int g = p >> 4, pp = p & 15;
-        // inverse of perm16: position pp holds row offset o with perm16(o) == pp
-        const int h = pp >> 3, a = (pp >> 2) & 1, b = pp & 3;
-        const int o = 8 * a + 4 * h + b;
-        x[j] = tile[16 * g + o][e];
-      }
-      u32x4 v;
-      v.x = pack_bf16x2(x[0], x[1]);
-      v.y = pack_bf16x2(x[2], x[3]);
-      v.z = pack_bf16x2(x[4], x[5]);
-      v.w = pack_bf16x2(x[6], x[7]);
-      *reinterpret_cast<u32x4*>(dstT + static_cast<int64_t>(e) * n_pad + r0 + p8) = v;
-    }
+    for (int j = 0; j < 8; ++j) x[j] = (gr < n && c8 + j < dim) ? src[gr * ld + c8 + j] : 0.0f;
+    u32x4 v;
+    v.x = pack_bf16x2(x[0], x[1]);
+    v.y = pack_bf16x2(x[2], x[3]);
+    v.z = pack_bf16x2(x[4], x[5]);
+    v.w = pack_bf16x2(x[6], x[7]);
+    *reinterpret_cast<u32x4*>(dst + gr * D + c8) = v;
   }
 }
 
@@ -137,20 +108,19 @@ __global__ void bias_kernel(const float* __restrict__ v, int64_t n, int64_t n_pa
   out[i] = (i < n) ? (v ? sign * v[i] : 0.0f) : pad;
 }
 
-// bias1[i] = -log2(e) logq[i] (0 if logq NULL) for i < n, -inf for n <= i < n_pad;
+// bias1[i] = -logq[i] (0 if logq NULL) for i < n, -inf for n <= i < n_pad;
 // bias2[i] = -inf for n <= i < n_pad (its [0, n) is written by combine_rows).
 __global__ void dual_bias_kernel(const float* __restrict__ logq, int64_t n, int64_t n_pad, float* __restrict__ bias1,
                                  float* __restrict__ bias2) {
   const int64_t i = blockIdx.x * 256ll + threadIdx.x;
   if (i >= n_pad) return;
-  bias1[i] = (i < n) ? (logq ? -kLog2e * logq[i] : 0.0f) : -INFINITY;
+  bias1[i] = (i < n) ? (logq ? -logq[i] : 0.0f) : -INFINITY;
   if (i >= n) bias2[i] = -INFINITY;
 }
 
 struct PassArgs {
   const __bf16* stat;     // [n_stat_pad, D] stationary rows (B operand)
-  const __bf16* strm;     // [n_strm_pad, D] streamed rows (A operand of S)
-  const __bf16* strmT;    // [D, n_strm_pad] permuted transposed image
+  const __bf16* strm;     // [n_strm_pad, D] streamed rows
   const float* bias;      // [n_strm_pad] accumulator init per streamed row
   int64_t n_stat_pad;
   int64_t n_strm_pad;
@@ -160,35 +130,68 @@ struct PassArgs {
   float* part_o;          // [S, n_stat_pad, D]
 };
 
-// ---------------------------------------------------------------------------
-// The pass kernel (MODE 0: rows pass, online softmax; MODE 1: cols pass, lse
-// known), software-pipelined so that the MFMA pipe never waits on the softmax:
-//   iteration t:  [S(t+1) = A(t+1) . B  ||  p(t) = exp2(S(t)), bf16 pack]
-//                 [O^T += X^T(t) . P^T(t) ||  l += sum p(t), max S(t+1)]
-// i.e. the exp/pack work of tile t issues between the score MFMAs of tile
-// t+1, and the row-sum / next max between the P.V MFMAs of tile t.
-// Tiles arrive by LDS-DMA (buffer_load ... lds: zero VGPR staging, the tile
-// offset is a scalar) into a 4-stage ring; one counted vmcnt + one s_barrier
-// per tile.  Waves 0-1 fetch the row-major image, waves 2-3 the transposed
-// one, wave 0 also the 64 biases.
-// Scores are in log2 units: the row-major image of q is prepared scaled by
-// log2(e) and the biases likewise, so p = exp2(s - m) is one subtract + one
-// v_exp per score.  (The row sum stays an fp32 add chain: a v_dot2 over the
-// packed weights miscompiles with this hipcc — it re-reads one source pair.)
-// Rows pass: lazy rescaling — the running max m only moves when a tile's max
-// exceeds it by more than 8 (log2 units), so p <= 2^8 and the 64-register O
-// rescale leaves the steady state (m, l, O stay consistent: lse = m + log l).
-constexpr float kLazyRescale = 8.0f;  // log2 units
-constexpr float kLn2 = 0.6931471805599453f;
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// Raw buffer descriptor (stride 0, byte-range checked) from wave-uniform values.
+__device__ __forceinline__ i32x4 buffer_desc(const void* base, unsigned bytes) {
+  const uint64_t b = reinterpret_cast<uint64_t>(base);
+  i32x4 d;
+  d.x = __builtin_amdgcn_readfirstlane(static_cast<int>(b & 0xffffffffu));
+  d.y = __builtin_amdgcn_readfirstlane(static_cast<int>((b >> 32) & 0xffffu));
+  d.z = __builtin_amdgcn_readfirstlane(static_cast<int>(bytes));
+  d.w = 0x00020000;
+  return d;
+}
+
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return static_cast<unsigned>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const char*)p));
+}
+
+// LDS-DMA (buffer_load ... lds, 64 lanes x 16 B or x 4 B at LDS address lds)
+// in inline asm: the compiler then does not track these LDS writes, and so
+// does not put an s_waitcnt vmcnt(0) in front of every ds_read_b64_tr_b16 (it
+// does for the builtin form).  Ordering against the reads is the explicit
+// counted vmcnt + s_barrier of the tile ring.
+__device__ __forceinline__ void dma_b128(i32x4 desc, unsigned voff, unsigned soff, unsigned lds) {
+  asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
+               :
+               : "v"(voff), "s"(desc), "s"(soff), "s"(lds)
+               : "memory");  // m0 is compiler-reserved and unused by this kernel otherwise
+}
+__device__ __forceinline__ void dma_b32(i32x4 desc, unsigned voff, unsigned soff, unsigned lds) {
+  asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %0, %1, %2 offen lds"
+               :
+               : "v"(voff), "s"(desc), "s"(soff), "s"(lds)
+               : "memory");  // m0 is compiler-reserved and unused by this kernel otherwise
+}
 
 template <int N>
-__device__ __forceinline__ void ib_wait_vmcnt() {
+__device__ __forceinline__ void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
 }
 
+// ---------------------------------------------------------------------------
+// The pass kernel.  MODE 0: rows pass (online softmax).  MODE 1: cols pass
+// (lse known: p = exp(S + bias) directly).
+//
+// Software pipeline, per tile t (one wave, 32 stationary rows):
+//   region A: the 2*KS score MFMAs of tile t+1 (look-ahead)  ||  exp2 + bf16
+//             pack of tile t's scores (the VALU fills the MFMA gaps);
+//   region B: the 4*DT P.V MFMAs of tile t  ||  row sums of tile t and the
+//             max of tile t+1 (rows pass).
+// Every MFMA step issues the fragment read AHEAD steps later, then its MFMA,
+// then its share of the VALU; __builtin_amdgcn_sched_barrier(0) pins that
+// order (left alone, the scheduler keeps one or two reads in flight and waits
+// lgkmcnt(0) before most MFMAs).  Unrolled by the ring period (4): the S(t) /
+// S(t+1) register sets swap roles without copies and all LDS offsets fold.
+// Tiles arrive by buffer_load ... lds (no VGPR staging; the tile offset is a
+// scalar soffset) into the ring; one counted vmcnt + one s_barrier per tile.
+// Rows pass: lazy rescaling — the running max m only moves when a tile's max
+// exceeds it by more than 8 (log2 units), so p <= 2^8 and the 64-register O
+// rescale leaves the steady state (m, l, O stay consistent: lse = m + log l).
 template <int D, int MODE>
-__global__ void __launch_bounds__(kThreads) inbatch_pipe_kernel(const PassArgs a) {
+__global__ void __launch_bounds__(kThreads) inbatch_pass_kernel(const PassArgs a) {
   using G = Geo<D>;
   extern __shared__ __attribute__((aligned(16))) char ring[];
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) / kWave);
@@ -207,55 +210,39 @@ __global__ void __launch_bounds__(kThreads) inbatch_pipe_kernel(const PassArgs a
   for (int s = 0; s < G::KS; ++s)
     bfrag[s] = *reinterpret_cast<const bf16x8*>(a.stat + stat_row * D + 16 * s + 8 * h);
 
-  // DMA plan of this wave: PPW pieces of the A image (waves 0-1) or of the
-  // T image (waves 2-3); lane offsets are tile-invariant, the tile moves the
-  // scalar offset only.  Swizzle applied on the source so pieces land
-  // lane-linear in the XOR-swizzled layout.
-  const bool is_t = wave >= 2;
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      is_t ? (void*)a.strmT : (void*)a.strm, 0, static_cast<int>(a.n_strm_pad * D * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t brsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.bias, 0, static_cast<int>(a.n_strm_pad * 4), 0x00020000);
+  // DMA plan: every wave moves PPW 1 KiB pieces of each tile image, wave 0
+  // also the 64 biases.  Per-lane source offsets are tile-invariant (the
+  // swizzle is applied on the source so pieces land lane-linear).
+  const i32x4 desc = buffer_desc(a.strm, static_cast<unsigned>(a.n_strm_pad * D * 2));
+  const i32x4 bdesc = buffer_desc(a.bias, static_cast<unsigned>(a.n_strm_pad * 4));
   unsigned voff[G::PPW];
 #pragma unroll
   for (int u = 0; u < G::PPW; ++u) {
-    const int p = (wave & 1) * G::PPW + u;
-    const int off = p * 1024 + lane * 16;
-    if (!is_t) {
-      const int row = off / (D * 2), chp = (off % (D * 2)) / 16;
-      const int ch = chp ^ ((row * G::CH / 16) % G::CH);
-      voff[u] = static_cast<unsigned>(row * D * 2 + ch * 16);
-    } else {
-      const int e = off / 128, chp = (off % 128) / 16;
-      const int ch = chp ^ ((e >> 1) & 7);
-      voff[u] = static_cast<unsigned>(static_cast<int64_t>(e) * a.n_strm_pad * 2 + ch * 16);
-    }
+    const int off = (wave * G::PPW + u) * 1024 + lane * 16;
+    const int row = off / (D * 2), chp = (off % (D * 2)) / 16;
+    // chunk ch lands in slot chp of its row iff a_off(row, ch) == row*2D + 16*chp
+    const int ch = (a_off<D>(row, chp) - row * (D * 2)) >> 4;  // the swizzle is an involution
+    voff[u] = static_cast<unsigned>(row * D * 2 + ch * 16);
   }
-  const int dst0 = (is_t ? G::A_BYTES : 0) + (wave & 1) * G::PPW * 1024;
+  const unsigned ring_lds = lds_addr(ring);
   auto issue = [&](int tile) {
-    const int64_t row0 = s_begin + static_cast<int64_t>(tile) * kTile;
-    const unsigned soff = static_cast<unsigned>(is_t ? row0 * 2 : row0 * D * 2);
-    char* st = ring + (tile % kRingStages) * G::STAGE_BYTES;
+    const unsigned row0 = static_cast<unsigned>(s_begin + static_cast<int64_t>(tile) * kTile);
+    const int stage = tile % kRingStages;
+    const unsigned st = ring_lds + stage * G::A_BYTES;
 #pragma unroll
-    for (int u = 0; u < G::PPW; ++u)
-      // (the explicit copy of voff[u] is needed: passing the captured array
-      // element itself drops the kernel's host-side stub with this hipcc)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(st + dst0 + u * 1024),
-                                               16, static_cast<unsigned>(voff[u]), soff, 0, 0);
-    if (wave == 0)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (__attribute__((address_space(3))) void*)(st + G::A_BYTES + G::T_BYTES),
-                                               4, lane * 4, static_cast<unsigned>(row0 * 4), 0, 0);
+    for (int u = 0; u < G::PPW; ++u) dma_b128(desc, voff[u], row0 * (D * 2), st + (wave * G::PPW + u) * 1024);
+    if (wave == 0) dma_b32(bdesc, lane * 4, row0 * 4, ring_lds + G::BIAS_OFF + stage * (kTile * 4));
   };
   // Wait until at most `ahead` issued tiles of this wave are still in flight.
   auto wait_tiles = [&](int ahead) {
     if (wave == 0) {
-      if (ahead >= 2) ib_wait_vmcnt<2 * (G::PPW + 1)>();
-      else if (ahead == 1) ib_wait_vmcnt<G::PPW + 1>();
-      else ib_wait_vmcnt<0>();
+      if (ahead >= 2) wait_vmcnt<2 * (G::PPW + 1)>();
+      else if (ahead == 1) wait_vmcnt<G::PPW + 1>();
+      else wait_vmcnt<0>();
     } else {
-      if (ahead >= 2) ib_wait_vmcnt<2 * G::PPW>();
-      else if (ahead == 1) ib_wait_vmcnt<G::PPW>();
-      else ib_wait_vmcnt<0>();
+      if (ahead >= 2) wait_vmcnt<2 * G::PPW>();
+      else if (ahead == 1) wait_vmcnt<G::PPW>();
+      else wait_vmcnt<0>();
     }
   };
 
@@ -264,58 +251,96 @@ __global__ void __launch_bounds__(kThreads) inbatch_pipe_kernel(const PassArgs a
   for (int dt = 0; dt < G::DT; ++dt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[dt][r] = 0.0f;
-  float m_run = -1.0e30f;
+  float m_run = -1.0e30f;  // natural-log units
   float l_run = 0.0f;
 
-  auto scores = [&](int tile, f32x16* sacc) {
-    const char* B = ring + (tile % kRingStages) * G::STAGE_BYTES;
-    const float* bias = reinterpret_cast<const float*>(B + G::A_BYTES + G::T_BYTES);
+  // Fragment reads.  Score step i: k-step i >> 1, sub-tile i & 1.
+  // P.V step j = (2 t + s2) DT + dt: X^T rows e = 32 dt + l32, k = streamed
+  // rows 32t + 16s2 + 8(k>>2) + 4h + (k&3) — the S^T accumulator's row order,
+  // gathered by two transposing reads of 4 rows x 16 columns per lane group.
+  // Every read is a per-lane base (the swizzle depends only on the low row
+  // bits) plus a compile-time offset (stage, sub-tile, row group): no address
+  // arithmetic in the loop.
+  int rbase[G::KS];        // row reads: a_off(l32, 2s + h)
+  int tbase[G::DT][2];     // transposed reads: rows 4h + tq + 8u, chunk 4dt + 2tg + tp/2
+  {
+    const int tq = (lane & 15) >> 2, tp = lane & 3, tg = (lane >> 4) & 1;
+#pragma unroll
+    for (int s = 0; s < G::KS; ++s) rbase[s] = a_off<D>(l32, 2 * s + h);
+#pragma unroll
+    for (int dt = 0; dt < G::DT; ++dt)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        tbase[dt][u] = a_off<D>(4 * h + tq + 8 * u, 4 * dt + 2 * tg + (tp >> 1)) + 8 * (tp & 1);
+  }
+  auto rd_a = [&](int stage, int i) {
+    return *reinterpret_cast<const bf16x8*>(ring + rbase[i >> 1] + (stage * G::A_BYTES + (i & 1) * 32 * 2 * D));
+  };
+  auto rd_t = [&](int stage, int j) {
+    const int dt = j % G::DT, g = j / G::DT;  // g = 2t + s2
+    typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+    const int roff = stage * G::A_BYTES + 16 * g * 2 * D;
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(ring + tbase[dt][0] + roff));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(ring + tbase[dt][1] + roff));
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  auto rd_bias = [&](int stage, f32x16* sacc) {
+    const float* bias = reinterpret_cast<const float*>(ring + G::BIAS_OFF + stage * (kTile * 4)) + 4 * h;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r4 = 0; r4 < 4; ++r4) {
-        const f32x4 b4 = *reinterpret_cast<const f32x4*>(bias + 32 * t + 8 * r4 + 4 * h);
-        sacc[t][4 * r4 + 0] = b4[0];
-        sacc[t][4 * r4 + 1] = b4[1];
-        sacc[t][4 * r4 + 2] = b4[2];
-        sacc[t][4 * r4 + 3] = b4[3];
-      }
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(bias + 32 * t + 8 * r4);
 #pragma unroll
-    for (int s = 0; s < G::KS; ++s)
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(B + a_off<D>(32 * t + l32, 2 * s + h));
-        sacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfrag[s], sacc[t], 0, 0, 0);
+        for (int u = 0; u < 4; ++u) sacc[t][4 * r4 + u] = b4[u];
       }
   };
-  auto tile_max = [&](const f32x16* sacc) {
-    float m0 = sacc[0][0], m1 = sacc[1][0];
+
+  auto scores_plain = [&](f32x16* sacc) {  // prologue: tile 0, stage 0
+    rd_bias(0, sacc);
 #pragma unroll
-    for (int r = 1; r < 16; r += 2) {
-      m0 = __builtin_elementwise_maximum(__builtin_elementwise_maximum(m0, sacc[0][r]), sacc[0][r + 1 < 16 ? r + 1 : r]);
-      m1 = __builtin_elementwise_maximum(__builtin_elementwise_maximum(m1, sacc[1][r]), sacc[1][r + 1 < 16 ? r + 1 : r]);
-    }
-    const float m = __builtin_elementwise_maximum(m0, m1);
+    for (int i = 0; i < 2 * G::KS; ++i)
+      sacc[i & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rd_a(0, i), bfrag[i >> 1], sacc[i & 1], 0, 0, 0);
+  };
+  auto half_max = [&](const f32x16* sacc) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < 32; k += 2)
+      m = __builtin_elementwise_maximum(__builtin_elementwise_maximum(m, sacc[k >> 4][k & 15]),
+                                        sacc[(k + 1) >> 4][(k + 1) & 15]);
     return __builtin_elementwise_maximum(m, __shfl_xor(m, 32, kWave));
   };
 
   const int pre = ntiles < kRingStages ? ntiles : kRingStages;
   for (int t = 0; t < pre; ++t) issue(t);
   f32x16 sa[2], sb[2];
-  float mx = -INFINITY;
+  float mx = -INFINITY;  // max of the scores waiting in sc (rows pass)
   if (ntiles > 0) {
     wait_tiles(pre - 1);  // tile 0 landed
     __builtin_amdgcn_s_barrier();
-    scores(0, sa);
-    if constexpr (MODE == 0) mx = tile_max(sa);
+    scores_plain(sa);
+    if constexpr (MODE == 0) mx = half_max(sa);
   }
 
-  // One tile: sc holds S(tile) (log2 units), sn receives S(tile+1).
-  auto step = [&](int tile, f32x16* sc, f32x16* sn) {
+  constexpr int NS = 2 * G::KS;  // score MFMAs per tile
+  constexpr int NP = 4 * G::DT;  // P.V MFMAs per tile
+#ifndef TT_IB_AHEAD
+#define TT_IB_AHEAD 3
+#endif
+  constexpr int AHEAD = TT_IB_AHEAD;  // fragment reads in flight
+  constexpr int EPS = 32 / NS;   // scores exponentiated per score step
+  constexpr int EPP = 32 / NP;   // row-sum terms per P.V step
+  constexpr int MX0 = NP / 2;    // P.V steps from which the next max runs
+  constexpr int EMX = 32 / (NP - MX0);
+
+  // One tile: sc holds S(tile), sn receives S(tile+1); STG = tile % 4.
+  auto step = [&](auto stg, int tile, f32x16* sc, f32x16* sn) {
+    constexpr int STG = decltype(stg)::value;
+    constexpr int NXT = (STG + 1) % kRingStages;
     if constexpr (MODE == 0) {
       if (__any(mx > m_run + kLazyRescale)) {
         const float m_new = __builtin_elementwise_maximum(m_run, mx);
-        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * kLog2e);
         l_run *= alpha;
 #pragma unroll
         for (int dt = 0; dt < G::DT; ++dt)
@@ -329,63 +354,86 @@ __global__ void __launch_bounds__(kThreads) inbatch_pipe_kernel(const PassArgs a
       wait_tiles(pre - 2);
       __builtin_amdgcn_s_barrier();
     }
-
-    // Region A: next scores || exp + pack of this tile.  (After the last
-    // tile the look-ahead reads a stale stage: harmless, never used.)
-    scores(tile + 1, sn);
-    const float mb = (MODE == 0) ? m_run : 0.0f;
+    // (after the last tile the look-ahead reads a stale stage: harmless, unused)
+    bf16x8 fr[AHEAD + 1];
+    auto prefetch = [&](int idx) {  // idx over the tile's NS + NP fragment reads
+      if (idx < NS) fr[idx % (AHEAD + 1)] = rd_a(NXT, idx);
+      else if (idx < NS + NP) fr[idx % (AHEAD + 1)] = rd_t(STG, idx - NS);
+    };
+    rd_bias(NXT, sn);
+#pragma unroll
+    for (int i = 0; i < AHEAD; ++i) prefetch(i);
+    const float mb = (MODE == 0) ? m_run * kLog2e : 0.0f;
     bf16x8 pf[4];
+    __builtin_amdgcn_sched_barrier(0);
+
+    // Region A: S(tile+1) MFMAs || p = exp2(s log2e - m log2e), bf16 pack.
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int i = 0; i < NS; ++i) {
+      prefetch(i + AHEAD);
+      sn[i & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[i % (AHEAD + 1)], bfrag[i >> 1], sn[i & 1], 0, 0, 0);
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        float p[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) p[j] = __builtin_amdgcn_exp2f(sc[t][8 * s2 + j] - mb);
-        u32x4 pk;
-        pk.x = pack_bf16x2(p[0], p[1]);
-        pk.y = pack_bf16x2(p[2], p[3]);
-        pk.z = pack_bf16x2(p[4], p[5]);
-        pk.w = pack_bf16x2(p[6], p[7]);
-        pf[2 * t + s2] = __builtin_bit_cast(bf16x8, pk);
-        if constexpr (MODE == 0) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) l_run += p[j];
+      for (int k = i * EPS; k < (i + 1) * EPS; ++k) {
+        sc[k >> 4][k & 15] = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[k >> 4][k & 15], kLog2e, -mb));
+        if ((k & 7) == 7) {
+          const int g = k >> 3, t = g >> 1, b = 8 * (g & 1);
+          u32x4 pk;
+          pk.x = pack_bf16x2(sc[t][b + 0], sc[t][b + 1]);
+          pk.y = pack_bf16x2(sc[t][b + 2], sc[t][b + 3]);
+          pk.z = pack_bf16x2(sc[t][b + 4], sc[t][b + 5]);
+          pk.w = pack_bf16x2(sc[t][b + 6], sc[t][b + 7]);
+          pf[g] = __builtin_bit_cast(bf16x8, pk);
         }
       }
+      __builtin_amdgcn_sched_barrier(0);
+    }
 
-    // Region B: P.V of this tile || the next tile's max.
-    const char* B = ring + (tile % kRingStages) * G::STAGE_BYTES;
+    // Region B: O^T += X^T . P^T of this tile || row sums, next tile's max.
+    float mxa = -INFINITY;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int j = 0; j < NP; ++j) {
+      prefetch(NS + j + AHEAD);
+      o[j % G::DT] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[(NS + j) % (AHEAD + 1)], pf[j / G::DT], o[j % G::DT],
+                                                              0, 0, 0);
+      if constexpr (MODE == 0) {
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
+        for (int k = j * EPP; k < (j + 1) * EPP; ++k) l_run += sc[k >> 4][k & 15];
+        asm volatile("" : "+v"(l_run));  // keep the adds here (else sunk past the loop)
+        if (j >= MX0) {
 #pragma unroll
-        for (int dt = 0; dt < G::DT; ++dt) {
-          const int e = 32 * dt + l32;
-          const bf16x8 tf = *reinterpret_cast<const bf16x8*>(B + G::A_BYTES + t_off(e, 4 * t + 2 * s2 + h));
-          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tf, pf[2 * t + s2], o[dt], 0, 0, 0);
+          for (int k = (j - MX0) * EMX; k < (j - MX0 + 1) * EMX; k += 2)
+            mxa = __builtin_elementwise_maximum(__builtin_elementwise_maximum(mxa, sn[k >> 4][k & 15]),
+                                                sn[(k + 1) >> 4][(k + 1) & 15]);
         }
-    if constexpr (MODE == 0) mx = tile_max(sn);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (MODE == 0) mx = __builtin_elementwise_maximum(mxa, __shfl_xor(mxa, 32, kWave));
 
     // Ring: tile+2 resident for the next step, this tile's stage free.
     if (tile + 2 < ntiles) {
+#ifndef TT_IB_PROBE_NOVMWAIT
       wait_tiles(tile + 3 < ntiles ? 1 : 0);
+#endif
+#ifndef TT_IB_PROBE_NOBARRIER
       __builtin_amdgcn_s_barrier();
+#endif
       if (tile + kRingStages < ntiles) issue(tile + kRingStages);
     }
   };
-  // Unrolled by two so the S(t) / S(t+1) register sets swap roles without copies.
-  for (int tile = 0; tile < ntiles; tile += 2) {
-    step(tile, sa, sb);
-    if (tile + 1 < ntiles) step(tile + 1, sb, sa);
+  // Unrolled by the ring period: every LDS offset is a compile-time constant.
+  for (int tile = 0; tile < ntiles; tile += 4) {
+    step(std::integral_constant<int, 0>(), tile, sa, sb);
+    if (tile + 1 < ntiles) step(std::integral_constant<int, 1>(), tile + 1, sb, sa);
+    if (tile + 2 < ntiles) step(std::integral_constant<int, 2>(), tile + 2, sa, sb);
+    if (tile + 3 < ntiles) step(std::integral_constant<int, 3>(), tile + 3, sb, sa);
   }
 
   const int64_t prow = static_cast<int64_t>(split) * a.n_stat_pad + stat_row;
   if constexpr (MODE == 0) {
     const float l_tot = l_run + __shfl_xor(l_run, 32, kWave);
     if (h == 0) {
-      a.part_m[prow] = m_run * kLn2;  // natural-log units for the combine
+      a.part_m[prow] = m_run;
       a.part_l[prow] = l_tot;
     }
   }
@@ -395,10 +443,8 @@ __global__ void __launch_bounds__(kThreads) inbatch_pipe_kernel(const PassArgs a
 #pragma unroll
     for (int r4 = 0; r4 < 4; ++r4) {
       f32x4 v;
-      v[0] = o[dt][4 * r4 + 0];
-      v[1] = o[dt][4 * r4 + 1];
-      v[2] = o[dt][4 * r4 + 2];
-      v[3] = o[dt][4 * r4 + 3];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = o[dt][4 * r4 + u];
       *reinterpret_cast<f32x4*>(po + 32 * dt + 8 * r4 + 4 * h) = v;
     }
 }
@@ -434,7 +480,7 @@ __global__ void __launch_bounds__(256) combine_rows_kernel(
     const float pos_logit = dot - (logq ? logq[pos] : 0.0f);
     lse_out[i] = lse;
     loss_out[i] = lse - pos_logit;
-    if (neg_lse_bias) neg_lse_bias[i] = -kLog2e * lse;
+    if (neg_lse_bias) neg_lse_bias[i] = -lse;
   }
 }
 
@@ -498,7 +544,6 @@ Plan make_plan(int64_t n_stat, int64_t n_strm, int dim) {
 struct PassWs {
   __bf16* stat;
   __bf16* strm;
-  __bf16* strmT;
   float* bias;
   float* part_m;
   float* part_l;
@@ -509,7 +554,6 @@ PassWs carve_pass(Carver& cv, const Plan& p) {
   PassWs w;
   w.stat = cv.take<__bf16>(p.stat_pad * p.D);
   w.strm = cv.take<__bf16>(p.strm_pad * p.D);
-  w.strmT = cv.take<__bf16>(p.strm_pad * p.D);
   w.bias = cv.take<float>(p.strm_pad);
   w.part_m = cv.take<float>(int64_t(p.split) * p.stat_pad);
   w.part_l = cv.take<float>(int64_t(p.split) * p.stat_pad);
@@ -524,20 +568,17 @@ size_t pass_bytes(int64_t n_stat, int64_t n_strm, int dim) {
 }
 
 template <int D>
-int launch_prep(const float* src, int64_t ld, int64_t n, int dim, int64_t n_pad, float scale, __bf16* dst,
-                __bf16* dstT, hipStream_t st) {
-  hipLaunchKernelGGL(prep_kernel<D>, dim3(n_pad / 64), dim3(256), 0, st, src, ld, n, dim, n_pad, scale, dst, dstT);
+int launch_prep(const float* src, int64_t ld, int64_t n, int dim, int64_t n_pad, __bf16* dst, hipStream_t st) {
+  hipLaunchKernelGGL(prep_kernel<D>, dim3(n_pad / 64), dim3(256), 0, st, src, ld, n, dim, dst);
   TT_CHECK_LAUNCH();
   return TT_OK;
 }
 
-// scale applies to the row-major image only (log2(e) for q, 1 for c).
-int prep(int D, const float* src, int64_t ld, int64_t n, int dim, int64_t n_pad, float scale, __bf16* dst,
-         __bf16* dstT, hipStream_t st) {
+int prep(int D, const float* src, int64_t ld, int64_t n, int dim, int64_t n_pad, __bf16* dst, hipStream_t st) {
   switch (D) {
-    case 32: return launch_prep<32>(src, ld, n, dim, n_pad, scale, dst, dstT, st);
-    case 64: return launch_prep<64>(src, ld, n, dim, n_pad, scale, dst, dstT, st);
-    default: return launch_prep<128>(src, ld, n, dim, n_pad, scale, dst, dstT, st);
+    case 32: return launch_prep<32>(src, ld, n, dim, n_pad, dst, st);
+    case 64: return launch_prep<64>(src, ld, n, dim, n_pad, dst, st);
+    default: return launch_prep<128>(src, ld, n, dim, n_pad, dst, st);
   }
 }
 
@@ -545,11 +586,11 @@ template <int D, int MODE>
 int launch_pass_d(dim3 grid, const PassArgs& a, hipStream_t st) {
   constexpr int shm = Geo<D>::LDS_BYTES;
   if (shm > 65536) {
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(inbatch_pipe_kernel<D, MODE>),
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(inbatch_pass_kernel<D, MODE>),
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, shm);
     TT_CHECK_HIP(attr);
   }
-  hipLaunchKernelGGL((inbatch_pipe_kernel<D, MODE>), grid, dim3(kThreads), shm, st, a);
+  hipLaunchKernelGGL((inbatch_pass_kernel<D, MODE>), grid, dim3(kThreads), shm, st, a);
   TT_CHECK_LAUNCH();
   return TT_OK;
 }
@@ -606,12 +647,12 @@ extern "C" int tt_inbatch_xent_rows(const float* q, int64_t ldq, int64_t n_rows,
   if (!workspace || cv.used() > workspace_bytes)
     return fail(TT_ERR_WORKSPACE, "tt_inbatch_xent_rows: workspace %zu < required %zu", workspace_bytes, cv.used());
   hipStream_t st = to_stream(stream);
-  if ((rc = prep(p.D, q, ldq, n_rows, dim, p.stat_pad, kLog2e, w.stat, nullptr, st))) return rc;
-  if ((rc = prep(p.D, c, ldc, n_cols, dim, p.strm_pad, 1.0f, w.strm, w.strmT, st))) return rc;
+  if ((rc = prep(p.D, q, ldq, n_rows, dim, p.stat_pad, w.stat, st))) return rc;
+  if ((rc = prep(p.D, c, ldc, n_cols, dim, p.strm_pad, w.strm, st))) return rc;
   hipLaunchKernelGGL(bias_kernel, dim3(ceil_div(p.strm_pad, 256)), dim3(256), 0, st, logq, n_cols, p.strm_pad,
-                     -kLog2e, -INFINITY, w.bias);
+                     -1.0f, -INFINITY, w.bias);
   TT_CHECK_LAUNCH();
-  PassArgs a{w.stat, w.strm, w.strmT, w.bias, p.stat_pad, p.strm_pad, p.per_split, w.part_m, w.part_l, w.part_o};
+  PassArgs a{w.stat, w.strm, w.bias, p.stat_pad, p.strm_pad, p.per_split, w.part_m, w.part_l, w.part_o};
   if ((rc = launch_pass<0>(p, a, st))) return rc;
   hipLaunchKernelGGL(combine_rows_kernel, dim3(ceil_div(n_rows, 4)), dim3(256), 0, st, w.part_m, w.part_l,
                      w.part_o, p.split, p.stat_pad, p.D, q, ldq, c, ldc, logq, n_rows, dim, pos_offset, lse,
@@ -636,12 +677,12 @@ extern "C" int tt_inbatch_xent_cols(const float* q, int64_t ldq, int64_t n_rows,
   if (!workspace || cv.used() > workspace_bytes)
     return fail(TT_ERR_WORKSPACE, "tt_inbatch_xent_cols: workspace %zu < required %zu", workspace_bytes, cv.used());
   hipStream_t st = to_stream(stream);
-  if ((rc = prep(p.D, c, ldc, n_cols, dim, p.stat_pad, 1.0f, w.stat, nullptr, st))) return rc;
-  if ((rc = prep(p.D, q, ldq, n_rows, dim, p.strm_pad, kLog2e, w.strm, w.strmT, st))) return rc;
+  if ((rc = prep(p.D, c, ldc, n_cols, dim, p.stat_pad, w.stat, st))) return rc;
+  if ((rc = prep(p.D, q, ldq, n_rows, dim, p.strm_pad, w.strm, st))) return rc;
   hipLaunchKernelGGL(bias_kernel, dim3(ceil_div(p.strm_pad, 256)), dim3(256), 0, st, lse, n_rows, p.strm_pad,
-                     -kLog2e, -INFINITY, w.bias);
+                     -1.0f, -INFINITY, w.bias);
   TT_CHECK_LAUNCH();
-  PassArgs a{w.stat, w.strm, w.strmT, w.bias, p.stat_pad, p.strm_pad, p.per_split, nullptr, nullptr, w.part_o};
+  PassArgs a{w.stat, w.strm, w.bias, p.stat_pad, p.strm_pad, p.per_split, nullptr, nullptr, w.part_o};
   if ((rc = launch_pass<1>(p, a, st))) return rc;
   hipLaunchKernelGGL(combine_cols_kernel, dim3(ceil_div(n_cols, 4)), dim3(256), 0, st, w.part_o, p.split,
                      p.stat_pad, p.D, q, ldq, logq, n_cols, dim, pos_offset, dc);
@@ -651,12 +692,12 @@ extern "C" int tt_inbatch_xent_cols(const float* q, int64_t ldq, int64_t n_rows,
 
 // ---------------------------------------------------------------------------
 // Single-device fused loss: rows and cols passes share one bf16 preparation of
-// q and c (row-major + transposed images), the cols pass's -lse bias is
+// q and c (one row-major image each), the cols pass's -lse bias is
 // written by the rows combine.  7 launches in total.
 namespace tt {
 namespace {
 struct FusedWs {
-  __bf16 *qb, *qbT, *cb, *cbT;
+  __bf16 *qb, *cb;
   float *bias_logq, *bias_lse;
   float *part_m, *part_l, *part_o_rows, *part_o_cols;
 };
@@ -677,9 +718,7 @@ FusedPlan fused_plan(int64_t n, int dim) {
 FusedWs carve_fused(Carver& cv, const FusedPlan& p) {
   FusedWs w;
   w.qb = cv.take<__bf16>(p.n_pad * p.D);
-  w.qbT = cv.take<__bf16>(p.n_pad * p.D);
   w.cb = cv.take<__bf16>(p.n_pad * p.D);
-  w.cbT = cv.take<__bf16>(p.n_pad * p.D);
   w.bias_logq = cv.take<float>(p.n_pad);
   w.bias_lse = cv.take<float>(p.n_pad);
   w.part_m = cv.take<float>(int64_t(p.split) * p.n_pad);
@@ -712,18 +751,18 @@ extern "C" int tt_inbatch_softmax_xent(const float* q, int64_t ldq, const float*
     return fail(TT_ERR_WORKSPACE, "tt_inbatch_softmax_xent: workspace %zu < required %zu", workspace_bytes,
                 cv.used());
   hipStream_t st = to_stream(stream);
-  if ((rc = prep(p.D, q, ldq, n, dim, p.n_pad, kLog2e, w.qb, w.qbT, st))) return rc;
-  if ((rc = prep(p.D, c, ldc, n, dim, p.n_pad, 1.0f, w.cb, w.cbT, st))) return rc;
+  if ((rc = prep(p.D, q, ldq, n, dim, p.n_pad, w.qb, st))) return rc;
+  if ((rc = prep(p.D, c, ldc, n, dim, p.n_pad, w.cb, st))) return rc;
   hipLaunchKernelGGL(dual_bias_kernel, dim3(ceil_div(p.n_pad, 256)), dim3(256), 0, st, logq, n, p.n_pad, w.bias_logq,
                      w.bias_lse);
   TT_CHECK_LAUNCH();
   const Plan pl{p.D, p.n_pad, p.n_pad, p.split, p.per_split};
-  PassArgs ar{w.qb, w.cb, w.cbT, w.bias_logq, p.n_pad, p.n_pad, p.per_split, w.part_m, w.part_l, w.part_o_rows};
+  PassArgs ar{w.qb, w.cb, w.bias_logq, p.n_pad, p.n_pad, p.per_split, w.part_m, w.part_l, w.part_o_rows};
   if ((rc = launch_pass<0>(pl, ar, st))) return rc;
   hipLaunchKernelGGL(combine_rows_kernel, dim3(ceil_div(n, 4)), dim3(256), 0, st, w.part_m, w.part_l, w.part_o_rows,
                      p.split, p.n_pad, p.D, q, ldq, c, ldc, logq, n, dim, (int64_t)0, lse, row_loss, dq, w.bias_lse);
   TT_CHECK_LAUNCH();
-  PassArgs ac{w.cb, w.qb, w.qbT, w.bias_lse, p.n_pad, p.n_pad, p.per_split, nullptr, nullptr, w.part_o_cols};
+  PassArgs ac{w.cb, w.qb, w.bias_lse, p.n_pad, p.n_pad, p.per_split, nullptr, nullptr, w.part_o_cols};
   if ((rc = launch_pass<1>(pl, ac, st))) return rc;
   hipLaunchKernelGGL(combine_cols_kernel, dim3(ceil_div(n, 4)), dim3(256), 0, st, w.part_o_cols, p.split, p.n_pad,
                      p.D, q, ldq, logq, n, dim, (int64_t)0, dc);
