@@ -80,42 +80,57 @@ __device__ __forceinline__ int a_off(int row, int ch) {
 }
 
 // ---------------------------------------------------------------------------
-// Prep: fp32 [n, ld] -> bf16 [n_pad, D] (zero padded).  One block = 64 rows.
+// Prep: fp32 [n, ld] -> bf16 [n_pad, D] (zero padded), optionally with the
+// pass's per-row bias vector: bias[i] = sign * bv[i] (0 if bv NULL) for i < n
+// and -inf for padded rows; bias2 (if set) gets -inf on padded rows (its
+// [0, n) is written later by combine_rows).  One launch preps up to two
+// matrices (blockIdx.y); one block = 32 rows, 8 elements per thread.
+struct PrepJob {
+  const float* src;
+  int64_t ld;
+  int64_t n;
+  __bf16* dst;
+  const float* bv;
+  float sign;
+  float* bias;
+  float* bias2;
+  int vec;  // src 16-B aligned, ld % 4 == 0, dim % 4 == 0: float4 loads
+};
+
 template <int D>
-__global__ void __launch_bounds__(256) prep_kernel(const float* __restrict__ src, int64_t ld, int64_t n,
-                                                   int dim, __bf16* __restrict__ dst) {
-  const int64_t r0 = blockIdx.x * 64ll;
-  for (int i = threadIdx.x; i < 64 * D / 8; i += 256) {
-    const int r = i / (D / 8), c8 = (i % (D / 8)) * 8;
-    const int64_t gr = r0 + r;
+__global__ void __launch_bounds__(256) prep_kernel(PrepJob j0, PrepJob j1, int dim) {
+  const PrepJob& j = blockIdx.y ? j1 : j0;
+  const int64_t r0 = blockIdx.x * 32ll;
+  constexpr int TPR = D / 8;  // threads per row
+  for (int i = threadIdx.x; i < 32 * TPR; i += 256) {
+    const int64_t r = r0 + i / TPR;
+    const int c8 = (i % TPR) * 8;
     float x[8];
+    if (r < j.n && j.vec) {
+      const float* row = j.src + r * j.ld + c8;
+      const f32x4 lo = c8 < dim ? *reinterpret_cast<const f32x4*>(row) : f32x4{0, 0, 0, 0};
+      const f32x4 hi = c8 + 4 < dim ? *reinterpret_cast<const f32x4*>(row + 4) : f32x4{0, 0, 0, 0};
 #pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] = (gr < n && c8 + j < dim) ? src[gr * ld + c8 + j] : 0.0f;
+      for (int u = 0; u < 4; ++u) {
+        x[u] = lo[u];
+        x[4 + u] = hi[u];
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = (r < j.n && c8 + u < dim) ? j.src[r * j.ld + c8 + u] : 0.0f;
+    }
     u32x4 v;
     v.x = pack_bf16x2(x[0], x[1]);
     v.y = pack_bf16x2(x[2], x[3]);
     v.z = pack_bf16x2(x[4], x[5]);
     v.w = pack_bf16x2(x[6], x[7]);
-    *reinterpret_cast<u32x4*>(dst + gr * D + c8) = v;
+    *reinterpret_cast<u32x4*>(j.dst + r * D + c8) = v;
   }
-}
-
-// bias[i] = sign * v[i] (v may be NULL -> 0) for i < n; pad value beyond.
-__global__ void bias_kernel(const float* __restrict__ v, int64_t n, int64_t n_pad, float sign, float pad,
-                            float* __restrict__ out) {
-  const int64_t i = blockIdx.x * 256ll + threadIdx.x;
-  if (i >= n_pad) return;
-  out[i] = (i < n) ? (v ? sign * v[i] : 0.0f) : pad;
-}
-
-// bias1[i] = -logq[i] (0 if logq NULL) for i < n, -inf for n <= i < n_pad;
-// bias2[i] = -inf for n <= i < n_pad (its [0, n) is written by combine_rows).
-__global__ void dual_bias_kernel(const float* __restrict__ logq, int64_t n, int64_t n_pad, float* __restrict__ bias1,
-                                 float* __restrict__ bias2) {
-  const int64_t i = blockIdx.x * 256ll + threadIdx.x;
-  if (i >= n_pad) return;
-  bias1[i] = (i < n) ? (logq ? -logq[i] : 0.0f) : -INFINITY;
-  if (i >= n) bias2[i] = -INFINITY;
+  if (j.bias && threadIdx.x < 32) {
+    const int64_t r = r0 + threadIdx.x;
+    j.bias[r] = (r < j.n) ? (j.bv ? j.sign * j.bv[r] : 0.0f) : -INFINITY;
+    if (j.bias2 && r >= j.n) j.bias2[r] = -INFINITY;
+  }
 }
 
 struct PassArgs {
@@ -449,34 +464,46 @@ __global__ void __launch_bounds__(kThreads) inbatch_pass_kernel(const PassArgs a
     }
 }
 
-// Rows combine: one wave per row.  lse, row loss, dq.
+// Split combines: D/4 lanes per row (float4 partials), 1024/D rows per block.
+// Rows: lse, row loss, dq = O / L - c_pos (and -lse as the cols-pass bias).
+template <int D>
 __global__ void __launch_bounds__(256) combine_rows_kernel(
     const float* __restrict__ part_m, const float* __restrict__ part_l, const float* __restrict__ part_o,
-    int nsplit, int64_t n_stat_pad, int D, const float* __restrict__ q, int64_t ldq, const float* __restrict__ c,
+    int nsplit, int64_t n_stat_pad, const float* __restrict__ q, int64_t ldq, const float* __restrict__ c,
     int64_t ldc, const float* __restrict__ logq, int64_t n_rows, int dim, int64_t pos_offset,
     float* __restrict__ lse_out, float* __restrict__ loss_out, float* __restrict__ dq,
     float* __restrict__ neg_lse_bias) {
-  const int64_t i = blockIdx.x * 4ll + threadIdx.x / kWave;
+  constexpr int LPR = D / 4;  // lanes per row
+  const int64_t i = blockIdx.x * (256ll / LPR) + threadIdx.x / LPR;
+  const int sub = threadIdx.x % LPR;
   if (i >= n_rows) return;
-  const int lane = lane_id();
   float M = -1.0e30f;
   for (int s = 0; s < nsplit; ++s) M = fmaxf(M, part_m[s * n_stat_pad + i]);
   float L = 0.0f;
-  for (int s = 0; s < nsplit; ++s) L += part_l[s * n_stat_pad + i] * expf(part_m[s * n_stat_pad + i] - M);
+  f32x4 o = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (int s = 0; s < nsplit; ++s) {
+    const float w = expf(part_m[s * n_stat_pad + i] - M);
+    L += part_l[s * n_stat_pad + i] * w;
+    const f32x4 ps = *reinterpret_cast<const f32x4*>(part_o + (s * n_stat_pad + i) * D + 4 * sub);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) o[u] += ps[u] * w;
+  }
   const float lse = M + logf(L);
+  const float inv = 1.0f / L;
   const int64_t pos = i + pos_offset;
   float dot = 0.0f;
-  for (int e = lane; e < dim; e += kWave) {
-    float oe = 0.0f;
-    for (int s = 0; s < nsplit; ++s)
-      oe += part_o[(s * n_stat_pad + i) * D + e] * expf(part_m[s * n_stat_pad + i] - M);
-    const float ce = c[pos * ldc + e];
-    if (dq) dq[i * dim + e] = oe / L - ce;
-    dot = __builtin_fmaf(q[i * ldq + e], ce, dot);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = 4 * sub + u;
+    if (e < dim) {
+      const float ce = c[pos * ldc + e];
+      if (dq) dq[i * dim + e] = o[u] * inv - ce;
+      dot = __builtin_fmaf(q[i * ldq + e], ce, dot);
+    }
   }
 #pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) dot += __shfl_xor(dot, m, kWave);
-  if (lane == 0) {
+  for (int m = LPR / 2; m >= 1; m >>= 1) dot += __shfl_xor(dot, m, LPR);
+  if (sub == 0) {
     const float pos_logit = dot - (logq ? logq[pos] : 0.0f);
     lse_out[i] = lse;
     loss_out[i] = lse - pos_logit;
@@ -484,21 +511,29 @@ __global__ void __launch_bounds__(256) combine_rows_kernel(
   }
 }
 
-// Cols combine: dc_j = exp(-logq_j) * sum_s O_s[j] - q_pos(j).
+// Cols: dc_j = exp(-logq_j) * sum_s O_s[j] - q_pos(j).
+template <int D>
 __global__ void __launch_bounds__(256) combine_cols_kernel(const float* __restrict__ part_o, int nsplit,
-                                                           int64_t n_stat_pad, int D, const float* __restrict__ q,
+                                                           int64_t n_stat_pad, const float* __restrict__ q,
                                                            int64_t ldq, const float* __restrict__ logq,
                                                            int64_t n_cols, int dim, int64_t pos_offset,
                                                            float* __restrict__ dc) {
-  const int64_t j = blockIdx.x * 4ll + threadIdx.x / kWave;
+  constexpr int LPR = D / 4;
+  const int64_t j = blockIdx.x * (256ll / LPR) + threadIdx.x / LPR;
+  const int sub = threadIdx.x % LPR;
   if (j >= n_cols) return;
-  const int lane = lane_id();
   const float scale = logq ? expf(-logq[j]) : 1.0f;
   const int64_t pos = j + pos_offset;
-  for (int e = lane; e < dim; e += kWave) {
-    float oe = 0.0f;
-    for (int s = 0; s < nsplit; ++s) oe += part_o[(s * n_stat_pad + j) * D + e];
-    dc[j * dim + e] = oe * scale - q[pos * ldq + e];
+  f32x4 o = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (int s = 0; s < nsplit; ++s) {
+    const f32x4 ps = *reinterpret_cast<const f32x4*>(part_o + (s * n_stat_pad + j) * D + 4 * sub);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) o[u] += ps[u];
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = 4 * sub + u;
+    if (e < dim) dc[j * dim + e] = o[u] * scale - q[pos * ldq + e];
   }
 }
 
@@ -510,7 +545,7 @@ int pick_dpad(int dim) {
 }
 
 #ifndef TT_INBATCH_WG_TARGET
-#define TT_INBATCH_WG_TARGET 256
+#define TT_INBATCH_WG_TARGET 512
 #endif
 // Splits of the streamed extent so that the grid has >= TT_INBATCH_WG_TARGET
 // workgroups (several per CU: two waves per SIMD hide each other's softmax).
@@ -567,19 +602,62 @@ size_t pass_bytes(int64_t n_stat, int64_t n_strm, int dim) {
   return cv.used();
 }
 
-template <int D>
-int launch_prep(const float* src, int64_t ld, int64_t n, int dim, int64_t n_pad, __bf16* dst, hipStream_t st) {
-  hipLaunchKernelGGL(prep_kernel<D>, dim3(n_pad / 64), dim3(256), 0, st, src, ld, n, dim, dst);
+PrepJob prep_job(const float* src, int64_t ld, int64_t n, int dim, __bf16* dst, const float* bv = nullptr,
+                 float* bias = nullptr, float* bias2 = nullptr) {
+  const int vec = (reinterpret_cast<uintptr_t>(src) % 16 == 0 && ld % 4 == 0 && dim % 4 == 0) ? 1 : 0;
+  return PrepJob{src, ld, n, dst, bv, -1.0f, bias, bias2, vec};
+}
+
+// Preps one or two matrices padded to n_pad rows (j1.src == NULL: one).
+int prep(int D, const PrepJob& j0, const PrepJob& j1, int dim, int64_t n_pad, hipStream_t st) {
+  const dim3 grid(static_cast<unsigned>(n_pad / 32), j1.src ? 2u : 1u);
+  switch (D) {
+    case 32: hipLaunchKernelGGL(prep_kernel<32>, grid, dim3(256), 0, st, j0, j1, dim); break;
+    case 64: hipLaunchKernelGGL(prep_kernel<64>, grid, dim3(256), 0, st, j0, j1, dim); break;
+    default: hipLaunchKernelGGL(prep_kernel<128>, grid, dim3(256), 0, st, j0, j1, dim); break;
+  }
   TT_CHECK_LAUNCH();
   return TT_OK;
 }
 
-int prep(int D, const float* src, int64_t ld, int64_t n, int dim, int64_t n_pad, __bf16* dst, hipStream_t st) {
+template <int D>
+void launch_combine_rows(dim3 grid, hipStream_t st, const float* pm, const float* pl, const float* po, int nsplit,
+                         int64_t n_stat_pad, const float* q, int64_t ldq, const float* c, int64_t ldc,
+                         const float* logq, int64_t n, int dim, int64_t pos_offset, float* lse, float* loss,
+                         float* dq, float* neg_lse) {
+  hipLaunchKernelGGL(combine_rows_kernel<D>, grid, dim3(256), 0, st, pm, pl, po, nsplit, n_stat_pad, q, ldq, c, ldc,
+                     logq, n, dim, pos_offset, lse, loss, dq, neg_lse);
+}
+
+int combine_rows(int D, hipStream_t st, const float* pm, const float* pl, const float* po, int nsplit,
+                 int64_t n_stat_pad, const float* q, int64_t ldq, const float* c, int64_t ldc, const float* logq,
+                 int64_t n, int dim, int64_t pos_offset, float* lse, float* loss, float* dq, float* neg_lse) {
+  const dim3 grid(static_cast<unsigned>(ceil_div(n, 1024 / D)));
   switch (D) {
-    case 32: return launch_prep<32>(src, ld, n, dim, n_pad, dst, st);
-    case 64: return launch_prep<64>(src, ld, n, dim, n_pad, dst, st);
-    default: return launch_prep<128>(src, ld, n, dim, n_pad, dst, st);
+    case 32: launch_combine_rows<32>(grid, st, pm, pl, po, nsplit, n_stat_pad, q, ldq, c, ldc, logq, n, dim,
+                                     pos_offset, lse, loss, dq, neg_lse); break;
+    case 64: launch_combine_rows<64>(grid, st, pm, pl, po, nsplit, n_stat_pad, q, ldq, c, ldc, logq, n, dim,
+                                     pos_offset, lse, loss, dq, neg_lse); break;
+    default: launch_combine_rows<128>(grid, st, pm, pl, po, nsplit, n_stat_pad, q, ldq, c, ldc, logq, n, dim,
+                                      pos_offset, lse, loss, dq, neg_lse); break;
   }
+  TT_CHECK_LAUNCH();
+  return TT_OK;
+}
+
+int combine_cols(int D, hipStream_t st, const float* po, int nsplit, int64_t n_stat_pad, const float* q,
+                 int64_t ldq, const float* logq, int64_t n, int dim, int64_t pos_offset, float* dc) {
+  const dim3 grid(static_cast<unsigned>(ceil_div(n, 1024 / D)));
+  switch (D) {
+    case 32: hipLaunchKernelGGL(combine_cols_kernel<32>, grid, dim3(256), 0, st, po, nsplit, n_stat_pad, q, ldq,
+                                logq, n, dim, pos_offset, dc); break;
+    case 64: hipLaunchKernelGGL(combine_cols_kernel<64>, grid, dim3(256), 0, st, po, nsplit, n_stat_pad, q, ldq,
+                                logq, n, dim, pos_offset, dc); break;
+    default: hipLaunchKernelGGL(combine_cols_kernel<128>, grid, dim3(256), 0, st, po, nsplit, n_stat_pad, q, ldq,
+                                logq, n, dim, pos_offset, dc); break;
+  }
+  TT_CHECK_LAUNCH();
+  return TT_OK;
 }
 
 template <int D, int MODE>
@@ -647,18 +725,13 @@ extern "C" int tt_inbatch_xent_rows(const float* q, int64_t ldq, int64_t n_rows,
   if (!workspace || cv.used() > workspace_bytes)
     return fail(TT_ERR_WORKSPACE, "tt_inbatch_xent_rows: workspace %zu < required %zu", workspace_bytes, cv.used());
   hipStream_t st = to_stream(stream);
-  if ((rc = prep(p.D, q, ldq, n_rows, dim, p.stat_pad, w.stat, st))) return rc;
-  if ((rc = prep(p.D, c, ldc, n_cols, dim, p.strm_pad, w.strm, st))) return rc;
-  hipLaunchKernelGGL(bias_kernel, dim3(ceil_div(p.strm_pad, 256)), dim3(256), 0, st, logq, n_cols, p.strm_pad,
-                     -1.0f, -INFINITY, w.bias);
-  TT_CHECK_LAUNCH();
+  const PrepJob none{};
+  if ((rc = prep(p.D, prep_job(q, ldq, n_rows, dim, w.stat), none, dim, p.stat_pad, st))) return rc;
+  if ((rc = prep(p.D, prep_job(c, ldc, n_cols, dim, w.strm, logq, w.bias), none, dim, p.strm_pad, st))) return rc;
   PassArgs a{w.stat, w.strm, w.bias, p.stat_pad, p.strm_pad, p.per_split, w.part_m, w.part_l, w.part_o};
   if ((rc = launch_pass<0>(p, a, st))) return rc;
-  hipLaunchKernelGGL(combine_rows_kernel, dim3(ceil_div(n_rows, 4)), dim3(256), 0, st, w.part_m, w.part_l,
-                     w.part_o, p.split, p.stat_pad, p.D, q, ldq, c, ldc, logq, n_rows, dim, pos_offset, lse,
-                     row_loss, dq, nullptr);
-  TT_CHECK_LAUNCH();
-  return TT_OK;
+  return combine_rows(p.D, st, w.part_m, w.part_l, w.part_o, p.split, p.stat_pad, q, ldq, c, ldc, logq, n_rows, dim,
+                      pos_offset, lse, row_loss, dq, nullptr);
 }
 
 extern "C" int tt_inbatch_xent_cols(const float* q, int64_t ldq, int64_t n_rows, const float* lse, const float* c,
@@ -677,23 +750,18 @@ extern "C" int tt_inbatch_xent_cols(const float* q, int64_t ldq, int64_t n_rows,
   if (!workspace || cv.used() > workspace_bytes)
     return fail(TT_ERR_WORKSPACE, "tt_inbatch_xent_cols: workspace %zu < required %zu", workspace_bytes, cv.used());
   hipStream_t st = to_stream(stream);
-  if ((rc = prep(p.D, c, ldc, n_cols, dim, p.stat_pad, w.stat, st))) return rc;
-  if ((rc = prep(p.D, q, ldq, n_rows, dim, p.strm_pad, w.strm, st))) return rc;
-  hipLaunchKernelGGL(bias_kernel, dim3(ceil_div(p.strm_pad, 256)), dim3(256), 0, st, lse, n_rows, p.strm_pad,
-                     -1.0f, -INFINITY, w.bias);
-  TT_CHECK_LAUNCH();
+  const PrepJob none{};
+  if ((rc = prep(p.D, prep_job(c, ldc, n_cols, dim, w.stat), none, dim, p.stat_pad, st))) return rc;
+  if ((rc = prep(p.D, prep_job(q, ldq, n_rows, dim, w.strm, lse, w.bias), none, dim, p.strm_pad, st))) return rc;
   PassArgs a{w.stat, w.strm, w.bias, p.stat_pad, p.strm_pad, p.per_split, nullptr, nullptr, w.part_o};
   if ((rc = launch_pass<1>(p, a, st))) return rc;
-  hipLaunchKernelGGL(combine_cols_kernel, dim3(ceil_div(n_cols, 4)), dim3(256), 0, st, w.part_o, p.split,
-                     p.stat_pad, p.D, q, ldq, logq, n_cols, dim, pos_offset, dc);
-  TT_CHECK_LAUNCH();
-  return TT_OK;
+  return combine_cols(p.D, st, w.part_o, p.split, p.stat_pad, q, ldq, logq, n_cols, dim, pos_offset, dc);
 }
 
 // ---------------------------------------------------------------------------
 // Single-device fused loss: rows and cols passes share one bf16 preparation of
 // q and c (one row-major image each), the cols pass's -lse bias is
-// written by the rows combine.  7 launches in total.
+// written by the rows combine.  5 launches in total.
 namespace tt {
 namespace {
 struct FusedWs {
@@ -751,21 +819,17 @@ extern "C" int tt_inbatch_softmax_xent(const float* q, int64_t ldq, const float*
     return fail(TT_ERR_WORKSPACE, "tt_inbatch_softmax_xent: workspace %zu < required %zu", workspace_bytes,
                 cv.used());
   hipStream_t st = to_stream(stream);
-  if ((rc = prep(p.D, q, ldq, n, dim, p.n_pad, w.qb, st))) return rc;
-  if ((rc = prep(p.D, c, ldc, n, dim, p.n_pad, w.cb, st))) return rc;
-  hipLaunchKernelGGL(dual_bias_kernel, dim3(ceil_div(p.n_pad, 256)), dim3(256), 0, st, logq, n, p.n_pad, w.bias_logq,
-                     w.bias_lse);
-  TT_CHECK_LAUNCH();
+  // one prep launch for both matrices; c's job also writes both bias vectors
+  if ((rc = prep(p.D, prep_job(q, ldq, n, dim, w.qb), prep_job(c, ldc, n, dim, w.cb, logq, w.bias_logq, w.bias_lse),
+                 dim, p.n_pad, st)))
+    return rc;
   const Plan pl{p.D, p.n_pad, p.n_pad, p.split, p.per_split};
   PassArgs ar{w.qb, w.cb, w.bias_logq, p.n_pad, p.n_pad, p.per_split, w.part_m, w.part_l, w.part_o_rows};
   if ((rc = launch_pass<0>(pl, ar, st))) return rc;
-  hipLaunchKernelGGL(combine_rows_kernel, dim3(ceil_div(n, 4)), dim3(256), 0, st, w.part_m, w.part_l, w.part_o_rows,
-                     p.split, p.n_pad, p.D, q, ldq, c, ldc, logq, n, dim, (int64_t)0, lse, row_loss, dq, w.bias_lse);
-  TT_CHECK_LAUNCH();
+  if ((rc = combine_rows(p.D, st, w.part_m, w.part_l, w.part_o_rows, p.split, p.n_pad, q, ldq, c, ldc, logq, n, dim,
+                         0, lse, row_loss, dq, w.bias_lse)))
+    return rc;
   PassArgs ac{w.cb, w.qb, w.bias_lse, p.n_pad, p.n_pad, p.per_split, nullptr, nullptr, w.part_o_cols};
   if ((rc = launch_pass<1>(pl, ac, st))) return rc;
-  hipLaunchKernelGGL(combine_cols_kernel, dim3(ceil_div(n, 4)), dim3(256), 0, st, w.part_o_cols, p.split, p.n_pad,
-                     p.D, q, ldq, logq, n, dim, (int64_t)0, dc);
-  TT_CHECK_LAUNCH();
-  return TT_OK;
+  return combine_cols(p.D, st, w.part_o_cols, p.split, p.n_pad, q, ldq, logq, n, dim, 0, dc);
 }
