@@ -52,10 +52,13 @@ constexpr int kTablesPerLaunch = 16;
 constexpr int kThreads = 256;
 constexpr int kPFJoin = 32;           // pieces loaded per batch in join
 constexpr int64_t kMaxLookups = int64_t(1) << 24;
+constexpr int kSrcShift = 28;  // sorted values: source << 28 | batch row (batch < 2^28)
 
 struct TableDesc {
   const int32_t* ids[TT_MAX_SOURCES];
-  int32_t goff[TT_MAX_SOURCES];
+  int32_t goff[TT_MAX_SOURCES];  // source column offsets in the table's grad
+  const float* grad;             // the table's gradient rows (call grad or per-table override)
+  int32_t gld;                   // its row stride (floats)
   float* table;
   float* slot0;
   float* slot1;
@@ -75,8 +78,6 @@ struct Job {
   int32_t num;
   int32_t id_bits;
   int64_t batch;
-  const float* grad;
-  int64_t grad_stride;
   uint32_t* keys_in;
   uint32_t* vals_in;
   const uint32_t* keys;  // sorted
@@ -117,9 +118,10 @@ __global__ void __launch_bounds__(kThreads) build_keys_kernel(const Job j, int t
   uint32_t id = invalid, val = 0xFFFFFFFFu;
   if (loc < T.n) {
     const int s = static_cast<int>(loc / j.batch);
-    const int32_t r = T.ids[s][loc - s * j.batch];
+    const int64_t b = loc - s * j.batch;
+    const int32_t r = T.ids[s][b];
     id = (r >= 0 && r < T.num_rows) ? static_cast<uint32_t>(r) : invalid;
-    val = static_cast<uint32_t>(loc);
+    val = (static_cast<uint32_t>(s) << kSrcShift) | static_cast<uint32_t>(b);  // source | batch row
   }
   j.keys_in[i] = (static_cast<uint32_t>(t) << j.id_bits) | id;
   j.vals_in[i] = val;
@@ -175,7 +177,8 @@ __device__ __forceinline__ void apply_row(const Job& j, const TableDesc& T, cons
 // 3. per block of kBlock sorted lookups: piece sums; complete segments applied.
 template <int OP>
 __global__ void __launch_bounds__(kThreads) block_sum_kernel(const Job j, const ApplyParams ap) {
-  const int gw = blockIdx.x * (kThreads / kWave) + threadIdx.x / kWave;
+  // wave-uniform (readfirstlane): the table descriptor is then read with scalar loads
+  const int gw = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x * (kThreads / kWave) + threadIdx.x / kWave));
   const int t = table_of_wave(j, gw);
   const TableDesc& T = j.t[t];
   const int P = T.lanes;
@@ -195,15 +198,19 @@ __global__ void __launch_bounds__(kThreads) block_sum_kernel(const Job j, const 
   const uint32_t kprev = blk > 0 ? j.keys[b0 - 1] : ~0u;
   const uint32_t knext = b0 + kBlock < tend ? j.keys[b0 + kBlock] : ~0u;
   // grad offsets (validated to fit 32 bits) and the segment structure; both are
-  // the same for every column this lane visits.
+  // the same for every column this lane visits.  The table's source offsets
+  // are read ONCE into registers (indexing T.goff[] by a per-lane source made
+  // the compiler re-load it from the kernarg block with a full wait per row).
+  const uint32_t gld = static_cast<uint32_t>(T.gld);
+  const uint32_t go0 = T.goff[0], go1 = T.goff[1], go2 = T.goff[2], go3 = T.goff[3];
+  const float* __restrict__ grad = T.grad;
   uint32_t ends = 0, apply = 0;
 #pragma unroll
   for (int r = 0; r < kBlock; ++r) {
-    if (off[r] != 0xFFFFFFFFu) {
-      const uint32_t s = off[r] / static_cast<uint32_t>(j.batch);
-      const uint32_t b = off[r] - s * static_cast<uint32_t>(j.batch);
-      off[r] = b * static_cast<uint32_t>(j.grad_stride) + static_cast<uint32_t>(T.goff[s]);
-    }
+    const uint32_t s = off[r] >> kSrcShift;
+    const uint32_t b = off[r] & ((1u << kSrcShift) - 1u);
+    const uint32_t o = b * gld + (s == 0 ? go0 : s == 1 ? go1 : s == 2 ? go2 : go3);
+    off[r] = off[r] != 0xFFFFFFFFu ? o : 0xFFFFFFFFu;
     if (r == kBlock - 1 || key[r + 1] != key[r]) ends |= 1u << r;
   }
   const bool head_cont = key[0] == kprev;
@@ -224,7 +231,7 @@ __global__ void __launch_bounds__(kThreads) block_sum_kernel(const Job j, const 
   for (int col = lane % P; col < T.dim; col += P) {
     float v[kBlock];
 #pragma unroll
-    for (int r = 0; r < kBlock; ++r) v[r] = off[r] != 0xFFFFFFFFu ? j.grad[off[r] + col] : 0.0f;
+    for (int r = 0; r < kBlock; ++r) v[r] = off[r] != 0xFFFFFFFFu ? grad[off[r] + col] : 0.0f;
     // segment sums, left in v[r] at each segment's last row
     float acc = 0.0f;
     int seg_begin = 0;
@@ -262,7 +269,8 @@ __global__ void __launch_bounds__(kThreads) block_sum_kernel(const Job j, const 
 // 4. segments spanning blocks: the block where one starts adds the pieces.
 template <int OP>
 __global__ void __launch_bounds__(kThreads) join_kernel(const Job j, const ApplyParams ap) {
-  const int gw = blockIdx.x * (kThreads / kWave) + threadIdx.x / kWave;
+  // wave-uniform (readfirstlane): the table descriptor is then read with scalar loads
+  const int gw = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x * (kThreads / kWave) + threadIdx.x / kWave));
   const int t = table_of_wave(j, gw);
   const TableDesc& T = j.t[t];
   const int P = T.lanes;
@@ -375,7 +383,10 @@ struct Plan {
   int end_bit;
 };
 
-int make_plan(const tt_sparse_table* tables, int cnt, int64_t batch, Plan* p) {
+// grad / grad_stride: the call's gradient (tables may override it); NULL for
+// a workspace-size query.
+int make_plan(const tt_sparse_table* tables, int cnt, int64_t batch, const float* grad, int64_t grad_stride,
+              Plan* p, bool size_query = false) {
   Job& j = p->job;
   j = Job{};
   j.num = cnt;
@@ -396,6 +407,14 @@ int make_plan(const tt_sparse_table* tables, int cnt, int64_t batch, Plan* p) {
       T.ids[q] = (q < s.num_sources) ? s.ids[q] : nullptr;
       T.goff[q] = (q < s.num_sources) ? s.grad_col_offset[q] : 0;
     }
+    T.grad = s.grad ? s.grad : grad;
+    T.gld = static_cast<int32_t>(s.grad ? s.grad_ld : grad_stride);
+    if (batch > 0 && !T.grad && !size_query) return fail(TT_ERR_BAD_ARG, "sparse: table %d has no gradient (NULL grad)", i);
+    int32_t max_off = 0;
+    for (int q = 0; q < s.num_sources; ++q) max_off = std::max(max_off, s.grad_col_offset[q]);
+    const int64_t gld = s.grad ? s.grad_ld : grad_stride;
+    if (gld < 0 || max_off < 0 || (batch > 0 && (batch - 1) * gld + max_off + s.dim >= (int64_t(1) << 31)))
+      return fail(TT_ERR_UNSUPPORTED, "sparse: table %d gradient rows exceed 2^31 floats", i);
     T.table = s.table;
     T.slot0 = s.slot0;
     T.slot1 = s.slot1;
@@ -471,7 +490,7 @@ size_t tables_ws_bytes(const tt_sparse_table* tables, int32_t num_tables, int64_
   for (int first = 0; first < num_tables; first += kTablesPerLaunch) {
     const int cnt = std::min(num_tables - first, kTablesPerLaunch);
     Plan p;
-    if (make_plan(tables + first, cnt, batch, &p)) return 0;
+    if (make_plan(tables + first, cnt, batch, nullptr, 0, &p, true)) return 0;
     Carver cv(nullptr, 0);
     carve_plan(cv, p, dense_dim);
     total = std::max(total, cv.used());
@@ -483,21 +502,17 @@ template <int OP>
 int run_sparse(const tt_sparse_table* tables, int32_t num_tables, int64_t batch, const float* grad,
                int64_t grad_stride, const ApplyParams& ap, void* workspace, size_t ws_bytes, hipStream_t st,
                int32_t* out_uniq = nullptr, float* out_sum = nullptr, int32_t* out_count = nullptr) {
-  TT_REQUIRE(grad_stride >= 0 && batch * grad_stride < (int64_t(1) << 31),
-             "sparse: grad buffer of %lld x %lld floats exceeds 2^31 elements", static_cast<long long>(batch),
-             static_cast<long long>(grad_stride));
+  TT_REQUIRE(batch < (int64_t(1) << kSrcShift), "sparse: batch %lld too large", static_cast<long long>(batch));
   for (int first = 0; first < num_tables; first += kTablesPerLaunch) {
     const int cnt = std::min(num_tables - first, kTablesPerLaunch);
     Plan p;
-    int rc = make_plan(tables + first, cnt, batch, &p);
+    int rc = make_plan(tables + first, cnt, batch, grad, grad_stride, &p);
     if (rc) return rc;
     Carver cv(workspace, ws_bytes);
     const int dense_dim = (OP == kWriteSum) ? tables[first].dim : 0;
     PlanWs w = carve_plan(cv, p, dense_dim);
     if (cv.used() > ws_bytes) return fail(TT_ERR_WORKSPACE, "sparse: workspace %zu < required %zu", ws_bytes, cv.used());
     Job& j = p.job;
-    j.grad = grad;
-    j.grad_stride = grad_stride;
     j.keys_in = w.keys_in;
     j.vals_in = w.vals_in;
     j.keys = w.keys;
@@ -585,7 +600,6 @@ extern "C" int tt_sparse_adagrad(const tt_sparse_table* tables, int32_t num_tabl
   int rc = validate_tables(tables, num_tables, batch, false);
   if (rc) return rc;
   if (batch == 0) return TT_OK;
-  TT_REQUIRE(grad != nullptr, "tt_sparse_adagrad: grad is NULL");
   const size_t need = tables_ws_bytes(tables, num_tables, batch, 0);
   if (!workspace || workspace_bytes < need)
     return fail(TT_ERR_WORKSPACE, "tt_sparse_adagrad: workspace %zu < required %zu", workspace_bytes, need);
@@ -604,7 +618,6 @@ extern "C" int tt_sparse_adam(const tt_sparse_table* tables, int32_t num_tables,
   int rc = validate_tables(tables, num_tables, batch, true);
   if (rc) return rc;
   TT_REQUIRE(step >= 1, "tt_sparse_adam: step must be >= 1");
-  TT_REQUIRE(batch == 0 || grad != nullptr, "tt_sparse_adam: grad is NULL");
   const size_t need = tables_ws_bytes(tables, num_tables, batch, 0);
   if (batch > 0 && (!workspace || workspace_bytes < need))
     return fail(TT_ERR_WORKSPACE, "tt_sparse_adam: workspace %zu < required %zu", workspace_bytes, need);
@@ -703,7 +716,6 @@ extern "C" int tt_sparse_scatter_sum(const tt_sparse_table* tables, int32_t num_
   int rc = validate_tables(tables, num_tables, batch, false, false);
   if (rc) return rc;
   if (batch == 0) return TT_OK;
-  TT_REQUIRE(grad != nullptr, "tt_sparse_scatter_sum: grad is NULL");
   const size_t need = tables_ws_bytes(tables, num_tables, batch, 0);
   if (!workspace || workspace_bytes < need)
     return fail(TT_ERR_WORKSPACE, "tt_sparse_scatter_sum: workspace %zu < required %zu", workspace_bytes, need);

@@ -81,6 +81,8 @@ class SparseTable(ctypes.Structure):
         ("num_sources", c_int32),
         ("ids", c_void_p * MAX_SOURCES),
         ("grad_col_offset", c_int32 * MAX_SOURCES),
+        ("grad", c_void_p),      # optional per-table gradient (NULL: the call's)
+        ("grad_ld", c_int64),
     ]
 
 

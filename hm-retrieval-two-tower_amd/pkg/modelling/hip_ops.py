@@ -170,19 +170,34 @@ def _sparse_tables(tables: Sequence[dict], batch: int, adam: bool, slots: bool =
                 raise ValueError(f"ids[{i}][{s}] must be contiguous [{batch}] int32")
             arr[i].ids[s] = x.data_ptr()
             arr[i].grad_col_offset[s] = o
+        g = t.get("grad")
+        if g is not None:  # per-table gradient buffer (e.g. another tower's input gradient)
+            _req(g, f"grad[{i}]", torch.float32, 2)
+            if g.shape[0] != batch:
+                raise ValueError(f"grad[{i}] must have {batch} rows")
+            arr[i].grad = g.data_ptr()
+            arr[i].grad_ld = _row_major(g, f"grad[{i}]")
     return arr
 
 
-def sparse_adagrad(tables: Sequence[dict], batch: int, grad: torch.Tensor, lr: float, epsilon: float) -> None:
-    """tables: dicts with table, slot0 (accumulator), ids [list], grad_col_offset [list]."""
-    _req(grad, "grad", torch.float32, 2)
-    ld = _row_major(grad, "grad")
+def sparse_adagrad(tables: Sequence[dict], batch: int, grad: Optional[torch.Tensor], lr: float,
+                   epsilon: float) -> None:
+    """tables: dicts with table, slot0 (accumulator), ids [list], grad_col_offset [list] and an
+    optional per-table "grad" [batch, *] that overrides the call's `grad` (which may then be None),
+    so one call — one sort — updates the tables of both towers."""
+    ld = 0
+    if grad is not None:
+        _req(grad, "grad", torch.float32, 2)
+        ld = _row_major(grad, "grad")
+    elif any(t.get("grad") is None for t in tables):
+        raise ValueError("grad is None but some table has no per-table grad")
     arr = _sparse_tables(tables, batch, adam=False)
     L = lib()
     need = L.tt_sparse_workspace_size(arr, len(tables), batch)
-    ws = Workspace.get(need, grad.device, "sparse")
-    check(L.tt_sparse_adagrad(arr, len(tables), batch, grad.data_ptr(), ld, lr, epsilon, ws.data_ptr(), ws.numel(),
-                              _stream()))
+    dev = grad.device if grad is not None else tables[0]["grad"].device
+    ws = Workspace.get(need, dev, "sparse")
+    check(L.tt_sparse_adagrad(arr, len(tables), batch, grad.data_ptr() if grad is not None else None, ld, lr, epsilon,
+                              ws.data_ptr(), ws.numel(), _stream()))
 
 
 def sparse_adam(tables: Sequence[dict], batch: int, grad: torch.Tensor, lr: float, beta1: float, beta2: float,

@@ -67,6 +67,7 @@ class Adagrad(_Optimizer):
 
     def _apply(self, towers) -> None:
         lr, eps, init = self.learning_rate, self.epsilon, self.initial_accumulator_value
+        specs, batch = [], None
         for tower in towers:
             flat = tower.dense.flat
             if flat.grad is not None:
@@ -75,12 +76,16 @@ class Adagrad(_Optimizer):
             layer = tower.input_layer
             if layer.last_grad is None or not layer.embedding_layers:
                 continue
-            specs = []
+            batch = layer.last_grad.shape[0]
             for src in layer.sparse_sources():
                 t = src["table"]
                 (acc,) = self._slot(t.weight, 1, init)
-                specs.append(dict(table=t.weight, slot0=acc, ids=src["ids"], grad_col_offset=src["grad_col_offset"]))
-            hip_ops.sparse_adagrad(specs, layer.last_grad.shape[0], layer.last_grad, lr, eps)
+                specs.append(dict(table=t.weight, slot0=acc, ids=src["ids"], grad_col_offset=src["grad_col_offset"],
+                                  grad=layer.last_grad))
+        if specs:
+            # every tower's tables in ONE call: one sort, one block pass (each
+            # table reads its own tower's input gradient)
+            hip_ops.sparse_adagrad(specs, batch, None, lr, eps)
 
 
 class Adam(_Optimizer):

@@ -117,6 +117,12 @@ typedef struct {
   int32_t num_sources; /* 1..TT_MAX_SOURCES                                     */
   const int32_t* ids[TT_MAX_SOURCES];      /* [batch] row ids per source         */
   int32_t grad_col_offset[TT_MAX_SOURCES]; /* column of the source's slice in grad */
+  /* Optional per-table gradient buffer: when non-NULL, this table's sources
+   * read rows b of grad + b*grad_ld (+ grad_col_offset[s]) instead of the
+   * call's grad / grad_stride — so ONE call (one sort) updates the tables of
+   * both towers, whose input gradients are separate buffers.                */
+  const float* grad;
+  int64_t grad_ld;
 } tt_sparse_table;
 
 size_t tt_sparse_workspace_size(const tt_sparse_table* tables, int32_t num_tables,

@@ -124,6 +124,29 @@ def test_sparse_adagrad_bitexact_multi_source(cuda):
         assert np.array_equal(da[i].cpu().numpy(), accs[i]), f"accum {i}"
 
 
+def test_sparse_adagrad_per_table_grads_one_call(cuda):
+    """Tables of two 'towers' updated in ONE call, each table reading its own
+    gradient buffer (tt_sparse_table.grad), equal the oracle bit for bit."""
+    rng = np.random.default_rng(11)
+    B = 3000
+    tq = rng.uniform(-0.05, 0.05, (5000, 64)).astype(np.float32)
+    tc = rng.uniform(-0.05, 0.05, (300, 32)).astype(np.float32)
+    aq, ac = np.full_like(tq, 0.1), np.full_like(tc, 0.1)
+    iq = zipf_ids(rng, B, 5000)
+    ic1, ic2 = zipf_ids(rng, B, 300), zipf_ids(rng, B, 300)
+    gq = rng.standard_normal((B, 70)).astype(np.float32)   # query-tower input grad, table at col 3
+    gc = rng.standard_normal((B, 68)).astype(np.float32)   # candidate grad, two sources of one table
+    d = [_t(x, cuda) for x in (tq, aq, tc, ac)]
+    specs = [dict(table=d[0], slot0=d[1], ids=[_t(iq, cuda)], grad_col_offset=[3], grad=_t(gq, cuda)),
+             dict(table=d[2], slot0=d[3], ids=[_t(ic1, cuda), _t(ic2, cuda)], grad_col_offset=[0, 36],
+                  grad=_t(gc, cuda))]
+    hip_ops.sparse_adagrad(specs, B, None, 0.05, 1e-7)
+    oracle.sparse_adagrad(tq, aq, iq, gq[:, 3:67], 0.05, 1e-7)
+    oracle.sparse_adagrad(tc, ac, np.concatenate([ic1, ic2]), np.concatenate([gc[:, 0:32], gc[:, 36:68]]), 0.05, 1e-7)
+    for got, ref in zip(d, (tq, aq, tc, ac)):
+        assert np.array_equal(got.cpu().numpy(), ref)
+
+
 def test_dense_adagrad_and_adam_bitexact(cuda):
     rng = np.random.default_rng(2)
     n = 100003
