@@ -440,9 +440,7 @@ class ShardedTrainStep:
             small_srcs.append(srcs_small)
         anchors = [layer._anchor for layer in layers]
         qi, ci = _ShardedGatherFn.apply(self, calls, B, widths, *anchors)
-        qe = m.query_tower.dense(qi)
-        ce = m.candidate_tower.dense(ci)
-        loss = m.loss(qe, ce, m.candidate_logq(batch))
+        loss = m.tower_loss(qi, ci, m.candidate_logq(batch))
         for t in m.towers:
             t.dense.flat.grad = None
         loss.backward()

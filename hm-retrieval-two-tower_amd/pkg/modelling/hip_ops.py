@@ -16,6 +16,8 @@ from pkg import _native
 from pkg._native import GatherSegment, SparseTable, check, lib
 
 __all__ = [
+    "relu_bias_grad",
+    "sum_slices",
     "gather_grouped",
     "sparse_adagrad",
     "sparse_adam",
@@ -266,6 +268,45 @@ def dedup_sum(ids: torch.Tensor, grad: torch.Tensor, num_rows: int) -> Tuple[tor
                          count.data_ptr(), ws.data_ptr(), ws.numel(), _stream()))
     u = int(count.item())
     return uniq[:u], summed[:u]
+
+
+def relu_bias_grad(gin: torch.Tensor, act: torch.Tensor, gscale: Optional[torch.Tensor] = None,
+                   out: Optional[torch.Tensor] = None, db: Optional[torch.Tensor] = None):
+    """K4 backward glue of a Dense(relu) layer: (gout, db) with
+    gout = (act > 0) * s * gin, s = gscale (a 1-element device tensor or None),
+    db = column sums of gout.  `out` may be gin itself."""
+    _req(gin, "gin", torch.float32, 2)
+    _req(act, "act", torch.float32, 2)
+    if gin.shape != act.shape:
+        raise ValueError("gin and act must have the same shape")
+    rows, cols = gin.shape
+    if out is None:
+        out = torch.empty_like(gin)
+    if db is None:
+        db = torch.empty(cols, dtype=torch.float32, device=gin.device)
+    _req(out, "out", torch.float32, 2)
+    if not db.is_contiguous() or db.numel() != cols:
+        raise ValueError("db must be a contiguous [cols] tensor")
+    if gscale is not None:
+        _req(gscale, "gscale", torch.float32)
+        if gscale.numel() != 1:
+            raise ValueError("gscale must have one element")
+    L = lib()
+    ws = Workspace.get(L.tt_relu_bias_grad_workspace_size(rows, cols), gin.device, "relu_bias_grad")
+    check(L.tt_relu_bias_grad(gin.data_ptr(), _row_major(gin, "gin"), gscale.data_ptr() if gscale is not None else None,
+                              act.data_ptr(), _row_major(act, "act"), rows, cols, out.data_ptr(),
+                              _row_major(out, "out"), db.data_ptr(), ws.data_ptr(), ws.numel(), _stream()))
+    return out, db
+
+
+def sum_slices(parts: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """out = parts.sum(0) for parts [S, ...] contiguous, slices added in order."""
+    _req(parts, "parts", torch.float32)
+    _req(out, "out", torch.float32)
+    if not parts.is_contiguous() or not out.is_contiguous() or parts[0].numel() != out.numel():
+        raise ValueError("parts must be contiguous [S, *out.shape] and out contiguous")
+    check(lib().tt_sum_slices(parts.data_ptr(), parts.shape[0], out.numel(), out.data_ptr(), _stream()))
+    return out
 
 
 def dense_adagrad(param: torch.Tensor, accum: torch.Tensor, grad: torch.Tensor, lr: float, epsilon: float) -> None:

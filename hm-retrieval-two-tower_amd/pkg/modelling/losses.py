@@ -17,7 +17,7 @@ import torch
 
 from pkg.modelling import hip_ops
 
-__all__ = ["InBatchSoftmaxCrossEntropy", "inbatch_softmax_xent"]
+__all__ = ["InBatchSoftmaxCrossEntropy", "inbatch_softmax_xent", "towers_inbatch_softmax_xent"]
 
 
 class _InBatchXent(torch.autograd.Function):
@@ -33,6 +33,44 @@ class _InBatchXent(torch.autograd.Function):
         dq, dc = ctx.saved_tensors
         s = g * ctx.scale
         return dq * s, dc * s, None, None
+
+
+class _TowersInBatchXent(torch.autograd.Function):
+    """Both tower MLPs and the in-batch loss as ONE autograd node.  The
+    backward hands the loss's incoming gradient to the top layers' fused
+    relu/bias kernels as a device scalar (no separate scaling pass over dQ,
+    dC) and overwrites dQ / dC in place (they are not needed afterwards)."""
+
+    @staticmethod
+    def forward(ctx, qi, ci, flat_q, flat_c, logq, stack_q, stack_c, scale):
+        qa = stack_q.forward_acts(qi, flat_q)
+        ca = stack_c.forward_acts(ci, flat_c)
+        _, row_loss, dq, dc = hip_ops.inbatch_fused(qa[-1], ca[-1], logq)
+        ctx.stacks = (stack_q, stack_c)
+        ctx.nq = len(qa)
+        ctx.scale = scale
+        ctx.save_for_backward(flat_q, flat_c, dq, dc, *qa, *ca)
+        return row_loss.sum() * scale
+
+    @staticmethod
+    def backward(ctx, g):
+        flat_q, flat_c, dq, dc, *acts = ctx.saved_tensors
+        qa, ca = acts[:ctx.nq], acts[ctx.nq:]
+        s = (g * ctx.scale if ctx.scale != 1.0 else g).reshape(1).float().contiguous()
+        stack_q, stack_c = ctx.stacks
+        gqi, gflat_q = stack_q.backward_acts(qa, flat_q, dq, s, ctx.needs_input_grad[0])
+        gci, gflat_c = stack_c.backward_acts(ca, flat_c, dc, s, ctx.needs_input_grad[1])
+        return gqi, gci, gflat_q, gflat_c, None, None, None, None
+
+
+def towers_inbatch_softmax_xent(qi: torch.Tensor, ci: torch.Tensor, stack_q, stack_c,
+                                logq: Optional[torch.Tensor] = None, reduction: str = "sum") -> torch.Tensor:
+    """Loss of the query tower on qi against the candidate tower on ci (tower
+    inputs [B, *]), fused into one autograd node; stack_* are DenseStacks."""
+    if reduction not in ("sum", "sum_over_batch_size", "mean"):
+        raise ValueError(f"unsupported reduction {reduction}")
+    scale = 1.0 if reduction == "sum" else 1.0 / qi.shape[0]
+    return _TowersInBatchXent.apply(qi, ci, stack_q.flat, stack_c.flat, logq, stack_q, stack_c, scale)
 
 
 def inbatch_softmax_xent(q: torch.Tensor, c: torch.Tensor, logq: Optional[torch.Tensor] = None,

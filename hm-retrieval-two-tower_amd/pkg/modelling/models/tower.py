@@ -6,7 +6,9 @@ zero bias, relu on every layer including the last (tower.py:45,48), so the
 joint embeddings are non-negative.  All kernels and biases of a tower live in
 ONE flat fp32 buffer (views per layer), so its gradient is one contiguous
 tensor and the dense optimizer step is a single tt_dense_* launch.  The GEMMs
-run through torch (hipBLASLt), fp32.
+run through torch (hipBLASLt, fp32, bias + relu fused into the forward GEMM's
+epilogue); the backward's relu mask + bias gradient and the split-K weight
+gradient reduction are libtt kernels (tt_relu_bias_grad, tt_sum_slices).
 """
 from __future__ import annotations
 
@@ -15,6 +17,7 @@ from typing import Dict, List, Optional, Tuple
 import torch
 
 from pkg.schema.features import Feature
+from pkg.modelling import hip_ops
 from pkg.modelling.device import default_device, make_generator
 from pkg.modelling.layers.input_layer import InputLayer
 from pkg.modelling.models.abstract_keras_model import AbstractKerasModel, TensorSpec
@@ -25,13 +28,13 @@ __all__ = ["Tower", "DenseStack"]
 def _splitk_mm_tn(a: torch.Tensor, g: torch.Tensor, out: torch.Tensor, splits: int = 16) -> None:
     """out = a^T g for tall a [B, fin], g [B, fout] (the weight gradient).
     hipBLASLt runs this skinny, K=B-long product on a handful of tiles; a
-    batched split over B (bmm of `splits` slices, then a sum) fills the GPU
-    (≈3x faster at B=16384)."""
+    batched split over B (bmm of `splits` slices, then tt_sum_slices in slice
+    order) fills the GPU (~3x faster at B=16384)."""
     B = a.shape[0]
     if B >= 4096 and B % splits == 0:
         part = torch.bmm(a.view(splits, B // splits, a.shape[1]).transpose(1, 2),
                          g.view(splits, B // splits, g.shape[1]))
-        torch.sum(part, 0, out=out)
+        hip_ops.sum_slices(part, out)
     else:
         torch.mm(a.t(), g, out=out)
 
@@ -43,32 +46,17 @@ class _DenseStackFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, flat, stack):
-        h = x
-        acts = [x]
-        for w, b in stack.params(flat):
-            h = torch.addmm(b, h, w)
-            h.relu_()
-            acts.append(h)
+        acts = stack.forward_acts(x, flat)
         ctx.stack = stack
         ctx.save_for_backward(flat, *acts)
-        return h
+        return acts[-1]
 
     @staticmethod
     def backward(ctx, gout):
         flat, *acts = ctx.saved_tensors
-        stack = ctx.stack
-        gflat = torch.empty_like(flat)
-        params = stack.params(flat)
-        gparams = stack.params(gflat)
-        g = gout
-        for li in range(len(params) - 1, -1, -1):
-            g = torch.ops.aten.threshold_backward(g, acts[li + 1], 0.0)
-            dw, db = gparams[li]
-            _splitk_mm_tn(acts[li], g, dw)
-            torch.sum(g, 0, out=db)
-            if li > 0 or ctx.needs_input_grad[0]:
-                g = torch.mm(g, params[li][0].t())
-        return (g if ctx.needs_input_grad[0] else None), gflat, None
+        gx, gflat = ctx.stack.backward_acts(acts, flat, gout.contiguous(), None, ctx.needs_input_grad[0],
+                                            inplace=False)
+        return gx, gflat, None
 
 
 class DenseStack:
@@ -94,13 +82,40 @@ class DenseStack:
         f = self.flat if flat is None else flat
         return [(f[w:w + fi * fo].view(fi, fo), f[b:b + fo]) for w, fi, fo, b in self.layout]
 
+    def forward_acts(self, x: torch.Tensor, flat: torch.Tensor) -> List[torch.Tensor]:
+        """[x, h_1, ..., h_L]: each layer one hipBLASLt GEMM with the bias + relu
+        epilogue fused (torch._addmm_activation)."""
+        acts = [x]
+        h = x
+        for w, b in self.params(flat):
+            h = torch._addmm_activation(b, h, w)
+            acts.append(h)
+        return acts
+
+    def backward_acts(self, acts: List[torch.Tensor], flat: torch.Tensor, gout: torch.Tensor,
+                      gscale: Optional[torch.Tensor], need_input_grad: bool, inplace: bool = True):
+        """(d x, d flat) from the saved activations.  Per layer: one tt_relu_bias_grad
+        (relu mask x the incoming gradient, times gscale on the top layer, and the
+        bias gradient), the weight gradient (split-K GEMM + tt_sum_slices) and the
+        input gradient (GEMM).  inplace: gout may be overwritten."""
+        gflat = torch.empty_like(flat)
+        params = self.params(flat)
+        gparams = self.params(gflat)
+        g = gout
+        for li in range(len(params) - 1, -1, -1):
+            dw, db = gparams[li]
+            top = li == len(params) - 1
+            g, _ = hip_ops.relu_bias_grad(g, acts[li + 1], gscale if top else None,
+                                          out=None if (top and not inplace) else g, db=db)
+            _splitk_mm_tn(acts[li], g, dw)
+            if li > 0 or need_input_grad:
+                g = torch.mm(g, params[li][0].t())
+        return (g if need_input_grad else None), gflat
+
     def __call__(self, x: torch.Tensor) -> torch.Tensor:
         if torch.is_grad_enabled() and (x.requires_grad or self.flat.requires_grad):
             return _DenseStackFn.apply(x, self.flat, self)
-        h = x
-        for w, b in self.params(self.flat.detach()):
-            h = torch.relu(torch.addmm(b, h, w))
-        return h
+        return self.forward_acts(x, self.flat.detach())[-1]
 
 
 class Tower(AbstractKerasModel):

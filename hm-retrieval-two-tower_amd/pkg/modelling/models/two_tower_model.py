@@ -22,7 +22,7 @@ from pkg.schema.features import Feature
 from pkg.schema.schema import Schema
 from pkg.modelling.device import default_device, make_generator
 from pkg.modelling.layers.logq_correction import LogQCorrection
-from pkg.modelling.losses import InBatchSoftmaxCrossEntropy
+from pkg.modelling.losses import InBatchSoftmaxCrossEntropy, towers_inbatch_softmax_xent
 from pkg.modelling.models.abstract_keras_model import AbstractKerasModel, TensorSpec
 from pkg.modelling.layers.input_layer import InputLayer
 from pkg.modelling.models.tower import Tower
@@ -114,9 +114,15 @@ class TwoTowerModel(AbstractKerasModel):
         q, c = self._split(x)
         with torch.set_grad_enabled(training):
             qi, ci = InputLayer.gather_many([self.query_tower.input_layer, self.candidate_tower.input_layer], [q, c])
-            qe = self.query_tower.dense(qi)
-            ce = self.candidate_tower.dense(ci)
-            return self.loss(qe, ce, self.candidate_logq(x))
+            return self.tower_loss(qi, ci, self.candidate_logq(x))
+
+    def tower_loss(self, qi: torch.Tensor, ci: torch.Tensor, logq: Optional[torch.Tensor]) -> torch.Tensor:
+        """Loss from the gathered tower inputs: with gradients, both MLPs and the
+        in-batch loss run as one autograd node (losses.towers_inbatch_softmax_xent)."""
+        if torch.is_grad_enabled():
+            return towers_inbatch_softmax_xent(qi, ci, self.query_tower.dense, self.candidate_tower.dense, logq,
+                                               self.loss.reduction)
+        return self.loss(self.query_tower.dense(qi), self.candidate_tower.dense(ci), logq)
 
     def compile(self, loss=None, optimizer=None, **kwargs) -> None:
         """Keras-style compile: the loss must be the in-batch softmax CE

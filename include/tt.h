@@ -163,6 +163,23 @@ int tt_dedup_sum(const int32_t* ids, int64_t n, int64_t num_rows,
                  int32_t* unique_ids, float* summed, int32_t* num_unique,
                  void* workspace, size_t workspace_bytes, tt_stream_t stream);
 
+/* K4 backward glue of the tower MLPs (Dense + ReLU, tower.py:45,48; TF's
+ * ReluGrad + BiasAddGrad beside the MatMul gradients):
+ *   gout = (act > 0) * s * gin with s = *gscale (device scalar, NULL -> 1),
+ *   db   = column sums of gout (64-row blocks in row order; the block
+ *          partials in 16 consecutive chunks, each in order; then the chunk
+ *          sums in order: deterministic).  gout may alias gin.
+ * act is the layer's relu output (the mask), all matrices row-major. */
+size_t tt_relu_bias_grad_workspace_size(int64_t rows, int32_t cols);
+int tt_relu_bias_grad(const float* gin, int64_t ldg, const float* gscale,
+                      const float* act, int64_t lda, int64_t rows, int32_t cols,
+                      float* gout, int64_t ldo, float* db, void* workspace,
+                      size_t workspace_bytes, tt_stream_t stream);
+/* out[i] = sum over s < nslices of parts[s*n + i] (slices in order): the
+ * split-K reduction of a weight gradient computed as batched partial GEMMs. */
+int tt_sum_slices(const float* parts, int32_t nslices, int64_t n, float* out,
+                  tt_stream_t stream);
+
 /* K10  Dense optimizer steps on a flat parameter buffer (tower MLP weights).
  * ResourceApplyAdagradV2 / ResourceApplyAdam (optimizer_factory.py:15-18). */
 int tt_dense_adagrad(float* param, float* accum, const float* grad, int64_t n,

@@ -147,6 +147,50 @@ def test_sparse_adagrad_per_table_grads_one_call(cuda):
         assert np.array_equal(got.cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("rows,cols", [(16384, 256), (1000, 128), (7, 3), (130, 300)])
+def test_relu_bias_grad_matches_reference(cuda, rows, cols):
+    """tt_relu_bias_grad: gout bit-exact to mask * s * gin; db equals the
+    column sums in the kernel's order (64-row blocks, 16 chunks of block
+    partials, chunk sums) exactly."""
+    rng = np.random.default_rng(rows + cols)
+    g = rng.standard_normal((rows, cols)).astype(np.float32)
+    act = np.maximum(rng.standard_normal((rows, cols)), 0).astype(np.float32)
+    s = np.float32(0.37)
+    gout, db = hip_ops.relu_bias_grad(_t(g, cuda), _t(act, cuda), _t(np.array([s], np.float32), cuda))
+    ref = np.where(act > 0, g * s, np.float32(0)).astype(np.float32)
+    assert np.array_equal(gout.cpu().numpy(), ref)
+    blocks = [ref[i:i + 64] for i in range(0, rows, 64)]
+    part = []
+    for b in blocks:
+        acc = np.zeros(cols, np.float32)
+        for r in b:
+            acc = (acc + r).astype(np.float32)
+        part.append(acc)
+    chunk = (len(part) + 15) // 16
+    exp = np.zeros(cols, np.float32)
+    for k in range(16):
+        acc = np.zeros(cols, np.float32)
+        for p_ in part[k * chunk:(k + 1) * chunk]:
+            acc = (acc + p_).astype(np.float32)
+        exp = (exp + acc).astype(np.float32)
+    assert np.array_equal(db.cpu().numpy(), exp)
+    # in place, no scale
+    tg = _t(g, cuda)
+    hip_ops.relu_bias_grad(tg, _t(act, cuda), None, out=tg)
+    assert np.array_equal(tg.cpu().numpy(), np.where(act > 0, g, np.float32(0)))
+
+
+def test_sum_slices_in_order(cuda):
+    rng = np.random.default_rng(5)
+    parts = rng.standard_normal((16, 258, 256)).astype(np.float32)
+    out = torch.empty(258, 256, device=cuda)
+    hip_ops.sum_slices(_t(parts, cuda), out)
+    exp = np.zeros((258, 256), np.float32)
+    for p_ in parts:
+        exp = (exp + p_).astype(np.float32)
+    assert np.array_equal(out.cpu().numpy(), exp)
+
+
 def test_dense_adagrad_and_adam_bitexact(cuda):
     rng = np.random.default_rng(2)
     n = 100003
