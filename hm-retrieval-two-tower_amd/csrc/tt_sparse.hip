@@ -498,15 +498,23 @@ size_t tables_ws_bytes(const tt_sparse_table* tables, int32_t num_tables, int64_
   return total;
 }
 
+// Stages: the key build + sort depends only on the ids, so a caller may run
+// it early on a side stream (kStageSort) and the gradient-dependent block/join
+// pass later (kStageApply) with the same tables, batch and workspace.
+enum SparseStage { kStageAll = 0, kStageSort = 1, kStageApply = 2 };
+
 template <int OP>
 int run_sparse(const tt_sparse_table* tables, int32_t num_tables, int64_t batch, const float* grad,
                int64_t grad_stride, const ApplyParams& ap, void* workspace, size_t ws_bytes, hipStream_t st,
-               int32_t* out_uniq = nullptr, float* out_sum = nullptr, int32_t* out_count = nullptr) {
+               int32_t* out_uniq = nullptr, float* out_sum = nullptr, int32_t* out_count = nullptr,
+               int stage = kStageAll) {
   TT_REQUIRE(batch < (int64_t(1) << kSrcShift), "sparse: batch %lld too large", static_cast<long long>(batch));
+  TT_REQUIRE(stage == kStageAll || num_tables <= kTablesPerLaunch,
+             "sparse: a split sort/apply call takes at most %d tables", kTablesPerLaunch);
   for (int first = 0; first < num_tables; first += kTablesPerLaunch) {
     const int cnt = std::min(num_tables - first, kTablesPerLaunch);
     Plan p;
-    int rc = make_plan(tables + first, cnt, batch, grad, grad_stride, &p);
+    int rc = make_plan(tables + first, cnt, batch, grad, grad_stride, &p, stage == kStageSort);
     if (rc) return rc;
     Carver cv(workspace, ws_bytes);
     const int dense_dim = (OP == kWriteSum) ? tables[first].dim : 0;
@@ -520,11 +528,14 @@ int run_sparse(const tt_sparse_table* tables, int32_t num_tables, int64_t batch,
     j.pieces = w.pieces;
     j.dense_out = w.dense_out;
     j.dense_dim = dense_dim;
-    hipLaunchKernelGGL(build_keys_kernel, dim3(ceil_div(p.total, kThreads)), dim3(kThreads), 0, st, j, p.total);
-    TT_CHECK_LAUNCH();
-    size_t sb = p.sort_bytes;
-    TT_CHECK_HIP(rocprim::radix_sort_pairs(w.sort_tmp, sb, w.keys_in, w.keys, w.vals_in, w.vals,
-                                           static_cast<unsigned>(p.total), 0, p.end_bit, st, false));
+    if (stage != kStageApply) {
+      hipLaunchKernelGGL(build_keys_kernel, dim3(ceil_div(p.total, kThreads)), dim3(kThreads), 0, st, j, p.total);
+      TT_CHECK_LAUNCH();
+      size_t sb = p.sort_bytes;
+      TT_CHECK_HIP(rocprim::radix_sort_pairs(w.sort_tmp, sb, w.keys_in, w.keys, w.vals_in, w.vals,
+                                             static_cast<unsigned>(p.total), 0, p.end_bit, st, false));
+    }
+    if (stage == kStageSort) continue;
     const int blocks = static_cast<int>(ceil_div(p.waves, kThreads / kWave));
     hipLaunchKernelGGL(block_sum_kernel<OP>, dim3(blocks), dim3(kThreads), 0, st, j, ap);
     TT_CHECK_LAUNCH();
@@ -593,21 +604,45 @@ extern "C" size_t tt_sparse_workspace_size(const tt_sparse_table* tables, int32_
   return tables_ws_bytes(tables, num_tables, batch, 0);
 }
 
-extern "C" int tt_sparse_adagrad(const tt_sparse_table* tables, int32_t num_tables, int64_t batch,
-                                 const float* grad, int64_t grad_stride, float lr, float epsilon,
-                                 void* workspace, size_t workspace_bytes, tt_stream_t stream) {
+namespace tt {
+namespace {
+int sparse_adagrad_stage(const tt_sparse_table* tables, int32_t num_tables, int64_t batch, const float* grad,
+                         int64_t grad_stride, float lr, float epsilon, void* workspace, size_t workspace_bytes,
+                         tt_stream_t stream, int stage, const char* name) {
   clear_error();
   int rc = validate_tables(tables, num_tables, batch, false);
   if (rc) return rc;
   if (batch == 0) return TT_OK;
   const size_t need = tables_ws_bytes(tables, num_tables, batch, 0);
   if (!workspace || workspace_bytes < need)
-    return fail(TT_ERR_WORKSPACE, "tt_sparse_adagrad: workspace %zu < required %zu", workspace_bytes, need);
+    return fail(TT_ERR_WORKSPACE, "%s: workspace %zu < required %zu", name, workspace_bytes, need);
   ApplyParams ap{};
   ap.lr = lr;
   ap.eps = epsilon;
   return run_sparse<kAdagrad>(tables, num_tables, batch, grad, grad_stride, ap, workspace, workspace_bytes,
-                              to_stream(stream));
+                              to_stream(stream), nullptr, nullptr, nullptr, stage);
+}
+}  // namespace
+}  // namespace tt
+
+extern "C" int tt_sparse_adagrad(const tt_sparse_table* tables, int32_t num_tables, int64_t batch,
+                                 const float* grad, int64_t grad_stride, float lr, float epsilon,
+                                 void* workspace, size_t workspace_bytes, tt_stream_t stream) {
+  return sparse_adagrad_stage(tables, num_tables, batch, grad, grad_stride, lr, epsilon, workspace, workspace_bytes,
+                              stream, kStageAll, "tt_sparse_adagrad");
+}
+
+extern "C" int tt_sparse_sort(const tt_sparse_table* tables, int32_t num_tables, int64_t batch, void* workspace,
+                              size_t workspace_bytes, tt_stream_t stream) {
+  return sparse_adagrad_stage(tables, num_tables, batch, nullptr, 0, 0.0f, 0.0f, workspace, workspace_bytes, stream,
+                              kStageSort, "tt_sparse_sort");
+}
+
+extern "C" int tt_sparse_adagrad_sorted(const tt_sparse_table* tables, int32_t num_tables, int64_t batch,
+                                        const float* grad, int64_t grad_stride, float lr, float epsilon,
+                                        void* workspace, size_t workspace_bytes, tt_stream_t stream) {
+  return sparse_adagrad_stage(tables, num_tables, batch, grad, grad_stride, lr, epsilon, workspace, workspace_bytes,
+                              stream, kStageApply, "tt_sparse_adagrad_sorted");
 }
 
 extern "C" int tt_sparse_adam(const tt_sparse_table* tables, int32_t num_tables, int64_t batch,

@@ -112,6 +112,10 @@ _PROTOS = {
         [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
          c_void_p],
     ),
+    "tt_sparse_sort": (c_int32, [POINTER(SparseTable), c_int32, c_int64, c_void_p, c_size_t, c_void_p]),
+    "tt_sparse_adagrad_sorted": (
+        c_int32,
+        [POINTER(SparseTable), c_int32, c_int64, c_void_p, c_int64, c_float, c_float, c_void_p, c_size_t, c_void_p]),
     "tt_relu_bias_grad_workspace_size": (c_size_t, [c_int64, c_int32]),
     "tt_relu_bias_grad": (
         c_int32,

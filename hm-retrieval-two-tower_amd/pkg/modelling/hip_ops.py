@@ -20,6 +20,7 @@ __all__ = [
     "sum_slices",
     "gather_grouped",
     "sparse_adagrad",
+    "sparse_sort",
     "sparse_adam",
     "dedup_sum",
     "dense_adagrad",
@@ -183,10 +184,11 @@ def _sparse_tables(tables: Sequence[dict], batch: int, adam: bool, slots: bool =
 
 
 def sparse_adagrad(tables: Sequence[dict], batch: int, grad: Optional[torch.Tensor], lr: float,
-                   epsilon: float) -> None:
+                   epsilon: float, presorted: bool = False) -> None:
     """tables: dicts with table, slot0 (accumulator), ids [list], grad_col_offset [list] and an
     optional per-table "grad" [batch, *] that overrides the call's `grad` (which may then be None),
-    so one call — one sort — updates the tables of both towers."""
+    so one call — one sort — updates the tables of both towers.  presorted: the ids were
+    already sorted by sparse_sort(tables, batch) (same tables, stream-ordered before this)."""
     ld = 0
     if grad is not None:
         _req(grad, "grad", torch.float32, 2)
@@ -198,8 +200,19 @@ def sparse_adagrad(tables: Sequence[dict], batch: int, grad: Optional[torch.Tens
     need = L.tt_sparse_workspace_size(arr, len(tables), batch)
     dev = grad.device if grad is not None else tables[0]["grad"].device
     ws = Workspace.get(need, dev, "sparse")
-    check(L.tt_sparse_adagrad(arr, len(tables), batch, grad.data_ptr() if grad is not None else None, ld, lr, epsilon,
-                              ws.data_ptr(), ws.numel(), _stream()))
+    fn = L.tt_sparse_adagrad_sorted if presorted else L.tt_sparse_adagrad
+    check(fn(arr, len(tables), batch, grad.data_ptr() if grad is not None else None, ld, lr, epsilon,
+             ws.data_ptr(), ws.numel(), _stream()))
+
+
+def sparse_sort(tables: Sequence[dict], batch: int) -> None:
+    """First stage of sparse_adagrad(..., presorted=True): build and sort the lookup keys
+    (reads only the ids; no gradient needed), on the current stream."""
+    arr = _sparse_tables(tables, batch, adam=False)
+    L = lib()
+    need = L.tt_sparse_workspace_size(arr, len(tables), batch)
+    ws = Workspace.get(need, tables[0]["table"].device, "sparse")
+    check(L.tt_sparse_sort(arr, len(tables), batch, ws.data_ptr(), ws.numel(), _stream()))
 
 
 def sparse_adam(tables: Sequence[dict], batch: int, grad: torch.Tensor, lr: float, beta1: float, beta2: float,

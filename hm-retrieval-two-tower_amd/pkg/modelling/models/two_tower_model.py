@@ -141,6 +141,8 @@ class TwoTowerModel(AbstractKerasModel):
         if self.optimizer is None:
             raise RuntimeError("call compile(optimizer=...) before training")
         loss = self.compute_loss(data, training=True)
+        if hasattr(self.optimizer, "prepare"):
+            self.optimizer.prepare(self.towers)  # id sort of the embedding update, overlapped with backward
         for t in self.towers:
             t.dense.flat.grad = None
         loss.backward()

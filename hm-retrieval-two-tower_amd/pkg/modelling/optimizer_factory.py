@@ -64,28 +64,66 @@ class Adagrad(_Optimizer):
             raise ValueError(f"initial_accumulator_value must be non-negative: {initial_accumulator_value}")
         self.initial_accumulator_value = float(initial_accumulator_value)
         self.epsilon = float(epsilon)
+        self._prepared = None
+        self._side_streams = {}
+
+    def _sparse_specs(self, towers, with_grad: bool):
+        init = self.initial_accumulator_value
+        specs, batch = [], None
+        for tower in towers:
+            layer = tower.input_layer
+            if not layer.embedding_layers:
+                continue
+            if with_grad and layer.last_grad is None:
+                continue
+            for src in layer.sparse_sources():
+                t = src["table"]
+                (acc,) = self._slot(t.weight, 1, init)
+                batch = src["ids"][0].numel()
+                specs.append(dict(table=t.weight, slot0=acc, ids=src["ids"], grad_col_offset=src["grad_col_offset"],
+                                  grad=layer.last_grad if with_grad else None))
+        return specs, batch
+
+    def prepare(self, towers) -> None:
+        """Start the embedding update's id sort early, on a side stream (it reads
+        only the lookup ids of the last gather), so it overlaps the backward
+        pass; apply_gradients then joins it.  Optional: without it the sort
+        runs inside apply_gradients."""
+        self._prepared = None
+        if not torch.cuda.is_available():
+            return
+        specs, batch = self._sparse_specs(towers, with_grad=False)
+        if not specs or len(specs) > 16 or not batch:
+            return
+        cur = torch.cuda.current_stream()
+        side = self._side_streams.get(cur.device)
+        if side is None:
+            side = self._side_streams[cur.device] = torch.cuda.Stream(device=cur.device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            hip_ops.sparse_sort(specs, batch)
+        done = torch.cuda.Event()
+        done.record(side)
+        self._prepared = ([id(s["table"]) for s in specs], batch, done)
 
     def _apply(self, towers) -> None:
         lr, eps, init = self.learning_rate, self.epsilon, self.initial_accumulator_value
-        specs, batch = [], None
         for tower in towers:
             flat = tower.dense.flat
             if flat.grad is not None:
                 (acc,) = self._slot(flat, 1, init)
                 hip_ops.dense_adagrad(flat.data, acc, flat.grad, lr, eps)
-            layer = tower.input_layer
-            if layer.last_grad is None or not layer.embedding_layers:
-                continue
-            batch = layer.last_grad.shape[0]
-            for src in layer.sparse_sources():
-                t = src["table"]
-                (acc,) = self._slot(t.weight, 1, init)
-                specs.append(dict(table=t.weight, slot0=acc, ids=src["ids"], grad_col_offset=src["grad_col_offset"],
-                                  grad=layer.last_grad))
+        specs, batch = self._sparse_specs(towers, with_grad=True)
+        prepared, self._prepared = self._prepared, None
+        if prepared is not None:  # join the side stream before anything touches the workspace
+            torch.cuda.current_stream().wait_event(prepared[2])
         if specs:
             # every tower's tables in ONE call: one sort, one block pass (each
             # table reads its own tower's input gradient)
-            hip_ops.sparse_adagrad(specs, batch, None, lr, eps)
+            if prepared is not None and prepared[0] == [id(s["table"]) for s in specs] and prepared[1] == batch:
+                hip_ops.sparse_adagrad(specs, batch, None, lr, eps, presorted=True)
+            else:
+                hip_ops.sparse_adagrad(specs, batch, None, lr, eps)
 
 
 class Adam(_Optimizer):

@@ -135,6 +135,20 @@ int tt_sparse_adagrad(const tt_sparse_table* tables, int32_t num_tables,
                       float lr, float epsilon, void* workspace,
                       size_t workspace_bytes, tt_stream_t stream);
 
+/* The same update in two stages.  tt_sparse_sort builds and sorts the
+ * (table | row id, lookup) keys — it reads only the ids, so it can run early
+ * on a side stream, overlapped with the forward/backward compute;
+ * tt_sparse_adagrad_sorted then does the segmented sums and the apply.  Both
+ * calls must see the same tables (<= 16), batch and workspace, in that order.
+ * Results are identical to tt_sparse_adagrad. */
+int tt_sparse_sort(const tt_sparse_table* tables, int32_t num_tables,
+                   int64_t batch, void* workspace, size_t workspace_bytes,
+                   tt_stream_t stream);
+int tt_sparse_adagrad_sorted(const tt_sparse_table* tables, int32_t num_tables,
+                             int64_t batch, const float* grad, int64_t grad_stride,
+                             float lr, float epsilon, void* workspace,
+                             size_t workspace_bytes, tt_stream_t stream);
+
 /* Legacy Keras Adam sparse path: m,v decayed over the WHOLE slot, the scaled
  * duplicate-summed gradient scatter-added, then the WHOLE table updated with
  * lr_t = lr*sqrt(1-beta2^step)/(1-beta1^step) (step is 1-based). */
