@@ -142,29 +142,42 @@ def dist_env():
     return ws, rank, local
 
 
-def time_train(args, device, ws, rank):
-    from pkg.modelling.models.two_tower_model import GraphedTrainStep, TwoTowerModel
+def build_model(device, rank):
+    from pkg.modelling.models.two_tower_model import TwoTowerModel
     from pkg.modelling.optimizer_factory import OptimizerFactory
-    from pkg.modelling.distributed import ShardedTrainStep
 
     schema = main_schema()
     data = SyntheticHM(device, seed=1234, stream=rank)
     schema.set_candidate_prob_lookup(data.prob_lookup())
     model = TwoTowerModel.create_from_schema(schema, "article_id", device=device, seed=0)
     model.compile(optimizer=OptimizerFactory.get_optimizer("adagrad", {"learning_rate": 0.05}))
+    return model, data
+
+
+def time_train(args, model, data, device, ws):
+    """Times args.steps train steps (after args.warmup) bracketed by barrier +
+    synchronize; returns (max-over-ranks seconds, final loss).  At N>1 (or
+    --train-mode sharded) the large tables of `model` move into the
+    row-sharded step, so kernel-level timings must run before this."""
+    from pkg.modelling.models.two_tower_model import GraphedTrainStep
+    from pkg.modelling.distributed import ShardedTrainStep
+
     B = args.batch
     pool = [data.batch(B) for _ in range(4)]
     torch.cuda.synchronize()
-    if ws > 1:
+    if ws > 1 or args.train_mode == "sharded":
         # large tables (customer, postal, article) row-sharded over the ranks
         step = ShardedTrainStep(model, shard_min_rows=100_000)
-        run = lambda i: step(pool[i % len(pool)])
+        # the next batch's routing (ids only) runs a step ahead on a side stream
+        run = lambda i: step(pool[i % len(pool)], next_batch=pool[(i + 1) % len(pool)])
     else:
         step = GraphedTrainStep(model, pool[0], warmup=2)
         packed = [step.pack(b) for b in pool]  # one D2D copy per step
         run = lambda i: step(packed=packed[i % len(packed)])
     for i in range(args.warmup):
         run(i)
+    if getattr(step, "host_times", None) is not None:
+        step.host_times.clear()
     torch.cuda.synchronize()
     if ws > 1:
         torch.distributed.barrier()
@@ -183,13 +196,19 @@ def time_train(args, device, ws, rank):
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
     loss = float(out["loss"].item())
-    return model, data, dt, loss
+    if getattr(step, "host_times", None):
+        print("host ms/step by phase:", {k: round(v / args.steps * 1e3, 3)
+                                         for k, v in step.host_times.items()}, file=sys.stderr)  # timed steps only
+    return dt, loss
 
 
 def time_inbatch_kernel(model, data, device, B: int, reps: int = 20):
-    """Dominant kernel of the step: the fused rows pass (S = Q C^T, logQ,
-    online softmax, P.C) on the step's own embeddings.  Timed with HIP events
-    on the launching (current) stream over `reps` back-to-back launches."""
+    """Dominant kernels of the step: the two passes of the fused in-batch
+    softmax CE (tt_inbatch_softmax_xent, the entry the train step calls) on
+    the step's own embeddings.  Each pass kernel alone is bracketed by HIP
+    events recorded on its launch stream (tt_probe_arm), per launch, over
+    `reps` calls; the whole entry (prep + rows pass + combine + cols pass +
+    combine) is timed beside it."""
     from pkg.modelling import hip_ops
 
     batch = data.batch(B)
@@ -199,24 +218,26 @@ def time_inbatch_kernel(model, data, device, B: int, reps: int = 20):
         logq = model.candidate_logq(batch)
     E = q.shape[1]
     for _ in range(3):
-        hip_ops.inbatch_rows(q, c, logq)
+        hip_ops.inbatch_fused(q, c, logq)
     stream = torch.cuda.current_stream()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev = lambda: torch.cuda.Event(enable_timing=True)
+    rows, cols = [], []
+    e0, e1 = ev(), ev()
     e0.record(stream)
     for _ in range(reps):
-        hip_ops.inbatch_rows(q, c, logq)
+        r, k = (ev(), ev()), (ev(), ev())
+        hip_ops.probe_arm(hip_ops.PROBE_INBATCH_ROWS, *r)
+        hip_ops.probe_arm(hip_ops.PROBE_INBATCH_COLS, *k)
+        hip_ops.inbatch_fused(q, c, logq)
+        rows.append(r)
+        cols.append(k)
     e1.record(stream)
     e1.synchronize()
-    ms_rows = e0.elapsed_time(e1) / reps
-    lse, _, _ = hip_ops.inbatch_rows(q, c, logq)
-    e0.record(stream)
-    for _ in range(reps):
-        hip_ops.inbatch_cols(q, lse, c, logq)
-    e1.record(stream)
-    e1.synchronize()
-    ms_cols = e0.elapsed_time(e1) / reps
+    ms_entry = e0.elapsed_time(e1) / reps
+    ms_rows = sum(a.elapsed_time(b) for a, b in rows) / reps
+    ms_cols = sum(a.elapsed_time(b) for a, b in cols) / reps
     flops = 4.0 * B * B * E  # S (2 B^2 E) + P.C (2 B^2 E) per pass
-    return flops, ms_rows, ms_cols
+    return flops, ms_rows, ms_cols, ms_entry
 
 
 def pmc_traffic(kernel: str):
@@ -403,22 +424,31 @@ def main():
     ap.add_argument("--no-index", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--train-mode", choices=("auto", "sharded"), default="auto",
+                    help="sharded: run the N>1 row-sharded step (ShardedTrainStep) even on one rank")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
-    if ws > 1:
+    if ws > 1 or args.train_mode == "sharded":
         torch.cuda.set_device(local)
+        if ws == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", torch.cuda.current_device())
 
-    model, data, dt, loss = time_train(args, device, ws, rank)
+    model, data = build_model(device, rank)
     B = args.batch
+    # kernel-level timings on the unsharded model, before the train step takes its tables
+    flops, ms_rows, ms_cols, ms_entry = time_inbatch_kernel(model, data, device, B)
+    gather = time_gather(model, data, device, B)
+    dt, loss = time_train(args, model, data, device, ws)
     pairs = ws * B * args.steps
     value = pairs / dt
     ms_per_step = dt / args.steps * 1e3
 
-    flops, ms_rows, ms_cols = time_inbatch_kernel(model, data, device, B)
-    gather = time_gather(model, data, device, B)
     achieved = flops / (ms_rows * 1e-3) / 1e12
     result = {
         "metric": "positive pairs/sec (train) + index QPS @ Recall@100, 1/2/4/8 MI355X",
@@ -443,16 +473,18 @@ def main():
         },
         "final_loss": loss,
         "roofline": {
-            "kernel": "tt_inbatch_xent_rows: bf16 prep + inbatch_pass_kernel<128,0> (S=QC^T-logq, online softmax, "
-                      "P.C) + combine_rows_kernel, timed as one op",
+            "kernel": "inbatch_pass_kernel<128,0> (rows pass of tt_inbatch_softmax_xent: S=QC^T-logq, online "
+                      "softmax, P.C), HIP events around each launch on its stream",
             "bound": "mfma",
             "achieved": achieved,
             "peak": MI355X_BF16_DENSE_TFLOPS,
             "unit": "TFLOP/s",
             "frac": achieved / MI355X_BF16_DENSE_TFLOPS,
-            "traffic": pmc_traffic("inbatch_pass_kernel"),
-            "ms_per_launch_rows_op": ms_rows,
-            "ms_per_launch_cols_op": ms_cols,
+            "traffic": pmc_traffic("inbatch_pass_kernel<128, 0>"),
+            "ms_per_launch": ms_rows,
+            "cols_pass": {"kernel": "inbatch_pass_kernel<128,1>", "ms_per_launch": ms_cols,
+                          "achieved": flops / (ms_cols * 1e-3) / 1e12},
+            "ms_fused_entry": ms_entry,
             "algorithmic_flops_per_launch": flops,
         },
         "gather_roofline": gather,
@@ -463,7 +495,7 @@ def main():
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if ws > 1:
+    if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 
 

@@ -18,8 +18,29 @@ int fail(int code, const char* fmt, ...) {
 
 void clear_error() { g_last_error[0] = 0; }
 
+// One-shot kernel timing probes (tt_probe_arm): the next launch of the armed
+// kernel on this thread is bracketed by the caller's events.
+static thread_local hipEvent_t g_probe[TT_PROBE_COUNT][2] = {};
+
+void probe_begin(int kernel, hipStream_t st) {
+  if (g_probe[kernel][0]) (void)hipEventRecord(g_probe[kernel][0], st);
+}
+
+void probe_end(int kernel, hipStream_t st) {
+  if (g_probe[kernel][1]) (void)hipEventRecord(g_probe[kernel][1], st);
+  g_probe[kernel][0] = g_probe[kernel][1] = nullptr;
+}
+
 }  // namespace tt
 
 extern "C" const char* tt_version(void) { return "tt 0.1.0 gfx950"; }
 
 extern "C" const char* tt_last_error(void) { return tt::g_last_error; }
+
+extern "C" int tt_probe_arm(int32_t kernel, void* ev_start, void* ev_stop) {
+  tt::clear_error();
+  TT_REQUIRE(kernel >= 0 && kernel < TT_PROBE_COUNT, "tt_probe_arm: unknown kernel %d", kernel);
+  tt::g_probe[kernel][0] = static_cast<hipEvent_t>(ev_start);
+  tt::g_probe[kernel][1] = static_cast<hipEvent_t>(ev_stop);
+  return TT_OK;
+}

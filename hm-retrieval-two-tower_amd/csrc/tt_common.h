@@ -14,6 +14,9 @@ namespace tt {
 // ---- host-side error plumbing -------------------------------------------
 int fail(int code, const char* fmt, ...);
 void clear_error();
+// Timing probes armed by tt_probe_arm (no-ops unless armed).
+void probe_begin(int kernel, hipStream_t st);
+void probe_end(int kernel, hipStream_t st);
 
 #define TT_REQUIRE(cond, ...)                                  \
   do {                                                         \

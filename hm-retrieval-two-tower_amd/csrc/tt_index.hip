@@ -1231,16 +1231,20 @@ extern "C" int tt_bruteforce_search(const void* index, const float* cand, int64_
     ScreenArgs sa{index, w.qb, w.margin2, nq, n_cand, n_pad, k, p.S, p.R, w.buf, w.count, w.thr};
     ScreenCArgs ca{index, w.qb, w.margin2, nq, n_pad, k, p.R, w.buf, w.count};
     int rc;
+    probe_begin(TT_PROBE_INDEX_SCREEN, st);
     switch (D) {
       case 32: rc = launch_screen<32>(p, sa, ca, nq_pad, st); break;
       case 64: rc = launch_screen<64>(p, sa, ca, nq_pad, st); break;
       default: rc = launch_screen<128>(p, sa, ca, nq_pad, st); break;
     }
+    probe_end(TT_PROBE_INDEX_SCREEN, st);
     if (rc) return rc;
     FinalArgs fa{queries + q0 * ldq, ldq, cand, ldc, n_cand, dim, k, p.S, p.H, p.R, p.L, p.P, vec4, 0, nq,
                  index_offset, w.margin2, w.buf, w.count, p.bins ? w.thr : nullptr, out_scores + q0 * k,
                  out_idx + q0 * k};
+    probe_begin(TT_PROBE_INDEX_FINALIZE, st);
     hipLaunchKernelGGL(finalize_kernel, dim3(nq), dim3(kWave), shm, st, fa);
+    probe_end(TT_PROBE_INDEX_FINALIZE, st);
     TT_CHECK_LAUNCH();
   }
   return TT_OK;

@@ -120,8 +120,10 @@ __global__ void __launch_bounds__(kThreads) build_keys_kernel(const Job j, int t
     const int s = static_cast<int>(loc / j.batch);
     const int64_t b = loc - s * j.batch;
     const int32_t r = T.ids[s][b];
-    id = (r >= 0 && r < T.num_rows) ? static_cast<uint32_t>(r) : invalid;
-    val = (static_cast<uint32_t>(s) << kSrcShift) | static_cast<uint32_t>(b);  // source | batch row
+    const bool ok = r >= 0 && r < T.num_rows;
+    id = ok ? static_cast<uint32_t>(r) : invalid;
+    // invalid lookups keep no gradient offset: nothing reads their rows
+    val = ok ? (static_cast<uint32_t>(s) << kSrcShift) | static_cast<uint32_t>(b) : 0xFFFFFFFFu;
   }
   j.keys_in[i] = (static_cast<uint32_t>(t) << j.id_bits) | id;
   j.vals_in[i] = val;
@@ -286,6 +288,8 @@ __global__ void __launch_bounds__(kThreads) join_kernel(const Job j, const Apply
   const uint32_t klast = key[kBlock - 1];
   const bool tail_cont = (b0 + kBlock < tend) && j.keys[b0 + kBlock] == klast;
   if (!tail_cont) return;
+  // the invalid-id run (sorted last in the region) is never applied: skip its join
+  if ((klast & ((1u << j.id_bits) - 1u)) >= static_cast<uint32_t>(T.num_rows)) return;
   // the continuing segment must START in this block
   int seg_start = kBlock - 1;
 #pragma unroll

@@ -19,6 +19,7 @@ __all__ = [
     "GatherCall",
     "RowTable",
     "SparseTable",
+    "RouteLookup",
     "MAX_SEGMENTS",
     "MAX_SOURCES",
     "lib",
@@ -71,6 +72,14 @@ class RowTable(ctypes.Structure):
     ]
 
 
+class RouteLookup(ctypes.Structure):
+    _fields_ = [
+        ("ids", c_void_p),
+        ("num_rows", c_int64),
+        ("tag", c_int32),
+    ]
+
+
 class SparseTable(ctypes.Structure):
     _fields_ = [
         ("table", c_void_p),
@@ -90,6 +99,7 @@ class SparseTable(ctypes.Structure):
 _PROTOS = {
     "tt_version": (c_char_p, []),
     "tt_last_error": (c_char_p, []),
+    "tt_probe_arm": (c_int32, [c_int32, c_void_p, c_void_p]),
     "tt_gather_grouped": (c_int32, [POINTER(GatherSegment), c_int32, c_int64, c_void_p, c_int64, c_void_p]),
     "tt_gather_multi": (c_int32, [POINTER(GatherCall), c_int32, c_int64, c_void_p]),
     "tt_gather_tagged": (c_int32, [POINTER(RowTable), c_int32, c_int32, c_void_p, c_void_p, c_int64, c_void_p, c_int64,
@@ -116,6 +126,12 @@ _PROTOS = {
     "tt_sparse_adagrad_sorted": (
         c_int32,
         [POINTER(SparseTable), c_int32, c_int64, c_void_p, c_int64, c_float, c_float, c_void_p, c_size_t, c_void_p]),
+    "tt_route_workspace_size": (c_size_t, [c_int32, c_int64, c_int32, c_int64, c_int32]),
+    "tt_route_requests": (
+        c_int32,
+        [POINTER(RouteLookup), c_int32, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_size_t, c_void_p]),
+    "tt_route_owner": (c_int32, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "tt_relu_bias_grad_workspace_size": (c_size_t, [c_int64, c_int32]),
     "tt_relu_bias_grad": (
         c_int32,

@@ -23,12 +23,17 @@ defaults are the libtt kernels and the product never falls back to them.
 """
 from __future__ import annotations
 
+import logging
+import os
+import time
 from dataclasses import dataclass
 from typing import Any, Callable, Dict, Iterable, List, Optional, Tuple
 
 import numpy as np
 import torch
 import torch.distributed as dist
+
+logger = logging.getLogger(__name__)
 
 __all__ = ["IndexOps", "ShardedBruteForceIndex", "DataParallelTrainStep", "shard_range", "all_gather_cat",
            "EmbeddingOps", "ShardedTables", "ShardedTrainStep"]
@@ -174,6 +179,55 @@ class DataParallelTrainStep:
 
 
 # --------------------------------------------------------------------------- row-sharded tables
+def torch_route_requests(lookups: List[Tuple[torch.Tensor, int, int]], world: int, num_tags: int):
+    """Restatement of tt_route_requests in torch ops (the CPU/gloo tests'
+    implementation): (send [R, 2], counts [world] int64, num_requests [1],
+    idx [L, B])."""
+    dev = lookups[0][0].device
+    B = lookups[0][0].numel()
+    by_tag: Dict[int, List[int]] = {}
+    for i, (_, _, tag) in enumerate(lookups):
+        by_tag.setdefault(tag, []).append(i)
+    req_ids, req_tags, inverse, starts = [], [], {}, {}
+    off = 0
+    for tag in sorted(by_tag):
+        rows = lookups[by_tag[tag][0]][1]
+        ids = torch.cat([lookups[i][0].reshape(-1) for i in by_tag[tag]])
+        ids = torch.where((ids >= 0) & (ids < rows), ids, torch.full_like(ids, -1))
+        uniq, inv = torch.unique(ids, sorted=True, return_inverse=True)
+        req_ids.append(uniq.to(torch.int32))
+        req_tags.append(torch.full_like(uniq, tag, dtype=torch.int32))
+        inverse[tag] = inv
+        starts[tag] = off
+        off += uniq.numel()
+    req_ids = torch.cat(req_ids)
+    req_tags = torch.cat(req_tags)
+    R = req_ids.numel()
+    owner = torch.remainder(req_ids, world)  # invalid (-1) ids go to rank world-1
+    owner_sorted, perm = torch.sort(owner.to(torch.int64), stable=True)
+    send = torch.stack([req_ids[perm], req_tags[perm]], 1).contiguous()
+    counts = torch.bincount(owner_sorted, minlength=world).to(torch.int64)
+    inv_perm = torch.empty_like(perm)
+    inv_perm[perm] = torch.arange(R, device=dev)
+    idx = torch.empty(len(lookups), B, dtype=torch.int32, device=dev)
+    pos: Dict[int, int] = {}
+    for i, (ids, _, tag) in enumerate(lookups):
+        k = pos.get(tag, 0)
+        u = inverse[tag][k:k + B]
+        pos[tag] = k + B
+        idx[i] = inv_perm[starts[tag] + u].to(torch.int32)
+    return send, counts, torch.tensor([R], dtype=torch.int32, device=dev), idx
+
+
+def torch_route_owner(recv: torch.Tensor, world: int, num_tags: int):
+    tags = recv[:, 1].contiguous()
+    gid = recv[:, 0]
+    rows = torch.where(gid >= 0, torch.div(gid, world, rounding_mode="floor"), torch.full_like(gid, -1))
+    rows = rows.to(torch.int32).contiguous()
+    tids = torch.stack([torch.where(tags == t, rows, torch.full_like(rows, -1)) for t in range(num_tags)])
+    return tags, rows, tids.reshape(num_tags, -1)
+
+
 @dataclass
 class EmbeddingOps:
     """Kernels of the row-sharded path (defaults: libtt; tests inject CPU ones)."""
@@ -182,18 +236,37 @@ class EmbeddingOps:
     scatter_sum: Callable[..., None]
     sparse_adagrad: Callable[..., None]
     dense_adagrad: Callable[..., None]
+    route_requests: Callable[..., Any] = torch_route_requests
+    route_owner: Callable[..., Any] = torch_route_owner
 
     @staticmethod
     def hip() -> "EmbeddingOps":
         from pkg.modelling import hip_ops
 
-        return EmbeddingOps(hip_ops.gather_multi, hip_ops.gather_tagged, hip_ops.sparse_scatter_sum,
-                            hip_ops.sparse_adagrad, hip_ops.dense_adagrad)
+        # distinct workspaces: the scatter-sum runs inside the captured middle of
+        # ShardedTrainStep (fixed size), the owner-side Adagrad outside it with
+        # a size that varies per step — it must never move the graph's buffer
+        return EmbeddingOps(hip_ops.gather_multi, hip_ops.gather_tagged,
+                            lambda specs, b, g: hip_ops.sparse_scatter_sum(specs, b, g, ws_tag="sparse_mid"),
+                            lambda specs, b, g, lr, eps: hip_ops.sparse_adagrad(specs, b, g, lr, eps,
+                                                                                ws_tag="sparse_owner"),
+                            hip_ops.dense_adagrad, hip_ops.route_requests, hip_ops.route_owner)
 
 
 def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits: List[int], in_splits: List[int], group) -> torch.Tensor:
     dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
     return out
+
+
+class _Route:
+    """Where one batch's sharded lookups go and come back from; depends only on
+    the ids, so it can be computed a step ahead (ShardedTables.route)."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+    def tensors(self) -> List[torch.Tensor]:
+        return [self.tags, self.rows, *self.table_ids, *self.idx]
 
 
 class ShardedTables:
@@ -203,10 +276,13 @@ class ShardedTables:
     of each table and of its Adagrad accumulator.
 
     One exchange per step for all sharded tables:
-      forward   requests: each rank dedups its lookups per table, buckets the
-                distinct (table, row) pairs by owner and sends them with one
-                all_to_all; owners answer with one tt_gather_tagged launch and
-                one all_to_all of rows back.
+      routing   (ids only: can run a step ahead, on a side stream, over its
+                own process group) each rank dedups its lookups per table,
+                buckets the distinct (table, row) requests by owner and sends
+                them with one all_to_all (plus one tiny count exchange — the
+                step's only host sync);
+      forward   owners answer with one tt_gather_tagged launch and one
+                all_to_all of rows back;
       backward  each rank sums its lookup gradients per request
                 (tt_sparse_scatter_sum, same order as the single-GPU dedup),
                 one all_to_all sends them to the owners, and each owner applies
@@ -246,84 +322,65 @@ class ShardedTables:
     def local_rows(self, name: str) -> int:
         return self.shard[name].shape[0]
 
+    # -- routing (ids only) ------------------------------------------------
+    def route(self, lookups: List[Tuple[str, torch.Tensor]], group=None) -> _Route:
+        """lookups: (table name, ids [B] int32).  Collectives run on `group`
+        (default: the tables' group) and on the current stream."""
+        group = self.group if group is None else group
+        W, T = self.world, len(self.names)
+        dev = lookups[0][1].device
+        tagged = [(ids.reshape(-1), self.rows[name], self.names.index(name)) for name, ids in lookups]
+        send, send_counts, _, idx = self.ops.route_requests(tagged, W, T)
+        recv_counts = torch.empty_like(send_counts)
+        _a2a(recv_counts, send_counts, [1] * W, [1] * W, group)
+        counts = torch.stack([send_counts, recv_counts]).cpu()  # the one host sync of the step
+        s_split, r_split = counts[0].tolist(), counts[1].tolist()
+        R = int(sum(s_split))
+        recv = torch.empty(sum(r_split), 2, dtype=torch.int32, device=dev)
+        _a2a(recv, send[:R], r_split, s_split, group)
+        tags, rows, tids = self.ops.route_owner(recv, W, T)
+        return _Route(s_split=s_split, r_split=r_split, R=R, n_recv=int(sum(r_split)), tags=tags, rows=rows,
+                      table_ids=list(tids.unbind(0)), idx=list(idx.unbind(0)), dev=dev)
+
     # -- forward -----------------------------------------------------------
+    def fetch_routed(self, rt: _Route, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Rows of the routed requests, [R, dim] (into out[:R] when given)."""
+        reply = torch.empty(rt.n_recv, self.dim, dtype=torch.float32, device=rt.dev)
+        self.ops.gather_tagged([self.shard[n] for n in self.names], rt.tags, rt.rows, reply)
+        got = out[:rt.R] if out is not None else torch.empty(rt.R, self.dim, dtype=torch.float32, device=rt.dev)
+        _a2a(got, reply, rt.s_split, rt.r_split, self.group)
+        return got
+
     def fetch(self, lookups: List[Tuple[str, torch.Tensor]]) -> Tuple[torch.Tensor, List[torch.Tensor]]:
         """lookups: (table name, ids [B] int32) -> (rows [R, dim], row index per
         lookup [B] int32): lookup l's embedding of batch row b is rows[idx_l[b]]."""
-        W = self.world
-        dev = lookups[0][1].device
-        by_table: Dict[str, List[int]] = {}
-        for i, (name, _) in enumerate(lookups):
-            by_table.setdefault(name, []).append(i)
-        req_ids, req_tags, inverse, starts = [], [], {}, {}
-        off = 0
-        for ti, name in enumerate(self.names):
-            if name not in by_table:
-                continue
-            ids = torch.cat([lookups[i][1].reshape(-1) for i in by_table[name]])
-            ids = torch.where((ids >= 0) & (ids < self.rows[name]), ids, torch.full_like(ids, -1))
-            uniq, inv = torch.unique(ids, sorted=True, return_inverse=True)
-            req_ids.append(uniq.to(torch.int32))
-            req_tags.append(torch.full_like(uniq, ti, dtype=torch.int32))
-            inverse[name] = inv
-            starts[name] = off
-            off += uniq.numel()
-        req_ids = torch.cat(req_ids)
-        req_tags = torch.cat(req_tags)
-        R = req_ids.numel()
-        owner = torch.remainder(req_ids, W)  # invalid (-1) ids go to rank W-1 and answer zeros
-        owner_sorted, perm = torch.sort(owner.to(torch.int64), stable=True)
-        send = torch.stack([req_ids[perm], req_tags[perm]], 1).contiguous()
-        send_counts = torch.bincount(owner_sorted, minlength=W).to(torch.int64)
-        recv_counts = torch.empty_like(send_counts)
-        _a2a(recv_counts, send_counts, [1] * W, [1] * W, self.group)
-        counts = torch.stack([send_counts, recv_counts]).cpu()  # the one host sync of the step
-        s_split, r_split = counts[0].tolist(), counts[1].tolist()
-        recv = torch.empty(sum(r_split), 2, dtype=torch.int32, device=dev)
-        _a2a(recv, send, r_split, s_split, self.group)
-        # owner: answer every request with one launch
-        tags = recv[:, 1].contiguous()
-        gid = recv[:, 0]
-        rows = torch.where(gid >= 0, torch.div(gid, W, rounding_mode="floor"), torch.full_like(gid, -1))
-        rows = rows.to(torch.int32).contiguous()
-        reply = torch.empty(tags.numel(), self.dim, dtype=torch.float32, device=dev)
-        self.ops.gather_tagged([self.shard[n] for n in self.names], tags, rows, reply)
-        got = torch.empty(R, self.dim, dtype=torch.float32, device=dev)
-        _a2a(got, reply, s_split, r_split, self.group)
-        # position of request (table, unique u) in `got`
-        inv_perm = torch.empty_like(perm)
-        inv_perm[perm] = torch.arange(R, device=dev)
-        idx = []
-        pos_in_table: Dict[str, int] = {}
-        for name, ids in lookups:
-            k = pos_in_table.get(name, 0)
-            n = ids.numel()
-            u = inverse[name][k:k + n]
-            pos_in_table[name] = k + n
-            idx.append(inv_perm[starts[name] + u].to(torch.int32).contiguous())
-        self._ctx = dict(s_split=s_split, r_split=r_split, tags=tags, rows=rows, R=R, dev=dev)
-        return got, idx
+        rt = self.route(lookups)
+        self._ctx = rt
+        return self.fetch_routed(rt), rt.idx
 
     # -- backward + update -------------------------------------------------
+    def apply_routed(self, rt: _Route, g_req: torch.Tensor, lr: float, eps: float) -> None:
+        """g_req[:R]: the per-request gradient sums of the routed requests;
+        returns them to the owners, which apply Adagrad to their shards."""
+        recv = torch.empty(rt.n_recv, self.dim, dtype=torch.float32, device=rt.dev)
+        _a2a(recv, g_req[:rt.R], rt.r_split, rt.s_split, self.group)
+        specs = [dict(table=self.shard[name], slot0=self.acc[name], ids=[rt.table_ids[ti]], grad_col_offset=[0])
+                 for ti, name in enumerate(self.names)]
+        if recv.shape[0] > 0:
+            self.ops.sparse_adagrad(specs, recv.shape[0], recv, lr, eps)
+
     def apply(self, grads: List[Tuple[torch.Tensor, List[Tuple[torch.Tensor, int]]]], lr: float, eps: float) -> None:
         """grads: per gradient matrix [B, width] its (row index from fetch, column)
         sources.  Sums per request, returns the sums to the owners, and applies
         Adagrad to the local shards."""
-        c = self._ctx
-        g_req = torch.zeros(c["R"], self.dim, dtype=torch.float32, device=c["dev"])
+        rt = self._ctx
+        g_req = torch.zeros(rt.R, self.dim, dtype=torch.float32, device=rt.dev)
         for gmat, sources in grads:
             if not sources:
                 continue
             spec = [dict(table=g_req, ids=[s[0] for s in sources], grad_col_offset=[s[1] for s in sources])]
             self.ops.scatter_sum(spec, gmat.shape[0], gmat)
-        recv = torch.empty(len(c["tags"]), self.dim, dtype=torch.float32, device=c["dev"])
-        _a2a(recv, g_req, c["r_split"], c["s_split"], self.group)
-        specs = []
-        for ti, name in enumerate(self.names):
-            ids = torch.where(c["tags"] == ti, c["rows"], torch.full_like(c["rows"], -1)).contiguous()
-            specs.append(dict(table=self.shard[name], slot0=self.acc[name], ids=[ids], grad_col_offset=[0]))
-        if recv.shape[0] > 0:
-            self.ops.sparse_adagrad(specs, recv.shape[0], recv, lr, eps)
+        self.apply_routed(rt, g_req, lr, eps)
         self._ctx = None
 
     def gather_full(self, name: str) -> torch.Tensor:
@@ -361,16 +418,33 @@ class ShardedTrainStep:
     """
     Data-parallel train step with the large embedding tables row-sharded
     (ShardedTables) and the small ones replicated.  Per-replica in-batch
-    negatives, as DataParallelTrainStep.  Per step: the sharded-table exchange
-    (3 all_to_all + one tiny count exchange), one all_reduce bucket holding the
-    MLP gradients, the dense gradients of the small tables and the loss.
-    Sparse work per rank stays ~constant as ranks are added (each owner updates
-    only its rows), unlike gathering every replica's sparse gradients.
+    negatives, as DataParallelTrainStep.  Sparse work per rank stays ~constant
+    as ranks are added (each owner updates only its rows), unlike gathering
+    every replica's sparse gradients.
+
+    Per step, on the compute stream:
+      1. owners answer the routed row requests (tt_gather_tagged) and one
+         all_to_all brings the rows back into a static buffer;
+      2. the static middle — both towers' gathers (one tt_gather_multi), the
+         MLPs + fused in-batch loss forward and backward, the per-request
+         gradient sums of the sharded tables and the dense gradients of the
+         small ones (ONE tt_sparse_scatter_sum: one sort), packed with the MLP
+         gradients and the loss into one bucket — replayed as a hipGraph
+         from the second step on;
+      3. one all_to_all returns the per-request sums to the owners, which
+         apply tt_sparse_adagrad to their shards;
+      4. one all_reduce of the bucket, then tt_dense_adagrad on the two tower
+         MLP buffers and on ONE flat buffer holding every small table.
+    Routing (dedup + owner bucketing + request exchange; ids only) of the
+    NEXT batch, when passed as `next_batch`, runs on a side stream over its
+    own process group while this step computes, so its host sync does not
+    stall the compute stream.
 
     Adagrad (the reference's optimizer, main.py:100-101) only.
     """
 
-    def __init__(self, model, shard_min_rows: int = 100_000, group=None, ops: Optional[EmbeddingOps] = None):
+    def __init__(self, model, shard_min_rows: int = 100_000, group=None, ops: Optional[EmbeddingOps] = None,
+                 use_graph: bool = True):
         from pkg.modelling.optimizer_factory import Adagrad
 
         opt = model.optimizer
@@ -381,8 +455,9 @@ class ShardedTrainStep:
         self.ops = ops or EmbeddingOps.hip()
         self.world = dist.get_world_size(group)
         self.lr, self.eps, self.init = opt.learning_rate, opt.epsilon, opt.initial_accumulator_value
+        self.use_graph = use_graph
         big: Dict[str, torch.Tensor] = {}
-        self.small: Dict[str, Any] = {}
+        self.small: Dict[Any, Any] = {}
         for tower in model.towers:
             for name, t in tower.input_layer.embedding_layers.items():
                 key = (id(tower), name)
@@ -396,85 +471,205 @@ class ShardedTrainStep:
             for t in tower.input_layer.embedding_layers.values():
                 if hasattr(t, "_shard_key"):
                     t.weight = None
-        self._small_acc = {k: torch.full_like(t.weight, self.init) for k, t in self.small.items()}
+        # every small (replicated) table becomes a view of ONE flat buffer, so
+        # its dense gradient is one zero-fill and its update one launch
+        dev = model.device
+        n_small = sum(t.weight.numel() for t in self.small.values())
+        self._small_flat = torch.empty(max(n_small, 1), dtype=torch.float32, device=dev)
+        self._small_grad = torch.zeros_like(self._small_flat)
+        self._small_views: Dict[Any, Tuple[torch.Tensor, torch.Tensor]] = {}
+        off = 0
+        for key, t in self.small.items():
+            n = t.weight.numel()
+            self._small_flat[off:off + n].copy_(t.weight.reshape(-1))
+            t.weight = self._small_flat[off:off + n].view(t.num_rows, t.dim)
+            self._small_views[key] = (t.weight, self._small_grad[off:off + n].view(t.num_rows, t.dim))
+            off += n
+        self._small_acc = torch.full_like(self._small_flat, self.init)
         self._dense_acc = [torch.full_like(t.dense.flat, self.init) for t in model.towers]
+        self._route_group = dist.new_group(list(range(self.world)), backend=dist.get_backend(group)) \
+            if self.world > 1 else group
+        self._side = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
+        self._pending = None     # (batch object id, _Route) routed a step ahead
+        self._static = None      # static batch / request buffers (set up on the first call)
+        self._graph = None
+        self._calls = 0
         self._out_grads = None
+        self.host_times: Optional[Dict[str, float]] = {} if os.environ.get("TT_HOST_PROFILE") else None
 
-    def __call__(self, batch: Dict[str, Any]) -> Dict[str, torch.Tensor]:
+    def _tick(self, name: str, t0: float) -> float:
+        t1 = time.perf_counter()
+        if self.host_times is not None:
+            self.host_times[name] = self.host_times.get(name, 0.0) + (t1 - t0)
+        return t1
+
+    # -- static buffers ----------------------------------------------------
+    def _lookups(self, batch) -> List[Tuple[str, torch.Tensor, int, int]]:
+        """(shard key, ids, tower index, column offset) of every sharded lookup."""
         m = self.model
         q, c = m._split(batch)
+        out = []
+        for li, (layer, x) in enumerate(zip([t.input_layer for t in m.towers], [q, c])):
+            for f, off in zip(layer.categorical_features, layer.column_offsets()):
+                t = layer.embedding_layers[f.name]
+                if hasattr(t, "_shard_key"):
+                    out.append((t._shard_key, layer._ids(x[f.name]), li, off))
+        return out
+
+    def _setup(self, batch) -> None:
+        m = self.model
+        dev = m.device
+        self._static = {}
+        for k, v in batch.items():
+            t = v if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v))
+            t = t.reshape(-1).to(dev)
+            if t.dtype not in (torch.float32, torch.int32):
+                t = t.to(torch.float32 if t.is_floating_point() else torch.int32)
+            self._static[k] = torch.empty_like(t)
+        lk = self._lookups(self._static)
+        B = next(iter(self._static.values())).numel()
+        self._B = B
+        cap = max(len(lk) * B, 1)  # distinct requests <= lookups
+        dim = self.tables.dim if self.tables is not None else 1
+        self._got = torch.zeros(cap, dim, dtype=torch.float32, device=dev)
+        self._g_req = torch.zeros(cap, dim, dtype=torch.float32, device=dev)
+        self._idx = [torch.zeros(B, dtype=torch.int32, device=dev) for _ in lk]
+        n_bucket = sum(t.dense.flat.numel() for t in m.towers) + self._small_grad.numel() + 1
+        self._bucket = torch.zeros(n_bucket, dtype=torch.float32, device=dev)
+
+    def _load(self, batch) -> None:
+        for k, v in batch.items():
+            t = v if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v))
+            self._static[k].copy_(t.reshape(-1), non_blocking=True)
+
+    # -- the static middle (graph-captured) --------------------------------
+    def _middle(self) -> None:
+        m = self.model
+        x = self._static
+        q, c = m._split(x)
         layers = [t.input_layer for t in m.towers]
-        xs = [q, c]
-        B = None
-        calls, widths, sharded_srcs = [], [], []
-        lookups = []
-        for li, (layer, x) in enumerate(zip(layers, xs)):
-            for f, off in zip(layer.categorical_features, layer.column_offsets()):
-                t = layer.embedding_layers[f.name]
-                if hasattr(t, "_shard_key"):
-                    lookups.append((t._shard_key, layer._ids(x[f.name]), li, off))
-        got, idx = (self.tables.fetch([(k, ids) for k, ids, _, _ in lookups]) if lookups else (None, []))
-        small_srcs = []
-        for li, (layer, x) in enumerate(zip(layers, xs)):
-            segs, srcs_big, srcs_small = [], [], []
+        calls, widths, big_srcs, small_srcs = [], [], {}, {}
+        j = 0
+        for li, (layer, xx) in enumerate(zip(layers, [q, c])):
+            segs = []
             for f in layer.numerical_features:
-                v = x[f.name]
-                v = (v if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v, np.float32)))
-                v = v.reshape(-1).to(device=layer.device, dtype=torch.float32).contiguous()
-                segs.append((v, None, len(segs)))
+                segs.append((xx[f.name].to(torch.float32), None, len(segs)))
             for f, off in zip(layer.categorical_features, layer.column_offsets()):
                 t = layer.embedding_layers[f.name]
                 if hasattr(t, "_shard_key"):
-                    j = next(i for i, lk in enumerate(lookups) if lk[2] == li and lk[3] == off)
-                    segs.append((got, idx[j], off))
-                    srcs_big.append((idx[j], off))
+                    segs.append((self._got, self._idx[j], off))
+                    big_srcs.setdefault(t._shard_key, (li, []))[1].append((self._idx[j], off))
+                    j += 1
                 else:
-                    ids = layer._ids(x[f.name])
+                    ids = layer._ids(xx[f.name])
                     segs.append((t.weight, ids, off))
-                    srcs_small.append((f.name, ids, off))
-            B = segs[0][1].numel() if segs[0][1] is not None else segs[0][0].numel()
-            out = torch.empty(B, layer.row_stride, dtype=torch.float32, device=layer.device)
+                    small_srcs.setdefault((id(m.towers[li]), f.name), (li, []))[1].append((ids, off))
+            out = torch.empty(self._B, layer.row_stride, dtype=torch.float32, device=layer.device)
             calls.append((segs, out))
             widths.append(layer.output_dim)
-            sharded_srcs.append(srcs_big)
-            small_srcs.append(srcs_small)
         anchors = [layer._anchor for layer in layers]
-        qi, ci = _ShardedGatherFn.apply(self, calls, B, widths, *anchors)
-        loss = m.tower_loss(qi, ci, m.candidate_logq(batch))
+        qi, ci = _ShardedGatherFn.apply(self, calls, self._B, widths, *anchors)
+        loss = m.tower_loss(qi, ci, m.candidate_logq(x))
         for t in m.towers:
             t.dense.flat.grad = None
         loss.backward()
         grads = self._out_grads
-        # sharded tables: per-request sums -> owners -> Adagrad on the shards
+        # one scatter-sum call: per-request sums of the sharded tables' lookups
+        # (rows of g_req, disjoint per table) and dense small-table gradients
+        self._small_grad.zero_()
+        specs = []
+        for key, (li, srcs) in big_srcs.items():
+            specs.append(dict(table=self._g_req, ids=[s[0] for s in srcs], grad_col_offset=[s[1] for s in srcs],
+                              grad=grads[li]))
+        for key, (li, srcs) in small_srcs.items():
+            specs.append(dict(table=self._small_views[key][1], ids=[s[0] for s in srcs],
+                              grad_col_offset=[s[1] for s in srcs], grad=grads[li]))
+        if specs:
+            self.ops.scatter_sum(specs, self._B, grads[0])
+        torch.cat([t.dense.flat.grad.reshape(-1) for t in m.towers]
+                  + [self._small_grad, loss.detach().reshape(1)], out=self._bucket)
+
+    # -- one step ----------------------------------------------------------
+    def _route(self, batch) -> _Route:
+        return self.tables.route([(k, ids) for k, ids, _, _ in self._lookups(batch)], group=self._route_group)
+
+    def prefetch(self, batch) -> None:
+        """Route `batch` (the next step's) on the side stream now."""
+        if self.tables is None:
+            return
+        ready = torch.cuda.Event()
+        ready.record()  # the batch's ids exist before the work already queued here
+        with torch.cuda.stream(self._side):
+            self._side.wait_event(ready)
+            rt = self._route(batch)
+            rt.event = torch.cuda.Event()
+            rt.event.record(self._side)
+        self._pending = (id(batch), rt)
+
+    def __call__(self, batch: Dict[str, Any], next_batch: Optional[Dict[str, Any]] = None) -> Dict[str, torch.Tensor]:
+        m = self.model
+        tm = time.perf_counter()
+        if self._static is None:
+            self._setup(batch)
+        cur = torch.cuda.current_stream() if self._side is not None else None
+        if next_batch is not None and self._side is not None:
+            pre = torch.cuda.Event()
+            pre.record(cur)
+        self._load(batch)
+        tm = self._tick("load", tm)
+        rt = None
         if self.tables is not None:
-            self.tables.apply([(g, srcs) for g, srcs in zip(grads, sharded_srcs)], self.lr, self.eps)
-        # one all_reduce bucket: MLP grads, small-table dense grads, loss
-        parts = [t.dense.flat.grad.reshape(-1) for t in m.towers]
-        small_grads = []
-        for li, (layer, srcs) in enumerate(zip(layers, small_srcs)):
-            by_name: Dict[str, List[Tuple[torch.Tensor, int]]] = {}
-            for name, ids, off in srcs:
-                by_name.setdefault(name, []).append((ids, off))
-            specs = []
-            for name, s in by_name.items():
-                t = layer.embedding_layers[name]
-                gdense = torch.zeros_like(t.weight)
-                small_grads.append(((id(m.towers[li]), name), t, gdense))
-                specs.append(dict(table=gdense, ids=[x[0] for x in s], grad_col_offset=[x[1] for x in s]))
-            if specs:
-                self.ops.scatter_sum(specs, grads[li].shape[0], grads[li])
-        parts += [g.reshape(-1) for _, _, g in small_grads]
-        parts.append(loss.detach().reshape(1))
-        bucket = torch.cat(parts)
-        dist.all_reduce(bucket, group=self.group)
+            if self._pending is not None and self._pending[0] == id(batch):
+                rt = self._pending[1]
+                cur.wait_event(rt.event)
+                for t in rt.tensors():  # made on the side stream, read on this one
+                    t.record_stream(cur)
+            else:
+                rt = self._route(batch)
+            self._pending = None
+            tm = self._tick("route_wait", tm)
+            self.tables.fetch_routed(rt, out=self._got)
+            for buf, ix in zip(self._idx, rt.idx):
+                buf.copy_(ix)
+            tm = self._tick("fetch", tm)
+        if self._graph is None and self.use_graph and self._calls >= 1 and cur is not None:
+            try:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._middle()
+                self._graph = g
+            except Exception as e:  # keep training eagerly (still the HIP kernels)
+                logger.warning(f"ShardedTrainStep: graph capture failed ({e!r}); running eagerly")
+                self.use_graph = False
+        if self._graph is not None:
+            self._graph.replay()
+        else:
+            self._middle()
+        self._calls += 1
+        tm = self._tick("middle", tm)
+        if rt is not None:
+            self.tables.apply_routed(rt, self._g_req, self.lr, self.eps)
+        tm = self._tick("apply", tm)
+        dist.all_reduce(self._bucket, group=self.group)
         off = 0
         for ti, t in enumerate(m.towers):
             n = t.dense.flat.numel()
-            self.ops.dense_adagrad(t.dense.flat.data, self._dense_acc[ti], bucket[off:off + n].view_as(t.dense.flat),
+            self.ops.dense_adagrad(t.dense.flat.data, self._dense_acc[ti], self._bucket[off:off + n].view_as(t.dense.flat),
                                    self.lr, self.eps)
             off += n
-        for key, t, g in small_grads:
-            n = g.numel()
-            self.ops.dense_adagrad(t.weight, self._small_acc[key], bucket[off:off + n].view_as(g), self.lr, self.eps)
-            off += n
-        return {"loss": bucket[off:off + 1].reshape(())}
+        n = self._small_grad.numel()
+        if self.small:
+            self.ops.dense_adagrad(self._small_flat, self._small_acc, self._bucket[off:off + n], self.lr, self.eps)
+        off += n
+        loss = self._bucket[off:off + 1].reshape(()).clone()
+        tm = self._tick("dense", tm)
+        if next_batch is not None and self._side is not None and self.tables is not None:
+            ready = pre
+            with torch.cuda.stream(self._side):
+                self._side.wait_event(ready)
+                rt2 = self._route(next_batch)
+                rt2.event = torch.cuda.Event()
+                rt2.event.record(self._side)
+            self._pending = (id(next_batch), rt2)
+        self._tick("prefetch", tm)
+        return {"loss": loss}

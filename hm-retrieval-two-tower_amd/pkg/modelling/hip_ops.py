@@ -28,6 +28,9 @@ __all__ = [
     "inbatch_rows",
     "inbatch_cols",
     "inbatch_fused",
+    "probe_arm",
+    "route_requests",
+    "route_owner",
     "bruteforce_build",
     "bruteforce_search",
     "topk_merge",
@@ -184,7 +187,7 @@ def _sparse_tables(tables: Sequence[dict], batch: int, adam: bool, slots: bool =
 
 
 def sparse_adagrad(tables: Sequence[dict], batch: int, grad: Optional[torch.Tensor], lr: float,
-                   epsilon: float, presorted: bool = False) -> None:
+                   epsilon: float, presorted: bool = False, ws_tag: str = "sparse") -> None:
     """tables: dicts with table, slot0 (accumulator), ids [list], grad_col_offset [list] and an
     optional per-table "grad" [batch, *] that overrides the call's `grad` (which may then be None),
     so one call — one sort — updates the tables of both towers.  presorted: the ids were
@@ -199,7 +202,7 @@ def sparse_adagrad(tables: Sequence[dict], batch: int, grad: Optional[torch.Tens
     L = lib()
     need = L.tt_sparse_workspace_size(arr, len(tables), batch)
     dev = grad.device if grad is not None else tables[0]["grad"].device
-    ws = Workspace.get(need, dev, "sparse")
+    ws = Workspace.get(need, dev, ws_tag)
     fn = L.tt_sparse_adagrad_sorted if presorted else L.tt_sparse_adagrad
     check(fn(arr, len(tables), batch, grad.data_ptr() if grad is not None else None, ld, lr, epsilon,
              ws.data_ptr(), ws.numel(), _stream()))
@@ -227,7 +230,7 @@ def sparse_adam(tables: Sequence[dict], batch: int, grad: torch.Tensor, lr: floa
                            ws.data_ptr(), ws.numel(), _stream()))
 
 
-def sparse_scatter_sum(tables: Sequence[dict], batch: int, grad: torch.Tensor) -> None:
+def sparse_scatter_sum(tables: Sequence[dict], batch: int, grad: torch.Tensor, ws_tag: str = "sparse") -> None:
     """tables: dicts with table (zero-filled dense gradient [rows, dim]), ids
     [list], grad_col_offset [list]; every touched row receives its
     duplicate-summed gradient (tt_sparse_scatter_sum)."""
@@ -236,9 +239,50 @@ def sparse_scatter_sum(tables: Sequence[dict], batch: int, grad: torch.Tensor) -
     arr = _sparse_tables(tables, batch, adam=False, slots=False)
     L = lib()
     need = L.tt_sparse_workspace_size(arr, len(tables), batch)
-    ws = Workspace.get(need, grad.device, "sparse")
+    ws = Workspace.get(need, grad.device, ws_tag)
     check(L.tt_sparse_scatter_sum(arr, len(tables), batch, grad.data_ptr(), ld, ws.data_ptr(), ws.numel(),
                                   _stream()))
+
+
+def route_requests(lookups: Sequence[Tuple[torch.Tensor, int, int]], world: int, num_tags: int):
+    """lookups: (ids [B] int32, table rows, tag).  Returns (send [L*B, 2] int32
+    capacity, counts [world] int64, num_requests [1] int32, idx [L, B] int32)
+    from tt_route_requests (owner-major deduplicated requests)."""
+    L = len(lookups)
+    B = lookups[0][0].numel()
+    dev = lookups[0][0].device
+    arr = (_native.RouteLookup * L)()
+    max_rows = 1
+    for i, (ids, rows, tag) in enumerate(lookups):
+        _req(ids, f"ids[{i}]", torch.int32, 1)
+        if ids.numel() != B or not ids.is_contiguous():
+            raise ValueError("route: every lookup needs a contiguous [B] int32 id tensor")
+        arr[i].ids = ids.data_ptr()
+        arr[i].num_rows = int(rows)
+        arr[i].tag = int(tag)
+        max_rows = max(max_rows, int(rows))
+    send = torch.empty(L * B, 2, dtype=torch.int32, device=dev)
+    counts = torch.empty(world, dtype=torch.int64, device=dev)
+    nreq = torch.empty(1, dtype=torch.int32, device=dev)
+    idx = torch.empty(L, B, dtype=torch.int32, device=dev)
+    lib_ = lib()
+    ws = Workspace.get(lib_.tt_route_workspace_size(L, B, world, max_rows, num_tags), dev, "route")
+    check(lib_.tt_route_requests(arr, L, B, world, num_tags, send.data_ptr(), counts.data_ptr(), nreq.data_ptr(),
+                                 idx.data_ptr(), ws.data_ptr(), ws.numel(), _stream()))
+    return send, counts, nreq, idx
+
+
+def route_owner(recv: torch.Tensor, world: int, num_tags: int):
+    """recv [n, 2] int32 requests received by this owner -> (tags [n], local rows
+    [n], table_ids [num_tags, n]) from tt_route_owner."""
+    _req(recv, "recv", torch.int32, 2)
+    n = recv.shape[0]
+    tags = torch.empty(n, dtype=torch.int32, device=recv.device)
+    rows = torch.empty(n, dtype=torch.int32, device=recv.device)
+    tids = torch.empty(num_tags, n, dtype=torch.int32, device=recv.device)
+    check(lib().tt_route_owner(recv.contiguous().data_ptr(), n, world, num_tags, tags.data_ptr(), rows.data_ptr(),
+                               tids.data_ptr(), _stream()))
+    return tags, rows, tids
 
 
 def gather_tagged(tables: Sequence[torch.Tensor], tags: torch.Tensor, rows: torch.Tensor,
@@ -342,6 +386,20 @@ def dense_adam(param, m, v, grad, lr, beta1, beta2, epsilon, step) -> None:
 
 # --------------------------------------------------------------------------
 # K5+K6+K7 fused in-batch softmax cross-entropy
+# --------------------------------------------------------------------------
+# Measurement hook: time ONE kernel of a multi-launch entry point (tt_probe_arm)
+PROBE_INBATCH_ROWS, PROBE_INBATCH_COLS, PROBE_INDEX_SCREEN, PROBE_INDEX_FINALIZE = range(4)
+
+
+def probe_arm(kernel: int, start: "torch.cuda.Event", stop: "torch.cuda.Event") -> None:
+    """The next launch of `kernel` on this thread records `start` / `stop`
+    (timing-enabled torch.cuda.Events) on its own launch stream."""
+    for ev in (start, stop):
+        if not ev.cuda_event:  # torch creates the HIP event on first record
+            ev.record()
+    check(lib().tt_probe_arm(kernel, start.cuda_event, stop.cuda_event))
+
+
 def _opt_ptr(t: Optional[torch.Tensor], name: str, n: int) -> Optional[int]:
     if t is None:
         return None

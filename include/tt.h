@@ -42,6 +42,20 @@ const char* tt_version(void);
 /* Thread-local description of the last error ("" if none). */
 const char* tt_last_error(void);
 
+/* Measurement hook (no reference counterpart): the NEXT launch of `kernel`
+ * issued by the calling thread is bracketed by hipEventRecord(ev_start) and
+ * hipEventRecord(ev_stop) on its launch stream; the probe then disarms.  Lets
+ * a benchmark time one kernel of a multi-launch entry point with HIP events
+ * on the stream it runs on.  ev_start/ev_stop are hipEvent_t (NULL disarms). */
+enum {
+  TT_PROBE_INBATCH_ROWS = 0, /* inbatch_pass_kernel<D,0> (rows pass)        */
+  TT_PROBE_INBATCH_COLS = 1, /* inbatch_pass_kernel<D,1> (cols pass)        */
+  TT_PROBE_INDEX_SCREEN = 2, /* screen kernel of tt_bruteforce_search       */
+  TT_PROBE_INDEX_FINALIZE = 3, /* finalize kernel of tt_bruteforce_search   */
+  TT_PROBE_COUNT = 4
+};
+int tt_probe_arm(int32_t kernel, void* ev_start, void* ev_stop);
+
 /* ------------------------------------------------------------------------ *
  * K2+K3  Grouped embedding gather + concat.
  * Replaces InputLayer.call  (pkg/modelling/layers/input_layer.py:45-69):
@@ -91,6 +105,36 @@ typedef struct {
 int tt_gather_tagged(const tt_row_table* tables, int32_t num_tables, int32_t dim,
                      const int32_t* tags, const int32_t* rows, int64_t n,
                      float* out, int64_t out_stride, tt_stream_t stream);
+
+/* Request routing for row-sharded tables (no reference counterpart: the
+ * reference trains on one CPU; this is the exchange the data-parallel step
+ * needs).  Global row r of a sharded table lives on rank
+ * r % world.  tt_route_requests deduplicates a rank's lookups into ONE
+ * request list, owner-major (inside an owner: by tag, then row ascending; an
+ * id outside its table becomes row -1, owned by rank world-1, sorted first):
+ *   send [R, 2] int32 (global row, tag), counts [world] int64 (requests per
+ *   owner, R = their sum, also written to *num_requests), idx [num_lookups,
+ *   batch] int32 = the position in `send` of each lookup's request.
+ * Capacity: send holds num_lookups*batch pairs.  tt_route_owner expands the
+ * n requests an owner received (recv [n, 2]) into tags [n], local rows [n]
+ * (gid / world, -1 if invalid) and per tag the local rows of that tag's
+ * requests with -1 elsewhere (table_ids [num_tags, n]). */
+typedef struct {
+  const int32_t* ids; /* [batch] row ids of one lookup (one feature)        */
+  int64_t num_rows;   /* rows of the (global) table it reads               */
+  int32_t tag;        /* table index, 0..num_tags-1                         */
+} tt_route_lookup;
+
+size_t tt_route_workspace_size(int32_t num_lookups, int64_t batch, int32_t world,
+                               int64_t max_rows, int32_t num_tags);
+int tt_route_requests(const tt_route_lookup* lookups, int32_t num_lookups,
+                      int64_t batch, int32_t world, int32_t num_tags,
+                      int32_t* send, long long* counts, int32_t* num_requests,
+                      int32_t* idx, void* workspace, size_t workspace_bytes,
+                      tt_stream_t stream);
+int tt_route_owner(const int32_t* recv, int64_t n, int32_t world,
+                   int32_t num_tags, int32_t* tags, int32_t* rows,
+                   int32_t* table_ids, tt_stream_t stream);
 
 /* ------------------------------------------------------------------------ *
  * K8+K9  Sparse optimizer step on embedding tables.

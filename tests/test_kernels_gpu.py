@@ -396,3 +396,56 @@ def test_recall_hits(cuda):
     hits = torch.zeros(3, dtype=torch.int64, device=cuda)
     hip_ops.recall_hits(_t(true, cuda), _t(cand, cuda), ks, hits)
     assert hits.cpu().tolist() == [acc.hits[k] for k in ks]
+
+
+# --------------------------------------------------------------------------- sharded-table routing
+@pytest.mark.parametrize("world", [1, 3, 8])
+def test_route_requests_match_torch_restatement(cuda, world):
+    """tt_route_requests / tt_route_owner equal the torch restatement
+    (distributed.torch_route_requests) element for element: owner-major
+    deduplicated requests (tag, then row ascending; invalid ids as row -1 on
+    rank world-1), per-owner counts and each lookup's request position."""
+    from pkg.modelling.distributed import torch_route_owner, torch_route_requests
+
+    rng = np.random.default_rng(world)
+    B = 3000
+    rows = [5000, 700, 1371980]
+    # lookups: tag 0 twice (a table read by two features), tags 1 and 2; Zipf + out-of-range ids
+    spec = [(0, zipf_ids(rng, B, 5000)), (1, rng.integers(-3, 705, B).astype(np.int32)),
+            (0, rng.integers(-1, 5003, B).astype(np.int32)), (2, zipf_ids(rng, B, 1371980, 1.05))]
+    lookups = [(_t(ids, cuda), rows[tag], tag) for tag, ids in spec]
+    send, counts, nreq, idx = hip_ops.route_requests(lookups, world, 3)
+    rs, rc, rn, ri = torch_route_requests(lookups, world, 3)
+    R = int(rn.item())
+    assert int(nreq.item()) == R == int(counts.sum().item())
+    assert torch.equal(counts, rc)
+    assert torch.equal(send[:R], rs)
+    assert torch.equal(idx, ri)
+    # every lookup's request names its own (row, tag)
+    for (tag, ids), ix in zip(spec, idx.cpu().numpy()):
+        ok = (ids >= 0) & (ids < rows[tag])
+        got = send[:R].cpu().numpy()[ix]
+        assert np.array_equal(got[:, 1], np.full(B, tag))
+        assert np.array_equal(got[:, 0], np.where(ok, ids, -1))
+    tags, lrows, tids = hip_ops.route_owner(send[:R].contiguous(), world, 3)
+    et, er, eids = torch_route_owner(send[:R].contiguous(), world, 3)
+    assert torch.equal(tags, et) and torch.equal(lrows, er) and torch.equal(tids, eids)
+
+
+def test_sparse_adagrad_mostly_invalid_ids_bitexact(cuda):
+    """Lookups whose ids are mostly outside the table (the owner-side update
+    of a sharded step marks other tables' requests -1) leave only the valid
+    rows updated, bit-exact against the restatement."""
+    rng = np.random.default_rng(11)
+    n, V, D = 20000, 3000, 128
+    ids = np.where(rng.random(n) < 0.7, -1, zipf_ids(rng, n, V)).astype(np.int32)
+    grad = rng.standard_normal((n, D)).astype(np.float32)
+    w = rng.uniform(-0.05, 0.05, (V, D)).astype(np.float32)
+    acc = np.full((V, D), 0.1, np.float32)
+    ref_w, ref_acc = w.copy(), acc.copy()
+    oracle.sparse_adagrad(ref_w, ref_acc, ids, grad, 0.05, 1e-7)
+    tw, ta = _t(w, cuda), _t(acc, cuda)
+    hip_ops.sparse_adagrad([dict(table=tw, slot0=ta, ids=[_t(ids, cuda)], grad_col_offset=[0])], n, _t(grad, cuda),
+                           0.05, 1e-7)
+    assert np.array_equal(tw.cpu().numpy(), ref_w)
+    assert np.array_equal(ta.cpu().numpy(), ref_acc)
