@@ -14,10 +14,13 @@ train_step (gather, towers, fused in-batch CE fwd+bwd, MLP backward, dense
 
 N>1 (torchrun, one process per GPU, RCCL): weak scaling, each rank runs the
 same C3 step on its own batch of 16384 with per-replica in-batch negatives
-(the reference's train_step under data parallelism); dense gradients are
-all-reduced and sparse (id, gradient) rows all-gathered so every replica
-applies the identical global update.  value = total pairs / max-over-ranks
-time.
+(the reference's train_step under data parallelism).  The large tables
+(customer, postal, article) are row-sharded over the ranks (all_to_all of
+requested rows forward, of per-row gradient sums backward, Adagrad on the
+owner); small tables, MLP gradients and the loss share one all_reduce
+bucket (ShardedTrainStep).  value = total pairs / max-over-ranks time.  The
+index line at N>1 is configs[3] candidate-sharded (ShardedBruteForceIndex,
+all_to_all of per-shard top-k lists to each query block's owner + merge).
 
 The JSON line also carries the roofline of the dominant kernel (the fused
 in-batch rows pass, bf16 MFMA), the index QPS of BASELINE configs[3] at a
@@ -309,7 +312,8 @@ def time_gather(model, data, device, B: int, reps: int = 50):
             "bound": "hbm",
             "achieved": gbs, "peak": MI355X_HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / MI355X_HBM_PEAK_GBS,
             "algorithmic_bytes_per_launch": nbytes, "ms_per_launch": ms,
-            "traffic": pmc_traffic("gather_grouped_kernel"),
+            "traffic": (pmc_traffic("gather_grouped_kernel") or {}).get("bytes_per_launch"),
+            "traffic_source": (pmc_traffic("gather_grouped_kernel") or {}).get("source"),
             "note": "Zipf ids: popular rows hit L2/Infinity Cache, so the algorithmic rate can exceed HBM"}
 
 
@@ -349,6 +353,56 @@ def time_index(device, n_queries: int, n_cand: int, k: int, E: int = 128, check:
             res["recall_at_100_vs_exact"] = float(np.mean([len(set(a) & set(b)) / k for a, b in zip(gi, ri)]))
         except Exception as e:  # the check is informative only
             res["check_error"] = repr(e)
+    return res
+
+
+def time_index_sharded(device, n_queries: int, n_cand: int, k: int, ws: int, rank: int, E: int = 128,
+                       check: int = 256):
+    """configs[3] candidate-sharded over the ranks (ShardedBruteForceIndex):
+    rank r owns candidate rows shard_range(N, G, r) and searches every query;
+    one all_to_all hands each query block's per-shard lists to its owner,
+    which merges them (tt_topk_merge).  Strong scaling: Q and N fixed.  QPS =
+    Q / max-over-ranks wall time of search_owned, barrier + sync both sides."""
+    from pkg.modelling.distributed import ShardedBruteForceIndex, shard_range
+
+    g = torch.Generator(device=device)
+    g.manual_seed(1)
+    C = torch.relu(torch.randn(n_cand, E, generator=g, device=device))
+    g.manual_seed(2)
+    Q = torch.relu(torch.randn(n_queries, E, generator=g, device=device))
+    Q[::100] = 0.0
+    b, e = shard_range(n_cand, ws, rank)
+    idx = ShardedBruteForceIndex(k, None, C[b:e].contiguous(), b)
+    idx.search_owned(Q[:4096 * ws])  # warm (workspaces)
+    torch.cuda.synchronize()
+    torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    (qb, qe), s, i = idx.search_owned(Q)
+    torch.cuda.synchronize()
+    torch.distributed.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], device=device, dtype=torch.float64)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    dt = float(t.item())
+    tf = 2.0 * n_queries * n_cand * E / dt / 1e12
+    res = {"queries": n_queries, "candidates": n_cand, "k": k, "dim": E, "shards": ws, "seconds": dt,
+           "qps": n_queries / dt, "scaling": "strong (candidates row-sharded over the ranks, all queries)",
+           "roofline": {"bound": "mfma", "achieved": tf, "peak": MI355X_BF16_DENSE_TFLOPS * ws, "unit": "TFLOP/s",
+                        "frac": tf / (MI355X_BF16_DENSE_TFLOPS * ws),
+                        "note": "2*Q*N*E scoring flops / wall time incl. all_to_all + merge, vs G x dense bf16 peak"}}
+    if rank == 0 and check:
+        try:
+            from oracle import oracle
+
+            sel = np.linspace(qb, qe - 1, check).astype(np.int64)
+            _, ri, _ = oracle.bruteforce_topk(Q[sel].cpu().numpy(), C.cpu().numpy(), k)
+            gi = i[sel - qb].cpu().numpy()
+            res["exact_match_rows"] = int((gi == ri).all(axis=1).sum())
+            res["checked_rows"] = int(check)
+        except Exception as ex:  # informative only
+            res["check_error"] = repr(ex)
     return res
 
 
@@ -426,10 +480,12 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--train-mode", choices=("auto", "sharded"), default="auto",
                     help="sharded: run the N>1 row-sharded step (ShardedTrainStep) even on one rank")
+    ap.add_argument("--index-mode", choices=("auto", "sharded"), default="auto",
+                    help="sharded: run the N>1 candidate-sharded index (search_owned) even on one rank")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
-    if ws > 1 or args.train_mode == "sharded":
+    if ws > 1 or args.train_mode == "sharded" or args.index_mode == "sharded":
         torch.cuda.set_device(local)
         if ws == 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -480,7 +536,8 @@ def main():
             "peak": MI355X_BF16_DENSE_TFLOPS,
             "unit": "TFLOP/s",
             "frac": achieved / MI355X_BF16_DENSE_TFLOPS,
-            "traffic": pmc_traffic("inbatch_pass_kernel<128, 0>"),
+            "traffic": (pmc_traffic("inbatch_pass_kernel<128, 0>") or {}).get("bytes_per_launch"),
+            "traffic_source": (pmc_traffic("inbatch_pass_kernel<128, 0>") or {}).get("source"),
             "ms_per_launch": ms_rows,
             "cols_pass": {"kernel": "inbatch_pass_kernel<128,1>", "ms_per_launch": ms_cols,
                           "achieved": flops / (ms_cols * 1e-3) / 1e12},
@@ -489,8 +546,10 @@ def main():
         },
         "gather_roofline": gather,
     }
-    if rank == 0 and ws == 1 and not args.no_index:
+    if ws == 1 and args.index_mode == "auto" and not args.no_index:
         result["index"] = time_index(device, args.index_queries, HM_VOCAB["article_id"], 100)
+    elif not args.no_index:
+        result["index"] = time_index_sharded(device, args.index_queries, HM_VOCAB["article_id"], 100, ws, rank)
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:

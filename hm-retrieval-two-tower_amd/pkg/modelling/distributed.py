@@ -119,6 +119,27 @@ class ShardedBruteForceIndex:
         all_i = all_gather_cat(i, self.group)
         return self.ops.merge(all_s, all_i, k)
 
+    def search_owned(self, query_embeddings: torch.Tensor, k: Optional[int] = None
+                     ) -> Tuple[Tuple[int, int], torch.Tensor, torch.Tensor]:
+        """Global top-k of this rank's query block only: ((begin, end), scores
+        [end-begin, k], indices).  Query block r = shard_range(Q, world, r).
+        One all_to_all moves each shard's lists for block r to rank r, so a
+        rank receives Q/G·G·k entries instead of the all-gather's Q·G·k, and
+        the merge work is split over the ranks too."""
+        k = k or self.k
+        Q = int(query_embeddings.shape[0])
+        s, i = self.ops.search(self.image, self.cand, query_embeddings.contiguous(), k, self.offset)
+        blocks = [shard_range(Q, self.world, r) for r in range(self.world)]
+        in_splits = [(e - b) * k for b, e in blocks]
+        mb, me = blocks[self.rank]
+        out_splits = [(me - mb) * k] * self.world
+        rs = torch.empty(self.world, me - mb, k, dtype=s.dtype, device=s.device)
+        ri = torch.empty(self.world, me - mb, k, dtype=i.dtype, device=i.device)
+        _a2a(rs.reshape(-1), s.reshape(-1), out_splits, in_splits, self.group)
+        _a2a(ri.reshape(-1), i.reshape(-1), out_splits, in_splits, self.group)
+        ms, mi = self.ops.merge(rs, ri, k)
+        return (mb, me), ms, mi
+
     def __call__(self, queries: Dict[str, Any]):
         with torch.no_grad():
             emb = self.query_model(queries)

@@ -47,7 +47,8 @@ def _index_worker(rank, world, port, q, c, k, out):
     b, e = shard_range(c.shape[0], world, rank)
     idx = ShardedBruteForceIndex(k, None, torch.from_numpy(c[b:e]), b, ops=_oracle_ops())
     s, i = idx.search(torch.from_numpy(q))
-    out[rank] = (s.numpy(), i.numpy(), idx.num_candidates)
+    blk, os_, oi = idx.search_owned(torch.from_numpy(q))
+    out[rank] = (s.numpy(), i.numpy(), idx.num_candidates, blk, os_.numpy(), oi.numpy())
     dist.destroy_process_group()
 
 
@@ -64,10 +65,15 @@ def test_sharded_index_equals_unsharded(world):
     out = mp.Manager().dict()
     mp.spawn(_index_worker, args=(world, _free_port(), q, c, k, out), nprocs=world, join=True)
     rs, ri, _ = oracle.bruteforce_topk(q, c, k)
+    covered = []
     for r in range(world):
-        s, i, n = out[r]
+        s, i, n, (b, e), os_, oi = out[r]
         assert n == 301
         assert np.array_equal(i, ri) and np.array_equal(s, rs)
+        # search_owned: this rank's query block only, same global lists
+        assert np.array_equal(oi, ri[b:e]) and np.array_equal(os_, rs[b:e])
+        covered += list(range(b, e))
+    assert covered == list(range(q.shape[0]))
 
 
 class _Dense:
