@@ -83,7 +83,15 @@ __global__ void __launch_bounds__(256) sum_slices_kernel(const float* __restrict
                                                          float* __restrict__ out) {
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += static_cast<int64_t>(gridDim.x) * 256) {
     float acc = 0.0f;
-    for (int s = 0; s < nslices; ++s) acc += parts[s * n + i];
+    int s = 0;
+    for (; s + 8 <= nslices; s += 8) {  // 8 loads in flight, added in slice order
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = parts[(s + u) * n + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; s < nslices; ++s) acc += parts[s * n + i];
     out[i] = acc;
   }
 }

@@ -4,11 +4,16 @@
 Dense layers follow Keras defaults: kernel [fan_in, units] glorot_uniform,
 zero bias, relu on every layer including the last (tower.py:45,48), so the
 joint embeddings are non-negative.  All kernels and biases of a tower live in
-ONE flat fp32 buffer (views per layer), so its gradient is one contiguous
-tensor and the dense optimizer step is a single tt_dense_* launch.  The GEMMs
-run through torch (hipBLASLt, fp32, bias + relu fused into the forward GEMM's
-epilogue); the backward's relu mask + bias gradient and the split-K weight
-gradient reduction are libtt kernels (tt_relu_bias_grad, tt_sum_slices).
+ONE flat fp32 buffer (views per layer; each layer's bias right after its
+kernel), so its gradient is one contiguous tensor and the dense optimizer
+step is a single tt_dense_* launch.  Two GEMM backends (DenseStack.backend):
+  * "hipblaslt" (default): torch fp32 GEMMs (bias + relu in the forward
+    GEMM's epilogue); libtt's tt_relu_bias_grad for the ReluGrad/BiasAddGrad
+    pair and tt_sum_slices for the split-K weight gradient;
+  * "tt": libtt's tt_gemm on bf16 MFMA (GEMM_BF16X3 hi/lo split =
+    fp32-faithful, or GEMM_BF16): bias + relu fused into the forward
+    epilogue, the relu mask applied while loading the gradient operand, the
+    bias gradient as the ones-row of the weight-gradient GEMM.
 """
 from __future__ import annotations
 
@@ -37,6 +42,17 @@ def _splitk_mm_tn(a: torch.Tensor, g: torch.Tensor, out: torch.Tensor, splits: i
         hip_ops.sum_slices(part, out)
     else:
         torch.mm(a.t(), g, out=out)
+
+
+def _weight_grad_splits(rows: int, fan_in: int, fan_out: int) -> int:
+    """Split-K factor of the weight-gradient GEMM ([fan_in+1, fan_out] over
+    `rows`): enough workgroups to fill 256 CUs twice, >= 256 rows per split."""
+    bm = 64 if fan_out > 128 else 128
+    tiles = -(-(fan_in + 1) // bm) * -(-fan_out // (16384 // bm))
+    s = 1
+    while tiles * s < 512 and rows // (2 * s) >= 256:
+        s *= 2
+    return s
 
 
 class _DenseStackFn(torch.autograd.Function):
@@ -77,27 +93,36 @@ class DenseStack:
             flat[w_off:w_off + fi * fo] = w.reshape(-1)
         self.flat = flat.to(device).requires_grad_(True)
         self.out_dim = fan_in
+        # GEMM backend: "hipblaslt" (torch fp32 GEMMs + libtt relu/bias-grad and
+        # split-K reduction) or "tt" (libtt tt_gemm, bf16 MFMA; `precision`
+        # GEMM_BF16X3 = fp32-faithful hi/lo split, GEMM_BF16 = plain bf16)
+        self.backend = "hipblaslt"
+        self.precision = hip_ops.GEMM_BF16X3
 
     def params(self, flat: Optional[torch.Tensor] = None):
         f = self.flat if flat is None else flat
         return [(f[w:w + fi * fo].view(fi, fo), f[b:b + fo]) for w, fi, fo, b in self.layout]
 
     def forward_acts(self, x: torch.Tensor, flat: torch.Tensor) -> List[torch.Tensor]:
-        """[x, h_1, ..., h_L]: each layer one hipBLASLt GEMM with the bias + relu
-        epilogue fused (torch._addmm_activation)."""
+        """[x, h_1, ..., h_L] with h_l = relu(h_{l-1} W_l + b_l)."""
+        if self.backend == "tt":
+            return self._forward_tt(x, flat)
         acts = [x]
         h = x
         for w, b in self.params(flat):
-            h = torch._addmm_activation(b, h, w)
+            h = torch._addmm_activation(b, h, w)  # hipBLASLt, bias + relu epilogue
             acts.append(h)
         return acts
 
     def backward_acts(self, acts: List[torch.Tensor], flat: torch.Tensor, gout: torch.Tensor,
                       gscale: Optional[torch.Tensor], need_input_grad: bool, inplace: bool = True):
-        """(d x, d flat) from the saved activations.  Per layer: one tt_relu_bias_grad
-        (relu mask x the incoming gradient, times gscale on the top layer, and the
-        bias gradient), the weight gradient (split-K GEMM + tt_sum_slices) and the
-        input gradient (GEMM).  inplace: gout may be overwritten."""
+        """(d x, d flat) from the saved activations.  hipBLASLt backend, per
+        layer: one tt_relu_bias_grad (relu mask x the incoming gradient, times
+        gscale on the top layer, and the bias gradient), the weight gradient
+        (split-K GEMM + tt_sum_slices) and the input gradient (GEMM).
+        inplace: gout may be overwritten."""
+        if self.backend == "tt":
+            return self._backward_tt(acts, flat, gout, gscale, need_input_grad)
         gflat = torch.empty_like(flat)
         params = self.params(flat)
         gparams = self.params(gflat)
@@ -110,6 +135,47 @@ class DenseStack:
             _splitk_mm_tn(acts[li], g, dw)
             if li > 0 or need_input_grad:
                 g = torch.mm(g, params[li][0].t())
+        return (g if need_input_grad else None), gflat
+
+    def _forward_tt(self, x: torch.Tensor, flat: torch.Tensor) -> List[torch.Tensor]:
+        """libtt backend: one tt_gemm per layer (bias + relu in the epilogue)."""
+        acts = [x]
+        h = x
+        for w, b in self.params(flat):
+            out = torch.empty(h.shape[0], w.shape[1], dtype=torch.float32, device=h.device)
+            h = hip_ops.gemm(h, w, out, bias=b, relu=True, precision=self.precision)
+            acts.append(h)
+        return acts
+
+    def _backward_tt(self, acts: List[torch.Tensor], flat: torch.Tensor, gout: torch.Tensor,
+                     gscale: Optional[torch.Tensor], need_input_grad: bool):
+        """libtt backend.  Per layer l (G = relu'(h_l) * s * g, s = gscale on the
+        top layer, applied inside the GEMM loads): [dW_l; db_l] = [h_{l-1}; 1]^T G
+        as one split-K tt_gemm + tt_sum_slices written straight into the flat
+        gradient, and g_{l-1} = G W_l^T.  gout is not modified."""
+        gflat = torch.empty_like(flat)
+        params = self.params(flat)
+        g = gout
+        for li in range(len(params) - 1, -1, -1):
+            w_off, fi, fo, _ = self.layout[li]
+            w = params[li][0]
+            x, act = acts[li], acts[li + 1]
+            s = gscale if li == len(params) - 1 else None
+            rows = x.shape[0]
+            dwb = gflat[w_off:w_off + (fi + 1) * fo].view(fi + 1, fo)
+            splits = _weight_grad_splits(rows, fi, fo)
+            if splits > 1:
+                part = hip_ops.Workspace.get(splits * (fi + 1) * fo * 4, x.device, "dense_wgrad")
+                part = part[:splits * (fi + 1) * fo * 4].view(torch.float32).view(splits, fi + 1, fo)
+                hip_ops.gemm(x, g, part, a_t=True, mask=act, mask_on="b", scale=s, ones_row=True, splits=splits,
+                             precision=self.precision)
+                hip_ops.sum_slices(part, dwb)
+            else:
+                hip_ops.gemm(x, g, dwb, a_t=True, mask=act, mask_on="b", scale=s, ones_row=True,
+                             precision=self.precision)
+            if li > 0 or need_input_grad:
+                gx = torch.empty(rows, fi, dtype=torch.float32, device=x.device)
+                g = hip_ops.gemm(g, w, gx, b_t=True, mask=act, mask_on="a", scale=s, precision=self.precision)
         return (g if need_input_grad else None), gflat
 
     def __call__(self, x: torch.Tensor) -> torch.Tensor:

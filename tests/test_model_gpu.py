@@ -112,15 +112,21 @@ def _cpu_mirror(m):
     return ref
 
 
-@pytest.mark.parametrize("zipf", [True, False])
-def test_train_steps_match_cpu_restatement(cuda, zipf):
+@pytest.mark.parametrize("zipf,backend,precision", [(True, "hipblaslt", None), (False, "hipblaslt", None),
+                                                    (True, "tt", "x3"), (False, "tt", "x3"), (True, "tt", "bf16")])
+def test_train_steps_match_cpu_restatement(cuda, zipf, backend, precision):
     """First step: every parameter update within 1e-2 rel of the fp32 CPU
     restatement (bf16 MFMA operands in the fused loss give ~1e-3 per-example
     gradient error, amplified where a batch-summed gradient cancels).  Then the
     loss trajectory over 3 steps within 2e-3 rel (parameters themselves drift
     apart: lr 0.05 on a 0.1 accumulator moves embeddings by about their own
-    scale every step, so any rounding difference is amplified)."""
+    scale every step, so any rounding difference is amplified).  Both tower
+    GEMM backends: hipBLASLt fp32 and libtt tt_gemm (bf16x3 and plain bf16)."""
     m = _small_model(cuda)
+    for t in (m.query_tower, m.candidate_tower):
+        t.dense.backend = backend
+        if precision:
+            t.dense.precision = hip_ops.GEMM_BF16X3 if precision == "x3" else hip_ops.GEMM_BF16
     ref = _cpu_mirror(m)
     rng = np.random.default_rng(5)
 
@@ -149,7 +155,11 @@ def test_train_steps_match_cpu_restatement(cuda, zipf):
             after, r = snapshot(), ref_snapshot()
             for k in after:  # includes the shared ptn table (one combined update of both lookups)
                 d_gpu, d_ref = after[k] - before[k], r[k] - before[k]
-                assert np.linalg.norm(d_gpu - d_ref) <= 1e-2 * np.linalg.norm(d_ref), k
+                # plain-bf16 tower GEMMs round activations and weights too (another
+                # ~2^-9 per operand before the same cancellation; measured ~5e-2 on
+                # the query tables): 8e-2, which is why the product keeps fp32-faithful GEMMs
+                tol = 8e-2 if precision == "bf16" else 1e-2
+                assert np.linalg.norm(d_gpu - d_ref) <= tol * np.linalg.norm(d_ref), k
 
 
 def test_graph_replay_equals_eager(cuda):
