@@ -65,17 +65,20 @@ def _row_major(t: torch.Tensor, name: str) -> int:
 
 
 class Workspace:
-    """Grow-only device scratch buffers, one per (device, tag).
+    """Grow-only device scratch buffers, one per (device, scope, tag).
 
     Buffers are reused across calls on the same stream; allocate (warm) them
-    before capturing a hipGraph so replays never allocate.
+    before capturing a hipGraph so replays never allocate.  Work issued on a
+    concurrent stream runs inside its own `Workspace.scope(name)` so the two
+    streams never share a buffer.
     """
 
     _bufs: Dict[Tuple[int, str], torch.Tensor] = {}
+    _scope = ""
 
     @classmethod
     def get(cls, nbytes: int, device: torch.device, tag: str) -> torch.Tensor:
-        key = (device.index if device.index is not None else torch.cuda.current_device(), tag)
+        key = (device.index if device.index is not None else torch.cuda.current_device(), cls._scope + tag)
         buf = cls._bufs.get(key)
         if buf is None or buf.numel() < nbytes:
             buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
@@ -85,6 +88,19 @@ class Workspace:
     @classmethod
     def clear(cls) -> None:
         cls._bufs.clear()
+
+    class scope:  # noqa: N801 - context manager named like the operation
+        def __init__(self, name: str):
+            self.name = name
+
+        def __enter__(self):
+            self.prev = Workspace._scope
+            Workspace._scope = self.name + "/"
+            return self
+
+        def __exit__(self, *exc):
+            Workspace._scope = self.prev
+            return False
 
 
 # --------------------------------------------------------------------------

@@ -35,16 +35,36 @@ class _InBatchXent(torch.autograd.Function):
         return dq * s, dc * s, None, None
 
 
+_SIDE: dict = {}
+
+
+def _tower_stream(device: torch.device) -> torch.cuda.Stream:
+    """The stream the candidate tower's MLP runs on, beside the query tower's."""
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=device)
+    return _SIDE[key]
+
+
 class _TowersInBatchXent(torch.autograd.Function):
-    """Both tower MLPs and the in-batch loss as ONE autograd node.  The
-    backward hands the loss's incoming gradient to the top layers' fused
-    relu/bias kernels as a device scalar (no separate scaling pass over dQ,
-    dC) and overwrites dQ / dC in place (they are not needed afterwards)."""
+    """Both tower MLPs and the in-batch loss as ONE autograd node.  The two
+    towers' MLPs are independent chains of small GEMMs, so the candidate
+    tower's forward and backward run on a second stream concurrently with
+    the query tower's (fork / join with stream waits: captured as parallel
+    branches of the step's hipGraph).  The backward hands the loss's incoming
+    gradient to the top layers' fused relu/bias kernels as a device scalar (no
+    separate scaling pass over dQ, dC) and overwrites dQ / dC in place (they
+    are not needed afterwards)."""
 
     @staticmethod
     def forward(ctx, qi, ci, flat_q, flat_c, logq, stack_q, stack_c, scale):
+        main = torch.cuda.current_stream()
+        side = _tower_stream(qi.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side), hip_ops.Workspace.scope("tower_c"):
+            ca = stack_c.forward_acts(ci, flat_c)
         qa = stack_q.forward_acts(qi, flat_q)
-        ca = stack_c.forward_acts(ci, flat_c)
+        main.wait_stream(side)
         _, row_loss, dq, dc = hip_ops.inbatch_fused(qa[-1], ca[-1], logq)
         ctx.stacks = (stack_q, stack_c)
         ctx.nq = len(qa)
@@ -58,8 +78,13 @@ class _TowersInBatchXent(torch.autograd.Function):
         qa, ca = acts[:ctx.nq], acts[ctx.nq:]
         s = (g * ctx.scale if ctx.scale != 1.0 else g).reshape(1).float().contiguous()
         stack_q, stack_c = ctx.stacks
+        main = torch.cuda.current_stream()
+        side = _tower_stream(dq.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side), hip_ops.Workspace.scope("tower_c"):
+            gci, gflat_c = stack_c.backward_acts(ca, flat_c, dc, s, ctx.needs_input_grad[1])
         gqi, gflat_q = stack_q.backward_acts(qa, flat_q, dq, s, ctx.needs_input_grad[0])
-        gci, gflat_c = stack_c.backward_acts(ca, flat_c, dc, s, ctx.needs_input_grad[1])
+        main.wait_stream(side)
         return gqi, gci, gflat_q, gflat_c, None, None, None, None
 
 

@@ -24,6 +24,7 @@ from pkg.modelling.device import default_device, make_generator
 from pkg.modelling.layers.logq_correction import LogQCorrection
 from pkg.modelling.losses import InBatchSoftmaxCrossEntropy, towers_inbatch_softmax_xent
 from pkg.modelling.models.abstract_keras_model import AbstractKerasModel, TensorSpec
+from pkg.modelling import hip_ops
 from pkg.modelling.layers.input_layer import InputLayer
 from pkg.modelling.models.tower import Tower
 
@@ -108,7 +109,12 @@ class TwoTowerModel(AbstractKerasModel):
             self._logq_rows = self.logq_correction.row_table(feat, self.device)
         ids = x[self.candidate_id_col]
         ids = ids if isinstance(ids, torch.Tensor) else torch.as_tensor(np.asarray(ids))
-        return self._logq_rows.index_select(0, ids.reshape(-1).to(self.device, torch.int64))
+        ids = ids.reshape(-1).to(self.device, torch.int32).contiguous()
+        # one libtt gather launch: the logq table is a 1-wide embedding of the
+        # candidate ids (ids outside the table read 0 = the missing-id value)
+        out = torch.empty(ids.numel(), 1, dtype=torch.float32, device=self.device)
+        hip_ops.gather_grouped([(self._logq_rows.view(-1, 1), ids, 0)], ids.numel(), out)
+        return out.view(-1)
 
     def compute_loss(self, x: Dict[str, Any], training: bool = True) -> torch.Tensor:
         q, c = self._split(x)
