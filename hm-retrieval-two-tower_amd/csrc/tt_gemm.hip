@@ -423,60 +423,68 @@ __global__ void __launch_bounds__(256) pack_weight_kernel(const float* __restric
   *reinterpret_cast<uint2*>(img + slot) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
 }
 
+// Tall-operand staging: a wave's 32-row panel moves in 32-deep chunks.  A
+// chunk is read row-contiguously (load instruction i: lane l reads 16 B at
+// row 8i + l/8, depth 4(l%8): 8 rows x 128 B per instruction, the pattern
+// that streams at the CU's full load rate; loading straight into MFMA
+// fragments would put 32 rows in every instruction), converted to bf16 with
+// the relu mask applied, written to the wave's own LDS chunk buffer in
+// fragment order, and read back as A fragments.  Up to P chunks are in flight
+// (a register ring indexed at compile time under full unrolling).
+constexpr int kWsMaxChunks = 9;  // K <= 288
+constexpr int kWsChunkElems = 32 * 32;  // bf16 per wave chunk buffer
+
 template <int NB, bool MASKA>
 __global__ void __launch_bounds__(256) gemm_wstat_kernel(const WsArgs a) {
-  // CH 16-deep steps per load chunk: the raw fp32 chunk (2 x 16 B per lane
-  // per step, twice with the mask) is converted to bf16 fragments, then the
-  // next chunk's loads go out and overlap this chunk's MFMAs.  Without a mask
-  // K <= 288 is at most two chunks.
-  constexpr int CH = MASKA ? 4 : 9;
-  extern __shared__ __attribute__((aligned(16))) __bf16 wlds[];  // [Kp/16][NB][64 lanes][8]
+  constexpr int P = MASKA ? 4 : (NB >= 9 ? 6 : kWsMaxChunks);  // chunks in flight
+  extern __shared__ __attribute__((aligned(16))) __bf16 wlds[];  // [Kp/16][NB][64 lanes][8] + chunk buffers
   const int tid = threadIdx.x, wave = tid / kWave, lane = lane_id();
   const int nw = blockDim.x / kWave, nthreads = blockDim.x;
   const float s = a.scale ? *a.scale : 1.0f;
   const int nks = a.Kp / 16;
-  const int nchunks = (nks + CH - 1) / CH;
+  const int nchunks = (a.K + 31) / 32;
   const int64_t panels = (a.M + 31) / 32;
-  const int kh = 8 * (lane >> 5);  // this lane's 8 depths within a 16-deep step
+  __bf16* abuf = wlds + static_cast<size_t>(a.Kp) * NB * 32 + wave * 2 * kWsChunkElems;
+  const int lr = lane >> 3, lk = 4 * (lane & 7);  // row within 8, depth within the chunk
 
-  f32x4 raw[CH][2], rawm[MASKA ? CH : 1][2];
-  auto issue = [&](int64_t p, int c) {
-    const int64_t row = p * 32 + (lane & 31);
-    const bool rok = row < a.M;
-    const float* arow = a.A + (rok ? row : 0) * a.lda;
-    const float* mrow = MASKA ? a.mask + (rok ? row : 0) * a.ldm : nullptr;
+  f32x4 ring[P][4], mring[MASKA ? P : 1][4];
+  auto issue = [&](int64_t p, int c, f32x4 (&dst)[4], f32x4 (&mdst)[4]) {
 #pragma unroll
-    for (int t = 0; t < CH; ++t) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int k4 = (c * CH + t) * 16 + kh + 4 * h;
-        f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f}, m = {1.0f, 1.0f, 1.0f, 1.0f};
-        if (rok && k4 < a.K) {
-          if (a.vec && k4 + 4 <= a.lda && (!MASKA || k4 + 4 <= a.ldm)) {
-            // whole 16-B vector inside the row's storage: load it, zero the
-            // depths past K (no scalar tail: its waits would serialise the chunk)
-            v = *reinterpret_cast<const f32x4*>(arow + k4);
-            if (MASKA) m = *reinterpret_cast<const f32x4*>(mrow + k4);
+    for (int i = 0; i < 4; ++i) {
+      const int64_t row = p * 32 + 8 * i + lr;
+      const int k = 32 * c + lk;
+      f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f}, m = {1.0f, 1.0f, 1.0f, 1.0f};
+      if (row < a.M && k < a.K) {
+        const float* ap = a.A + row * a.lda + k;
+        const float* mp = MASKA ? a.mask + row * a.ldm + k : nullptr;
+        if (a.vec && k + 4 <= a.lda && (!MASKA || k + 4 <= a.ldm)) {
+          v = *reinterpret_cast<const f32x4*>(ap);
+          if (MASKA) m = *reinterpret_cast<const f32x4*>(mp);
+          if (k + 4 > a.K) {
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-              if (k4 + e >= a.K) v[e] = 0.0f;
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if (k4 + e < a.K) {
-                v[e] = arow[k4 + e];
-                if (MASKA) m[e] = mrow[k4 + e];
-              }
+              if (k + e >= a.K) v[e] = 0.0f;
           }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (k + e < a.K) {
+              v[e] = ap[e];
+              if (MASKA) m[e] = mp[e];
+            }
         }
-        raw[t][h] = v;
-        if (MASKA) rawm[t][h] = m;
       }
+      dst[i] = v;
+      if (MASKA) mdst[i] = m;
     }
   };
 
   int64_t p = static_cast<int64_t>(blockIdx.x) * nw + wave;
-  if (p < panels) issue(p, 0);  // first chunk in flight while the weight is staged
+  if (p < panels) {  // first chunks in flight while the weight is staged
+#pragma unroll
+    for (int c = 0; c < P; ++c)
+      if (c < nchunks) issue(p, c, ring[c], mring[MASKA ? c : 0]);
+  }
 
   // copy the packed weight image into LDS: 16-B pieces, 8 in flight per
   // thread, start rotated per workgroup so the workgroups do not all hit the
@@ -504,36 +512,40 @@ __global__ void __launch_bounds__(256) gemm_wstat_kernel(const WsArgs a) {
   __syncthreads();
 
   for (; p < panels; p += static_cast<int64_t>(gridDim.x) * nw) {
+    const int64_t pnext = p + static_cast<int64_t>(gridDim.x) * nw;
     f32x16 acc[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) acc[b] = f32x16{};
-    for (int c = 0; c < nchunks; ++c) {
-      bf16x8 af[CH];
 #pragma unroll
-      for (int t = 0; t < CH; ++t) {
-        f32x4 v0 = raw[t][0], v1 = raw[t][1];
-        if (MASKA) {
-          v0 = apply_mask(v0, rawm[t][0], s);
-          v1 = apply_mask(v1, rawm[t][1], s);
+    for (int c = 0; c < kWsMaxChunks; ++c) {
+      if (c < nchunks) {
+        __bf16* buf = abuf + (c & 1) * kWsChunkElems;
+        // chunk c -> bf16 fragments in this wave's buffer: element (row r,
+        // depth k) at lane slot (r + 32 * ((k / 8) % 2)) of step k / 16
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          f32x4 v = ring[c % P][i];
+          if (MASKA) v = apply_mask(v, mring[c % P][i], s);
+          const int r = 8 * i + lr;
+          const int slot = ((((lk >> 4) * 64) + r + 32 * ((lk >> 3) & 1)) << 3) + (lk & 7);
+          *reinterpret_cast<uint2*>(buf + slot) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
         }
+        if (c + P < nchunks) issue(p, c + P, ring[c % P], mring[MASKA ? c % P : 0]);
+        else if (c + P - nchunks < P && pnext < panels)  // next panel's first chunks
+          issue(pnext, c + P - nchunks, ring[c % P], mring[MASKA ? c % P : 0]);
+        if (a.probe & 2) continue;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          af[t][e] = static_cast<__bf16>(v0[e]);
-          af[t][4 + e] = static_cast<__bf16>(v1[e]);
+        for (int t = 0; t < 2; ++t) {
+          const int ks = 2 * c + t;
+          if (ks >= nks) break;
+          const bf16x8 af = *reinterpret_cast<const bf16x8*>(buf + ((t * 64 + lane) << 3));
+          bf16x8 bf[NB];  // all of the step's B fragments in flight before the MFMAs
+#pragma unroll
+          for (int b = 0; b < NB; ++b)
+            bf[b] = *reinterpret_cast<const bf16x8*>(wlds + (((ks * NB + b) * 64 + lane) << 3));
+#pragma unroll
+          for (int b = 0; b < NB; ++b) acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf[b], acc[b], 0, 0, 0);
         }
-      }
-      if (c + 1 < nchunks) issue(p, c + 1);
-      else if (p + static_cast<int64_t>(gridDim.x) * nw < panels)
-        issue(p + static_cast<int64_t>(gridDim.x) * nw, 0);  // next panel's first chunk
-#pragma unroll
-      for (int t = 0; t < CH; ++t) {
-        const int ks = c * CH + t;
-        if (ks >= nks || (a.probe & 2)) break;
-        bf16x8 bf[NB];  // all of the step's B fragments in flight before the MFMAs
-#pragma unroll
-        for (int b = 0; b < NB; ++b) bf[b] = *reinterpret_cast<const bf16x8*>(wlds + (((ks * NB + b) * 64 + lane) << 3));
-#pragma unroll
-        for (int b = 0; b < NB; ++b) acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[t], bf[b], acc[b], 0, 0, 0);
       }
     }
     // bias + relu applied in registers first, so the stores below depend on
@@ -579,9 +591,12 @@ __global__ void __launch_bounds__(256) gemm_wstat_kernel(const WsArgs a) {
 
 template <int NB, bool MASKA>
 int launch_wstat_nb(const WsArgs& w, hipStream_t st) {
-  const size_t lds = static_cast<size_t>(w.Kp) * NB * 32 * sizeof(__bf16);
   const int64_t panels = (w.M + 31) / 32;
-  const int nw = (w.probe >> 8) ? (w.probe >> 8) : kWsWaves;
+  // one workgroup per CU (the weight image fills LDS): 2 waves per workgroup
+  // once there are >= 512 panels so all 256 CUs stream, else 4
+  const int nw = (w.probe >> 8) ? (w.probe >> 8) : (panels >= 512 ? 2 : kWsWaves);
+  const size_t lds = static_cast<size_t>(w.Kp) * NB * 32 * sizeof(__bf16) +
+                     static_cast<size_t>(nw) * 2 * kWsChunkElems * sizeof(__bf16);
   const int64_t grid = std::min<int64_t>(ceil_div(panels, nw), 256);
   static bool attr_set = false;  // allow > 64 KiB of dynamic LDS (once per instantiation)
   if (!attr_set) {
@@ -589,6 +604,7 @@ int launch_wstat_nb(const WsArgs& w, hipStream_t st) {
                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kWsLdsMax)));
     attr_set = true;
   }
+  if (lds > kWsLdsMax) return fail(TT_ERR_UNSUPPORTED, "tt_gemm: weight image + chunk buffers exceed LDS");
   hipLaunchKernelGGL((gemm_wstat_kernel<NB, MASKA>), dim3(static_cast<unsigned>(grid)), dim3(nw * kWave), lds,
                      st, w);
   TT_CHECK_LAUNCH();
@@ -697,7 +713,10 @@ extern "C" int tt_gemm(int32_t a_col_major, int32_t b_col_major, int64_t M, int6
   {
     const int64_t Kp = round_up(K > 0 ? K : 1, 16);
     const bool form = !x3 && splits == 1 && !a_col_major && ones_row < 0 && mask_operand != 2 && N <= 288 &&
-                      static_cast<size_t>(Kp) * round_up(N, 32) * sizeof(uint16_t) <= kWsLdsMax &&
+                      K <= 32 * kWsMaxChunks &&
+                      static_cast<size_t>(Kp) * round_up(N, 32) * sizeof(uint16_t) +
+                              static_cast<size_t>(M >= 512 * 32 ? 2 : kWsWaves) * 2 * kWsChunkElems * sizeof(uint16_t) <=
+                          kWsLdsMax &&
                       (mask_operand == 0 || b_col_major) && ldc * 32 < (1ll << 31) &&
                       workspace != nullptr && workspace_bytes >= tt_gemm_workspace_size(N, K);
     if (form) {
