@@ -1,4 +1,4 @@
-// K14 recall hits and the per-shard top-k merge.
+// K14 recall hits and the per-shard top-k merge; the loss reduction.
 //
 // tt_recall_hits restates IndexRecall.__call__
 // (/root/reference/pkg/modelling/metrics/index_recall.py:52-58):
@@ -15,6 +15,29 @@ namespace tt {
 namespace {
 
 constexpr int kMaxKs = 16;
+
+// loss = scale * sum(x[0..n)): one workgroup, thread t sums t, t+1024, ...
+// in order, then a fixed-shape LDS tree (deterministic; the reference's
+// reduce_sum over the per-example CE, runner.py:78-83 with reduction SUM).
+__global__ void __launch_bounds__(1024) sum_kernel(const float* __restrict__ x, int64_t n, float scale,
+                                                   float* __restrict__ out) {
+  __shared__ float red[1024];
+  float acc = 0.0f;
+  int64_t i = threadIdx.x;
+  for (; i + 3 * 1024 < n; i += 4 * 1024) {
+    const float a = x[i], b = x[i + 1024], c = x[i + 2048], d = x[i + 3072];
+    acc = ((acc + a) + b) + c;
+    acc = acc + d;
+  }
+  for (; i < n; i += 1024) acc += x[i];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 512; w > 0; w >>= 1) {
+    if (static_cast<int>(threadIdx.x) < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0] * scale;
+}
 
 struct RecallArgs {
   const int32_t* true_ids;
@@ -128,6 +151,14 @@ extern "C" int tt_recall_hits(const int32_t* true_ids, const int32_t* cand_ids, 
   }
   a.hits = reinterpret_cast<unsigned long long*>(hits);
   hipLaunchKernelGGL(recall_hits_kernel, dim3(ceil_div(batch, 256)), dim3(256), 0, to_stream(stream), a);
+  TT_CHECK_LAUNCH();
+  return TT_OK;
+}
+
+extern "C" int tt_sum(const float* x, int64_t n, float scale, float* out, tt_stream_t stream) {
+  clear_error();
+  TT_REQUIRE(n >= 0 && out != nullptr && (n == 0 || x != nullptr), "tt_sum: bad arguments");
+  hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(1024), 0, to_stream(stream), x, n, scale, out);
   TT_CHECK_LAUNCH();
   return TT_OK;
 }

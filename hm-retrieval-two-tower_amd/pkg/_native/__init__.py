@@ -144,6 +144,7 @@ _PROTOS = {
          c_void_p, c_int64, c_void_p, c_int32, c_void_p, c_int64, c_int32, c_int64, c_int32, c_void_p, c_size_t,
          c_void_p]),
     "tt_gemm_workspace_size": (c_size_t, [c_int64, c_int64]),
+    "tt_sum": (c_int32, [c_void_p, c_int64, c_float, c_void_p, c_void_p]),
     "tt_dense_adagrad": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p]),
     "tt_dense_adam": (
         c_int32,

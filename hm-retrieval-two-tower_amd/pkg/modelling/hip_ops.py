@@ -19,6 +19,7 @@ __all__ = [
     "relu_bias_grad",
     "sum_slices",
     "gemm",
+    "loss_sum",
     "GEMM_BF16",
     "GEMM_BF16X3",
     "gather_grouped",
@@ -386,6 +387,16 @@ def sum_slices(parts: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
 
 
 GEMM_BF16, GEMM_BF16X3 = 0, 1
+
+
+def loss_sum(x: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
+    """0-d tensor scale * x.sum() (tt_sum: one deterministic launch)."""
+    _req(x, "x", torch.float32)
+    if not x.is_contiguous():
+        raise ValueError("x must be contiguous")
+    out = torch.empty((), dtype=torch.float32, device=x.device)
+    check(lib().tt_sum(x.data_ptr(), x.numel(), float(scale), out.data_ptr(), _stream()))
+    return out
 
 
 def _operand(t: torch.Tensor, name: str) -> Tuple[int, int]:

@@ -26,7 +26,7 @@ class _InBatchXent(torch.autograd.Function):
         lse, row_loss, dq, dc = hip_ops.inbatch_fused(q, c, logq)
         ctx.scale = scale
         ctx.save_for_backward(dq, dc)
-        return row_loss.sum() * scale
+        return hip_ops.loss_sum(row_loss, scale)
 
     @staticmethod
     def backward(ctx, g):
@@ -70,7 +70,7 @@ class _TowersInBatchXent(torch.autograd.Function):
         ctx.nq = len(qa)
         ctx.scale = scale
         ctx.save_for_backward(flat_q, flat_c, dq, dc, *qa, *ca)
-        return row_loss.sum() * scale
+        return hip_ops.loss_sum(row_loss, scale)
 
     @staticmethod
     def backward(ctx, g):
@@ -107,7 +107,7 @@ def inbatch_softmax_xent(q: torch.Tensor, c: torch.Tensor, logq: Optional[torch.
     scale = 1.0 if reduction == "sum" else 1.0 / q.shape[0]
     if not q.requires_grad and not c.requires_grad:
         lse, row_loss, _ = hip_ops.inbatch_rows(q, c, logq, want_dq=False)
-        return row_loss.sum() * scale
+        return hip_ops.loss_sum(row_loss, scale)
     return _InBatchXent.apply(q, c, logq, scale)
 
 

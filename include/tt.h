@@ -353,6 +353,11 @@ int tt_topk_merge(const float* scores, const int32_t* idx, int32_t num_lists,
                   int64_t n_queries, int32_t k_in, int32_t k_out,
                   float* out_scores, int32_t* out_idx, tt_stream_t stream);
 
+/* The in-batch loss's batch reduction (CategoricalCrossentropy reduction
+ * SUM, runner.py:78-83): out[0] = scale * sum(x[0..n)), one deterministic
+ * single-workgroup launch. */
+int tt_sum(const float* x, int64_t n, float scale, float* out, tt_stream_t stream);
+
 /* ------------------------------------------------------------------------ *
  * K14  Recall hits (IndexRecall.__call__, metrics/index_recall.py:52-58):
  * hits[t] += #{b : true_ids[b] in cand_ids[b, 0:ks[t]]}.  hits is int64

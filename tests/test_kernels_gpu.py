@@ -271,6 +271,20 @@ def test_gemm_rejects_bad_shapes(cuda):
         hip_ops.gemm(a, torch.empty(4, 3, device=cuda), torch.empty(8, 4, device=cuda))
 
 
+@pytest.mark.parametrize("n", [0, 1, 1023, 16384, 100003])
+def test_loss_sum_deterministic(cuda, n):
+    """tt_sum: scale * sum within fp32 summation error of the fp64 sum, and
+    bit-identical across calls (fixed order)."""
+    rng = np.random.default_rng(n)
+    x = rng.uniform(0, 20, n).astype(np.float32)
+    t = _t(x, cuda)
+    a = hip_ops.loss_sum(t, 0.5).item()
+    b = hip_ops.loss_sum(t, 0.5).item()
+    ref = 0.5 * x.astype(np.float64).sum()
+    assert a == b
+    assert abs(a - ref) <= 1e-5 * max(abs(ref), 1.0)
+
+
 def test_dense_adagrad_and_adam_bitexact(cuda):
     rng = np.random.default_rng(2)
     n = 100003
