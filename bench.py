@@ -171,8 +171,8 @@ def time_train(args, model, data, device, ws):
     if ws > 1 or args.train_mode == "sharded":
         # large tables (customer, postal, article) row-sharded over the ranks
         step = ShardedTrainStep(model, shard_min_rows=100_000)
-        # the next batch's routing (ids only) runs a step ahead on a side stream
-        run = lambda i: step(pool[i % len(pool)], next_batch=pool[(i + 1) % len(pool)])
+        # routing (ids only) runs two batches ahead on a side stream
+        run = lambda i: step(pool[i % len(pool)], ahead=[pool[(i + 1) % len(pool)], pool[(i + 2) % len(pool)]])
     else:
         step = GraphedTrainStep(model, pool[0], warmup=2)
         packed = [step.pack(b) for b in pool]  # one D2D copy per step
@@ -484,6 +484,12 @@ def main():
                     help="sharded: run the N>1 candidate-sharded index (search_owned) even on one rank")
     args = ap.parse_args()
 
+    # stdout carries exactly one JSON line: everything else written to fd 1
+    # (RCCL's version banner, library chatter) goes to stderr
+    sys.stdout.flush()
+    real_stdout = os.dup(1)
+    os.dup2(2, 1)
+
     ws, rank, local = dist_env()
     if ws > 1 or args.train_mode == "sharded" or args.index_mode == "sharded":
         torch.cuda.set_device(local)
@@ -553,7 +559,8 @@ def main():
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        sys.stdout.flush()
+        os.write(real_stdout, (json.dumps(result) + "\n").encode())
     if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 

@@ -17,10 +17,12 @@
 //
 // MI355X shape: one launch builds 64-bit keys (owner, tag, row+1) with the
 // lookup index as value, one rocPRIM radix sort over the key bits in use,
-// then ONE workgroup (1024 threads, each a contiguous run of sorted keys)
-// finds the heads, block-scans them and writes send / idx / counts; a few
-// hundred thousand lookups per step make that a ~10 us pass, with no
-// device-wide scan or atomics.
+// then two coalesced passes over the sorted keys (one key per thread): block
+// head counts, and per block its prefix (a wave sums the earlier blocks'
+// counts), an in-block scan and the send / idx / per-owner count writes.
+// (A single-workgroup scan with a contiguous run per thread took 166 us at
+// 49k lookups: every load instruction touched 64 lines and each thread's
+// loop was a chain of dependent misses.)
 #include <algorithm>
 #include <rocprim/device/device_radix_sort.hpp>
 
@@ -65,55 +67,77 @@ __global__ void __launch_bounds__(256) route_keys_kernel(const RouteArgs a) {
   a.vals_in[i] = static_cast<uint32_t>(i);
 }
 
-__global__ void __launch_bounds__(kScanThreads) route_scan_kernel(const unsigned long long* keys, const uint32_t* vals,
-                                                                  int64_t total, int32_t world, int32_t num_tags,
-                                                                  int32_t id_bits, int32_t* send, int32_t* idx,
-                                                                  long long* counts, int32_t* num_requests) {
+// Heads of the sorted key runs = distinct requests.  Pass 1: per block of
+// kScanThreads consecutive sorted keys (one per thread, coalesced), the
+// number of heads.  Pass 2: each block adds up the counts of the blocks
+// before it (wave-parallel), scans its own heads and writes send / idx and
+// its per-owner counts (LDS, then one atomic per owner per block into the
+// zeroed counts); the last block writes the request total.
+__global__ void __launch_bounds__(kScanThreads) route_heads_kernel(const unsigned long long* keys, int64_t total,
+                                                                   int32_t* block_heads) {
+  __shared__ int wsum[kScanThreads / kWave];
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kScanThreads + threadIdx.x;
+  const int head = (i < total && (i == 0 || keys[i] != keys[i - 1])) ? 1 : 0;
+  const int c = __popcll(__ballot(head));
+  if (lane_id() == 0) wsum[threadIdx.x / kWave] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int k = 0; k < kScanThreads / kWave; ++k) t += wsum[k];
+    block_heads[blockIdx.x] = t;
+  }
+}
+
+__global__ void __launch_bounds__(kScanThreads) route_write_kernel(const unsigned long long* keys, const uint32_t* vals,
+                                                                   int64_t total, int32_t world, int32_t num_tags,
+                                                                   int32_t id_bits, const int32_t* block_heads,
+                                                                   int32_t* send, int32_t* idx, long long* counts,
+                                                                   int32_t* num_requests) {
   __shared__ int wsum[kScanThreads / kWave + 1];
   __shared__ int cnt[kMaxWorld];
+  __shared__ int base_s;
   for (int o = threadIdx.x; o < world; o += kScanThreads) cnt[o] = 0;
-  const int64_t per = (total + kScanThreads - 1) / kScanThreads;
-  const int64_t i0 = threadIdx.x * per;
-  const int64_t i1 = i0 + per < total ? i0 + per : total;
-  int heads = 0;
-  for (int64_t i = i0; i < i1; ++i) heads += (i == 0 || keys[i] != keys[i - 1]) ? 1 : 0;
-  // block exclusive scan of the per-thread head counts
   const int lane = lane_id(), w = threadIdx.x / kWave;
-  int x = heads;
+  if (w == 0) {  // requests in the blocks before this one
+    int t = 0;
+    for (int b = lane; b < static_cast<int>(blockIdx.x); b += kWave) t += block_heads[b];
 #pragma unroll
-  for (int off = 1; off < kWave; off <<= 1) {
-    const int y = __shfl_up(x, off, kWave);
-    if (lane >= off) x += y;
+    for (int m = 32; m >= 1; m >>= 1) t += __shfl_xor(t, m, kWave);
+    if (lane == 0) base_s = t;
   }
-  if (lane == kWave - 1) wsum[w] = x;
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kScanThreads + threadIdx.x;
+  const unsigned long long k = i < total ? keys[i] : 0ull;
+  const int head = (i < total && (i == 0 || k != keys[i - 1])) ? 1 : 0;
+  const uint64_t m = __ballot(head);
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  const int incl = __popcll(m & (lt | (1ull << lane)));  // heads up to and including this lane
+  if (lane == kWave - 1) wsum[w] = incl;
   __syncthreads();
   if (threadIdx.x == 0) {
     int run = 0;
-    for (int k = 0; k < kScanThreads / kWave; ++k) {
-      const int t = wsum[k];
-      wsum[k] = run;
+    for (int q = 0; q < kScanThreads / kWave; ++q) {
+      const int t = wsum[q];
+      wsum[q] = run;
       run += t;
     }
     wsum[kScanThreads / kWave] = run;
   }
   __syncthreads();
-  int u = wsum[w] + x - heads - 1;  // index of the current request
-  const unsigned long long mask = (1ull << id_bits) - 1ull;
-  for (int64_t i = i0; i < i1; ++i) {
-    const unsigned long long k = keys[i];
-    if (i == 0 || k != keys[i - 1]) {
-      ++u;
+  if (i < total) {
+    const int u = base_s + wsum[w] + incl - 1;  // request index of this key's run
+    if (head) {
+      const unsigned long long mask = (1ull << id_bits) - 1ull;
       const unsigned long long ot = k >> id_bits;
-      const int owner = static_cast<int>(ot / num_tags);
       send[2 * static_cast<int64_t>(u)] = static_cast<int32_t>(static_cast<long long>(k & mask) - 1);
       send[2 * static_cast<int64_t>(u) + 1] = static_cast<int32_t>(ot % num_tags);
-      atomicAdd(&cnt[owner], 1);
+      atomicAdd(&cnt[static_cast<int>(ot / num_tags)], 1);
     }
     idx[vals[i]] = u;
   }
   __syncthreads();
-  for (int o = threadIdx.x; o < world; o += kScanThreads) counts[o] = cnt[o];
-  if (threadIdx.x == 0) *num_requests = wsum[kScanThreads / kWave];
+  for (int o = threadIdx.x; o < world; o += kScanThreads)
+    if (cnt[o]) atomicAdd(reinterpret_cast<unsigned long long*>(counts + o), static_cast<unsigned long long>(cnt[o]));
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *num_requests = base_s + wsum[kScanThreads / kWave];
 }
 
 __global__ void __launch_bounds__(256) route_owner_kernel(const int32_t* recv, int64_t n, int32_t world,
@@ -171,6 +195,7 @@ struct RouteWs {
   unsigned long long *keys_in, *keys;
   uint32_t *vals_in, *vals;
   void* sort_tmp;
+  int32_t* block_heads;
 };
 
 RouteWs carve_route(Carver& cv, const RoutePlan& p) {
@@ -180,6 +205,7 @@ RouteWs carve_route(Carver& cv, const RoutePlan& p) {
   w.vals_in = cv.take<uint32_t>(p.total);
   w.vals = cv.take<uint32_t>(p.total);
   w.sort_tmp = cv.take<char>(static_cast<int64_t>(p.sort_bytes) + 256);
+  w.block_heads = cv.take<int32_t>(ceil_div(p.total, kScanThreads));
   return w;
 }
 
@@ -236,8 +262,12 @@ extern "C" int tt_route_requests(const tt_route_lookup* lookups, int32_t num_loo
   size_t sb = p.sort_bytes;
   TT_CHECK_HIP(rocprim::radix_sort_pairs(w.sort_tmp, sb, w.keys_in, w.keys, w.vals_in, w.vals,
                                          static_cast<unsigned>(p.total), 0, p.end_bit, st, false));
-  hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, w.keys, w.vals, p.total, world, num_tags,
-                     p.id_bits, send, idx, counts, num_requests);
+  const unsigned nb = static_cast<unsigned>(ceil_div(p.total, kScanThreads));
+  TT_CHECK_HIP(hipMemsetAsync(counts, 0, static_cast<size_t>(world) * sizeof(long long), st));
+  hipLaunchKernelGGL(route_heads_kernel, dim3(nb), dim3(kScanThreads), 0, st, w.keys, p.total, w.block_heads);
+  TT_CHECK_LAUNCH();
+  hipLaunchKernelGGL(route_write_kernel, dim3(nb), dim3(kScanThreads), 0, st, w.keys, w.vals, p.total, world,
+                     num_tags, p.id_bits, w.block_heads, send, idx, counts, num_requests);
   TT_CHECK_LAUNCH();
   return TT_OK;
 }

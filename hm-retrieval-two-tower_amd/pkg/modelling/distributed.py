@@ -27,7 +27,7 @@ import logging
 import os
 import time
 from dataclasses import dataclass
-from typing import Any, Callable, Dict, Iterable, List, Optional, Tuple
+from typing import Any, Callable, Dict, Iterable, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -347,6 +347,13 @@ class ShardedTables:
     def route(self, lookups: List[Tuple[str, torch.Tensor]], group=None) -> _Route:
         """lookups: (table name, ids [B] int32).  Collectives run on `group`
         (default: the tables' group) and on the current stream."""
+        return self.route_finish(self.route_begin(lookups, group))
+
+    def route_begin(self, lookups: List[Tuple[str, torch.Tensor]], group=None) -> dict:
+        """First half of route(), no host sync: dedup + owner bucketing and the
+        count exchange are enqueued on the current stream, the counts copied
+        to pinned host memory behind an event.  route_finish() completes it
+        (by then the counts have long landed, so its wait is free)."""
         group = self.group if group is None else group
         W, T = self.world, len(self.names)
         dev = lookups[0][1].device
@@ -354,14 +361,29 @@ class ShardedTables:
         send, send_counts, _, idx = self.ops.route_requests(tagged, W, T)
         recv_counts = torch.empty_like(send_counts)
         _a2a(recv_counts, send_counts, [1] * W, [1] * W, group)
-        counts = torch.stack([send_counts, recv_counts]).cpu()  # the one host sync of the step
-        s_split, r_split = counts[0].tolist(), counts[1].tolist()
+        both = torch.stack([send_counts, recv_counts])
+        pinned = dev.type == "cuda"
+        host = torch.empty(both.shape, dtype=both.dtype, pin_memory=pinned)
+        host.copy_(both, non_blocking=pinned)
+        ev = None
+        if pinned:
+            ev = torch.cuda.Event()
+            ev.record()
+        return dict(group=group, dev=dev, send=send, idx=idx, host=host, event=ev, keep=(both, send_counts))
+
+    def route_finish(self, pend: dict) -> _Route:
+        W, T = self.world, len(self.names)
+        t0 = time.perf_counter()
+        if pend["event"] is not None:
+            pend["event"].synchronize()  # the step's one host sync, normally long complete
+        pend["sync_s"] = time.perf_counter() - t0
+        s_split, r_split = pend["host"][0].tolist(), pend["host"][1].tolist()
         R = int(sum(s_split))
-        recv = torch.empty(sum(r_split), 2, dtype=torch.int32, device=dev)
-        _a2a(recv, send[:R], r_split, s_split, group)
+        recv = torch.empty(sum(r_split), 2, dtype=torch.int32, device=pend["dev"])
+        _a2a(recv, pend["send"][:R], r_split, s_split, pend["group"])
         tags, rows, tids = self.ops.route_owner(recv, W, T)
         return _Route(s_split=s_split, r_split=r_split, R=R, n_recv=int(sum(r_split)), tags=tags, rows=rows,
-                      table_ids=list(tids.unbind(0)), idx=list(idx.unbind(0)), dev=dev)
+                      table_ids=list(tids.unbind(0)), idx=list(pend["idx"].unbind(0)), dev=pend["dev"])
 
     # -- forward -----------------------------------------------------------
     def fetch_routed(self, rt: _Route, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -511,7 +533,9 @@ class ShardedTrainStep:
         self._route_group = dist.new_group(list(range(self.world)), backend=dist.get_backend(group)) \
             if self.world > 1 else group
         self._side = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
-        self._pending = None     # (batch object id, _Route) routed a step ahead
+        self._pending = None     # (batch object id, _Route) routed ahead (prefetch())
+        self._inflight: List[Tuple[int, dict, int]] = []  # (batch id, route_begin state, step begun)
+        self._ready: Dict[int, _Route] = {}               # batch id -> finished route
         self._static = None      # static batch / request buffers (set up on the first call)
         self._graph = None
         self._calls = 0
@@ -540,13 +564,20 @@ class ShardedTrainStep:
     def _setup(self, batch) -> None:
         m = self.model
         dev = m.device
+        # the batch lives in one int32 [K, B] and one fp32 [F, B] buffer, loaded
+        # with one stacking launch each
         self._static = {}
+        kinds = {}
         for k, v in batch.items():
             t = v if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v))
-            t = t.reshape(-1).to(dev)
-            if t.dtype not in (torch.float32, torch.int32):
-                t = t.to(torch.float32 if t.is_floating_point() else torch.int32)
-            self._static[k] = torch.empty_like(t)
+            kinds[k] = torch.float32 if t.is_floating_point() else torch.int32
+            B0 = t.numel()
+        self._int_keys = sorted(k for k, d in kinds.items() if d == torch.int32)
+        self._float_keys = sorted(k for k, d in kinds.items() if d == torch.float32)
+        self._ibuf = torch.empty(max(len(self._int_keys), 1), B0, dtype=torch.int32, device=dev)
+        self._fbuf = torch.empty(max(len(self._float_keys), 1), B0, dtype=torch.float32, device=dev)
+        self._static.update({k: self._ibuf[i] for i, k in enumerate(self._int_keys)})
+        self._static.update({k: self._fbuf[i] for i, k in enumerate(self._float_keys)})
         lk = self._lookups(self._static)
         B = next(iter(self._static.values())).numel()
         self._B = B
@@ -559,9 +590,17 @@ class ShardedTrainStep:
         self._bucket = torch.zeros(n_bucket, dtype=torch.float32, device=dev)
 
     def _load(self, batch) -> None:
-        for k, v in batch.items():
+        dev = self._ibuf.device
+
+        def col(k, dtype):
+            v = batch[k]
             t = v if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v))
-            self._static[k].copy_(t.reshape(-1), non_blocking=True)
+            return t.reshape(-1).to(device=dev, dtype=dtype)
+
+        if self._int_keys:
+            torch.stack([col(k, torch.int32) for k in self._int_keys], out=self._ibuf)
+        if self._float_keys:
+            torch.stack([col(k, torch.float32) for k in self._float_keys], out=self._fbuf)
 
     # -- the static middle (graph-captured) --------------------------------
     def _middle(self) -> None:
@@ -614,6 +653,9 @@ class ShardedTrainStep:
     def _route(self, batch) -> _Route:
         return self.tables.route([(k, ids) for k, ids, _, _ in self._lookups(batch)], group=self._route_group)
 
+    def _route_begin(self, batch) -> dict:
+        return self.tables.route_begin([(k, ids) for k, ids, _, _ in self._lookups(batch)], group=self._route_group)
+
     def prefetch(self, batch) -> None:
         """Route `batch` (the next step's) on the side stream now."""
         if self.tables is None:
@@ -627,21 +669,42 @@ class ShardedTrainStep:
             rt.event.record(self._side)
         self._pending = (id(batch), rt)
 
-    def __call__(self, batch: Dict[str, Any], next_batch: Optional[Dict[str, Any]] = None) -> Dict[str, torch.Tensor]:
+    def __call__(self, batch: Dict[str, Any], next_batch: Optional[Dict[str, Any]] = None,
+                 ahead: Optional[Sequence[Dict[str, Any]]] = None) -> Dict[str, torch.Tensor]:
+        """One step on `batch`.  `ahead` (or `next_batch`): upcoming batches in
+        order.  Their routing (ids only) starts on the side stream at the start
+        of this step and is finished (the one host sync) at the end of a LATER
+        step, so the host never waits for routing work queued behind compute:
+        with ahead=[b+1, b+2] the route of b+2 begins now and completes at the
+        end of the next step."""
         m = self.model
         tm = time.perf_counter()
         if self._static is None:
             self._setup(batch)
         cur = torch.cuda.current_stream() if self._side is not None else None
-        if next_batch is not None and self._side is not None:
-            pre = torch.cuda.Event()
-            pre.record(cur)
+        upcoming = list(ahead) if ahead is not None else ([next_batch] if next_batch is not None else [])
+        if upcoming and self._side is not None and self.tables is not None:
+            known = set(self._ready) | {k for k, _, _ in self._inflight}
+            todo = [b for b in upcoming if id(b) not in known and b is not batch]
+            if todo:
+                pre = torch.cuda.Event()
+                pre.record(cur)  # the batches' ids exist before the work queued here
+                with torch.cuda.stream(self._side):
+                    self._side.wait_event(pre)
+                    for b in todo:
+                        self._inflight.append((id(b), self._route_begin(b), self._calls))
         self._load(batch)
         tm = self._tick("load", tm)
         rt = None
         if self.tables is not None:
-            if self._pending is not None and self._pending[0] == id(batch):
+            key = id(batch)
+            if key not in self._ready and any(k == key for k, _, _ in self._inflight):
+                self._finish_routes(lambda k, step: k == key)  # needed now
+            if key in self._ready:
+                rt = self._ready.pop(key)
+            elif self._pending is not None and self._pending[0] == key:
                 rt = self._pending[1]
+            if rt is not None:
                 cur.wait_event(rt.event)
                 for t in rt.tensors():  # made on the side stream, read on this one
                     t.record_stream(cur)
@@ -684,13 +747,26 @@ class ShardedTrainStep:
         off += n
         loss = self._bucket[off:off + 1].reshape(()).clone()
         tm = self._tick("dense", tm)
-        if next_batch is not None and self._side is not None and self.tables is not None:
-            ready = pre
-            with torch.cuda.stream(self._side):
-                self._side.wait_event(ready)
-                rt2 = self._route(next_batch)
-                rt2.event = torch.cuda.Event()
-                rt2.event.record(self._side)
-            self._pending = (id(next_batch), rt2)
+        if self._inflight:
+            # routes begun in an earlier step: their counts landed long ago.  With
+            # only one batch of look-ahead, finish this step's too (waits here).
+            now = self._calls - 1
+            self._finish_routes(lambda k, step: step < now or len(upcoming) < 2)
         self._tick("prefetch", tm)
         return {"loss": loss}
+
+    def _finish_routes(self, which) -> None:
+        keep = []
+        for key, pend, step in self._inflight:
+            if which(key, step):
+                with torch.cuda.stream(self._side):
+                    rt = self.tables.route_finish(pend)
+                    rt.event = torch.cuda.Event()
+                    rt.event.record(self._side)
+                    rt.keep = pend  # its device buffers stay alive until the route is used
+                self._ready[key] = rt
+                if self.host_times is not None:
+                    self.host_times["route_sync"] = self.host_times.get("route_sync", 0.0) + pend["sync_s"]
+            else:
+                keep.append((key, pend, step))
+        self._inflight = keep
