@@ -269,7 +269,10 @@ __device__ __noinline__ int compact_region(uint2* region, int n, float thr) {
 }
 
 constexpr int kStages = 4;     // LDS ring: tile i computed while tiles i+1..i+3 land
-constexpr int kWarmTiles = 64; // bins-only warm-up tiles per split (4096 candidates)
+#ifndef TT_WARM_TILES
+#define TT_WARM_TILES 64
+#endif
+constexpr int kWarmTiles = TT_WARM_TILES;  // bins-only warm-up tiles per split (4096 candidates)
 
 template <int D>
 __global__ void __launch_bounds__(kScreenThreads) screen_bins_kernel(const ScreenArgs a) {

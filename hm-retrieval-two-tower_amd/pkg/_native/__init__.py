@@ -27,7 +27,9 @@ __all__ = [
     "EXPORTED_SYMBOLS",
 ]
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtt.so")
+# TT_LIB_PATH: a variant build for timing tools (tools/index_variants.sh); the
+# package default is the in-tree libtt.so
+LIB_PATH = os.environ.get("TT_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtt.so")
 MAX_SEGMENTS = 32
 MAX_SOURCES = 4
 

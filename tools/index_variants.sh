@@ -1,0 +1,25 @@
+# Build libtt variants of the index screen (CPU side, here):
+#   bash tools/index_variants.sh build
+# and time them on the GPU box:
+#   bash tools/index_variants.sh run
+set -e
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+VARIANTS="base:|warm128:-DTT_WARM_TILES=128|warm256:-DTT_WARM_TILES=256|warm32:-DTT_WARM_TILES=32"
+if [ "$1" = build ]; then
+  mkdir -p $ROOT/tools/bin
+  IFS='|'; for v in $VARIANTS; do
+    name=${v%%:*}; flags=${v#*:}
+    out=$ROOT/tools/bin/obj_$name; mkdir -p $out
+    unset IFS
+    make -s -j8 -C $ROOT/hm-retrieval-two-tower_amd/csrc OUTDIR=$out HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wall -Wno-unused-function -munsafe-fp-atomics $flags"
+    cp $out/libtt.so $ROOT/tools/bin/libtt_$name.so
+    IFS='|'
+  done
+else
+  IFS='|'; for v in $VARIANTS; do
+    name=${v%%:*}; unset IFS
+    echo "== $name"
+    TT_LIB_PATH=$ROOT/tools/bin/libtt_$name.so timeout -k 10 120 python3 $ROOT/tools/time_index.py
+    IFS='|'
+  done
+fi
