@@ -362,7 +362,9 @@ def time_index_sharded(device, n_queries: int, n_cand: int, k: int, ws: int, ran
     rank r owns candidate rows shard_range(N, G, r) and searches every query;
     one all_to_all hands each query block's per-shard lists to its owner,
     which merges them (tt_topk_merge).  Strong scaling: Q and N fixed.  QPS =
-    Q / max-over-ranks wall time of search_owned, barrier + sync both sides."""
+    Q / max-over-ranks wall time of search_owned, barrier + sync both sides.
+    Beside it, `query_sharded`: the same queries split over the ranks against
+    replicated candidates (QueryShardedBruteForceIndex, no exchange)."""
     from pkg.modelling.distributed import ShardedBruteForceIndex, shard_range
 
     g = torch.Generator(device=device)
@@ -392,6 +394,26 @@ def time_index_sharded(device, n_queries: int, n_cand: int, k: int, ws: int, ran
            "roofline": {"bound": "mfma", "achieved": tf, "peak": MI355X_BF16_DENSE_TFLOPS * ws, "unit": "TFLOP/s",
                         "frac": tf / (MI355X_BF16_DENSE_TFLOPS * ws),
                         "note": "2*Q*N*E scoring flops / wall time incl. all_to_all + merge, vs G x dense bf16 peak"}}
+    # the same queries query-sharded over replicated candidates (no exchange)
+    from pkg.modelling.distributed import QueryShardedBruteForceIndex
+
+    qidx = QueryShardedBruteForceIndex(k, None, C)
+    qidx.search_owned(Q[:4096 * ws])  # warm
+    torch.cuda.synchronize()
+    torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    qidx.search_owned(Q)
+    torch.cuda.synchronize()
+    torch.distributed.barrier()
+    torch.cuda.synchronize()
+    dq = time.perf_counter() - t0
+    t = torch.tensor([dq], device=device, dtype=torch.float64)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    dq = float(t.item())
+    res["query_sharded"] = {"seconds": dq, "qps": n_queries / dq,
+                            "scaling": "strong (queries split over the ranks, candidates replicated)",
+                            "roofline_frac": 2.0 * n_queries * n_cand * E / dq / 1e12 / (MI355X_BF16_DENSE_TFLOPS * ws)}
     if rank == 0 and check:
         try:
             from oracle import oracle

@@ -151,7 +151,9 @@ class TwoTowerModel(AbstractKerasModel):
             self.optimizer.prepare(self.towers)  # id sort of the embedding update, overlapped with backward
         for t in self.towers:
             t.dense.flat.grad = None
-        loss.backward()
+        if getattr(self, "_one", None) is None or self._one.device != loss.device:
+            self._one = torch.ones((), dtype=loss.dtype, device=loss.device)
+        loss.backward(self._one)  # a persistent seed: no ones-fill launch per step
         self.optimizer.apply_gradients(self.towers)
         return {"loss": loss.detach()}
 

@@ -42,7 +42,11 @@ def _oracle_ops():
 
 def _index_worker(rank, world, port, q, c, k, out):
     _init(rank, world, port)
-    from pkg.modelling.distributed import ShardedBruteForceIndex, shard_range
+    from pkg.modelling.distributed import QueryShardedBruteForceIndex, ShardedBruteForceIndex, shard_range
+
+    qidx = QueryShardedBruteForceIndex(k, None, torch.from_numpy(c), ops=_oracle_ops())
+    qs_s, qs_i = qidx.search(torch.from_numpy(q))
+    out[("q", rank)] = (qs_s.numpy(), qs_i.numpy())
 
     b, e = shard_range(c.shape[0], world, rank)
     idx = ShardedBruteForceIndex(k, None, torch.from_numpy(c[b:e]), b, ops=_oracle_ops())
@@ -73,6 +77,8 @@ def test_sharded_index_equals_unsharded(world):
         # search_owned: this rank's query block only, same global lists
         assert np.array_equal(oi, ri[b:e]) and np.array_equal(os_, rs[b:e])
         covered += list(range(b, e))
+        qs_s, qs_i = out[("q", r)]  # query-sharded: every rank holds the full answer
+        assert np.array_equal(qs_i, ri) and np.array_equal(qs_s, rs)
     assert covered == list(range(q.shape[0]))
 
 
