@@ -1,10 +1,12 @@
-# Build libtt variants of the index screen (CPU side, here):
+# Build libtt variants (compile-time knobs; default: the index screen's
+# warm-up length; VARIANTS="name:-DFLAG=..|..." and SCRIPT=tools/x.py override):
 #   bash tools/index_variants.sh build
 # and time them on the GPU box:
 #   bash tools/index_variants.sh run
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
-VARIANTS="base:|warm128:-DTT_WARM_TILES=128|warm256:-DTT_WARM_TILES=256|warm32:-DTT_WARM_TILES=32"
+VARIANTS=${VARIANTS:-"base:|warm128:-DTT_WARM_TILES=128|warm256:-DTT_WARM_TILES=256|warm32:-DTT_WARM_TILES=32"}
+SCRIPT=${SCRIPT:-tools/time_index.py}
 if [ "$1" = build ]; then
   mkdir -p $ROOT/tools/bin
   IFS='|'; for v in $VARIANTS; do
@@ -19,7 +21,7 @@ else
   IFS='|'; for v in $VARIANTS; do
     name=${v%%:*}; unset IFS
     echo "== $name"
-    TT_LIB_PATH=$ROOT/tools/bin/libtt_$name.so timeout -k 10 120 python3 $ROOT/tools/time_index.py
+    TT_LIB_PATH=$ROOT/tools/bin/libtt_$name.so timeout -k 10 120 python3 $ROOT/$SCRIPT
     IFS='|'
   done
 fi
