@@ -49,8 +49,9 @@ def _mm_fast_fp32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     gfx950 an emulated mode measured at ~4e-6 relative error vs fp64 for the
     C3 tower shapes, i.e. fp32-faithful).  For the input-gradient GEMM it
     selects a far better kernel when N is not a tile multiple (query tower,
-    N = 258: 45.8 -> 21.4 us); the forward and weight-gradient GEMMs gain
-    nothing and keep the default."""
+    N = 258: 44.7 -> 19.4 us; candidate N = 200: 24.1 -> 20.0 us; at N = 256
+    it is 7 % slower, and the forward and weight-gradient GEMMs gain nothing:
+    tools/tf32_probe.py), so only ragged input-gradient GEMMs take it."""
     prev = torch.backends.cuda.matmul.allow_tf32
     torch.backends.cuda.matmul.allow_tf32 = True
     try:
@@ -149,7 +150,9 @@ class DenseStack:
                                           out=None if (top and not inplace) else g, db=db)
             _splitk_mm_tn(acts[li], g, dw)
             if li > 0 or need_input_grad:
-                g = _mm_fast_fp32(g, params[li][0].t())
+                w = params[li][0]
+                # fast path only where it picks the better kernel (ragged output widths)
+                g = _mm_fast_fp32(g, w.t()) if w.shape[0] % 64 else torch.mm(g, w.t())
         return (g if need_input_grad else None), gflat
 
     def _forward_tt(self, x: torch.Tensor, flat: torch.Tensor) -> List[torch.Tensor]:
