@@ -29,6 +29,8 @@ for fin, fout in ((258, 256), (200, 256), (256, 128)):
         y = X @ W
         err = ((y.double() - X.double() @ W.double()).norm() / (X.double() @ W.double()).norm()).item()
         r = {"fwd": t(lambda: torch._addmm_activation(b, X, W)), "dx": t(lambda: torch.mm(G, W.t())),
-             "dw_bmm16": t(lambda: torch.bmm(X.view(16, B // 16, fin).transpose(1, 2), G.view(16, B // 16, fout)))}
+             "dw_mm": t(lambda: torch.mm(X.t(), G)),
+             **{f"dw_bmm{S}": t(lambda S=S: torch.bmm(X.view(S, B // S, fin).transpose(1, 2),
+                                                      G.view(S, B // S, fout))) for S in (8, 16, 32, 64)}}
         print(fin, fout, "fast" if flag else "fp32", f"rel err {err:.1e}", {k: round(v, 1) for k, v in r.items()},
               flush=True)
