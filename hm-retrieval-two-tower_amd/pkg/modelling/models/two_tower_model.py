@@ -147,13 +147,20 @@ class TwoTowerModel(AbstractKerasModel):
         if self.optimizer is None:
             raise RuntimeError("call compile(optimizer=...) before training")
         loss = self.compute_loss(data, training=True)
-        if hasattr(self.optimizer, "prepare"):
-            self.optimizer.prepare(self.towers)  # id sort of the embedding update, overlapped with backward
+        fwd_done = None
+        if hasattr(self.optimizer, "prepare") and loss.is_cuda:
+            fwd_done = torch.cuda.Event()
+            fwd_done.record()
         for t in self.towers:
             t.dense.flat.grad = None
         if getattr(self, "_one", None) is None or self._one.device != loss.device:
             self._one = torch.ones((), dtype=loss.dtype, device=loss.device)
         loss.backward(self._one)  # a persistent seed: no ones-fill launch per step
+        if fwd_done is not None:
+            # the embedding update's id sort needs only the forward's ids; issued
+            # after the backward (so the backward's chains are launched first)
+            # but ordered only after the forward, it overlaps the backward
+            self.optimizer.prepare(self.towers, after=fwd_done)
         self.optimizer.apply_gradients(self.towers)
         return {"loss": loss.detach()}
 

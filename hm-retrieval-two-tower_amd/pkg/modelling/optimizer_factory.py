@@ -15,7 +15,7 @@ apply_gradients.
 """
 from __future__ import annotations
 
-from typing import Any, Dict, List
+from typing import Any, Dict, List, Optional
 import logging
 
 import torch
@@ -84,11 +84,12 @@ class Adagrad(_Optimizer):
                                   grad=layer.last_grad if with_grad else None))
         return specs, batch
 
-    def prepare(self, towers) -> None:
+    def prepare(self, towers, after: Optional[torch.cuda.Event] = None) -> None:
         """Start the embedding update's id sort early, on a side stream (it reads
         only the lookup ids of the last gather), so it overlaps the backward
-        pass; apply_gradients then joins it.  Optional: without it the sort
-        runs inside apply_gradients."""
+        pass; apply_gradients then joins it.  `after`: an event of the current
+        stream the sort must follow (default: everything queued so far).
+        Optional: without it the sort runs inside apply_gradients."""
         self._prepared = None
         if not torch.cuda.is_available():
             return
@@ -99,7 +100,10 @@ class Adagrad(_Optimizer):
         side = self._side_streams.get(cur.device)
         if side is None:
             side = self._side_streams[cur.device] = torch.cuda.Stream(device=cur.device)
-        side.wait_stream(cur)
+        if after is not None:
+            side.wait_event(after)  # ordered after that point of this stream only
+        else:
+            side.wait_stream(cur)
         with torch.cuda.stream(side):
             hip_ops.sparse_sort(specs, batch)
         done = torch.cuda.Event()
