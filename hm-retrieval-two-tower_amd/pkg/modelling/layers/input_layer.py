@@ -64,9 +64,9 @@ class _MultiGatherFn(torch.autograd.Function):
     """Several InputLayers of one batch gathered by one tt_gather_multi launch."""
 
     @staticmethod
-    def forward(ctx, layers, seglists, batch, *anchors):
+    def forward(ctx, layers, seglists, batch, extra, *anchors):
         outs = [torch.empty(batch, l.row_stride, dtype=torch.float32, device=l.device) for l in layers]
-        hip_ops.gather_multi(list(zip(seglists, outs)), batch)
+        hip_ops.gather_multi(list(zip(seglists, outs)) + list(extra), batch)
         ctx.layers = layers
         return tuple(o[:, : l.output_dim] for o, l in zip(outs, layers))
 
@@ -76,7 +76,7 @@ class _MultiGatherFn(torch.autograd.Function):
             if g is not None and g.stride(1) != 1:
                 g = g.contiguous()
             layer.last_grad = g
-        return (None, None, None) + (None,) * len(ctx.layers)
+        return (None, None, None, None) + (None,) * len(ctx.layers)
 
 
 class InputLayer:
@@ -179,16 +179,23 @@ class InputLayer:
         return _GatherFn.apply(self._anchor, self, segments, batch)
 
     @staticmethod
-    def gather_many(layers: Sequence["InputLayer"], xs: Sequence[Dict[str, torch.Tensor]]) -> List[torch.Tensor]:
+    def gather_many(layers: Sequence["InputLayer"], xs: Sequence[Dict[str, torch.Tensor]],
+                    extra: Sequence = ()) -> List[torch.Tensor]:
         """The outputs of several InputLayers on one batch from ONE gather launch
-        (the query and candidate towers of a train step)."""
+        (the query and candidate towers of a train step).  `extra`: further
+        (segments, out) calls of the same batch riding in that launch without
+        gradients (the logQ lookup)."""
         prepared = [l._segments(x) for l, x in zip(layers, xs)]
         batches = {b for _, b in prepared}
         if len(batches) != 1:
             raise ValueError(f"gather_many needs one batch size, got {sorted(batches)}")
-        if sum(len(segs) for segs, _ in prepared) > hip_ops._native.MAX_SEGMENTS:
-            return [_GatherFn.apply(l._anchor, l, segs, b) for l, (segs, b) in zip(layers, prepared)]
-        return list(_MultiGatherFn.apply(list(layers), [segs for segs, _ in prepared], batches.pop(),
+        nseg = sum(len(segs) for segs, _ in prepared) + sum(len(segs) for segs, _ in extra)
+        if nseg > hip_ops._native.MAX_SEGMENTS:
+            b = batches.pop()
+            for segs, out in extra:
+                hip_ops.gather_grouped(segs, b, out)
+            return [_GatherFn.apply(l._anchor, l, segs, bb) for l, (segs, bb) in zip(layers, prepared)]
+        return list(_MultiGatherFn.apply(list(layers), [segs for segs, _ in prepared], batches.pop(), list(extra),
                                          *[l._anchor for l in layers]))
 
     def sparse_sources(self) -> List[dict]:

@@ -116,11 +116,29 @@ class TwoTowerModel(AbstractKerasModel):
         hip_ops.gather_grouped([(self._logq_rows.view(-1, 1), ids, 0)], ids.numel(), out)
         return out.view(-1)
 
+    def _logq_call(self, x: Dict[str, Any]):
+        """(segments, out) of the logQ lookup as a 1-wide gather call, or None
+        when logQ comes another way (precomputed in the batch / disabled)."""
+        if self.logq_correction is None or LOGQ_KEY in x:
+            return None
+        ids = x[self.candidate_id_col]
+        if not isinstance(ids, torch.Tensor) or ids.device.type != "cuda" or ids.dtype != torch.int32:
+            return None
+        if self._logq_rows is None:
+            feat = next(f for f in self.candidate_features if f.name == self.candidate_id_col)
+            self._logq_rows = self.logq_correction.row_table(feat, self.device)
+        ids = ids.reshape(-1).contiguous()
+        out = torch.empty(ids.numel(), 1, dtype=torch.float32, device=self.device)
+        return [(self._logq_rows.view(-1, 1), ids, 0)], out
+
     def compute_loss(self, x: Dict[str, Any], training: bool = True) -> torch.Tensor:
         q, c = self._split(x)
         with torch.set_grad_enabled(training):
-            qi, ci = InputLayer.gather_many([self.query_tower.input_layer, self.candidate_tower.input_layer], [q, c])
-            return self.tower_loss(qi, ci, self.candidate_logq(x))
+            call = self._logq_call(x)  # rides in the towers' gather launch
+            qi, ci = InputLayer.gather_many([self.query_tower.input_layer, self.candidate_tower.input_layer], [q, c],
+                                            extra=[call] if call is not None else ())
+            logq = call[1].view(-1) if call is not None else self.candidate_logq(x)
+            return self.tower_loss(qi, ci, logq)
 
     def tower_loss(self, qi: torch.Tensor, ci: torch.Tensor, logq: Optional[torch.Tensor]) -> torch.Tensor:
         """Loss from the gathered tower inputs: with gradients, both MLPs and the
