@@ -162,6 +162,25 @@ def test_train_steps_match_cpu_restatement(cuda, zipf, backend, precision):
                 assert np.linalg.norm(d_gpu - d_ref) <= tol * np.linalg.norm(d_ref), k
 
 
+@pytest.mark.parametrize("B", [1, 2, 37, 1000])
+def test_ragged_batch_train_step_matches_cpu_restatement(cuda, B):
+    """Batch sizes off every tile multiple (the reference's last partial batch,
+    tfrecord_dataset.py:97 has no drop_remainder), including B = 1 (the loss
+    of a one-column softmax is 0 in exact arithmetic; here lse comes from the
+    bf16-MFMA score and the positive logit from the fp32 one, so it is 0 to
+    within the bf16 rounding of that score: atol 1e-4)."""
+    m = _small_model(cuda, seed=B)
+    ref = _cpu_mirror(m)
+    rng = np.random.default_rng(B)
+    b = _batch(cuda, rng, B, True)
+    lq = m.candidate_logq(b).cpu().numpy()
+    rl = ref.step([b["cust"].cpu().numpy(), b["post"].cpu().numpy()],
+                  [b["art"].cpu().numpy(), b["ptn"].cpu().numpy(), b["ptn"].cpu().numpy()], lq)
+    gl = float(m.train_step(b)["loss"].item())
+    assert np.isfinite(gl)
+    assert abs(gl - rl) <= 2e-3 * abs(rl) + 1e-4, (gl, rl)
+
+
 def test_graph_replay_equals_eager(cuda):
     a, b = _small_model(cuda, seed=3), _small_model(cuda, seed=3)
     rng = np.random.default_rng(1)
