@@ -212,7 +212,10 @@ __global__ void __launch_bounds__(kThreads) block_sum_kernel(const Job j, const 
     const uint32_t s = off[r] >> kSrcShift;
     const uint32_t b = off[r] & ((1u << kSrcShift) - 1u);
     const uint32_t o = b * gld + (s == 0 ? go0 : s == 1 ? go1 : s == 2 ? go2 : go3);
-    off[r] = off[r] != 0xFFFFFFFFu ? o : 0xFFFFFFFFu;
+    // a (source, row) outside this call's gradient (stale presorted workspace)
+    // never reaches memory: it reads as padding
+    const bool in = s < static_cast<uint32_t>(T.num_sources) && b < static_cast<uint32_t>(j.batch);
+    off[r] = (off[r] != 0xFFFFFFFFu && in) ? o : 0xFFFFFFFFu;
     if (r == kBlock - 1 || key[r + 1] != key[r]) ends |= 1u << r;
   }
   const bool head_cont = key[0] == kprev;

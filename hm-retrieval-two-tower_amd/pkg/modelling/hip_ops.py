@@ -96,7 +96,7 @@ class Workspace:
 
         def __enter__(self):
             self.prev = Workspace._scope
-            Workspace._scope = self.name + "/"
+            Workspace._scope = self.name + "/" if self.name else ""  # "": the root scope
             return self
 
         def __exit__(self, *exc):

@@ -57,7 +57,7 @@ class _TowersInBatchXent(torch.autograd.Function):
     are not needed afterwards)."""
 
     @staticmethod
-    def forward(ctx, qi, ci, flat_q, flat_c, logq, stack_q, stack_c, scale):
+    def forward(ctx, qi, ci, flat_q, flat_c, logq, stack_q, stack_c, scale, on_tower=None):
         main = torch.cuda.current_stream()
         side = _tower_stream(qi.device)
         side.wait_stream(main)
@@ -69,6 +69,7 @@ class _TowersInBatchXent(torch.autograd.Function):
         ctx.stacks = (stack_q, stack_c)
         ctx.nq = len(qa)
         ctx.scale = scale
+        ctx.on_tower = on_tower
         ctx.save_for_backward(flat_q, flat_c, dq, dc, *qa, *ca)
         return hip_ops.loss_sum(row_loss, scale)
 
@@ -83,19 +84,28 @@ class _TowersInBatchXent(torch.autograd.Function):
         side.wait_stream(main)
         with torch.cuda.stream(side), hip_ops.Workspace.scope("tower_c"):
             gci, gflat_c = stack_c.backward_acts(ca, flat_c, dc, s, ctx.needs_input_grad[1])
+            if ctx.on_tower is not None:  # this tower's updates, beside the other tower's backward
+                ctx.on_tower(1, gci, gflat_c)
         gqi, gflat_q = stack_q.backward_acts(qa, flat_q, dq, s, ctx.needs_input_grad[0])
+        if ctx.on_tower is not None:
+            ctx.on_tower(0, gqi, gflat_q)
         main.wait_stream(side)
-        return gqi, gci, gflat_q, gflat_c, None, None, None, None
+        return gqi, gci, gflat_q, gflat_c, None, None, None, None, None
 
 
 def towers_inbatch_softmax_xent(qi: torch.Tensor, ci: torch.Tensor, stack_q, stack_c,
-                                logq: Optional[torch.Tensor] = None, reduction: str = "sum") -> torch.Tensor:
+                                logq: Optional[torch.Tensor] = None, reduction: str = "sum",
+                                on_tower=None) -> torch.Tensor:
     """Loss of the query tower on qi against the candidate tower on ci (tower
-    inputs [B, *]), fused into one autograd node; stack_* are DenseStacks."""
+    inputs [B, *]), fused into one autograd node; stack_* are DenseStacks.
+    on_tower(i, input_grad, flat_grad), if given, is called in the backward as
+    soon as tower i's (0 query, 1 candidate) gradients exist, on the stream and
+    workspace scope they were produced in (the fused train step applies the
+    optimizer there)."""
     if reduction not in ("sum", "sum_over_batch_size", "mean"):
         raise ValueError(f"unsupported reduction {reduction}")
     scale = 1.0 if reduction == "sum" else 1.0 / qi.shape[0]
-    return _TowersInBatchXent.apply(qi, ci, stack_q.flat, stack_c.flat, logq, stack_q, stack_c, scale)
+    return _TowersInBatchXent.apply(qi, ci, stack_q.flat, stack_c.flat, logq, stack_q, stack_c, scale, on_tower)
 
 
 def inbatch_softmax_xent(q: torch.Tensor, c: torch.Tensor, logq: Optional[torch.Tensor] = None,

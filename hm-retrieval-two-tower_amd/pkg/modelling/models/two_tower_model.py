@@ -59,6 +59,9 @@ class TwoTowerModel(AbstractKerasModel):
         If provided, logQ correction is applied before the loss.
     """
 
+    # apply each tower's Adagrad step inside the backward (see train_step)
+    fused_optimizer_apply: bool = False
+
     def __init__(self, query_features: List[Feature], candidate_features: List[Feature], candidate_id_col: str,
                  joint_embedding_size: int, query_tower_units: Optional[List[int]] = None,
                  candidate_tower_units: Optional[List[int]] = None,
@@ -145,7 +148,7 @@ class TwoTowerModel(AbstractKerasModel):
         in-batch loss run as one autograd node (losses.towers_inbatch_softmax_xent)."""
         if torch.is_grad_enabled():
             return towers_inbatch_softmax_xent(qi, ci, self.query_tower.dense, self.candidate_tower.dense, logq,
-                                               self.loss.reduction)
+                                               self.loss.reduction, getattr(self, "_on_tower", None))
         return self.loss(self.query_tower.dense(qi), self.candidate_tower.dense(ci), logq)
 
     def compile(self, loss=None, optimizer=None, **kwargs) -> None:
@@ -161,12 +164,27 @@ class TwoTowerModel(AbstractKerasModel):
 
     def train_step(self, data: Dict[str, Any]) -> Dict[str, torch.Tensor]:
         """One optimisation step on a batch of positive pairs; returns the
-        (device) loss without synchronising."""
+        (device) loss without synchronising.  With fused_optimizer_apply (opt-in,
+        Adagrad on the GPU) each tower's dense and sparse updates are applied
+        inside the backward, the moment that tower's gradients exist (the
+        candidate tower's beside the query tower's backward); the updates are
+        the same as applying them afterwards (each table and MLP buffer is
+        touched by one tower only).  Not yet measured on the GPU, hence off."""
+        from pkg.modelling.optimizer_factory import Adagrad
+
         if self.optimizer is None:
             raise RuntimeError("call compile(optimizer=...) before training")
-        loss = self.compute_loss(data, training=True)
+        fused = self.fused_optimizer_apply and isinstance(self.optimizer, Adagrad) and self.device.type == "cuda"
+        self._on_tower = self._apply_tower if fused else None
+        try:
+            loss = self.compute_loss(data, training=True)
+        finally:
+            self._on_tower = None
         fwd_done = None
-        if hasattr(self.optimizer, "prepare") and loss.is_cuda:
+        if fused:
+            # one id sort per tower on a side stream, before the backward needs it
+            self.optimizer.prepare_towers(self.towers, ["", "tower_c"])
+        elif hasattr(self.optimizer, "prepare") and loss.is_cuda:
             fwd_done = torch.cuda.Event()
             fwd_done.record()
         for t in self.towers:
@@ -174,13 +192,19 @@ class TwoTowerModel(AbstractKerasModel):
         if getattr(self, "_one", None) is None or self._one.device != loss.device:
             self._one = torch.ones((), dtype=loss.dtype, device=loss.device)
         loss.backward(self._one)  # a persistent seed: no ones-fill launch per step
-        if fwd_done is not None:
-            # the embedding update's id sort needs only the forward's ids; issued
-            # after the backward (so the backward's chains are launched first)
-            # but ordered only after the forward, it overlaps the backward
-            self.optimizer.prepare(self.towers, after=fwd_done)
-        self.optimizer.apply_gradients(self.towers)
+        if fused:
+            self.optimizer.iterations += 1
+        else:
+            if fwd_done is not None:
+                # the embedding update's id sort needs only the forward's ids; issued
+                # after the backward (so the backward's chains are launched first)
+                # but ordered only after the forward, it overlaps the backward
+                self.optimizer.prepare(self.towers, after=fwd_done)
+            self.optimizer.apply_gradients(self.towers)
         return {"loss": loss.detach()}
+
+    def _apply_tower(self, i: int, input_grad: Optional[torch.Tensor], flat_grad: torch.Tensor) -> None:
+        self.optimizer.apply_tower(self.towers[i], input_grad, flat_grad)
 
     def fit(self, dataset: Iterable[Dict[str, Any]], epochs: int = 1, callbacks=None,
             use_graph: bool = False) -> Dict[str, List[float]]:

@@ -67,22 +67,68 @@ class Adagrad(_Optimizer):
         self._prepared = None
         self._side_streams = {}
 
-    def _sparse_specs(self, towers, with_grad: bool):
+    def _sparse_specs(self, towers, with_grad: bool, grad: Optional[torch.Tensor] = None):
         init = self.initial_accumulator_value
         specs, batch = [], None
         for tower in towers:
             layer = tower.input_layer
             if not layer.embedding_layers:
                 continue
-            if with_grad and layer.last_grad is None:
+            g = grad if grad is not None else layer.last_grad
+            if with_grad and g is None:
                 continue
             for src in layer.sparse_sources():
                 t = src["table"]
                 (acc,) = self._slot(t.weight, 1, init)
                 batch = src["ids"][0].numel()
                 specs.append(dict(table=t.weight, slot0=acc, ids=src["ids"], grad_col_offset=src["grad_col_offset"],
-                                  grad=layer.last_grad if with_grad else None))
+                                  grad=g if with_grad else None))
         return specs, batch
+
+    # -- per-tower application from inside the backward (TwoTowerModel.train_step)
+    def prepare_towers(self, towers, scopes: List[str]) -> None:
+        """One id sort per tower (tower i's workspace scope scopes[i]) on the
+        side stream, before the backward, so each tower's update can be applied
+        by apply_tower the moment that tower's gradients exist."""
+        self._tower_prep = {}
+        if not torch.cuda.is_available():
+            return
+        cur = torch.cuda.current_stream()
+        side = self._side_streams.get(cur.device)
+        if side is None:
+            side = self._side_streams[cur.device] = torch.cuda.Stream(device=cur.device)
+        side.wait_stream(cur)
+        for tower, scope in zip(towers, scopes):
+            specs, batch = self._sparse_specs([tower], with_grad=False)
+            if not specs or len(specs) > 16 or not batch:
+                continue
+            with torch.cuda.stream(side), hip_ops.Workspace.scope(scope):
+                hip_ops.sparse_sort(specs, batch)
+                key = hip_ops.Workspace._scope  # the apply must find its sorted keys in this scope's buffer
+            done = torch.cuda.Event()
+            done.record(side)
+            self._tower_prep[id(tower)] = ([id(s["table"]) for s in specs], batch, done, key)
+
+    def apply_tower(self, tower, input_grad: Optional[torch.Tensor], flat_grad: torch.Tensor) -> None:
+        """Tower's dense Adagrad step and its tables' sparse step, on the current
+        stream and workspace scope (the ones prepare_towers used for it)."""
+        lr, eps, init = self.learning_rate, self.epsilon, self.initial_accumulator_value
+        flat = tower.dense.flat
+        (acc,) = self._slot(flat, 1, init)
+        hip_ops.dense_adagrad(flat.data, acc, flat_grad, lr, eps)
+        if input_grad is None:
+            return
+        specs, batch = self._sparse_specs([tower], with_grad=True, grad=input_grad)
+        prep = self._tower_prep.pop(id(tower), None) if hasattr(self, "_tower_prep") else None
+        if not specs:
+            return
+        if prep is not None:
+            torch.cuda.current_stream().wait_event(prep[2])
+        if (prep is not None and prep[0] == [id(s["table"]) for s in specs] and prep[1] == batch
+                and prep[3] == hip_ops.Workspace._scope):
+            hip_ops.sparse_adagrad(specs, batch, None, lr, eps, presorted=True)
+        else:
+            hip_ops.sparse_adagrad(specs, batch, None, lr, eps)
 
     def prepare(self, towers, after: Optional[torch.cuda.Event] = None) -> None:
         """Start the embedding update's id sort early, on a side stream (it reads
