@@ -179,3 +179,21 @@ def test_hip_ops_reject_cpu_tensors():
         hip_ops.inbatch_rows(q, q, None)
     with pytest.raises(ValueError, match="GPU"):
         hip_ops.gather_grouped([(torch.zeros(3, 2), torch.zeros(4, dtype=torch.int32), 0)], 4, torch.zeros(4, 2))
+
+
+def test_workspace_scopes_nest_and_empty_scope_is_root():
+    """A sort issued under scope(s) and the apply that reads its buffer must
+    resolve the same key; scope("") is the root scope (the key prefix is "")."""
+    from pkg.modelling.hip_ops import Workspace
+    from pkg.modelling.models.two_tower_model import TwoTowerModel
+
+    assert Workspace._scope == ""
+    with Workspace.scope(""):
+        assert Workspace._scope == ""
+    with Workspace.scope("tower_c"):
+        assert Workspace._scope == "tower_c/"
+        with Workspace.scope(""):
+            assert Workspace._scope == ""
+        assert Workspace._scope == "tower_c/"
+    assert Workspace._scope == ""
+    assert TwoTowerModel.fused_optimizer_apply is False  # opt-in until measured on the GPU
