@@ -346,11 +346,18 @@ def time_index(device, n_queries: int, n_cand: int, k: int, E: int = 128, check:
             from oracle import oracle
 
             sel = np.linspace(0, n_queries - 1, check).astype(np.int64)
-            _, ri, _ = oracle.bruteforce_topk(Q[sel].cpu().numpy(), C.cpu().numpy(), k)
+            qs, cs = Q[sel].cpu().numpy(), C.cpu().numpy()
+            t0 = time.perf_counter()
+            _, ri, used = oracle.bruteforce_topk(qs, cs, k)
+            t_cpu = time.perf_counter() - t0
             gi = i[sel].cpu().numpy()
             res["exact_match_rows"] = int((gi == ri).all(axis=1).sum())
             res["checked_rows"] = int(check)
             res["recall_at_100_vs_exact"] = float(np.mean([len(set(a) & set(b)) / k for a, b in zip(gi, ri)]))
+            # the same exact search on the host: the C restatement (fp32 fmaf chain + top-k)
+            res["cpu_baseline"] = {"value": check / t_cpu, "unit": "queries/s", "cores": int(used), "kind": "port",
+                                   "sample": f"{check} of the queries x {n_cand} candidates, top-{k}, "
+                                             f"oracle/tt_oracle.c (fp32 fmaf chain), {t_cpu:.1f}s"}
         except Exception as e:  # the check is informative only
             res["check_error"] = repr(e)
     return res
@@ -493,10 +500,10 @@ def cpu_baseline(seconds_budget: float = 20.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=16384)
-    ap.add_argument("--index-queries", type=int, default=262144)
+    ap.add_argument("--index-queries", type=int, default=1_000_000)
     ap.add_argument("--no-index", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)

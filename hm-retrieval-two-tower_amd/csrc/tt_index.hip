@@ -9,9 +9,12 @@
 // and the returned scores are those fp32 values.
 //
 // Screening bound.  A bf16 MFMA score s~ differs from the exact chain s by at
-// most M_q = eps * |q| * max_c |c| with eps = 2^-8 + 2^-14 (bf16 rounding of
-// both operands 2^-8 + 2^-18, fp32 accumulation of 128 products and the exact
-// chain's own rounding each below 2^-16).  If tau is a lower bound of the
+// most M_q = eps * |q| * max_c |c| with eps = 2^-7 + 2^-14: bf16 has 8
+// significant bits, so round-to-nearest moves each operand by at most 2^-8 of
+// itself and a product of two rounded operands by at most 2^-7 + 2^-16
+// (summed over k: <= (2^-7 + 2^-16) sum_k |q_k c_k| <= ... |q| |c|); fp32
+// accumulation of <= 128 exact bf16 products and the exact chain's own
+// rounding add below 2^-17 each.  If tau is a lower bound of the
 // K-th largest screened score, every member of the exact top-K has
 // s~ >= tau - 2 M_q, so "s~ > next_down(tau - 2 M_q)" loses nothing.
 //
@@ -75,7 +78,7 @@ constexpr int kBinsMaxK = 2 * kBins;               // bins path serves k <= 128
 #endif
 constexpr int kLaneCap = TT_LANE_CAP;              // entries per (query, split, lane half)
 constexpr int kMaxSplits = 8;
-constexpr float kScreenEps = 0.00396728515625f;    // 2^-8 + 2^-14
+constexpr float kScreenEps = 0.00787353515625f;    // 2^-7 + 2^-14
 constexpr int64_t kMaxChunk = 65536;               // queries per screening pass
 #ifndef TT_SHORTLIST_BUDGET
 #define TT_SHORTLIST_BUDGET (size_t(1) << 30)

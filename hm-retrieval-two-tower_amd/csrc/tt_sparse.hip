@@ -54,6 +54,21 @@ constexpr int kPFJoin = 32;           // pieces loaded per batch in join
 constexpr int64_t kMaxLookups = int64_t(1) << 24;
 constexpr int kSrcShift = 28;  // sorted values: source << 28 | batch row (batch < 2^28)
 
+// Workspace header (first 256 B of every sparse workspace).  The sort stage
+// stamps the fingerprint of the lookups it sorted; the block / join passes
+// compare it with their own call's before touching a table, and record a
+// mismatch (a presorted apply on another call's keys) or an out-of-call
+// (source, row) in `error` instead of applying anything from that block.
+// tt_sparse_status() reads and clears `error`.
+constexpr uint32_t kHdrMagic = 0x54545350u;  // "TTSP"
+constexpr int kHdrBytes = 256;
+enum : uint32_t { kErrStaleKeys = 1u, kErrOutOfCall = 2u };
+struct SparseHeader {
+  uint32_t magic;
+  uint32_t error;
+  uint32_t fp0, fp1;  // fingerprint of the sorted call
+};
+
 struct TableDesc {
   const int32_t* ids[TT_MAX_SOURCES];
   int32_t goff[TT_MAX_SOURCES];  // source column offsets in the table's grad
@@ -85,7 +100,20 @@ struct Job {
   float* pieces;
   float* dense_out;      // kWriteSum: per-sorted-index segment sums [total][dim_max]
   int32_t dense_dim;
+  SparseHeader* hdr;     // workspace header
+  uint32_t fp0, fp1;     // this call's fingerprint
 };
+
+// The apply passes' guard: the sorted keys must be this call's.  Wave-uniform.
+__device__ __forceinline__ bool keys_are_mine(const Job& j) {
+  const uint32_t f0 = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&j.hdr->fp0, __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_AGENT));
+  const uint32_t f1 = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&j.hdr->fp1, __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_AGENT));
+  if (f0 == j.fp0 && f1 == j.fp1) return true;
+  if (lane_id() == 0) atomicOr(&j.hdr->error, kErrStaleKeys);
+  return false;
+}
 
 enum ApplyOp { kWriteSum = 0, kAdagrad = 1, kAdamScatter = 2, kScatterSum = 3 };
 
@@ -127,6 +155,14 @@ __global__ void __launch_bounds__(kThreads) build_keys_kernel(const Job j, int t
   }
   j.keys_in[i] = (static_cast<uint32_t>(t) << j.id_bits) | id;
   j.vals_in[i] = val;
+  if (i == 0) {  // stamp the workspace with this call's fingerprint
+    if (j.hdr->magic != kHdrMagic) {  // fresh workspace: no recorded error yet
+      j.hdr->error = 0u;
+      j.hdr->magic = kHdrMagic;
+    }
+    j.hdr->fp0 = j.fp0;
+    j.hdr->fp1 = j.fp1;
+  }
 }
 
 // The optimizer update of one distinct row, split into a load phase and a
@@ -187,6 +223,7 @@ __global__ void __launch_bounds__(kThreads) block_sum_kernel(const Job j, const 
   const int lane = lane_id();
   const int blk = (gw - T.wave_begin) * (kWave / P) + lane / P;
   const int nblk = T.n_pad / kBlock;
+  if (!keys_are_mine(j)) return;
   if (blk >= nblk) return;
   const int b0 = T.base + blk * kBlock;   // first sorted index of the block
   const int tend = T.base + T.n_pad;      // end of the table's region
@@ -207,16 +244,22 @@ __global__ void __launch_bounds__(kThreads) block_sum_kernel(const Job j, const 
   const uint32_t go0 = T.goff[0], go1 = T.goff[1], go2 = T.goff[2], go3 = T.goff[3];
   const float* __restrict__ grad = T.grad;
   uint32_t ends = 0, apply = 0;
+  bool out_of_call = false;
 #pragma unroll
   for (int r = 0; r < kBlock; ++r) {
     const uint32_t s = off[r] >> kSrcShift;
     const uint32_t b = off[r] & ((1u << kSrcShift) - 1u);
     const uint32_t o = b * gld + (s == 0 ? go0 : s == 1 ? go1 : s == 2 ? go2 : go3);
-    // a (source, row) outside this call's gradient (stale presorted workspace)
-    // never reaches memory: it reads as padding
+    // a (source, row) outside this call's gradient can only come from keys
+    // that are not this call's: reported, and the block applies nothing
     const bool in = s < static_cast<uint32_t>(T.num_sources) && b < static_cast<uint32_t>(j.batch);
+    out_of_call = out_of_call || (off[r] != 0xFFFFFFFFu && !in);
     off[r] = (off[r] != 0xFFFFFFFFu && in) ? o : 0xFFFFFFFFu;
     if (r == kBlock - 1 || key[r + 1] != key[r]) ends |= 1u << r;
+  }
+  if (out_of_call) {
+    atomicOr(&j.hdr->error, kErrOutOfCall);
+    return;
   }
   const bool head_cont = key[0] == kprev;
   const bool tail_cont = key[kBlock - 1] == knext;
@@ -282,6 +325,7 @@ __global__ void __launch_bounds__(kThreads) join_kernel(const Job j, const Apply
   const int lane = lane_id();
   const int blk = (gw - T.wave_begin) * (kWave / P) + lane / P;
   const int nblk = T.n_pad / kBlock;
+  if (!keys_are_mine(j)) return;
   if (blk >= nblk) return;
   const int b0 = T.base + blk * kBlock;
   const int tend = T.base + T.n_pad;
@@ -442,6 +486,27 @@ int make_plan(const tt_sparse_table* tables, int cnt, int64_t batch, const float
   p->total = base;
   p->waves = waves;
   p->piece_floats = poff;
+  // fingerprint of what the sort stage sorts (ids, tables, batch): two
+  // independent 32-bit FNV-1a hashes
+  uint32_t h0 = 2166136261u, h1 = 0x9747b28cu;
+  auto mix = [&](uint64_t v) {
+    for (int b = 0; b < 8; ++b) {
+      const uint32_t byte = static_cast<uint32_t>(v >> (8 * b)) & 0xFFu;
+      h0 = (h0 ^ byte) * 16777619u;
+      h1 = (h1 ^ (byte + 0x5bu)) * 0x01000193u + 0x3c6ef372u;
+    }
+  };
+  mix(static_cast<uint64_t>(batch));
+  mix(static_cast<uint64_t>(cnt));
+  for (int i = 0; i < cnt; ++i) {
+    const tt_sparse_table& s = tables[i];
+    mix(reinterpret_cast<uintptr_t>(s.table));
+    mix(static_cast<uint64_t>(s.num_rows));
+    mix((static_cast<uint64_t>(s.dim) << 32) | static_cast<uint32_t>(s.num_sources));
+    for (int q = 0; q < s.num_sources; ++q) mix(reinterpret_cast<uintptr_t>(s.ids[q]));
+  }
+  j.fp0 = h0;
+  j.fp1 = h1;
   size_t sb = 0;
   uint32_t* np = nullptr;
   hipError_t e = rocprim::radix_sort_pairs(nullptr, sb, np, np, np, np, static_cast<unsigned>(base), 0, p->end_bit,
@@ -454,6 +519,7 @@ int make_plan(const tt_sparse_table* tables, int cnt, int64_t batch, const float
 
 // Workspace carve for one plan (also used for the size query with base=null).
 struct PlanWs {
+  SparseHeader* hdr;
   uint32_t *keys_in, *vals_in, *keys, *vals;
   float* pieces;
   float* dense_out;
@@ -461,6 +527,7 @@ struct PlanWs {
 };
 PlanWs carve_plan(Carver& cv, const Plan& p, int dense_dim) {
   PlanWs w;
+  w.hdr = reinterpret_cast<SparseHeader*>(cv.take<char>(kHdrBytes));  // always at offset 0
   w.keys_in = cv.take<uint32_t>(p.total);
   w.vals_in = cv.take<uint32_t>(p.total);
   w.keys = cv.take<uint32_t>(p.total);
@@ -535,6 +602,7 @@ int run_sparse(const tt_sparse_table* tables, int32_t num_tables, int64_t batch,
     j.pieces = w.pieces;
     j.dense_out = w.dense_out;
     j.dense_dim = dense_dim;
+    j.hdr = w.hdr;
     if (stage != kStageApply) {
       hipLaunchKernelGGL(build_keys_kernel, dim3(ceil_div(p.total, kThreads)), dim3(kThreads), 0, st, j, p.total);
       TT_CHECK_LAUNCH();
@@ -721,6 +789,23 @@ extern "C" int tt_dedup_sum(const int32_t* ids, int64_t n, int64_t num_rows, con
   ApplyParams ap{};
   return run_sparse<kWriteSum>(&t, 1, n, grad, grad_stride, ap, workspace, workspace_bytes, to_stream(stream),
                                unique_ids, summed, num_unique);
+}
+
+extern "C" int tt_sparse_status(void* workspace, size_t workspace_bytes, tt_stream_t stream) {
+  clear_error();
+  TT_REQUIRE(workspace && workspace_bytes >= static_cast<size_t>(kHdrBytes), "tt_sparse_status: no workspace");
+  hipStream_t st = to_stream(stream);
+  SparseHeader h{};
+  TT_CHECK_HIP(hipMemcpyAsync(&h, workspace, sizeof(h), hipMemcpyDeviceToHost, st));
+  TT_CHECK_HIP(hipStreamSynchronize(st));
+  if (h.magic != kHdrMagic || h.error == 0u) return TT_OK;
+  const uint32_t zero = 0u;
+  TT_CHECK_HIP(hipMemcpyAsync(static_cast<char*>(workspace) + offsetof(SparseHeader, error), &zero, sizeof(zero),
+                              hipMemcpyHostToDevice, st));
+  TT_CHECK_HIP(hipStreamSynchronize(st));
+  return fail(TT_ERR_BAD_ARG, "sparse: %s%s(error word 0x%x); those blocks applied nothing",
+              (h.error & kErrStaleKeys) ? "an apply found sorted keys of another call (stale presorted workspace) " : "",
+              (h.error & kErrOutOfCall) ? "a sorted lookup pointed outside the call's gradient " : "", h.error);
 }
 
 extern "C" int tt_dense_adagrad(float* param, float* accum, const float* grad, int64_t n, float lr,

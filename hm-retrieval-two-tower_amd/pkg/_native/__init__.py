@@ -128,6 +128,7 @@ _PROTOS = {
     "tt_sparse_adagrad_sorted": (
         c_int32,
         [POINTER(SparseTable), c_int32, c_int64, c_void_p, c_int64, c_float, c_float, c_void_p, c_size_t, c_void_p]),
+    "tt_sparse_status": (c_int32, [c_void_p, c_size_t, c_void_p]),
     "tt_route_workspace_size": (c_size_t, [c_int32, c_int64, c_int32, c_int64, c_int32]),
     "tt_route_requests": (
         c_int32,

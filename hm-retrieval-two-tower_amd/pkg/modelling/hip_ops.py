@@ -25,6 +25,7 @@ __all__ = [
     "gather_grouped",
     "sparse_adagrad",
     "sparse_sort",
+    "sparse_status",
     "sparse_adam",
     "dedup_sum",
     "dense_adagrad",
@@ -82,9 +83,17 @@ class Workspace:
         key = (device.index if device.index is not None else torch.cuda.current_device(), cls._scope + tag)
         buf = cls._bufs.get(key)
         if buf is None or buf.numel() < nbytes:
-            buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+            # zeroed once (a fresh sparse workspace carries no recorded error)
+            buf = torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=device)
             cls._bufs[key] = buf
         return buf
+
+    @classmethod
+    def existing(cls, device: torch.device, tag: str, scope: Optional[str] = None) -> Optional[torch.Tensor]:
+        """The buffer of (device, scope, tag) if it was ever allocated."""
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        pre = cls._scope if scope is None else (scope + "/" if scope else "")
+        return cls._bufs.get((idx, pre + tag))
 
     @classmethod
     def clear(cls) -> None:
@@ -226,6 +235,16 @@ def sparse_adagrad(tables: Sequence[dict], batch: int, grad: Optional[torch.Tens
     fn = L.tt_sparse_adagrad_sorted if presorted else L.tt_sparse_adagrad
     check(fn(arr, len(tables), batch, grad.data_ptr() if grad is not None else None, ld, lr, epsilon,
              ws.data_ptr(), ws.numel(), _stream()))
+
+
+def sparse_status(device: torch.device, ws_tag: str = "sparse", scope: Optional[str] = None) -> None:
+    """Raise TTError if a sparse apply on this workspace recorded an error
+    (keys of another call, tt_sparse_status) since the last check.  Synchronises
+    the current stream."""
+    ws = Workspace.existing(device, ws_tag, scope)
+    if ws is None:
+        return
+    check(lib().tt_sparse_status(ws.data_ptr(), ws.numel(), _stream()))
 
 
 def sparse_sort(tables: Sequence[dict], batch: int) -> None:

@@ -17,7 +17,7 @@ import torch
 
 from pkg.modelling import hip_ops
 
-__all__ = ["InBatchSoftmaxCrossEntropy", "inbatch_softmax_xent", "towers_inbatch_softmax_xent"]
+__all__ = ["InBatchSoftmaxCrossEntropy", "inbatch_softmax_xent", "towers_inbatch_softmax_xent", "TOWER_C_SCOPE"]
 
 
 class _InBatchXent(torch.autograd.Function):
@@ -36,6 +36,10 @@ class _InBatchXent(torch.autograd.Function):
 
 
 _SIDE: dict = {}
+
+# Workspace scope of the candidate tower's work on its own stream (the fused
+# train step sorts and applies that tower's embedding update in this scope).
+TOWER_C_SCOPE = "tower_c"
 
 
 def _tower_stream(device: torch.device) -> torch.cuda.Stream:
@@ -61,7 +65,7 @@ class _TowersInBatchXent(torch.autograd.Function):
         main = torch.cuda.current_stream()
         side = _tower_stream(qi.device)
         side.wait_stream(main)
-        with torch.cuda.stream(side), hip_ops.Workspace.scope("tower_c"):
+        with torch.cuda.stream(side), hip_ops.Workspace.scope(TOWER_C_SCOPE):
             ca = stack_c.forward_acts(ci, flat_c)
         qa = stack_q.forward_acts(qi, flat_q)
         main.wait_stream(side)
@@ -82,7 +86,7 @@ class _TowersInBatchXent(torch.autograd.Function):
         main = torch.cuda.current_stream()
         side = _tower_stream(dq.device)
         side.wait_stream(main)
-        with torch.cuda.stream(side), hip_ops.Workspace.scope("tower_c"):
+        with torch.cuda.stream(side), hip_ops.Workspace.scope(TOWER_C_SCOPE):
             gci, gflat_c = stack_c.backward_acts(ca, flat_c, dc, s, ctx.needs_input_grad[1])
             if ctx.on_tower is not None:  # this tower's updates, beside the other tower's backward
                 ctx.on_tower(1, gci, gflat_c)

@@ -22,7 +22,7 @@ from pkg.schema.features import Feature
 from pkg.schema.schema import Schema
 from pkg.modelling.device import default_device, make_generator
 from pkg.modelling.layers.logq_correction import LogQCorrection
-from pkg.modelling.losses import InBatchSoftmaxCrossEntropy, towers_inbatch_softmax_xent
+from pkg.modelling.losses import TOWER_C_SCOPE, InBatchSoftmaxCrossEntropy, towers_inbatch_softmax_xent
 from pkg.modelling.models.abstract_keras_model import AbstractKerasModel, TensorSpec
 from pkg.modelling import hip_ops
 from pkg.modelling.layers.input_layer import InputLayer
@@ -59,14 +59,14 @@ class TwoTowerModel(AbstractKerasModel):
         If provided, logQ correction is applied before the loss.
     """
 
-    # apply each tower's Adagrad step inside the backward (see train_step)
-    fused_optimizer_apply: bool = False
-
     def __init__(self, query_features: List[Feature], candidate_features: List[Feature], candidate_id_col: str,
                  joint_embedding_size: int, query_tower_units: Optional[List[int]] = None,
                  candidate_tower_units: Optional[List[int]] = None,
                  candidate_prob_lookup: Optional[Dict[str, float]] = None,
-                 device: Optional[torch.device] = None, seed: Optional[int] = None):
+                 device: Optional[torch.device] = None, seed: Optional[int] = None,
+                 fused_optimizer_apply: bool = False):
+        # apply each tower's Adagrad step inside the backward (see train_step)
+        self.fused_optimizer_apply = bool(fused_optimizer_apply)
         self.query_features = query_features
         self.candidate_features = candidate_features
         if candidate_id_col not in [f.name for f in candidate_features]:
@@ -169,7 +169,7 @@ class TwoTowerModel(AbstractKerasModel):
         inside the backward, the moment that tower's gradients exist (the
         candidate tower's beside the query tower's backward); the updates are
         the same as applying them afterwards (each table and MLP buffer is
-        touched by one tower only).  Not yet measured on the GPU, hence off."""
+        touched by one tower only; tests/test_model_gpu.py checks bit-identity)."""
         from pkg.modelling.optimizer_factory import Adagrad
 
         if self.optimizer is None:
@@ -183,7 +183,7 @@ class TwoTowerModel(AbstractKerasModel):
         fwd_done = None
         if fused:
             # one id sort per tower on a side stream, before the backward needs it
-            self.optimizer.prepare_towers(self.towers, ["", "tower_c"])
+            self.optimizer.prepare_towers(self.towers, ["", TOWER_C_SCOPE])
         elif hasattr(self.optimizer, "prepare") and loss.is_cuda:
             fwd_done = torch.cuda.Event()
             fwd_done.record()
@@ -194,6 +194,10 @@ class TwoTowerModel(AbstractKerasModel):
         loss.backward(self._one)  # a persistent seed: no ones-fill launch per step
         if fused:
             self.optimizer.iterations += 1
+            # the update is applied: a later apply_gradients must not apply it again
+            for t in self.towers:
+                t.dense.flat.grad = None
+                t.input_layer.last_grad = None
         else:
             if fwd_done is not None:
                 # the embedding update's id sort needs only the forward's ids; issued

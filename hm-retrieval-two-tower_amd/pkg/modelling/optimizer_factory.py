@@ -116,19 +116,21 @@ class Adagrad(_Optimizer):
         flat = tower.dense.flat
         (acc,) = self._slot(flat, 1, init)
         hip_ops.dense_adagrad(flat.data, acc, flat_grad, lr, eps)
+        prep = getattr(self, "_tower_prep", {}).pop(id(tower), None)
         if input_grad is None:
             return
         specs, batch = self._sparse_specs([tower], with_grad=True, grad=input_grad)
-        prep = self._tower_prep.pop(id(tower), None) if hasattr(self, "_tower_prep") else None
         if not specs:
             return
-        if prep is not None:
-            torch.cuda.current_stream().wait_event(prep[2])
-        if (prep is not None and prep[0] == [id(s["table"]) for s in specs] and prep[1] == batch
-                and prep[3] == hip_ops.Workspace._scope):
-            hip_ops.sparse_adagrad(specs, batch, None, lr, eps, presorted=True)
-        else:
+        if prep is None:  # prepare_towers skipped this tower: sort here
             hip_ops.sparse_adagrad(specs, batch, None, lr, eps)
+            return
+        torch.cuda.current_stream().wait_event(prep[2])
+        if (prep[0] != [id(s["table"]) for s in specs] or prep[1] != batch
+                or prep[3] != hip_ops.Workspace._scope):
+            raise RuntimeError(f"apply_tower: presorted state {prep[0]}/{prep[1]}/{prep[3]!r} does not match "
+                               f"this apply ({[id(s['table']) for s in specs]}/{batch}/{hip_ops.Workspace._scope!r})")
+        hip_ops.sparse_adagrad(specs, batch, None, lr, eps, presorted=True)
 
     def prepare(self, towers, after: Optional[torch.cuda.Event] = None) -> None:
         """Start the embedding update's id sort early, on a side stream (it reads
@@ -170,10 +172,25 @@ class Adagrad(_Optimizer):
         if specs:
             # every tower's tables in ONE call: one sort, one block pass (each
             # table reads its own tower's input gradient)
-            if prepared is not None and prepared[0] == [id(s["table"]) for s in specs] and prepared[1] == batch:
+            if prepared is None:
+                hip_ops.sparse_adagrad(specs, batch, None, lr, eps)
+            elif prepared[0] == [id(s["table"]) for s in specs] and prepared[1] == batch:
                 hip_ops.sparse_adagrad(specs, batch, None, lr, eps, presorted=True)
             else:
-                hip_ops.sparse_adagrad(specs, batch, None, lr, eps)
+                raise RuntimeError(f"apply_gradients: presorted state {prepared[0]}/{prepared[1]} does not match "
+                                   f"this apply ({[id(s['table']) for s in specs]}/{batch})")
+
+    def check_status(self, device: Optional[torch.device] = None) -> None:
+        """Raise if any sparse apply since the last check found keys that were
+        not its call's (libtt records it on the device instead of applying;
+        tt_sparse_status).  Synchronises the current stream."""
+        from pkg.modelling.losses import TOWER_C_SCOPE
+
+        if not torch.cuda.is_available():
+            return
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        for scope in ("", TOWER_C_SCOPE):
+            hip_ops.sparse_status(dev, "sparse", scope)
 
 
 class Adam(_Optimizer):

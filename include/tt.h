@@ -193,6 +193,17 @@ int tt_sparse_adagrad_sorted(const tt_sparse_table* tables, int32_t num_tables,
                              float lr, float epsilon, void* workspace,
                              size_t workspace_bytes, tt_stream_t stream);
 
+/* The sparse calls never fault on a mismatched workspace: the sort stage
+ * stamps the first 256 bytes of the workspace with a fingerprint of the
+ * lookups it sorted, and the apply passes (of every sparse entry point above
+ * and below) check it before touching a table.  A presorted apply that finds
+ * another call's keys (or a sorted lookup pointing outside the call's
+ * gradient) applies nothing from the affected blocks and records the error
+ * in the header.  tt_sparse_status synchronises `stream`, returns
+ * TT_ERR_BAD_ARG (message in tt_last_error) if an error was recorded since
+ * the last check, and clears it.  A fresh workspace should start zeroed. */
+int tt_sparse_status(void* workspace, size_t workspace_bytes, tt_stream_t stream);
+
 /* Legacy Keras Adam sparse path: m,v decayed over the WHOLE slot, the scaled
  * duplicate-summed gradient scatter-added, then the WHOLE table updated with
  * lr_t = lr*sqrt(1-beta2^step)/(1-beta1^step) (step is 1-based). */

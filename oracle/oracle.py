@@ -163,6 +163,27 @@ def inbatch_softmax_xent(q: np.ndarray, c: np.ndarray, logq: Optional[np.ndarray
     }
 
 
+# bf16 operands (8 significant bits, round to nearest): unit roundoff 2^-8 per
+# operand, so a product of two rounded operands is within 2^-7 + 2^-16 of the
+# exact one; fp32 accumulation of <= 128 exact bf16 products adds < 2^-17.
+BF16_DOT_EPS = 2.0 ** -7 + 2.0 ** -15
+
+
+def inbatch_error_bound(q: np.ndarray, c: np.ndarray, pos_offset: int = 0) -> Dict[str, np.ndarray]:
+    """Certified bound of the fused bf16-MFMA loss against the exact one.
+
+    Each score S'_ij is computed from bf16(q_i) . bf16(c_j):
+      |S~_ij - S_ij| <= d_ij = BF16_DOT_EPS * sum_k |q_ik| |c_jk|.
+    lse is a softmax-weighted mean of the perturbations, so
+      |lse~_i - lse_i| <= max_j d_ij  (+ fp32 softmax arithmetic, ~1e-5 |lse|),
+    and the positive logit is an fp32 dot product, so the row loss has the
+    same bound and the batch loss at most the sum of the rows'.
+    Returns dict(lse=[R], loss=float)."""
+    A = np.abs(np.asarray(q, np.float64)) @ np.abs(np.asarray(c, np.float64)).T
+    row = BF16_DOT_EPS * A.max(axis=1)
+    return {"lse": row, "loss": float(row.sum())}
+
+
 # ---------------------------------------------------------------------------
 # a3/a4: dedup + sparse Adagrad (legacy Keras optimizer; see tt_oracle.c)
 def dedup_sum(ids: np.ndarray, grad: np.ndarray, chunk: int = 0) -> Tuple[np.ndarray, np.ndarray]:

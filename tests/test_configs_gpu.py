@@ -1,0 +1,170 @@
+"""GPU: the BASELINE.json configurations at their own sizes, against the CPU
+restatement (oracle/).
+
+- C2: H&M vocabularies, emb 64, towers [256] -> 64, batch 4096: three full
+  train steps (gather, towers, fused in-batch CE, MLP backward, dense +
+  sparse Adagrad) vs oracle.CpuTwoTower: loss within 1e-3 rel every step,
+  first-step update of every table and MLP buffer within 1e-2 rel;
+- C4: 105,542 x 128 candidates, top-100 (and the reference runner's k = 1000
+  at test_batch_size 2048, /root/reference/main.py:99,107): indices and
+  scores bit-exact vs the fp32 fmaf-chain oracle;
+- C5: a 100M x 128 fp32 table (51.2 GB + 51.2 GB accumulator) through
+  ShardedTables at world 1 (RCCL): fetched rows bit-exact, the touched rows
+  after one Adagrad apply bit-exact vs oracle.sparse_adagrad.
+"""
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+import bench
+from oracle import oracle
+from pkg.modelling.models.two_tower_model import TwoTowerModel
+from pkg.modelling.optimizer_factory import OptimizerFactory
+
+pytestmark = pytest.mark.gpu
+
+
+def _mirror(m):
+    """oracle.CpuTwoTower with the model's current weights; one table object per
+    distinct feature name (main.py declares product_type_name twice)."""
+    def tables(layer):
+        by_name = {}
+        for f in layer.categorical_features:
+            if f.name not in by_name:
+                by_name[f.name] = layer.embedding_layers[f.name].weight.cpu().numpy().copy()
+        return [by_name[f.name] for f in layer.categorical_features]
+
+    def dense(t):
+        return [(w.detach().cpu().numpy(), b.detach().cpu().numpy()) for w, b in t.dense.params()]
+
+    ref = oracle.CpuTwoTower(tables(m.query_tower.input_layer), tables(m.candidate_tower.input_layer),
+                             dense(m.query_tower), dense(m.candidate_tower), 0.05)
+    for tabs, accs in ((ref.q_tables, ref.q_acc), (ref.c_tables, ref.c_acc)):
+        first = {}
+        for i, t in enumerate(tabs):  # shared table -> shared accumulator
+            j = first.setdefault(id(t), i)
+            accs[i] = accs[j]
+    return ref
+
+
+def test_c2_train_steps_match_cpu_restatement(cuda):
+    schema = bench.main_schema(emb_big=64, joint=64, hidden=(256,))
+    data = bench.SyntheticHM(cuda, seed=7)
+    schema.set_candidate_prob_lookup(data.prob_lookup())
+    m = TwoTowerModel.create_from_schema(schema, "article_id", device=cuda, seed=0)
+    m.compile(optimizer=OptimizerFactory.get_optimizer("adagrad", {"learning_rate": 0.05}))
+    ref = _mirror(m)
+    qf = m.query_tower.input_layer.categorical_features
+    cf = m.candidate_tower.input_layer.categorical_features
+    B = 4096
+
+    def touched(layer, batch):
+        out = {}
+        for f in layer.categorical_features:
+            ids = np.unique(batch[f.name].cpu().numpy())
+            out.setdefault(f.name, set()).update(ids.tolist())
+        return {k: np.array(sorted(v)) for k, v in out.items()}
+
+    for step in range(3):
+        b = data.batch(B)
+        lq = m.candidate_logq(b).cpu().numpy()
+        rows = {**touched(m.query_tower.input_layer, b), **touched(m.candidate_tower.input_layer, b)}
+        before = {n: layer.embedding_layers[n].weight[torch.as_tensor(rows[n], device=cuda).long()].cpu().numpy()
+                  for layer in (m.query_tower.input_layer, m.candidate_tower.input_layer)
+                  for n in layer.embedding_layers}
+        mlp_before = [t.dense.flat.detach().cpu().numpy().copy() for t in m.towers]
+        rl = ref.step([b[f.name].cpu().numpy() for f in qf], [b[f.name].cpu().numpy() for f in cf], lq)
+        gl = float(m.train_step(b)["loss"].item())
+        assert abs(gl - rl) <= 1e-3 * abs(rl), (step, gl, rl)
+        if step == 0:
+            refs = {}
+            for feats, tabs in ((qf, ref.q_tables), (cf, ref.c_tables)):
+                for f, t in zip(feats, tabs):
+                    refs[f.name] = t
+            for layer in (m.query_tower.input_layer, m.candidate_tower.input_layer):
+                for n, tab in layer.embedding_layers.items():
+                    r = rows[n]
+                    got = tab.weight[torch.as_tensor(r, device=cuda).long()].cpu().numpy()
+                    d_gpu, d_ref = got - before[n], refs[n][r] - before[n]
+                    assert np.linalg.norm(d_gpu - d_ref) <= 1e-2 * np.linalg.norm(d_ref), n
+            flat = lambda layers: np.concatenate([np.concatenate([w.reshape(-1), bb]) for w, bb in layers])
+            for t, mb, rlay in zip(m.towers, mlp_before, (ref.q_layers, ref.c_layers)):
+                d_gpu = t.dense.flat.detach().cpu().numpy() - mb
+                d_ref = flat(rlay) - mb
+                assert np.linalg.norm(d_gpu - d_ref) <= 1e-2 * np.linalg.norm(d_ref)
+    m.optimizer.check_status(cuda)
+
+
+def _c4_data(cuda, Q, seed=2):
+    g = torch.Generator(device=cuda)
+    g.manual_seed(1)
+    C = torch.relu(torch.randn(bench.HM_VOCAB["article_id"], 128, generator=g, device=cuda))
+    g.manual_seed(seed)
+    Qm = torch.relu(torch.randn(Q, 128, generator=g, device=cuda))
+    Qm[::100] = 0.0  # all-zero queries: every score ties at 0 -> lowest indices
+    return C, Qm
+
+
+@pytest.mark.parametrize("Q,k", [(2048, 100), (512, 1000)])
+def test_c4_index_full_candidates_bitexact(cuda, Q, k):
+    """configs[3] candidate count (105,542 x 128, relu data, 1 % zero queries)."""
+    from pkg.modelling import hip_ops
+
+    C, Qm = _c4_data(cuda, Q)
+    image = hip_ops.bruteforce_build(C)
+    s, i = hip_ops.bruteforce_search(image, C, Qm, k)
+    rs, ri, _ = oracle.bruteforce_topk(Qm.cpu().numpy(), C.cpu().numpy(), k)
+    assert np.array_equal(i.cpu().numpy(), ri)
+    assert np.array_equal(s.cpu().numpy(), rs)
+
+
+def test_c5_100m_row_table_world1(cuda):
+    """A 100M x 128 table (BASELINE configs[4]) through ShardedTables at world
+    1: fetch = the exact rows; one apply = oracle Adagrad on the touched rows
+    (bit-exact, same block summation order), untouched rows unchanged."""
+    import torch.distributed as dist
+
+    from pkg.modelling.distributed import ShardedTables
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device(cuda))
+    try:
+        V, D, B = 100_000_000, 128, 65536
+        g = torch.Generator(device=cuda)
+        g.manual_seed(5)
+        table = torch.empty(V, D, device=cuda).uniform_(-0.05, 0.05, generator=g)
+        st = ShardedTables({"big": table, "__rows__": {"big": V}}, full_tables=False)
+        del table
+        rng = np.random.default_rng(3)
+        ids_np = (((rng.zipf(1.8, B) - 1) % V) * 7919 % V).astype(np.int32)  # Zipf-like, spread over the table
+        ids_np[:1000] = rng.integers(0, V, 1000)  # plus uniform ids
+        ids = torch.as_tensor(ids_np, device=cuda)
+        rows, (idx,) = st.fetch([("big", ids)])
+        uniq = np.unique(ids_np)
+        ut = torch.as_tensor(uniq, device=cuda).long()
+        ref_rows = st.shard["big"][ut].cpu().numpy()
+        got = rows[idx.long()].cpu().numpy()
+        pos = np.searchsorted(uniq, ids_np)
+        assert np.array_equal(got, ref_rows[pos])
+        grad = torch.as_tensor(rng.standard_normal((B, D)).astype(np.float32), device=cuda)
+        before_untouched = st.shard["big"][:64].clone()
+        st.apply([(grad, [(idx, 0)])], 0.05, 1e-7)
+        torch.cuda.synchronize()
+        # oracle on the compacted touched rows (monotonic remap keeps the sort order)
+        t_ref = ref_rows.copy()
+        a_ref = np.full_like(t_ref, 0.1)
+        oracle.sparse_adagrad(t_ref, a_ref, pos.astype(np.int32), grad.cpu().numpy(), 0.05)
+        assert np.array_equal(st.shard["big"][ut].cpu().numpy(), t_ref)
+        assert np.array_equal(st.acc["big"][ut].cpu().numpy(), a_ref)
+        mask = ~np.isin(np.arange(64), uniq)
+        assert torch.equal(st.shard["big"][:64][torch.as_tensor(mask, device=cuda)],
+                           before_untouched[torch.as_tensor(mask, device=cuda)])
+    finally:
+        dist.destroy_process_group()
+        torch.cuda.empty_cache()

@@ -185,15 +185,14 @@ def test_workspace_scopes_nest_and_empty_scope_is_root():
     """A sort issued under scope(s) and the apply that reads its buffer must
     resolve the same key; scope("") is the root scope (the key prefix is "")."""
     from pkg.modelling.hip_ops import Workspace
-    from pkg.modelling.models.two_tower_model import TwoTowerModel
+    from pkg.modelling.losses import TOWER_C_SCOPE
 
     assert Workspace._scope == ""
     with Workspace.scope(""):
         assert Workspace._scope == ""
-    with Workspace.scope("tower_c"):
-        assert Workspace._scope == "tower_c/"
+    with Workspace.scope(TOWER_C_SCOPE):
+        assert Workspace._scope == TOWER_C_SCOPE + "/"
         with Workspace.scope(""):
             assert Workspace._scope == ""
-        assert Workspace._scope == "tower_c/"
+        assert Workspace._scope == TOWER_C_SCOPE + "/"
     assert Workspace._scope == ""
-    assert TwoTowerModel.fused_optimizer_apply is False  # opt-in until measured on the GPU

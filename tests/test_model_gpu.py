@@ -9,8 +9,8 @@
 - the C3 shape (B=16384, E=128) in-batch passes against a torch fp64
   reference of the same op (row blocks);
 - modelling_runner end to end on a tiny encoded dataset.
-Tolerances: loss rel 2e-3; parameter-update rel 2e-2 (bf16 MFMA operands in
-the loss); index ids bit-exact.
+Tolerances: loss rel 1e-3 (north star); first-step parameter updates rel
+1e-2 (bf16 MFMA operands in the loss gradients); index ids bit-exact.
 """
 import json
 import os
@@ -75,7 +75,7 @@ def test_index_recall_with_gpu_index(cuda):
     assert all(isinstance(v, np.float64) for v in rec.metric.values())
 
 
-def _small_model(cuda, seed=0, logq=True):
+def _small_model(cuda, seed=0, logq=True, fused=False):
     V = [str(i) for i in range(300)]
     qf = [Feature("cust", dtypes.string, FeatureFamily.QUERY, embedding_size=16, vocab=V),
           Feature("post", dtypes.string, FeatureFamily.QUERY, embedding_size=8, vocab=V[:50])]
@@ -84,7 +84,7 @@ def _small_model(cuda, seed=0, logq=True):
           Feature("ptn", dtypes.string, FeatureFamily.CANDIDATE, embedding_size=4, vocab=V[:20])]
     rng = np.random.default_rng(seed)
     probs = {str(i): float(p) for i, p in enumerate(rng.dirichlet(np.ones(300)))} if logq else None
-    m = TwoTowerModel(qf, cf, "art", 32, [64], [64], probs, device=cuda, seed=seed)
+    m = TwoTowerModel(qf, cf, "art", 32, [64], [64], probs, device=cuda, seed=seed, fused_optimizer_apply=fused)
     m.compile(optimizer=OptimizerFactory.get_optimizer("adagrad", {"learning_rate": 0.05}))
     return m
 
@@ -118,7 +118,7 @@ def test_train_steps_match_cpu_restatement(cuda, zipf, backend, precision):
     """First step: every parameter update within 1e-2 rel of the fp32 CPU
     restatement (bf16 MFMA operands in the fused loss give ~1e-3 per-example
     gradient error, amplified where a batch-summed gradient cancels).  Then the
-    loss trajectory over 3 steps within 2e-3 rel (parameters themselves drift
+    loss trajectory over 3 steps within 1e-3 rel (parameters themselves drift
     apart: lr 0.05 on a 0.1 accumulator moves embeddings by about their own
     scale every step, so any rounding difference is amplified).  Both tower
     GEMM backends: hipBLASLt fp32 and libtt tt_gemm (bf16x3 and plain bf16)."""
@@ -150,7 +150,7 @@ def test_train_steps_match_cpu_restatement(cuda, zipf, backend, precision):
         rl = ref.step([b["cust"].cpu().numpy(), b["post"].cpu().numpy()],
                       [b["art"].cpu().numpy(), b["ptn"].cpu().numpy(), b["ptn"].cpu().numpy()], lq)
         gl = float(m.train_step(b)["loss"].item())
-        assert abs(gl - rl) <= 2e-3 * abs(rl), (step, gl, rl)
+        assert abs(gl - rl) <= 1e-3 * abs(rl), (step, gl, rl)
         if step == 0:
             after, r = snapshot(), ref_snapshot()
             for k in after:  # includes the shared ptn table (one combined update of both lookups)
@@ -168,7 +168,8 @@ def test_ragged_batch_train_step_matches_cpu_restatement(cuda, B):
     tfrecord_dataset.py:97 has no drop_remainder), including B = 1 (the loss
     of a one-column softmax is 0 in exact arithmetic; here lse comes from the
     bf16-MFMA score and the positive logit from the fp32 one, so it is 0 to
-    within the bf16 rounding of that score: atol 1e-4)."""
+    within the bf16 rounding of that score: atol 1e-4, far above the certified
+    bound of a score of this model's magnitude)."""
     m = _small_model(cuda, seed=B)
     ref = _cpu_mirror(m)
     rng = np.random.default_rng(B)
@@ -178,7 +179,79 @@ def test_ragged_batch_train_step_matches_cpu_restatement(cuda, B):
                   [b["art"].cpu().numpy(), b["ptn"].cpu().numpy(), b["ptn"].cpu().numpy()], lq)
     gl = float(m.train_step(b)["loss"].item())
     assert np.isfinite(gl)
-    assert abs(gl - rl) <= 2e-3 * abs(rl) + 1e-4, (gl, rl)
+    assert abs(gl - rl) <= 1e-3 * abs(rl) + 1e-4, (gl, rl)
+
+
+def _state(m):
+    out = {}
+    for t, name in ((m.query_tower, "q"), (m.candidate_tower, "c")):
+        out[name + ".mlp"] = t.dense.flat.detach().clone()
+        out[name + ".mlp_acc"] = m.optimizer._slot(t.dense.flat, 1, 0.1)[0].clone()
+        for n, layer in t.input_layer.embedding_layers.items():
+            out[f"{name}.{n}"] = layer.weight.detach().clone()
+            out[f"{name}.{n}.acc"] = m.optimizer._slot(layer.weight, 1, 0.1)[0].clone()
+    return out
+
+
+def test_fused_optimizer_apply_bit_identical_to_unfused(cuda):
+    """fused_optimizer_apply (each tower's dense + sparse Adagrad applied inside
+    the backward, on the tower's stream and workspace scope) gives bit-identical
+    tables, accumulators and MLP buffers to the unfused step, at ragged batch
+    sizes that change between steps (stale presorted workspaces of another
+    size must be detected, never read); the first step also matches the CPU
+    restatement; no sparse error is recorded (tt_sparse_status)."""
+    a, b = _small_model(cuda, seed=11), _small_model(cuda, seed=11, fused=True)
+    ref = _cpu_mirror(b)
+    rng = np.random.default_rng(9)
+    for i, B in enumerate((512, 37, 256, 1, 300)):
+        x = _batch(cuda, rng, B, True)
+        la = a.train_step(x)["loss"]
+        lb = b.train_step(x)["loss"]
+        if i == 0:
+            lq = b.candidate_logq(x).cpu().numpy()
+            rl = ref.step([x["cust"].cpu().numpy(), x["post"].cpu().numpy()],
+                          [x["art"].cpu().numpy(), x["ptn"].cpu().numpy(), x["ptn"].cpu().numpy()], lq)
+            assert abs(float(lb) - rl) <= 1e-3 * abs(rl)
+            r = ref.c_tables[0]
+            got = b.candidate_tower.input_layer.embedding_layers["art"].weight.cpu().numpy()
+            before = _small_model(cuda, seed=11).candidate_tower.input_layer.embedding_layers["art"].weight
+            d_ref, d_gpu = r - before.cpu().numpy(), got - before.cpu().numpy()
+            assert np.linalg.norm(d_gpu - d_ref) <= 1e-2 * np.linalg.norm(d_ref)
+        assert torch.equal(la, lb), (i, B)
+        sa, sb = _state(a), _state(b)
+        for k in sa:
+            assert torch.equal(sa[k], sb[k]), (i, B, k)
+        # the fused step leaves nothing for a later apply_gradients to re-apply
+        assert all(t.dense.flat.grad is None and t.input_layer.last_grad is None for t in b.towers)
+    a.optimizer.check_status(cuda)
+    b.optimizer.check_status(cuda)
+
+
+def test_stale_presorted_workspace_is_reported_not_applied(cuda):
+    """A presorted sparse apply whose workspace holds another call's sorted
+    keys applies nothing and is reported by tt_sparse_status (TTError), the
+    table left untouched; a matching apply afterwards reports nothing."""
+    from pkg._native import TTError
+
+    rng = np.random.default_rng(2)
+    V, D, B = 1000, 16, 512
+    t = torch.as_tensor(rng.uniform(-0.05, 0.05, (V, D)).astype(np.float32), device=cuda)
+    acc = torch.full_like(t, 0.1)
+    ids_a = torch.as_tensor(rng.integers(0, V, B).astype(np.int32), device=cuda)
+    ids_b = torch.as_tensor(rng.integers(0, V, B).astype(np.int32), device=cuda)
+    g = torch.as_tensor(rng.standard_normal((B, D)).astype(np.float32), device=cuda)
+    spec = lambda ids: [dict(table=t, slot0=acc, ids=[ids], grad_col_offset=[0], grad=g)]
+    with hip_ops.Workspace.scope("stale_test"):
+        hip_ops.sparse_sort(spec(ids_a), B)
+        before = t.clone()
+        hip_ops.sparse_adagrad(spec(ids_b), B, None, 0.05, 1e-7, presorted=True)  # keys are ids_a's
+        with pytest.raises(TTError, match="another call"):
+            hip_ops.sparse_status(cuda, "sparse")
+        assert torch.equal(t, before)
+        hip_ops.sparse_sort(spec(ids_b), B)
+        hip_ops.sparse_adagrad(spec(ids_b), B, None, 0.05, 1e-7, presorted=True)
+        hip_ops.sparse_status(cuda, "sparse")
+        assert not torch.equal(t, before)
 
 
 def test_graph_replay_equals_eager(cuda):
