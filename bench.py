@@ -145,14 +145,15 @@ def dist_env():
     return ws, rank, local
 
 
-def build_model(device, rank):
+def build_model(device, rank, fused_apply: bool = False):
     from pkg.modelling.models.two_tower_model import TwoTowerModel
     from pkg.modelling.optimizer_factory import OptimizerFactory
 
     schema = main_schema()
     data = SyntheticHM(device, seed=1234, stream=rank)
     schema.set_candidate_prob_lookup(data.prob_lookup())
-    model = TwoTowerModel.create_from_schema(schema, "article_id", device=device, seed=0)
+    model = TwoTowerModel.create_from_schema(schema, "article_id", device=device, seed=0,
+                                             fused_optimizer_apply=fused_apply)
     model.compile(optimizer=OptimizerFactory.get_optimizer("adagrad", {"learning_rate": 0.05}))
     return model, data
 
@@ -505,6 +506,8 @@ def main():
     ap.add_argument("--batch", type=int, default=16384)
     ap.add_argument("--index-queries", type=int, default=1_000_000)
     ap.add_argument("--no-index", action="store_true")
+    ap.add_argument("--fused-apply", action="store_true",
+                    help="apply each tower's Adagrad inside the backward (TwoTowerModel fused_optimizer_apply)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--train-mode", choices=("auto", "sharded"), default="auto",
@@ -530,7 +533,7 @@ def main():
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", torch.cuda.current_device())
 
-    model, data = build_model(device, rank)
+    model, data = build_model(device, rank, args.fused_apply)
     B = args.batch
     # kernel-level timings on the unsharded model, before the train step takes its tables
     flops, ms_rows, ms_cols, ms_entry = time_inbatch_kernel(model, data, device, B)
