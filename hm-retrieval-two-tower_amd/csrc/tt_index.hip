@@ -8,53 +8,57 @@
 //   s = fmaf(q[D-1], c[D-1], ... fmaf(q[0], c[0], 0))
 // and the returned scores are those fp32 values.
 //
-// Screening bound.  A bf16 MFMA score s~ differs from the exact chain s by at
-// most M_q = eps * |q| * max_c |c| with eps = 2^-7 + 2^-14: bf16 has 8
-// significant bits, so round-to-nearest moves each operand by at most 2^-8 of
-// itself and a product of two rounded operands by at most 2^-7 + 2^-16
-// (summed over k: <= (2^-7 + 2^-16) sum_k |q_k c_k| <= ... |q| |c|); fp32
-// accumulation of <= 128 exact bf16 products and the exact chain's own
-// rounding add below 2^-17 each.  If tau is a lower bound of the
-// K-th largest screened score, every member of the exact top-K has
-// s~ >= tau - 2 M_q, so "s~ > next_down(tau - 2 M_q)" loses nothing.
+// Screening bound.  A bf16 MFMA score s~ and the exact chain s differ by at
+// most eps * sum_k |q_k c_k| with eps = 2^-7 + 2^-10: round-to-nearest bf16
+// moves each operand by at most 2^-8 of itself, so a product of two rounded
+// operands by at most 2^-7 + 2^-16; the bf16 products are exact in fp32 and
+// the fp32 accumulation of <= 128 of them, like the exact chain's own
+// rounding, adds below 2^-16 each.  Two forms of the bound:
+//   relative  (query and every candidate non-negative, e.g. the towers' final
+//             ReLU, tower.py:48): sum |q_k c_k| = s, so
+//             s in [s~(1 - eps) - tiny, s~(1 + eps) + tiny];
+//   absolute  (otherwise): |s - s~| <= M_q = eps |q|_2 max_c |c|_2.
+// lb(s~) / ub(s~) below are those interval ends.
 //
-// Design (MI355X):
-//  screen (k <= 128, the bins path) — one workgroup = 8 waves x 32 queries;
-//    the queries' bf16 fragments stay in VGPRs (B operand), 64-candidate
-//    bf16 tiles stream through double-buffered, XOR-swizzled LDS with global
-//    loads issued two tiles ahead, and are scored with
-//    v_mfma_f32_32x32x16_bf16 (S^T: each lane holds 16 candidates of one
-//    query).  Per register: one v_max into a per-lane "bin" (64 bins per lane,
-//    128 per query, each the running maximum over a fixed residue class of
-//    candidates) and one v_cmp against the query's threshold; survivors are
-//    appended to a lane-private HBM shortlist (no atomics, no cross-lane
-//    work).  At geometrically spaced tiles the lanes refresh their
-//    threshold in parallel from the bins: the K-th largest of 128 bin maxima
-//    (distinct candidates) is a lower bound of the K-th screened score.
-//    Small query batches split the candidates over up to 8 workgroups per
-//    query block (split = blockIdx % S keeps a split on fixed XCDs, so its
-//    slice stays in that L2); splits share thresholds through a per-query
-//    atomicMax.
-//  screen (k > 128, the compaction path) — per-query wave shortlists compacted
-//    by a bitwise K-th search when they fill.
-//  finalize — one wave per query: shortlist entries above the final
-//    threshold are gathered into LDS, cut by a coarse K-th search,
-//    rescored with the exact fp32 fmaf chain, the exact top-K is selected on
-//    (score, -index) and ranked with an LDS bitonic sort.  A query whose
-//    shortlist cannot be bounded (massive near-ties) is answered by an exact
-//    fp32 scan with the same machinery.
+// Design (MI355X, one chip):
+//  prep     bf16 query rows, per-query bound mode / margin, zero-query flag.
+//  screen   one workgroup = 8 waves x 64 queries (two 32-query sets per wave,
+//           their bf16 fragments in VGPRs as the B operand); 64-candidate bf16
+//           tiles stream through a 4-stage LDS ring filled by LDS-DMA
+//           (global_load_lds, XOR-swizzled 16-B chunks) and are scored with
+//           v_mfma_f32_32x32x16_bf16 (S^T: each lane holds 16 candidates of one
+//           query).  Phase 1 scans a spread sample of the split's tiles and
+//           keeps per-register running maxima ("bins": 64 per query, each over
+//           a fixed residue class of sampled candidates); the j-th largest bin
+//           is an ESTIMATE tau of the score at rank ~R of the split (R ~ 3k).
+//           Phase 2 scans every tile once: a score s~ > tau is appended to a
+//           lane-private list (no atomics); that is one compare per score and
+//           a store for ~R/N of them.  tau is NOT assumed to be a bound.
+//  finalize one wave per query: radix-selects the k-th largest screened score
+//           sK over its lists, certifies the screen — X = lb(sK) > ub(tau)
+//           of every list means every candidate that can still belong to the
+//           exact top-k (ub(s~) >= X) scored above its list's tau and was
+//           kept — keeps the entries with ub(s~) >= X, rescores them with the
+//           exact fp32 chain, selects the exact top-k on (score, -index) and
+//           ranks them with an LDS bitonic sort.  A query that fails the
+//           certificate, overflows a list, or cannot be cut into LDS goes to
+//           the fallback list.
+//  fallback persistent grid: an exact fp32 scan of every candidate for each
+//           failed query (rare: estimation tails, massive exact ties).
+//  Zero queries score exactly +0 against every candidate in both paths; their
+//  answer (indices 0..k-1 by the tie rule) is written directly.
 #include <cmath>
 
 #include "tt_common.h"
 
-// Probe hooks for tools/index_probe.hip (never defined in the library build):
-//   TT_INDEX_STATS    count inserts / compactions / overflows
-//   TT_INDEX_NOINSERT screening threshold pinned above every score
 #ifdef TT_INDEX_STATS
-__device__ unsigned long long g_index_stats[4];
+__device__ unsigned long long g_index_stats[4];  // list entries, certificate fails, cut sizes, other fails
 #define TT_STAT(i, v) atomicAdd(&g_index_stats[i], static_cast<unsigned long long>(v))
+#define TT_STAT0(i, v) \
+  if (lane_id() == 0) atomicAdd(&g_index_stats[i], static_cast<unsigned long long>(v))
 #else
 #define TT_STAT(i, v) ((void)0)
+#define TT_STAT0(i, v) ((void)0)
 #endif
 
 namespace tt {
@@ -63,27 +67,22 @@ namespace {
 #ifndef TT_SCREEN_WAVES
 #define TT_SCREEN_WAVES 8
 #endif
-constexpr int kScreenWaves = TT_SCREEN_WAVES;
-constexpr int kScreenThreads = kScreenWaves * kWave;
-constexpr int kQPerWave = 32;
-constexpr int kQPerWG = kScreenWaves * kQPerWave;  // 256 queries
-constexpr int kCTile = 64;                         // candidates per LDS tile
-#ifndef TT_BINS
-#define TT_BINS 64
+constexpr int kSWaves = TT_SCREEN_WAVES;
+constexpr int kSThreads = kSWaves * kWave;       // 512
+constexpr int kQPerWave = 64;                    // two 32-query sets
+constexpr int kQPerWG = kSWaves * kQPerWave;     // 512
+constexpr int kCTile = 64;                       // candidates per LDS tile
+constexpr int kStages = 4;                       // LDS ring depth
+constexpr int kMaxSample = 128;                  // sample tiles per split
+constexpr int kMaxSplits = 16;
+constexpr float kEps = 0.0087890625f;            // 2^-7 + 2^-10
+constexpr float kTiny = 1e-30f;
+#ifndef TT_LIST_BUDGET
+#define TT_LIST_BUDGET (size_t(2) << 30)
 #endif
-constexpr int kBins = TT_BINS;                     // per lane (128 per query)
-constexpr int kBinsMaxK = 2 * kBins;               // bins path serves k <= 128
-#ifndef TT_LANE_CAP
-#define TT_LANE_CAP 1024
-#endif
-constexpr int kLaneCap = TT_LANE_CAP;              // entries per (query, split, lane half)
-constexpr int kMaxSplits = 8;
-constexpr float kScreenEps = 0.00787353515625f;    // 2^-7 + 2^-14
-constexpr int64_t kMaxChunk = 65536;               // queries per screening pass
-#ifndef TT_SHORTLIST_BUDGET
-#define TT_SHORTLIST_BUDGET (size_t(1) << 30)
-#endif
-constexpr size_t kShortlistBudget = TT_SHORTLIST_BUDGET;  // bytes of shortlists per pass
+constexpr size_t kListBudget = TT_LIST_BUDGET;   // bytes of screened lists per chunk
+
+enum : int { kQZero = 1, kQRel = 2 };
 
 struct IndexHeader {
   int64_t n;
@@ -91,7 +90,8 @@ struct IndexHeader {
   int32_t dim;
   int32_t D;
   unsigned maxnorm_bits;  // max_c |c|_2 as float bits (non-negative)
-  unsigned pad[9];
+  unsigned has_neg;       // some candidate coordinate < 0
+  unsigned pad[8];
 };
 static_assert(sizeof(IndexHeader) == 64, "header");
 
@@ -102,12 +102,6 @@ inline int pick_dpad(int dim) {
   return 0;
 }
 
-inline int cap_for_k(int k) {
-  int c = 1024;
-  while (c < 2 * k + 2 * kCTile) c <<= 1;
-  return c;
-}
-
 inline int next_pow2(int x) {
   int p = 1;
   while (p < x) p <<= 1;
@@ -116,30 +110,53 @@ inline int next_pow2(int x) {
 
 size_t index_bytes(int64_t n, int dim) {
   const int D = pick_dpad(dim);
-  const int64_t n_pad = round_up(n, kCTile);
-  return 64 + static_cast<size_t>(n_pad) * D * 2 + static_cast<size_t>(n_pad) * 4;
+  return 64 + static_cast<size_t>(round_up(n, kCTile)) * D * 2;
 }
 
 __device__ __forceinline__ const __bf16* index_rows(const void* idx) {
   return reinterpret_cast<const __bf16*>(static_cast<const char*>(idx) + 64);
 }
-__device__ __forceinline__ const float* index_bias(const void* idx, int64_t n_pad, int D) {
-  return reinterpret_cast<const float*>(static_cast<const char*>(idx) + 64 + n_pad * D * 2);
+
+__device__ __forceinline__ float lb_of(float s, float m, bool rel) {
+  return rel ? s * (1.0f - kEps) - kTiny : s - m;
+}
+__device__ __forceinline__ float ub_of(float s, float m, bool rel) {
+  return rel ? s * (1.0f + kEps) + kTiny : s + m;
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt64() {
+  const int l = lane_id();
+  return (l == 0) ? 0ull : (~0ull >> (64 - l));
+}
+
+// Orders this wave's LDS accesses around it (a wave's LDS operations execute
+// in order; this stops the compiler moving them across).  The finalize and
+// fallback helpers below are wave-local, so several waves of one workgroup
+// may run them on their own LDS regions.
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ unsigned long long make_key(float s, unsigned idx) {
+  return (static_cast<unsigned long long>(float_order_key(s)) << 32) |
+         static_cast<unsigned long long>(0xFFFFFFFFu - idx);
 }
 
 // ---- build ----------------------------------------------------------------
-// Row-major bf16 image (zero padded to n_pad rows, D columns), bias (0 / -inf
-// for padding rows) and max row norm (one atomic per workgroup of 64 rows).
+// Row-major bf16 image (zero padded to n_pad rows, D columns), max row norm
+// and the has-negative flag (one atomic of each per workgroup).
 constexpr int kBuildRowsPerWave = 16;
 __global__ void __launch_bounds__(256) build_kernel(const float* __restrict__ cand, int64_t ldc, int64_t n, int dim,
                                                     int64_t n_pad, int D, void* index) {
   __shared__ float wmax[4];
+  __shared__ int wneg[4];
   IndexHeader* hdr = static_cast<IndexHeader*>(index);
   __bf16* rows = reinterpret_cast<__bf16*>(static_cast<char*>(index) + 64);
-  float* bias = reinterpret_cast<float*>(static_cast<char*>(index) + 64 + n_pad * D * 2);
   const int wave = threadIdx.x / kWave;
   const int lane = lane_id();
   float mx = 0.0f;
+  bool neg = false;
   for (int i = 0; i < kBuildRowsPerWave; ++i) {
     const int64_t r = (blockIdx.x * 4ll + wave) * kBuildRowsPerWave + i;
     if (r >= n_pad) break;
@@ -149,19 +166,24 @@ __global__ void __launch_bounds__(256) build_kernel(const float* __restrict__ ca
       const float x0 = (r < n && e < dim) ? cand[r * ldc + e] : 0.0f;
       const float x1 = (r < n && e + 1 < dim) ? cand[r * ldc + e + 1] : 0.0f;
       ss = __builtin_fmaf(x0, x0, __builtin_fmaf(x1, x1, ss));
+      neg = neg || x0 < 0.0f || x1 < 0.0f;
       reinterpret_cast<unsigned*>(rows + r * D)[e2] = pack_bf16x2(x0, x1);
     }
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) ss += __shfl_xor(ss, m, kWave);
-    if (lane == 0) bias[r] = (r < n) ? 0.0f : -INFINITY;
     if (r < n) mx = fmaxf(mx, sqrtf(ss));
   }
-  if (lane == 0) wmax[wave] = mx;
+  const bool wn = __ballot(neg) != 0;
+  if (lane == 0) {
+    wmax[wave] = mx;
+    wneg[wave] = wn ? 1 : 0;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     const float m = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
     // round the norm up so the bound stays an upper bound
     atomicMax(&hdr->maxnorm_bits, __float_as_uint(m * (1.0f + 1e-5f)));
+    if (wneg[0] | wneg[1] | wneg[2] | wneg[3]) atomicOr(&hdr->has_neg, 1u);
     if (blockIdx.x == 0) {
       hdr->n = n;
       hdr->n_pad = n_pad;
@@ -172,82 +194,54 @@ __global__ void __launch_bounds__(256) build_kernel(const float* __restrict__ ca
 }
 
 // ---- query prep ----------------------------------------------------------
-// bf16 rows [nq_pad, D] and the per-query screening margin 2*M_q.
+// bf16 rows [nq_pad, D]; per query the bound mode (relative when the query and
+// every candidate are non-negative), the absolute margin M_q, the zero flag.
 __global__ void query_prep_kernel(const float* __restrict__ q, int64_t ldq, int64_t nq, int dim, int64_t nq_pad,
-                                  int D, const void* index, __bf16* __restrict__ qb, float* __restrict__ margin2) {
+                                  int D, const void* index, __bf16* __restrict__ qb, int* __restrict__ qflags,
+                                  float* __restrict__ qmarg) {
   const int64_t r = blockIdx.x * 4ll + threadIdx.x / kWave;
   if (r >= nq_pad) return;
   const int lane = lane_id();
   float ss = 0.0f;
-  bool nz = false;
+  bool nz = false, neg = false;
   for (int e2 = lane; e2 < D / 2; e2 += kWave) {
     const int e = 2 * e2;
     const float x0 = (r < nq && e < dim) ? q[r * ldq + e] : 0.0f;
     const float x1 = (r < nq && e + 1 < dim) ? q[r * ldq + e + 1] : 0.0f;
     ss = __builtin_fmaf(x0, x0, __builtin_fmaf(x1, x1, ss));
     nz = nz || x0 != 0.0f || x1 != 0.0f;
+    neg = neg || x0 < 0.0f || x1 < 0.0f;
     reinterpret_cast<unsigned*>(qb + r * D)[e2] = pack_bf16x2(x0, x1);
   }
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) ss += __shfl_xor(ss, m, kWave);
   const bool nonzero = __ballot(nz) != 0;
+  const bool qneg = __ballot(neg) != 0;
   if (lane == 0) {
-    const float maxc = __uint_as_float(static_cast<const IndexHeader*>(index)->maxnorm_bits);
+    const IndexHeader* hdr = static_cast<const IndexHeader*>(index);
+    const float maxc = __uint_as_float(hdr->maxnorm_bits);
     const float qn = sqrtf(ss) * (1.0f + 1e-5f);
-    // 2 * eps * |q| * max|c|, rounded up; tiny absolute floor for subnormals.
-    // A zero query scores exactly +0 against every candidate in both paths, so
-    // its margin is 0 and ties resolve by index.
-    margin2[r] = (r < nq && nonzero) ? (2.0f * kScreenEps * qn * maxc) * (1.0f + 1e-5f) + 1e-30f : 0.0f;
+    const bool rel = !qneg && hdr->has_neg == 0;
+    qflags[r] = (nonzero ? 0 : kQZero) | (rel ? kQRel : 0);
+    qmarg[r] = (kEps * qn * maxc) * (1.0f + 1e-5f) + kTiny;
   }
 }
 
-__device__ __forceinline__ unsigned long long make_key(float s, unsigned idx) {
-  return (static_cast<unsigned long long>(float_order_key(s)) << 32) |
-         static_cast<unsigned long long>(0xFFFFFFFFu - idx);
-}
-
-// Largest float strictly below x (x finite).
-__device__ __forceinline__ float next_down(float x) {
-  if (x == 0.0f) return -__uint_as_float(1u);
-  const unsigned u = __float_as_uint(x);
-  return __uint_as_float(x > 0.0f ? u - 1u : u + 1u);
-}
-
-__device__ __forceinline__ uint64_t lanemask_lt64() {
-  const int l = lane_id();
-  return (l == 0) ? 0ull : (~0ull >> (64 - l));
-}
-
-// Largest v such that at least K of the wave's keys are >= v (keys distinct:
-// the K-th largest).  Keys of empty slots are 0.
-template <int NPL>
-__device__ unsigned long long kth_largest(const unsigned long long (&key)[NPL], int K) {
-  unsigned long long res = 0;
-#pragma unroll 1
-  for (int bit = 63; bit >= 0; --bit) {
-    const unsigned long long cand = res | (1ull << bit);
-    int c = 0;
-#pragma unroll
-    for (int i = 0; i < NPL; ++i) c += __popcll(__ballot(key[i] >= cand));
-    if (c >= K) res = cand;
-  }
-  return res;
-}
-
-// ---- screen, bins path (k <= 128) -------------------------------------------
+// ---- screen ----------------------------------------------------------------
 struct ScreenArgs {
   const void* index;
-  const __bf16* qb;      // [nq_pad, D]
-  const float* margin2;  // [nq_pad]
-  int64_t nq;            // real queries in this chunk
-  int64_t n;             // real candidates (rows >= n are zero padding)
+  const __bf16* qb;   // [nq_pad, D]
+  int64_t nq;         // real queries in this chunk
+  int64_t n;          // real candidates (rows >= n are zero padding)
   int64_t n_pad;
-  int k;
-  int S;                 // candidate splits
-  int R;                 // entries per (query, split, half) region
-  uint2* buf;            // [nq_pad][S][2][R] (score bits, candidate)
-  int* count;            // [nq_pad][S][2]; -1 = region overflowed
-  unsigned* thr;         // [nq_pad] order key of a valid strict threshold (0 = none)
+  int S;              // candidate splits
+  int NS;             // sample tiles per split (0: keep every score)
+  int jsel;           // tau = jsel-th largest of a query's 64 bins
+  int cap;            // entries per (query, split, lane half) list
+  unsigned index_offset;
+  uint2* buf;         // [nq_pad][S][2][cap] (score bits, index_offset + candidate)
+  int* count;         // [nq_pad][S][2]; -1 = list overflowed
+  float* tau;         // [nq_pad][S]
 };
 
 // s_waitcnt with only the vector-memory counter constrained (gfx9 encoding).
@@ -257,64 +251,79 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
 }
 
-// Keeps the entries of region[0..n) scoring above thr; returns their count.
-__device__ __noinline__ int compact_region(uint2* region, int n, float thr) {
-  int m = 0;
-  for (int j0 = 0; j0 < n; j0 += 16) {
-    uint2 e[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) e[u] = (j0 + u < n) ? region[j0 + u] : make_uint2(0u, 0u);
-#pragma unroll
-    for (int u = 0; u < 16; ++u)
-      if (j0 + u < n && __uint_as_float(e[u].x) > thr) region[m++] = e[u];
-  }
-  return m;
+// Waits until at most n of this wave's vector-memory ops are in flight (n
+// rounded down to a bucket: waiting for more is always safe).
+__device__ __forceinline__ void wait_vmcnt_atmost(int n) {
+  if (n >= 63) wait_vmcnt<63>();
+  else if (n >= 48) wait_vmcnt<48>();
+  else if (n >= 32) wait_vmcnt<32>();
+  else if (n >= 24) wait_vmcnt<24>();
+  else if (n >= 16) wait_vmcnt<16>();
+  else if (n >= 12) wait_vmcnt<12>();
+  else if (n >= 8) wait_vmcnt<8>();
+  else if (n >= 6) wait_vmcnt<6>();
+  else if (n >= 4) wait_vmcnt<4>();
+  else if (n >= 2) wait_vmcnt<2>();
+  else wait_vmcnt<0>();
 }
 
-constexpr int kStages = 4;     // LDS ring: tile i computed while tiles i+1..i+3 land
-#ifndef TT_WARM_TILES
-#define TT_WARM_TILES 64
-#endif
-constexpr int kWarmTiles = TT_WARM_TILES;  // bins-only warm-up tiles per split (4096 candidates)
+// jsel-th largest of the 64 values {bins of this lane, bins of lane ^ 32},
+// to a 16-bit order-key prefix (rounded down); -inf if fewer than jsel bins.
+__device__ float bins_select(const float (&ba)[16], const float (&bb)[16], int jsel) {
+  unsigned res = 0;
+#pragma unroll 1
+  for (int bit = 15; bit >= 0; --bit) {
+    const unsigned c = res | (1u << bit);
+    const float f = order_key_float(c << 16);  // smallest float with this prefix (NaN: none)
+    int n = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) n += ((ba[i] >= f) ? 1 : 0) + ((bb[i] >= f) ? 1 : 0);
+    n += __shfl_xor(n, 32, kWave);
+    if (n >= jsel) res = c;
+  }
+  const float t = order_key_float(res << 16);
+  return (t > -INFINITY) ? t : -INFINITY;  // NaN (no prefix found) -> keep everything
+}
 
-template <int D>
-__global__ void __launch_bounds__(kScreenThreads) screen_bins_kernel(const ScreenArgs a) {
+// SAMPLE = true: the estimate pass (phase 1) over the split's spread sample
+// tiles, writes tau[q][split].  SAMPLE = false: the scan (phase 2) of every
+// tile of the split against that tau.  Separate launches, so each keeps its
+// registers for its own loop.
+template <int D, bool SAMPLE>
+__global__ void __launch_bounds__(kSThreads) screen_kernel(const ScreenArgs a) {
   constexpr int KS = D / 16, CH = D / 8, RB = D * 2;
   constexpr int TILE_BYTES = kCTile * RB;                 // 16 KiB at D = 128
   constexpr int PIECES = TILE_BYTES / 1024;               // 1 KiB LDS-DMA pieces per tile
-  constexpr int PPW = PIECES >= kScreenWaves ? PIECES / kScreenWaves : 1;
-  __shared__ __attribute__((aligned(1024))) char smem[kStages * TILE_BYTES];  // tile ring (LDS-DMA)
+  constexpr int PPW = PIECES >= kSWaves ? PIECES / kSWaves : 1;
+  constexpr int RPS = 16 / KS;                            // filtered registers per k-step
+  __shared__ __attribute__((aligned(1024))) char smem[kStages * TILE_BYTES];
   const int tid = threadIdx.x;
   const int wave = tid / kWave;
   const int lane = lane_id();
   const int h = lane >> 5, l32 = lane & 31;
   const int split = static_cast<int>(blockIdx.x % a.S);
-  const int64_t qg = static_cast<int64_t>(blockIdx.x / a.S) * kQPerWG + wave * kQPerWave + l32;
+  const int64_t q0 = static_cast<int64_t>(blockIdx.x / a.S) * kQPerWG + wave * kQPerWave + l32;
+  const int64_t q1 = q0 + 32;
   const int ntiles = static_cast<int>(a.n_pad / kCTile);
   const int per = (ntiles + a.S - 1) / a.S;
   const int tb = split * per;
   const int nt = max(min(ntiles, tb + per) - tb, 0);
+  const int ns = min(a.NS, nt);
   const __bf16* crow = index_rows(a.index);
   const bool my_pieces = wave * PPW < PIECES;  // D = 32: waves 4..7 stage nothing
 
-  bf16x8 bfrag[KS];
+  bf16x8 bq0[KS], bq1[KS];
 #pragma unroll
-  for (int s = 0; s < KS; ++s) bfrag[s] = *reinterpret_cast<const bf16x8*>(a.qb + qg * D + 16 * s + 8 * h);
-  const float m2 = a.margin2[qg];
+  for (int s = 0; s < KS; ++s) {
+    bq0[s] = *reinterpret_cast<const bf16x8*>(a.qb + q0 * D + 16 * s + 8 * h);
+    bq1[s] = *reinterpret_cast<const bf16x8*>(a.qb + q1 * D + 16 * s + 8 * h);
+  }
   wait_vmcnt<0>();  // ordinary loads retired before the LDS-DMA ring starts
-  const bool live = qg < a.nq;
-  float thr = live ? -INFINITY : INFINITY;  // insertion threshold (strict)
-  float gthr = -INFINITY;                   // best globally valid strict threshold
-  float bins[kBins];
-#pragma unroll
-  for (int i = 0; i < kBins; ++i) bins[i] = -INFINITY;
-  uint2* region = a.buf + ((qg * a.S + split) * 2 + h) * static_cast<int64_t>(a.R);
-  int cnt = 0;
-  bool ovf = false;
 
-  // LDS image of a tile: row-major RB-byte rows, 16-B chunks XOR-swizzled by
-  // row; the swizzle is applied to the per-lane SOURCE address so that every
-  // 1 KiB DMA piece lands lane-linear.
+  // tile sequence: the spread sample, or every tile of the split
+  auto phys = [&](int u) { return SAMPLE ? tb + (u * nt) / ns : tb + u; };
+  const int nv = SAMPLE ? ns : nt;
+
   auto issue = [&](int tile, int stage) {
     const int64_t base = static_cast<int64_t>(tile) * kCTile;
 #pragma unroll
@@ -331,8 +340,7 @@ __global__ void __launch_bounds__(kScreenThreads) screen_bins_kernel(const Scree
       }
     }
   };
-  // wait until at most `ahead` tiles of this wave's DMA are still in flight
-  auto wait_tiles = [&](int ahead) {
+  auto wait_tiles = [&](int ahead) {  // at most `ahead` of this wave's tiles still in flight
     if (!my_pieces || ahead <= 0) {
       wait_vmcnt<0>();
     } else if (ahead == 1) {
@@ -341,397 +349,194 @@ __global__ void __launch_bounds__(kScreenThreads) screen_bins_kernel(const Scree
       wait_vmcnt<2 * PPW>();
     }
   };
-
-  // Lane-parallel threshold refresh: K-th largest of the pair's 128 bins by a
-  // 16-bit prefix search of their order keys (a lower bound of the K-th).
-  auto refresh = [&](bool warm) {
-    unsigned res = 0;
-#pragma unroll 1
-    for (int bit = 15; bit >= 0; --bit) {
-      const unsigned c = res | (1u << bit);
-      const float f = order_key_float(c << 16);  // smallest float with this key prefix (NaN: none)
-      int n = 0;
+  auto frag = [&](const char* B, int t, int s) {
+    const int row = 32 * t + l32, ch = 2 * s + h;
+    const int swz = (row * CH / 16) % CH;
+    return *reinterpret_cast<const bf16x8*>(B + row * RB + ((ch ^ swz) << 4));
+  };
+  auto mask_pad = [&](f32x16& acc, int64_t cfirst) {  // rows past n (last tile only)
 #pragma unroll
-      for (int i = 0; i < kBins; ++i) n += (bins[i] >= f) ? 1 : 0;
-      n += __shfl_xor(n, 32, kWave);
-      if (n >= a.k) res = c;
-    }
-    const float tau = order_key_float(res << 16);
-    // A zero query (m2 == 0, every score exactly 0) relies on a strict local
-    // threshold that is valid only for candidates after the certifying ones;
-    // the warm-up tiles are scanned again, so it skips the warm-up threshold
-    // and restarts its bins.
-    if (warm && m2 == 0.0f) {
-#pragma unroll
-      for (int i = 0; i < kBins; ++i) bins[i] = -INFINITY;
-    } else if (tau > -INFINITY && tau < INFINITY) {
-      const float local = m2 > 0.0f ? next_down(tau - m2) : tau;
-      const float pub = m2 > 0.0f ? local : next_down(tau);
-      gthr = fmaxf(gthr, pub);
-      thr = fmaxf(thr, local);
-    }
-    if (a.S > 1) {
-      unsigned g = float_order_key(gthr);
-      if (h == 0 && live) g = max(g, atomicMax(&a.thr[qg], g));
-      const unsigned g2 = __shfl_xor(g, 32, kWave);
-      gthr = fmaxf(gthr, order_key_float(g2 > g ? g2 : g));
-      thr = fmaxf(thr, gthr);
-    }
-    thr = fmaxf(thr, __shfl_xor(thr, 32, kWave));
-#ifdef TT_INDEX_NOINSERT
-    thr = 3.0e38f;
-#endif
+    for (int r = 0; r < 16; ++r)
+      if (cfirst + (r & 3) + 8 * (r >> 2) >= a.n) acc[r] = -INFINITY;
+  };
+  auto advance = [&](int u) {  // (sample) tile u consumed: wait for u + 1, barrier
+    if (u + 1 < nv) wait_tiles(min(u + kStages - 1, nv - 1) - (u + 1));
+    __builtin_amdgcn_s_barrier();
   };
 
-  // A lane whose region is nearly full drops the entries the globally valid
-  // threshold rules out (the strict local one of a zero-margin query is only
-  // valid for later candidates); if that does not make room the query is
-  // answered by the exact fallback.
-  auto self_compact = [&]() {
-    if (cnt > a.R - 2 * 16) {
-      cnt = compact_region(region, cnt, gthr);
-      TT_STAT(1, 1);
-      if (cnt > a.R - 2 * 16) {
-        ovf = true;
-        thr = INFINITY;
-        TT_STAT(2, 1);
-      }
-    }
-  };
-
-  // Warm-up: the first `pre` tiles of the split are scanned once for the bins
-  // only (no inserts), so the insertion threshold starts near the top few
-  // percent instead of at -inf; then the split is scanned from its start.
-  // Virtual tile v < pre is tile tb + v, v >= pre is tile tb + v - pre.
-  // pre is a multiple of 4 so a tile re-scanned after the warm-up lands in the
-  // same bins (Q = v & 3): every bin stays a maximum over distinct candidates.
-  const int pre = min(kWarmTiles, nt / 4) & ~3;
-  const int nv = pre + nt;
-  auto vtile = [&](int v) { return tb + (v < pre ? v : v - pre); };
 #pragma unroll
   for (int s = 0; s < kStages - 1; ++s)
-    if (s < nv) issue(vtile(s), s);
+    if (s < nv) issue(phys(s), s);
   wait_tiles(min(nv, kStages - 1) - 1);
   __builtin_amdgcn_s_barrier();
 
-  // Software pipeline at 32-candidate block granularity: the 8 MFMAs of a
-  // block are issued with the filter of the previous block (bins, threshold
-  // test, inserts) in their issue gaps.
-  // Tile v: [MFMA(v,0) | filter(v-1,1)] then [MFMA(v,1) | filter(v,0)].
-  // Q = v & 3 selects a tile's bins (static under the unroll by 4).
-  constexpr int PPS = 8 / KS;  // filter pairs per MFMA slot
-  f32x16 accf = {};            // block waiting to be filtered: tile v-1, block 1
-  int64_t cbase_f = 0;         // first candidate of that tile
-  bool scan_f = false;
-
-  auto filter_pair = [&](const f32x16& acc, const int Qb, const int t, const int pr, int64_t cbase, float tins) {
-    const float x = acc[2 * pr], y = acc[2 * pr + 1];
-    const float pm = __builtin_elementwise_maximum(x, y);
-    constexpr int NQ = kBins / 16;  // tile parities with their own bins
-    bins[(Qb % NQ) * 16 + t * 8 + pr] = __builtin_elementwise_maximum(bins[(Qb % NQ) * 16 + t * 8 + pr], pm);
-#ifndef TT_PROBE_LIGHT
-    if (pm > tins) {
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const float val = u ? y : x;
-        const int r = 2 * pr + u;
-        if (val > tins) {
-          const unsigned cidx = static_cast<unsigned>(cbase + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h);
-          region[cnt] = make_uint2(__float_as_uint(val), cidx);
-          ++cnt;
-          TT_STAT(0, 1);
+  if constexpr (SAMPLE) {
+  // ---- phase 1: sample tiles, bins only ------------------------------------
+    // bins: per lane and query set, 16 register positions x the 2 blocks of a tile
+    // (64 per query with the partner lane), running maxima of the sample.
+    float b0a[16], b0b[16], b1a[16], b1b[16];
+  #pragma unroll
+    for (int r = 0; r < 16; ++r) b0a[r] = b0b[r] = b1a[r] = b1b[r] = -INFINITY;
+    for (int u = 0; u < ns; ++u) {
+      if (u + kStages - 1 < nv) issue(phys(u + kStages - 1), (u + kStages - 1) % kStages);
+      const char* B = smem + (u % kStages) * TILE_BYTES;
+      const int64_t cbase = static_cast<int64_t>(phys(u)) * kCTile;
+  #pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        f32x16 c0 = {}, c1 = {};
+  #pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const bf16x8 af = frag(B, t, s);
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bq0[s], c0, 0, 0, 0);
+          c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bq1[s], c1, 0, 0, 0);
+        }
+        if (cbase + kCTile > a.n) {
+          mask_pad(c0, cbase + 32 * t + 4 * h);
+          mask_pad(c1, cbase + 32 * t + 4 * h);
+        }
+        float (&x0)[16] = t == 0 ? b0a : b0b;  // static under the unroll
+        float (&x1)[16] = t == 0 ? b1a : b1b;
+  #pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          x0[r] = __builtin_elementwise_maximum(x0[r], c0[r]);
+          x1[r] = __builtin_elementwise_maximum(x1[r], c1[r]);
         }
       }
+      advance(u);
     }
+    const float t0 = ns > 0 ? bins_select(b0a, b0b, a.jsel) : -INFINITY;
+    const float t1 = ns > 0 ? bins_select(b1a, b1b, a.jsel) : -INFINITY;
+    if (h == 0) {
+      a.tau[q0 * a.S + split] = t0;
+      a.tau[q1 * a.S + split] = t1;
+    }
+  }
+  if constexpr (!SAMPLE) {
+  // the estimate of the sample pass; queries past nq keep nothing
+  float tau0 = q0 < a.nq ? a.tau[q0 * a.S + split] : INFINITY;
+  float tau1 = q1 < a.nq ? a.tau[q1 * a.S + split] : INFINITY;
+
+  // ---- phase 2: every tile of the split once, keep s~ > tau -----------------
+  const int64_t lst0 = ((q0 * a.S + split) * 2 + h) * static_cast<int64_t>(a.cap);
+  const int64_t lst1 = ((q1 * a.S + split) * 2 + h) * static_cast<int64_t>(a.cap);
+  uint2* const reg0 = a.buf + lst0;
+  uint2* const reg1 = a.buf + lst1;
+  uint2* w0 = reg0;  // next free entry
+  uint2* w1 = reg1;
+  uint2* const lim0 = reg0 + (a.cap - 48);  // a list grows by <= 48 between two checks
+  uint2* const lim1 = reg1 + (a.cap - 48);
+  bool ovf0 = false, ovf1 = false;
+#ifdef TT_INDEX_NOINSERT  // probe build (tools/index_probe.hip): screen cost without list stores
+  tau0 = tau1 = __uint_as_float(a.cap > 0 ? 0x7f800000u : 0u);  // +inf, opaque to the compiler
 #endif
+
+  // Each wave reads a block's A fragments one block ahead (af / af2), so the
+  // ring barrier sits in the middle of a tile: at mid-tile u every wave holds
+  // block (u, 1) in registers, tile u + 1 has landed, and tile u + 4 is issued
+  // into the stage tile u vacated.  List stores share the vector-memory
+  // counter with the LDS-DMA, so the wait for tile u + 1 counts the ops each
+  // wave issued after that tile's DMA: windows wa / wb / wc = ops from the DMA
+  // of tile u + 1 / u + 2 / u + 3 up to the next DMA (da / db / dc = pieces).
+  int wa, wb, wc, da, db, dc;
+  auto keep = [&](float v, float tau, unsigned c, uint2*& w) {
+    // uniform skip when no lane keeps v; marked unlikely so that the common
+    // case falls through (a taken branch per score costs more than the test)
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(v > tau) != 0, 0)) {
+      if (v > tau) {
+        *w = make_uint2(__float_as_uint(v), c);
+        ++w;
+      }
+      ++wc;  // one store instruction issued
+    }
   };
-  auto mask_pad = [&](f32x16& acc, const int t, int64_t cbase) {  // zero padding rows of the last tile
+  f32x16 p0, p1;  // the block waiting to be filtered
+#pragma unroll
+  for (int r = 0; r < 16; ++r) p0[r] = p1[r] = -INFINITY;
+  unsigned pc = 0;  // its lane candidate base (index_offset + first + 4h)
+  auto filter_regs = [&](int r0) {
+#pragma unroll
+    for (int i = 0; i < RPS; ++i) {
+      const int r = r0 + i;
+      const unsigned c = pc + static_cast<unsigned>((r & 3) + 8 * (r >> 2));
+      keep(p0[r], tau0, c, w0);
+      keep(p1[r], tau1, c, w1);
+    }
+  };
+  const int dpieces = my_pieces ? PPW : 0;
+  bf16x8 af[KS], af2[KS];
+  auto load_frags = [&](bf16x8 (&f)[KS], const char* B, int t) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) f[s] = frag(B, t, s);
+  };
+  // MFMAs of block (t) of the tile at cbase from fragments f, the previous
+  // block's filter in their issue gaps; the results become the next p0 / p1.
+  // A block: its MFMAs, then its compares; the SIMD's other wave keeps the
+  // matrix pipe busy meanwhile.  (Measured alternatives, all slower or
+  // equal: the compares of block b-1 interleaved with the MFMAs of block b
+  // — 2 waves/SIMD spill, 1 wave/SIMD leaves the pipe idle — and staggering
+  // the two SIMD partners by half a block.)
+  auto block = [&](const bf16x8 (&f)[KS], int t, int64_t cbase) {
+    p0 = f32x16{};
+    p1 = f32x16{};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      p0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[s], bq0[s], p0, 0, 0, 0);
+      p1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[s], bq1[s], p1, 0, 0, 0);
+    }
     if (cbase + kCTile > a.n) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        if (cbase + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h >= a.n) acc[r] = -INFINITY;
+      mask_pad(p0, cbase + 32 * t + 4 * h);
+      mask_pad(p1, cbase + 32 * t + 4 * h);
     }
+    pc = a.index_offset + static_cast<unsigned>(cbase + 32 * t + 4 * h);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) filter_regs(s * RPS);
   };
-  // after the filter of main-scan tile j-1: refresh on a geometric schedule;
-  // j == 1 (pre > 0) is the first refresh after the warm-up tiles.
-  auto after_filter = [&](int j) {
-    const bool warm = pre > 0 && j == 1;
-    const bool due = warm || (j >= 2 && (j & (j - 1)) == 0) || (j > 0 && j % 128 == 0);
-    const bool full = __any(cnt > a.R - 2 * 32);
-    if (due || full) refresh(warm);
-    if (full) self_compact();
-  };
-
-  auto tile_body = [&](int v, const int Q) {
-    const int Qp = (Q + 3) & 3;
-    if (v + kStages - 1 < nv) issue(vtile(v + kStages - 1), (v + kStages - 1) % kStages);
-#ifdef TT_PROBE_NOLDS
-    const char* B = smem;  // probe: always the same stage (fragments stay cached)
-#else
-    const char* B = smem + (v % kStages) * TILE_BYTES;
-#endif
-    const int64_t cbase = static_cast<int64_t>(vtile(v)) * kCTile;
-    const bool scan = v >= pre;
-    const bool have_prev = v > 0;
-    const float tins_f = scan_f ? thr : INFINITY;
-    if (have_prev) mask_pad(accf, 1, cbase_f);
-    f32x16 acc0 = {}, acc1 = {};
-    auto block0 = [&](const bool with_filter) {  // block 0 of tile v | filter block 1 of tile v-1
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const int row = l32, ch = 2 * s + h;
-        const int swz = (row * CH / 16) % CH;
-#ifdef TT_PROBE_REGA
-        const bf16x8 af = bfrag[(s + 1) % KS];  // probe: no LDS reads
-#else
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(B + row * RB + ((ch ^ swz) << 4));
-#endif
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfrag[s], acc0, 0, 0, 0);
-        if (with_filter) {
-#pragma unroll
-          for (int u = 0; u < PPS; ++u) filter_pair(accf, Qp, 1, s * PPS + u, cbase_f, tins_f);
-        }
-      }
-    };
-    if (have_prev) {
-      block0(true);
-      after_filter(v - pre);
-    } else {
-      block0(false);
-    }
-    mask_pad(acc0, 0, cbase);
-    const float tins = scan ? thr : INFINITY;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {  // block 1 of tile v | filter block 0 of tile v
-      const int row = 32 + l32, ch = 2 * s + h;
-      const int swz = (row * CH / 16) % CH;
-#ifdef TT_PROBE_REGA
-      const bf16x8 af = bfrag[(s + 2) % KS];  // probe: no LDS reads
-#else
-      const bf16x8 af = *reinterpret_cast<const bf16x8*>(B + row * RB + ((ch ^ swz) << 4));
-#endif
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfrag[s], acc1, 0, 0, 0);
-#pragma unroll
-      for (int u = 0; u < PPS; ++u) filter_pair(acc0, Q, 0, s * PPS + u, cbase, tins);
-    }
-    accf = acc1;
-    cbase_f = cbase;
-    scan_f = scan;
-#ifndef TT_PROBE_NOBARRIER
-    if (v + 1 < nv) wait_tiles(min(v + kStages - 1, nv - 1) - (v + 1));  // tile v+1 landed
-    __builtin_amdgcn_s_barrier();
-#endif
-  };
-
-#ifdef TT_PROBE_NOUNROLL
-  for (int v = 0; v < nv; ++v) tile_body(v, 0);  // probe: one code copy (bins aliased)
-#else
-  for (int v = 0; v < nv; v += 4) {
-    tile_body(v, 0);
-    if (v + 1 < nv) tile_body(v + 1, 1);
-    if (v + 2 < nv) tile_body(v + 2, 2);
-    if (v + 3 < nv) tile_body(v + 3, 3);
+  // entering: tile 0 landed (barrier passed), tiles up to 2 issued, the
+  // stage of tile 3 free
+  dc = 0;
+  if (3 < nv) {
+    issue(phys(3), 3);
+    dc = dpieces;
   }
-#endif
-  if (nv > 0) {  // drain: filter the last block, final refresh
-    mask_pad(accf, 1, cbase_f);
-    const int Ql = (nv - 1) & 3;
-    const float tins_f = scan_f ? thr : INFINITY;
-#pragma unroll
-    for (int pr = 0; pr < 8; ++pr) {
-      switch (Ql) {  // static bin index per case
-        case 0: filter_pair(accf, 0, 1, pr, cbase_f, tins_f); break;
-        case 1: filter_pair(accf, 1, 1, pr, cbase_f, tins_f); break;
-        case 2: filter_pair(accf, 2, 1, pr, cbase_f, tins_f); break;
-        default: filter_pair(accf, 3, 1, pr, cbase_f, tins_f); break;
-      }
+  da = wa = (1 < nv) ? dpieces : 0;
+  db = wb = (2 < nv) ? dpieces : 0;
+  wc = dc;
+  if (0 < nv) load_frags(af, smem, 0);
+  for (int u = 0; u < nv; ++u) {
+    const char* B = smem + (u % kStages) * TILE_BYTES;
+    const int64_t cbase = static_cast<int64_t>(phys(u)) * kCTile;
+    if (w0 > lim0) {
+      ovf0 = true;
+      tau0 = INFINITY;
     }
-    refresh(false);
-  }
-  a.count[(qg * a.S + split) * 2 + h] = ovf ? -1 : cnt;
-  if (h == 0 && live && gthr > -INFINITY) atomicMax(&a.thr[qg], float_order_key(gthr));
-}
-
-// ---- screen, compaction path (k > 128) ---------------------------------------
-struct ScreenCArgs {
-  const void* index;
-  const __bf16* qb;
-  const float* margin2;
-  int64_t nq;
-  int64_t n_pad;
-  int k;
-  int cap;
-  uint2* buf;    // [nq_pad][cap]
-  int* count;    // [nq_pad]; -1 = overflow
-};
-
-// Compacts the shortlist buf[0..n) of one query with the whole wave.  Keeps
-// every entry that might still belong to the exact top-K given screened
-// scores within +-M of the exact ones (margin2 = 2M).  n <= 64*NPL.
-template <int NPL>
-__device__ int compact_shortlist(uint2* buf, int n, int K, float margin2, float* thr_out) {
-  const int lane = lane_id();
-  unsigned long long key[NPL];
-  uint2 ent[NPL];
-#pragma unroll
-  for (int i = 0; i < NPL; ++i) {
-    const int j = i * kWave + lane;
-    ent[i] = (j < n) ? buf[j] : make_uint2(0u, 0u);
-    key[i] = (j < n) ? make_key(__uint_as_float(ent[i].x), ent[i].y) : 0ull;
-  }
-  if (n <= K) {
-    *thr_out = -INFINITY;
-    return n;
-  }
-  const unsigned long long kk = kth_largest<NPL>(key, K);
-  const float sK = order_key_float(static_cast<unsigned>(kk >> 32));
-  const unsigned idxK = 0xFFFFFFFFu - static_cast<unsigned>(kk & 0xFFFFFFFFull);
-  float thr = sK - margin2;
-  if (margin2 > 0.0f) thr = next_down(thr);
-  int out = 0;
-#pragma unroll
-  for (int i = 0; i < NPL; ++i) {
-    const int j = i * kWave + lane;
-    const float s = __uint_as_float(ent[i].x) + 0.0f;
-    const bool keep = (j < n) && (s > thr || (s == thr && ent[i].y <= idxK));
-    const uint64_t m = __ballot(keep);
-    if (keep) buf[out + __popcll(m & lanemask_lt64())] = ent[i];
-    out += __popcll(m);
-  }
-  __threadfence_block();
-  *thr_out = thr;
-  return out;
-}
-
-template <int D, int NPL>
-__global__ void __launch_bounds__(kScreenThreads) screen_compact_kernel(const ScreenCArgs a) {
-  constexpr int KS = D / 16, CH = D / 8;
-  constexpr int A_BYTES = kCTile * D * 2;
-  constexpr int BUF_BYTES = A_BYTES + kCTile * 4;
-  constexpr int CPT = (kCTile * CH + kScreenThreads - 1) / kScreenThreads;
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF_BYTES];
-  __shared__ int cnt_s[kQPerWG];
-  __shared__ float thr_s[kQPerWG];
-  const int tid = threadIdx.x;
-  const int wave = tid / kWave;
-  const int lane = lane_id();
-  const int h = lane >> 5, l32 = lane & 31;
-  const int ql = wave * kQPerWave + l32;
-  const int64_t qg = static_cast<int64_t>(blockIdx.x) * kQPerWG + ql;
-  const __bf16* crow = index_rows(a.index);
-  const float* cbias = index_bias(a.index, a.n_pad, D);
-
-  bf16x8 bfrag[KS];
-#pragma unroll
-  for (int s = 0; s < KS; ++s) bfrag[s] = *reinterpret_cast<const bf16x8*>(a.qb + qg * D + 16 * s + 8 * h);
-  const float margin2 = a.margin2[qg];
-  if (tid < kQPerWG) {
-    const int64_t q = static_cast<int64_t>(blockIdx.x) * kQPerWG + tid;
-    cnt_s[tid] = 0;
-    thr_s[tid] = (q < a.nq) ? -INFINITY : INFINITY;
-  }
-  uint2* mybuf_base = a.buf + (static_cast<int64_t>(blockIdx.x) * kQPerWG + wave * kQPerWave) * a.cap;
-  bool ovf = false;
-
-  u32x4 ra[CPT];
-  float rb = 0.0f;
-  auto gload = [&](int64_t base) {
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int c = tid + kScreenThreads * i;
-      if (c < kCTile * CH) {
-        const int row = c / CH, ch = c % CH;
-        ra[i] = *reinterpret_cast<const u32x4*>(crow + (base + row) * D + ch * 8);
-      }
+    if (w1 > lim1) {
+      ovf1 = true;
+      tau1 = INFINITY;
     }
-    if (tid < kCTile) rb = cbias[base + tid];
-  };
-  auto lstore = [&](int b) {
-    char* B = smem + b * BUF_BYTES;
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int c = tid + kScreenThreads * i;
-      if (c < kCTile * CH) {
-        const int row = c / CH, ch = c % CH;
-        const int swz = (row * CH / 16) % CH;
-        *reinterpret_cast<u32x4*>(B + row * (CH * 16) + ((ch ^ swz) << 4)) = ra[i];
+    load_frags(af2, B, 1);
+    block(af, 0, cbase);
+    if (u + 1 < nv) {  // mid-tile: tile u + 1 landed, every wave holds block (u, 1)
+      wait_vmcnt_atmost((wa - da) + wb + wc);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      wa = wb;
+      da = db;
+      wb = wc;
+      db = dc;
+      dc = 0;
+      if (u + 4 < nv) {
+        issue(phys(u + 4), (u + 4) % kStages);
+        dc = dpieces;
       }
+      wc = dc;
+      load_frags(af, smem + ((u + 1) % kStages) * TILE_BYTES, 0);
     }
-    if (tid < kCTile) reinterpret_cast<float*>(B + A_BYTES)[tid] = rb;
-  };
-
-  const int ntiles = static_cast<int>(a.n_pad / kCTile);
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  float thr = thr_s[ql];
-
-  for (int tile = 0; tile < ntiles; ++tile) {
-    const int cur = tile & 1;
-    const bool more = tile + 1 < ntiles;
-    if (more) gload(static_cast<int64_t>(tile + 1) * kCTile);
-    const char* B = smem + cur * BUF_BYTES;
-    const float* bias = reinterpret_cast<const float*>(B + A_BYTES);
-
-    const bool need = cnt_s[ql] > a.cap - kCTile;
-    uint64_t needm = __ballot(need) & 0xFFFFFFFFull;
-    if (needm) __threadfence_block();
-    while (needm) {
-      const int qq = __ffsll(static_cast<long long>(needm)) - 1;
-      needm &= needm - 1;
-      const float mq = __shfl(margin2, qq, kWave);
-      float nthr;
-      const int nc = compact_shortlist<NPL>(mybuf_base + static_cast<int64_t>(qq) * a.cap,
-                                            cnt_s[wave * kQPerWave + qq], a.k, mq, &nthr);
-      if (lane == 0) {
-        if (nc > a.cap - kCTile) {  // cannot make room: exact fallback in finalize
-          cnt_s[wave * kQPerWave + qq] = 0;
-          thr_s[wave * kQPerWave + qq] = INFINITY;
-        } else {
-          cnt_s[wave * kQPerWave + qq] = nc;
-          thr_s[wave * kQPerWave + qq] = nthr;
-        }
-      }
-      if (nc > a.cap - kCTile && l32 == qq) ovf = true;
-      __builtin_amdgcn_wave_barrier();
-    }
-    thr = thr_s[ql];
-
-    const int64_t cbase = static_cast<int64_t>(tile) * kCTile;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      f32x16 acc;
-#pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4) {
-        const f32x4 b4 = *reinterpret_cast<const f32x4*>(bias + 32 * t + 8 * r4 + 4 * h);
-        acc[4 * r4 + 0] = b4[0];
-        acc[4 * r4 + 1] = b4[1];
-        acc[4 * r4 + 2] = b4[2];
-        acc[4 * r4 + 3] = b4[3];
-      }
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const int row = 32 * t + l32, ch = 2 * s + h;
-        const int swz = (row * CH / 16) % CH;
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(B + row * (CH * 16) + ((ch ^ swz) << 4));
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfrag[s], acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const bool hit = acc[r] > thr;
-        if (__any(hit)) {
-          if (hit) {
-            const int slot = atomicAdd(&cnt_s[ql], 1);
-            const unsigned cidx = static_cast<unsigned>(cbase + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h);
-            mybuf_base[static_cast<int64_t>(l32) * a.cap + slot] = make_uint2(__float_as_uint(acc[r]), cidx);
-          }
-        }
-      }
-    }
-    if (more) lstore(cur ^ 1);
-    __syncthreads();
+    block(af2, 1, cbase);
   }
-  if (h == 0) a.count[qg] = ovf ? -1 : cnt_s[ql];
+  const int cnt0 = static_cast<int>(w0 - reg0), cnt1 = static_cast<int>(w1 - reg1);
+  a.count[(q0 * a.S + split) * 2 + h] = ovf0 ? -1 : cnt0;
+  a.count[(q1 * a.S + split) * 2 + h] = ovf1 ? -1 : cnt1;
+  TT_STAT(0, cnt0 + cnt1);
+  }
 }
 
 // ---- finalize ------------------------------------------------------------
@@ -767,77 +572,49 @@ __device__ __forceinline__ float exact_score(const float* __restrict__ qs, const
   return acc;
 }
 
-struct FinalArgs {
-  const float* q;  // fp32 queries of this chunk
-  int64_t ldq;
-  const float* cand;
-  int64_t ldc;
-  int64_t n;
-  int dim;
-  int k;
-  int S;     // splits
-  int H;     // regions per split (2 bins path, 1 compaction path)
-  int R;     // entries per region
-  int L;     // LDS list capacity
-  int P;     // bitonic sort size (pow2 >= k)
-  int vec4;  // candidate rows are 16-byte aligned float4 rows
-  int pairs; // entries are (max of candidates c, c+1; c) pairs (bins path)
-  int64_t nq;
-  int64_t index_offset;
-  const float* margin2;
+// Lists of one query: `nseg` segments; segment j starts at
+// buf + seg_base(q, j) and holds count[q * nseg + j] entries (-1: overflowed);
+// its screen kept s~ > tau[q * tau_per_q + j / seg_per_tau].
+struct Lists {
   const uint2* buf;
   const int* count;
-  const unsigned* thr;  // null for the compaction path
-  float* out_s;
-  int32_t* out_i;
+  const float* tau;
+  int nseg;
+  int cap;          // region form: segment j of query q at (q * nseg + j) * cap
+  const int64_t* off;  // CSR form (cap == 0): segment j of query q at off[q * nseg + j]
+  int tau_per_q;
+  int seg_per_tau;
 };
 
-// Keeps list entries with sc > thr (in place, whole wave).  Returns the count.
-__device__ __forceinline__ int filter_list(float* sc, unsigned* id, int n, float thr) {
-  int out = 0;
-  for (int j0 = 0; j0 < n; j0 += kWave) {
-    const int j = j0 + lane_id();
-    const float s = j < n ? sc[j] : 0.0f;
-    const unsigned i = j < n ? id[j] : 0u;
-    const bool keep = j < n && s > thr;
-    const uint64_t m = __ballot(keep);
-    __syncthreads();  // all reads of this chunk before any write into it
-    if (keep) {
-      const int p = out + __popcll(m & lanemask_lt64());
-      sc[p] = s;
-      id[p] = i;
-    }
-    out += __popcll(m);
-  }
-  __syncthreads();
-  return out;
+__device__ __forceinline__ const uint2* seg_ptr(const Lists& L, int64_t q, int j) {
+  const int64_t i = q * L.nseg + j;
+  return L.buf + (L.cap ? i * L.cap : L.off[i]);
 }
 
-// Radix select on the list's score order keys with 8-bit digits and an LDS
-// histogram (one wave): after `passes` digits, `prefix` holds the top
-// 8*passes bits of the K-th largest key, `above` = #keys whose top bits are
-// greater, `at` = #keys sharing the prefix (above < K <= above + at).
+// Radix select with 8-bit digits and an LDS histogram (one wave) over keys
+// produced by `key_at(j)` for j < n (all lanes call with the same n).  After
+// `passes` digits, `prefix` holds the top 8*passes bits of the K-th largest
+// key, `above` = #keys whose top bits are greater, `at` = #keys sharing the
+// prefix (above < K <= above + at).
 struct Kth {
   unsigned prefix;
   int above;
   int at;
 };
 
-__device__ Kth radix_select(const float* sc, int n, int K, int passes, unsigned* hist) {
+template <class Hist>
+__device__ Kth radix_select(Hist&& fill, int K, int passes, unsigned* hist) {
   const int lane = lane_id();
   unsigned prefix = 0;
-  int above = 0, at = n;
+  int above = 0, at = 0;
   for (int d = 0; d < passes; ++d) {
     const int shift = 24 - 8 * d;
     const unsigned hi_mask = d == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
 #pragma unroll
     for (int u = 0; u < 4; ++u) hist[4 * lane + u] = 0;
-    __syncthreads();
-    for (int j = lane; j < n; j += kWave) {
-      const unsigned key = float_order_key(sc[j]);
-      if ((key & hi_mask) == prefix) atomicAdd(&hist[(key >> shift) & 0xFFu], 1u);
-    }
-    __syncthreads();
+    wsync();
+    fill(prefix, hi_mask, shift);
+    wsync();
     // counts at or above each bin: lane L owns bins 4L..4L+3
     unsigned h4[4];
 #pragma unroll
@@ -860,6 +637,10 @@ __device__ Kth radix_select(const float* sc, int n, int K, int passes, unsigned*
     for (int u = 0; u < 4; ++u)
       if (static_cast<int>(cum[u]) >= need) best = 4 * lane + u;
     const uint64_t m = __ballot(best >= 0);
+    if (m == 0) {  // fewer than K keys
+      wsync();
+      return Kth{0u, 0, -1};
+    }
     const int src = 63 - __clzll(m);
     const int b = __shfl(best, src, kWave);
     const int u = b & 3;
@@ -870,33 +651,27 @@ __device__ Kth radix_select(const float* sc, int n, int K, int passes, unsigned*
     above += static_cast<int>(cumb - hb);
     at = static_cast<int>(hb);
     prefix |= static_cast<unsigned>(b) << shift;
-    __syncthreads();
+    wsync();
   }
   return Kth{prefix, above, at};
 }
 
-// Screened cut: tau = lower bound of the K-th largest screened score (16-bit
-// key prefix); keeps s > next_down(tau - margin2).  Raises *thr.
-__device__ int coarse_cut(float* sc, unsigned* id, int n, int K, float margin2, float* thr, unsigned* hist) {
-  if (n <= K) return n;
-  const Kth r = radix_select(sc, n, K, 2, hist);
-  const float tau = order_key_float(r.prefix);
-  if (!(tau > -INFINITY)) return n;
-  const float t = next_down(margin2 > 0.0f ? tau - margin2 : tau);
-  if (t <= *thr) return n;
-  *thr = t;
-  return filter_list(sc, id, n, t);
-}
-
-// Exact selection: keeps exactly the K best entries by (score desc, index
-// asc); *thr = the K-th score (later candidates of an in-order scan need a
-// strictly larger score).
+// Exact selection in LDS: keeps exactly the K best entries by (score desc,
+// index asc); *thr = the K-th score (later candidates of an in-order scan need
+// a strictly larger score).
 __device__ int exact_select(float* sc, unsigned* id, int n, int K, float* thr, unsigned* hist) {
   if (n <= K) {
     *thr = -INFINITY;
     return n;
   }
-  const Kth r = radix_select(sc, n, K, 4, hist);
+  const Kth r = radix_select(
+      [&](unsigned prefix, unsigned hi_mask, int shift) {
+        for (int j = lane_id(); j < n; j += kWave) {
+          const unsigned key = float_order_key(sc[j]);
+          if ((key & hi_mask) == prefix) atomicAdd(&hist[(key >> shift) & 0xFFu], 1u);
+        }
+      },
+      K, 4, hist);
   const unsigned res = r.prefix;  // exact key of the K-th score
   const int need = K - r.above;   // ties at the K-th score to keep, lowest indices first
   unsigned cut = 0xFFFFFFFFu;
@@ -923,7 +698,7 @@ __device__ int exact_select(float* sc, unsigned* id, int n, int K, float* thr, u
     const unsigned key = float_order_key(s);
     const bool keep = j < n && (key > res || (key == res && i <= cut));
     const uint64_t m = __ballot(keep);
-    __syncthreads();
+    wsync();
     if (keep) {
       const int p = out + __popcll(m & lanemask_lt64());
       sc[p] = s;
@@ -931,137 +706,20 @@ __device__ int exact_select(float* sc, unsigned* id, int n, int K, float* thr, u
     }
     out += __popcll(m);
   }
-  __syncthreads();
+  wsync();
   *thr = order_key_float(res);
   return out;
 }
 
-__global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char fsm[];
-  float* qs = reinterpret_cast<float*>(fsm);  // query row (dim <= 128)
-  float* sc = qs + 128;
-  unsigned* id = reinterpret_cast<unsigned*>(sc + a.L);
-  unsigned long long* sk = reinterpret_cast<unsigned long long*>(id + a.L);
-  unsigned* hist = reinterpret_cast<unsigned*>(sk + a.P);  // 256 radix bins
-  const int64_t q = blockIdx.x;
+// Ranks the n <= P entries (score desc, index asc) and writes the first k.
+__device__ void rank_and_write(const float* sc, const unsigned* id, int n, int k, int P, unsigned long long* sk,
+                               float* out_s, int32_t* out_i) {
   const int lane = lane_id();
-#ifdef TT_INDEX_NOINSERT
-  return;  // probe build: the screen inserted nothing
-#endif
-  for (int e = lane; e < a.dim; e += kWave) qs[e] = a.q[q * a.ldq + e];
-  const float m2 = a.margin2[q];
-  float thr = (a.thr && a.thr[q]) ? order_key_float(a.thr[q]) : -INFINITY;
-  const int nreg = a.S * a.H;
-  bool ovf = false;
-  for (int r = 0; r < nreg; ++r) ovf = ovf || a.count[q * nreg + r] < 0;
-  __syncthreads();
-
-  int n = 0;
-  if (!ovf) {
-    // Gather the entries above the final threshold; cut whenever the list fills.
-    for (int r = 0; r < nreg && !ovf; ++r) {
-      const int c = a.count[q * nreg + r];
-      const uint2* reg = a.buf + (q * nreg + r) * static_cast<int64_t>(a.R);
-      for (int j0 = 0; j0 < c && !ovf; j0 += 4 * kWave) {
-        uint2 e[4];  // four chunks in flight
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int j = j0 + u * kWave + lane;
-          e[u] = j < c ? reg[j] : make_uint2(0u, 0u);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int j = j0 + u * kWave + lane;
-          const float s = __uint_as_float(e[u].x);
-          const bool keep = j < c && s > thr;
-          const uint64_t m = __ballot(keep);
-          if (keep) {
-            const int p = n + __popcll(m & lanemask_lt64());
-            sc[p] = s;
-            id[p] = e[u].y;
-          }
-          n += __popcll(m);
-          if (n > a.L - kWave) {
-            __syncthreads();
-            if (m2 > 0.0f) {
-              n = coarse_cut(sc, id, n, a.k, m2, &thr, hist);
-            } else {  // zero query: screened scores are exact, cut ties by index
-              float t;
-              n = exact_select(sc, id, n, a.k, &t, hist);
-              thr = fmaxf(thr, next_down(t));
-            }
-            if (n > a.L - kWave) {
-              ovf = true;
-              break;
-            }
-          }
-        }
-      }
-    }
-    __syncthreads();
-  }
-  if (!ovf) {
-    n = coarse_cut(sc, id, n, a.k, m2, &thr, hist);
-    ovf = n < a.k;  // cannot happen with a valid screen; answer exactly regardless
-  }
-  if (!ovf && a.pairs) {
-    // expand pair entries into their two candidates (c, c + 1), top chunk first
-    if (2 * n > a.L) {
-      ovf = true;
-    } else {
-      for (int j0 = (n - 1) / kWave * kWave; j0 >= 0; j0 -= kWave) {
-        const int j = j0 + lane;
-        const unsigned c = j < n ? id[j] : 0u;
-        __syncthreads();
-        if (j < n) {
-          id[2 * j] = c;
-          id[2 * j + 1] = c + 1;
-        }
-        __syncthreads();
-      }
-      n *= 2;
-    }
-  }
-  if (!ovf) {
-    for (int j = lane; j < n; j += kWave) {
-      const unsigned c = id[j];
-      sc[j] = c < static_cast<uint64_t>(a.n)
-                  ? exact_score(qs, a.cand + static_cast<int64_t>(c) * a.ldc, a.dim, a.vec4 != 0) + 0.0f
-                  : -INFINITY;  // c + 1 past the last candidate
-    }
-    __syncthreads();
-  } else {
-    // Exact fallback: scan every candidate with the fp32 chain (in index
-    // order, so a strict threshold at the K-th score is exact).
-    float ethr = -INFINITY;
-    n = 0;
-    for (int64_t c0 = 0; c0 < a.n; c0 += kWave) {
-      const int64_t c = c0 + lane;
-      float s = -INFINITY;
-      if (c < a.n) s = exact_score(qs, a.cand + c * a.ldc, a.dim, a.vec4 != 0) + 0.0f;
-      const bool keep = c < a.n && s > ethr;
-      const uint64_t m = __ballot(keep);
-      if (keep) {
-        const int p = n + __popcll(m & lanemask_lt64());
-        sc[p] = s;
-        id[p] = static_cast<unsigned>(c);
-      }
-      n += __popcll(m);
-      if (n > a.L - kWave) {
-        __syncthreads();
-        n = exact_select(sc, id, n, a.k, &ethr, hist);
-      }
-    }
-    __syncthreads();
-  }
-  float kth;
-  n = exact_select(sc, id, n, a.k, &kth, hist);
-  // Rank: bitonic sort of (score, -index) keys, descending.
-  for (int j = lane; j < a.P; j += kWave) sk[j] = j < n ? make_key(sc[j], id[j]) : 0ull;
-  for (int size = 2; size <= a.P; size <<= 1) {
+  for (int j = lane; j < P; j += kWave) sk[j] = j < n ? make_key(sc[j], id[j]) : 0ull;
+  for (int size = 2; size <= P; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      __syncthreads();
-      for (int i = lane; i < a.P / 2; i += kWave) {
+      wsync();
+      for (int i = lane; i < P / 2; i += kWave) {
         const int lo = 2 * i - (i & (stride - 1));
         const int hi = lo + stride;
         const bool desc = (lo & size) == 0;
@@ -1073,91 +731,386 @@ __global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
       }
     }
   }
-  __syncthreads();
-  for (int t = lane; t < a.k; t += kWave) {
+  wsync();
+  for (int t = lane; t < k; t += kWave) {
     const unsigned long long key = sk[t];
-    a.out_s[q * a.k + t] = order_key_float(static_cast<unsigned>(key >> 32));
-    a.out_i[q * a.k + t] =
-        static_cast<int32_t>(static_cast<int64_t>(0xFFFFFFFFu - static_cast<unsigned>(key)) + a.index_offset);
+    out_s[t] = order_key_float(static_cast<unsigned>(key >> 32));
+    out_i[t] = static_cast<int32_t>(0xFFFFFFFFu - static_cast<unsigned>(key));
+  }
+}
+
+struct FinalArgs {
+  const float* q;       // fp32 queries of this chunk
+  int64_t ldq;
+  const float* cand;    // fp32 rows; entry id e is row e - cand_offset
+  int64_t ldc;
+  int64_t n_rows;
+  int64_t cand_offset;
+  int64_t zero_base;    // id of row 0 in the output numbering (zero queries)
+  int dim;
+  int k;
+  int L;                // LDS list capacity
+  int P;                // bitonic sort size (pow2 >= k)
+  int vec4;             // candidate rows are 16-byte aligned float4 rows
+  int64_t nq;
+  const int* qflags;
+  const float* qmarg;
+  Lists lists;
+  float* out_s;
+  int32_t* out_i;
+  int* fail_count;
+  int* fail_list;
+};
+
+__host__ __device__ inline size_t final_lds_bytes(int L, int P) {
+  return 128 * sizeof(float) + static_cast<size_t>(L) * 8 + static_cast<size_t>(P) * 8 + 256 * sizeof(unsigned);
+}
+
+__global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char fsm[];
+  float* qs = reinterpret_cast<float*>(fsm);  // query row (dim <= 128)
+  float* sc = qs + 128;
+  unsigned* id = reinterpret_cast<unsigned*>(sc + a.L);
+  unsigned long long* sk = reinterpret_cast<unsigned long long*>(id + a.L);
+  unsigned* hist = reinterpret_cast<unsigned*>(sk + a.P);  // 256 radix bins
+  const int64_t q = blockIdx.x;
+  const int lane = lane_id();
+  const int K = a.k;
+  const Lists& Ls = a.lists;
+#ifdef TT_INDEX_NOINSERT
+  return;  // probe build: the screen kept nothing
+#endif
+  float* out_s = a.out_s + q * K;
+  int32_t* out_i = a.out_i + q * K;
+  const int fl = a.qflags[q];
+  if (fl & kQZero) {  // every score is exactly +0: indices 0..k-1 by the tie rule
+    for (int t = lane; t < K; t += kWave) {
+      out_s[t] = 0.0f;
+      out_i[t] = static_cast<int32_t>(a.zero_base + t);
+    }
+    return;
+  }
+  const bool rel = (fl & kQRel) != 0;
+  const float m = a.qmarg[q];
+  bool fail = false;
+  int ntot = 0;
+  float tmax = -INFINITY;
+  for (int j = 0; j < Ls.nseg; ++j) {
+    const int c = Ls.count[q * Ls.nseg + j];
+    fail = fail || c < 0;
+    ntot += c;
+  }
+  for (int j = 0; j < Ls.nseg; j += Ls.seg_per_tau) tmax = fmaxf(tmax, Ls.tau[q * Ls.tau_per_q + j / Ls.seg_per_tau]);
+  fail = fail || ntot < K;
+  float X = -INFINITY;
+  if (!fail) {
+    // K-th largest screened score to a 24-bit key prefix (rounded down)
+    const Kth r = radix_select(
+        [&](unsigned prefix, unsigned hi_mask, int shift) {
+          for (int j = 0; j < Ls.nseg; ++j) {
+            const int c = Ls.count[q * Ls.nseg + j];
+            const uint2* e = seg_ptr(Ls, q, j);
+            for (int i = lane; i < c; i += kWave) {
+              const unsigned key = float_order_key(__uint_as_float(e[i].x));
+              if ((key & hi_mask) == prefix) atomicAdd(&hist[(key >> shift) & 0xFFu], 1u);
+            }
+          }
+        },
+        K, 3, hist);
+    fail = r.at < 0;
+    if (!fail) {
+      // certificate (below) is the only reason counted in stats[1]
+      X = lb_of(order_key_float(r.prefix), m, rel);
+      // certificate: every list kept all s~ > tau, and ub(s~) <= ub(tau) < X
+      // rules a candidate out of the exact top-K (which has K members >= X).
+      fail = !(X > ub_of(tmax, m, rel));
+      if (fail) TT_STAT0(1, 1);
+    }
+  }
+  int n = 0;
+  if (!fail) {
+    for (int e = lane; e < a.dim; e += kWave) qs[e] = a.q[q * a.ldq + e];
+    for (int j = 0; j < Ls.nseg && !fail; ++j) {
+      const int c = Ls.count[q * Ls.nseg + j];
+      const uint2* e = seg_ptr(Ls, q, j);
+      for (int i0 = 0; i0 < c; i0 += kWave) {
+        const int i = i0 + lane;
+        const uint2 en = i < c ? e[i] : make_uint2(0u, 0u);
+        const bool keepit = i < c && ub_of(__uint_as_float(en.x), m, rel) >= X;
+        const uint64_t bm = __ballot(keepit);
+        if (n + __popcll(bm) > a.L) {
+          fail = true;
+          break;
+        }
+        if (keepit) {
+          const int p = n + __popcll(bm & lanemask_lt64());
+          id[p] = en.y;
+        }
+        n += __popcll(bm);
+      }
+    }
+    wsync();
+  }
+  if (fail) {
+    if (lane == 0) {
+      const int slot = atomicAdd(a.fail_count, 1);
+      a.fail_list[slot] = static_cast<int>(q);
+    }
+    TT_STAT0(3, 1);
+    return;
+  }
+  TT_STAT0(2, n);
+  for (int j = lane; j < n; j += kWave) {
+    const int64_t row = static_cast<int64_t>(id[j]) - a.cand_offset;
+    sc[j] = exact_score(qs, a.cand + row * a.ldc, a.dim, a.vec4 != 0) + 0.0f;
+  }
+  wsync();
+  float kth;
+  n = exact_select(sc, id, n, K, &kth, hist);
+  rank_and_write(sc, id, n, K, a.P, sk, out_s, out_i);
+}
+
+// Exact fallback for the queries the finalize could not certify.  A
+// persistent grid of 4-wave workgroups takes work items from a global
+// counter: item (f, p) scans part p of the candidate rows for failed query f
+// with the fp32 chain (wave w takes the part's 64-row chunks w, w + 4, ... in
+// index order, so a strict threshold at its running K-th score is exact),
+// merges its waves' exact top-K lists and writes them to scratch slot (f, p);
+// the workgroup that completes a query's last part merges the P lists and
+// writes the answer.  Queries beyond the scratch slots are scanned whole by
+// one workgroup.
+constexpr int kFbWaves = 4;
+constexpr int kFbSlots = 1024;       // failed queries served by the parallel form per chunk
+constexpr int kFbGrid = 512;         // persistent workgroups
+
+struct FallbackArgs {
+  const float* q;
+  int64_t ldq;
+  const float* cand;  // the rows to scan (all of them)
+  int64_t ldc;
+  int64_t n_rows;
+  int64_t id_base;    // output id of row 0
+  int dim;
+  int k;
+  int L;              // per-wave list capacity
+  int P;              // bitonic sort size
+  int parts;          // candidate parts per failed query (parts * k <= 8192)
+  int vec4;
+  const int* fail_count;
+  const int* fail_list;
+  int* ctrl;          // [0] item counter, [1 + f] parts done of slot f (zeroed per chunk)
+  uint2* scratch;     // [kFbSlots][parts][k]
+  int* scratch_n;     // [kFbSlots][parts]
+  float* out_s;
+  int32_t* out_i;
+};
+
+__host__ __device__ inline int fallback_merge_cap(int parts, int k) {
+  return parts * k > kFbWaves * k ? parts * k : kFbWaves * k;
+}
+__host__ __device__ inline size_t fallback_lds_bytes(int L, int P, int parts, int k) {
+  return 128 * sizeof(float) + static_cast<size_t>(kFbWaves) * (static_cast<size_t>(L) * 8 + 256 * sizeof(unsigned)) +
+         static_cast<size_t>(fallback_merge_cap(parts, k)) * 8 + static_cast<size_t>(P) * 8 + 16 * sizeof(int);
+}
+
+__global__ void __launch_bounds__(kFbWaves * kWave) fallback_kernel(const FallbackArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char fsm[];
+  const int wave = threadIdx.x / kWave;
+  const int lane = lane_id();
+  const int K = a.k, PT = a.parts;
+  float* qs = reinterpret_cast<float*>(fsm);
+  char* wbase = fsm + 128 * sizeof(float) + static_cast<size_t>(wave) * (static_cast<size_t>(a.L) * 8 + 1024);
+  float* sc = reinterpret_cast<float*>(wbase);
+  unsigned* id = reinterpret_cast<unsigned*>(sc + a.L);
+  unsigned* hist = id + a.L;
+  const int MC = fallback_merge_cap(PT, K);
+  char* mbase = fsm + 128 * sizeof(float) + static_cast<size_t>(kFbWaves) * (static_cast<size_t>(a.L) * 8 + 1024);
+  float* msc = reinterpret_cast<float*>(mbase);
+  unsigned* mid = reinterpret_cast<unsigned*>(msc + MC);
+  unsigned long long* sk = reinterpret_cast<unsigned long long*>(mid + MC);
+  int* sh = reinterpret_cast<int*>(sk + a.P);  // [0] item, [1..4] wave counts, [5] merge flag
+  const int nf = *a.fail_count;
+  const int npar = nf < kFbSlots ? nf : kFbSlots;
+  const int total = npar * PT + (nf - npar);
+  for (;;) {
+    __syncthreads();
+    if (threadIdx.x == 0) sh[0] = atomicAdd(&a.ctrl[0], 1);
+    __syncthreads();
+    const int item = sh[0];
+    if (item >= total) break;
+    const bool part = item < npar * PT;
+    const int f = part ? item / PT : npar + (item - npar * PT);
+    const int pi = part ? item % PT : 0;
+    const int64_t q = a.fail_list[f];
+    const int64_t r0 = part ? (a.n_rows * pi) / PT : 0;
+    const int64_t r1 = part ? (a.n_rows * (pi + 1)) / PT : a.n_rows;
+    for (int e = threadIdx.x; e < a.dim; e += blockDim.x) qs[e] = a.q[q * a.ldq + e];
+    __syncthreads();
+    float ethr = -INFINITY;
+    int n = 0;
+    for (int64_t c0 = r0 + static_cast<int64_t>(wave) * kWave; c0 < r1; c0 += kFbWaves * kWave) {
+      const int64_t c = c0 + lane;
+      float sv = -INFINITY;
+      if (c < r1) sv = exact_score(qs, a.cand + c * a.ldc, a.dim, a.vec4 != 0) + 0.0f;
+      const bool keepit = c < r1 && sv > ethr;
+      const uint64_t m = __ballot(keepit);
+      if (keepit) {
+        const int pp = n + __popcll(m & lanemask_lt64());
+        sc[pp] = sv;
+        id[pp] = static_cast<unsigned>(a.id_base + c);
+      }
+      n += __popcll(m);
+      if (n > a.L - kWave) {
+        wsync();
+        n = exact_select(sc, id, n, K, &ethr, hist);
+      }
+    }
+    wsync();
+    float kth;
+    n = exact_select(sc, id, n, K, &kth, hist);
+    for (int j = lane; j < n; j += kWave) {
+      msc[wave * K + j] = sc[j];
+      mid[wave * K + j] = id[j];
+    }
+    if (lane == 0) sh[1 + wave] = n;
+    __syncthreads();
+    if (wave == 0) {
+      int nm = sh[1];
+      for (int w = 1; w < kFbWaves; ++w) {  // compact the wave lists to the front
+        const int cw = sh[1 + w];
+        for (int j0 = 0; j0 < cw; j0 += kWave) {
+          const int j = j0 + lane;
+          const float sv = j < cw ? msc[w * K + j] : 0.0f;
+          const unsigned iv = j < cw ? mid[w * K + j] : 0u;
+          wsync();
+          if (j < cw) {
+            msc[nm + j] = sv;
+            mid[nm + j] = iv;
+          }
+          wsync();
+        }
+        nm += cw;
+      }
+      nm = exact_select(msc, mid, nm, K, &kth, hist);
+      if (!part) {
+        rank_and_write(msc, mid, nm, K, a.P, sk, a.out_s + q * K, a.out_i + q * K);
+        if (lane == 0) sh[5] = 0;
+      } else {
+        uint2* dst = a.scratch + (static_cast<int64_t>(f) * PT + pi) * K;
+        for (int j = lane; j < nm; j += kWave) dst[j] = make_uint2(__float_as_uint(msc[j]), mid[j]);
+        if (lane == 0) a.scratch_n[f * PT + pi] = nm;
+        __threadfence();  // the part's list is visible chip-wide before it is counted
+        int last = 0;
+        if (lane == 0) last = atomicAdd(&a.ctrl[1 + f], 1) == PT - 1;
+        last = __shfl(last, 0, kWave);
+        if (lane == 0) sh[5] = last;
+      }
+    }
+    __syncthreads();
+    if (part && sh[5] && wave == 0) {  // every part of query f is in scratch: merge them
+      __threadfence();
+      int nm = 0;
+      for (int pj = 0; pj < PT; ++pj) {
+        const int cj = a.scratch_n[f * PT + pj];
+        const uint2* src = a.scratch + (static_cast<int64_t>(f) * PT + pj) * K;
+        for (int j = lane; j < cj; j += kWave) {
+          const uint2 e = src[j];
+          msc[nm + j] = __uint_as_float(e.x);
+          mid[nm + j] = e.y;
+        }
+        nm += cj;
+      }
+      wsync();
+      nm = exact_select(msc, mid, nm, K, &kth, hist);
+      rank_and_write(msc, mid, nm, K, a.P, sk, a.out_s + q * K, a.out_i + q * K);
+    }
   }
 }
 
 // ---- host plan -------------------------------------------------------------
 struct SearchPlan {
-  bool bins;
-  int S, H, R, L, P;
+  int S, NS, jsel, cap, L, P, k, parts;
   int64_t chunk;
 };
 
-SearchPlan plan_search(int64_t nq, int64_t n_cand, int k) {
+// R = target list entries per query over the whole candidate set (~3k), split
+// evenly over `parts` = S splits x `shards` ranks screening disjoint ranges.
+SearchPlan plan_search(int64_t nq, int64_t n_cand, int k, int shards) {
   SearchPlan p{};
   const int64_t ntiles = ceil_div(n_cand, kCTile);
   p.P = next_pow2(k < 2 ? 2 : k);
-  p.bins = k <= kBinsMaxK;
-  p.H = p.bins ? 2 : 1;
-  p.R = p.bins ? kLaneCap : cap_for_k(k);
-  p.L = p.bins ? 1024 : (p.R > 2048 ? p.R : 2048);
-  p.S = 1;
-  p.chunk = nq < kMaxChunk ? (nq > 0 ? nq : 1) : kMaxChunk;
-  for (int pass = 0; pass < 3; ++pass) {
-    if (p.bins) {  // enough workgroups for the chip: split the candidates of few query blocks
-      const int64_t qblocks = ceil_div(p.chunk, kQPerWG);
-      p.S = 1;
-      while (p.S < kMaxSplits && qblocks * p.S * kScreenWaves < 2048 && ntiles / (2 * p.S) >= 64) p.S *= 2;
-#ifdef TT_FORCE_SPLITS
-      p.S = TT_FORCE_SPLITS;
-#endif
-    }
-    const size_t per_query = static_cast<size_t>(p.S) * p.H * p.R * sizeof(uint2);
-    int64_t chunk = static_cast<int64_t>(kShortlistBudget / per_query) / kQPerWG * kQPerWG;
-    if (chunk < kQPerWG) chunk = kQPerWG;
-    if (chunk > p.chunk) chunk = p.chunk;
-    p.chunk = chunk;
+  p.k = k;
+  p.parts = 8192 / k < 1 ? 1 : (8192 / k > 64 ? 64 : 8192 / k);
+  p.L = static_cast<int>(round_up(2 * static_cast<int64_t>(k) + 256, kWave));
+  const int64_t qblocks = ceil_div(nq > 0 ? nq : 1, kQPerWG);
+  p.S = 1;  // enough workgroups for the 256 CUs: split the candidates of few query blocks
+  while (p.S < kMaxSplits && qblocks * p.S < 256 && ntiles / (2 * p.S) >= 64) p.S *= 2;
+  const int64_t nts = ceil_div(ntiles, p.S);  // tiles per split
+  const double ns_cand = static_cast<double>(nts) * kCTile;
+  const double R = (3.0 * k + 100.0) / (static_cast<double>(p.S) * (shards > 0 ? shards : 1));
+  double mu;  // expected entries per (query, split, lane half)
+  if (nts < 16 || R >= 0.25 * ns_cand) {
+    p.NS = 0;  // keep every score of the split
+    p.jsel = 1;
+    mu = ns_cand / 2.0;
+  } else {
+    // 64 bins of NS samples each; the smallest bin must sit well below
+    // rank R: NS <= N ln64 / (1.5 R)
+    const double ns_max = ns_cand * std::log(64.0) / (1.5 * R);
+    int NS = static_cast<int>(nts / 4 < kMaxSample ? nts / 4 : kMaxSample);
+    if (NS > ns_max) NS = static_cast<int>(ns_max);
+    if (NS < 1) NS = 1;
+    p.NS = NS;
+    const double pbin = 1.0 - std::exp(-1.0 * NS * R / ns_cand);
+    int j = static_cast<int>(std::lround(64.0 * pbin));
+    p.jsel = j < 1 ? 1 : (j > 64 ? 64 : j);
+    mu = R / 2.0;
   }
+  p.cap = next_pow2(static_cast<int>(3.0 * mu) + 64);
+  const size_t per_query = static_cast<size_t>(p.S) * 2 * p.cap * sizeof(uint2);
+  int64_t chunk = static_cast<int64_t>(kListBudget / per_query) / kQPerWG * kQPerWG;
+  if (chunk < kQPerWG) chunk = kQPerWG;
+  const int64_t need = round_up(nq > 0 ? nq : 1, kQPerWG);
+  p.chunk = chunk < need ? chunk : need;
   return p;
-}
-
-size_t final_lds_bytes(const SearchPlan& p) {
-  return 128 * sizeof(float) + static_cast<size_t>(p.L) * 8 + static_cast<size_t>(p.P) * 8 + 256 * sizeof(unsigned);
 }
 
 struct SearchWs {
   __bf16* qb;
-  float* margin2;
+  int* qflags;
+  float* qmarg;
   uint2* buf;
   int* count;
-  unsigned* thr;
+  float* tau;
+  int* fail_count;  // [0] failures, then the fallback's ctrl words
+  int* fail_list;
+  uint2* fb_scratch;
+  int* fb_scratch_n;
 };
 
-SearchWs carve_search(Carver& cv, int64_t nq, int D, const SearchPlan& p) {
-  const int64_t chunk = nq < p.chunk ? nq : p.chunk;
-  const int64_t nq_pad = round_up(chunk > 0 ? chunk : 1, kQPerWG);
+SearchWs carve_search(Carver& cv, int D, const SearchPlan& p) {
+  const int64_t nq_pad = p.chunk;
   SearchWs w;
   w.qb = cv.take<__bf16>(nq_pad * D);
-  w.margin2 = cv.take<float>(nq_pad);
-  w.buf = cv.take<uint2>(nq_pad * p.S * p.H * static_cast<int64_t>(p.R));
-  w.count = cv.take<int>(nq_pad * p.S * p.H);
-  w.thr = cv.take<unsigned>(nq_pad);
+  w.qflags = cv.take<int>(nq_pad);
+  w.qmarg = cv.take<float>(nq_pad);
+  w.buf = cv.take<uint2>(nq_pad * p.S * 2 * static_cast<int64_t>(p.cap));
+  w.count = cv.take<int>(nq_pad * p.S * 2);
+  w.tau = cv.take<float>(nq_pad * p.S);
+  w.fail_count = cv.take<int>(2 + kFbSlots);
+  w.fail_list = cv.take<int>(nq_pad);
+  w.fb_scratch = cv.take<uint2>(static_cast<int64_t>(kFbSlots) * p.parts * p.k);
+  w.fb_scratch_n = cv.take<int>(static_cast<int64_t>(kFbSlots) * p.parts);
   return w;
 }
 
 template <int D>
-int launch_screen(const SearchPlan& p, const ScreenArgs& sa, const ScreenCArgs& ca, int64_t nq_pad, hipStream_t st) {
-  if (p.bins) {
-    hipLaunchKernelGGL(screen_bins_kernel<D>, dim3((nq_pad / kQPerWG) * p.S), dim3(kScreenThreads), 0, st, sa);
-    TT_CHECK_LAUNCH();
-    return TT_OK;
-  }
-  const dim3 grid(nq_pad / kQPerWG), block(kScreenThreads);
-  switch (p.R / kWave) {
-    case 16: hipLaunchKernelGGL((screen_compact_kernel<D, 16>), grid, block, 0, st, ca); break;
-    case 32: hipLaunchKernelGGL((screen_compact_kernel<D, 32>), grid, block, 0, st, ca); break;
-    case 64: hipLaunchKernelGGL((screen_compact_kernel<D, 64>), grid, block, 0, st, ca); break;
-    case 128: hipLaunchKernelGGL((screen_compact_kernel<D, 128>), grid, block, 0, st, ca); break;
-    default: return fail(TT_ERR_UNSUPPORTED, "tt_bruteforce_search: shortlist capacity %d", p.R);
-  }
-  TT_CHECK_LAUNCH();
-  return TT_OK;
+void launch_screen(const ScreenArgs& sa, int64_t nq_pad, hipStream_t st) {
+  const dim3 grid((nq_pad / kQPerWG) * sa.S), block(kSThreads);
+  hipLaunchKernelGGL((screen_kernel<D, true>), grid, block, 0, st, sa);
+  probe_begin(TT_PROBE_INDEX_SCREEN, st);
+  hipLaunchKernelGGL((screen_kernel<D, false>), grid, block, 0, st, sa);
+  probe_end(TT_PROBE_INDEX_SCREEN, st);
 }
 
 }  // namespace
@@ -1192,9 +1145,9 @@ extern "C" int tt_bruteforce_build(const float* cand, int64_t ldc, int64_t n_can
 
 extern "C" size_t tt_bruteforce_workspace_size(int64_t n_queries, int64_t n_cand, int32_t dim, int32_t k) {
   if (n_queries < 1 || n_cand < 1 || k < 1 || pick_dpad(dim) == 0) return 0;
-  const SearchPlan p = plan_search(n_queries, n_cand, k);
+  const SearchPlan p = plan_search(n_queries, n_cand, k, 1);
   Carver cv(nullptr, 0);
-  carve_search(cv, n_queries, pick_dpad(dim), p);
+  carve_search(cv, pick_dpad(dim), p);
   return cv.used();
 }
 
@@ -1215,42 +1168,48 @@ extern "C" int tt_bruteforce_search(const void* index, const float* cand, int64_
   if (n_queries == 0) return TT_OK;
   TT_REQUIRE(queries && out_scores && out_idx, "tt_bruteforce_search: NULL queries/outputs");
   const int D = pick_dpad(dim);
-  const SearchPlan p = plan_search(n_queries, n_cand, k);
+  const SearchPlan p = plan_search(n_queries, n_cand, k, 1);
   Carver cv(workspace, workspace_bytes);
-  SearchWs w = carve_search(cv, n_queries, D, p);
+  SearchWs w = carve_search(cv, D, p);
   if (!workspace || cv.used() > workspace_bytes)
     return fail(TT_ERR_WORKSPACE, "tt_bruteforce_search: workspace %zu < required %zu", workspace_bytes, cv.used());
   hipStream_t st = to_stream(stream);
   const int64_t n_pad = round_up(n_cand, kCTile);
-  const size_t shm = final_lds_bytes(p);
+  const size_t shm = final_lds_bytes(p.L, p.P);
   if (shm > 65536)
     TT_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(finalize_kernel),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(shm)));
+  const size_t fshm = fallback_lds_bytes(p.L, p.P, p.parts, k);
+  if (fshm > 65536)
+    TT_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fallback_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(fshm)));
   const int vec4 = (reinterpret_cast<uintptr_t>(cand) % 16 == 0 && ldc % 4 == 0 && dim % 4 == 0) ? 1 : 0;
   for (int64_t q0 = 0; q0 < n_queries; q0 += p.chunk) {
     const int64_t nq = (n_queries - q0 < p.chunk) ? n_queries - q0 : p.chunk;
     const int64_t nq_pad = round_up(nq, kQPerWG);
-    if (p.bins) TT_CHECK_HIP(hipMemsetAsync(w.thr, 0, nq_pad * sizeof(unsigned), st));
+    TT_CHECK_HIP(hipMemsetAsync(w.fail_count, 0, (2 + kFbSlots) * sizeof(int), st));
     hipLaunchKernelGGL(query_prep_kernel, dim3(ceil_div(nq_pad, 4)), dim3(256), 0, st, queries + q0 * ldq, ldq, nq,
-                       dim, nq_pad, D, index, w.qb, w.margin2);
+                       dim, nq_pad, D, index, w.qb, w.qflags, w.qmarg);
     TT_CHECK_LAUNCH();
-    ScreenArgs sa{index, w.qb, w.margin2, nq, n_cand, n_pad, k, p.S, p.R, w.buf, w.count, w.thr};
-    ScreenCArgs ca{index, w.qb, w.margin2, nq, n_pad, k, p.R, w.buf, w.count};
-    int rc;
-    probe_begin(TT_PROBE_INDEX_SCREEN, st);
+    ScreenArgs sa{index, w.qb, nq, n_cand, n_pad, p.S, p.NS, p.jsel, p.cap, static_cast<unsigned>(index_offset),
+                  w.buf, w.count, w.tau};
     switch (D) {
-      case 32: rc = launch_screen<32>(p, sa, ca, nq_pad, st); break;
-      case 64: rc = launch_screen<64>(p, sa, ca, nq_pad, st); break;
-      default: rc = launch_screen<128>(p, sa, ca, nq_pad, st); break;
+      case 32: launch_screen<32>(sa, nq_pad, st); break;
+      case 64: launch_screen<64>(sa, nq_pad, st); break;
+      default: launch_screen<128>(sa, nq_pad, st); break;
     }
-    probe_end(TT_PROBE_INDEX_SCREEN, st);
-    if (rc) return rc;
-    FinalArgs fa{queries + q0 * ldq, ldq, cand, ldc, n_cand, dim, k, p.S, p.H, p.R, p.L, p.P, vec4, 0, nq,
-                 index_offset, w.margin2, w.buf, w.count, p.bins ? w.thr : nullptr, out_scores + q0 * k,
-                 out_idx + q0 * k};
+    TT_CHECK_LAUNCH();
+    Lists ls{w.buf, w.count, w.tau, 2 * p.S, p.cap, nullptr, p.S, 2};
+    FinalArgs fa{queries + q0 * ldq, ldq, cand, ldc, n_cand, index_offset, index_offset, dim, k, p.L, p.P, vec4,
+                 nq, w.qflags, w.qmarg, ls, out_scores + q0 * k, out_idx + q0 * k, w.fail_count, w.fail_list};
     probe_begin(TT_PROBE_INDEX_FINALIZE, st);
     hipLaunchKernelGGL(finalize_kernel, dim3(nq), dim3(kWave), shm, st, fa);
     probe_end(TT_PROBE_INDEX_FINALIZE, st);
+    TT_CHECK_LAUNCH();
+    FallbackArgs fb{queries + q0 * ldq, ldq, cand, ldc, n_cand, index_offset, dim, k, p.L, p.P, p.parts, vec4,
+                    w.fail_count, w.fail_list, w.fail_count + 1, w.fb_scratch, w.fb_scratch_n,
+                    out_scores + q0 * k, out_idx + q0 * k};
+    hipLaunchKernelGGL(fallback_kernel, dim3(kFbGrid), dim3(kFbWaves * kWave), fshm, st, fb);
     TT_CHECK_LAUNCH();
   }
   return TT_OK;

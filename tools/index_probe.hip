@@ -1,7 +1,7 @@
 // Development probe for the brute-force index kernels: builds tt_index.hip
 // with its probe hooks and times search on relu(N(0,1)) data of the C4 shape.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -munsafe-fp-atomics \
-//     -I include -I hm-retrieval-two-tower_amd/csrc [-DTT_INDEX_STATS] [-DTT_INDEX_NOINSERT] \
+//     -I include -I hm-retrieval-two-tower_amd/csrc [-DTT_INDEX_STATS] [-DTT_INDEX_NOINSERT (screen keeps nothing)] \
 //     tools/index_probe.hip hm-retrieval-two-tower_amd/csrc/tt_api.cpp -o /tmp/probe
 #include <hiprand/hiprand_kernel.h>
 
@@ -58,8 +58,8 @@ int main(int argc, char** argv) {
 #ifdef TT_INDEX_STATS
     unsigned long long st[4];
     hipMemcpyFromSymbol(st, HIP_SYMBOL(g_index_stats), sizeof(st));
-    printf("  inserts/query %.1f  compactions/query %.2f  overflows %llu\n", double(st[0]) / nq, double(st[1]) / nq,
-           st[2]);
+    printf("  list entries/query %.1f  fallbacks %llu  cut entries/query %.1f\n", double(st[0]) / nq, st[1],
+           double(st[2]) / nq);
 #endif
   }
   std::vector<int32_t> hi(k);
