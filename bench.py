@@ -381,9 +381,8 @@ def time_index_sharded(device, n_queries: int, n_cand: int, k: int, ws: int, ran
     g.manual_seed(2)
     Q = torch.relu(torch.randn(n_queries, E, generator=g, device=device))
     Q[::100] = 0.0
-    b, e = shard_range(n_cand, ws, rank)
-    idx = ShardedBruteForceIndex(k, None, C[b:e].contiguous(), b)
-    idx.search_owned(Q[:4096 * ws])  # warm (workspaces)
+    idx = ShardedBruteForceIndex(k, None, C)
+    idx.search_owned(Q)  # warm: code + full-size workspaces, outside the timed region
     torch.cuda.synchronize()
     torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -406,7 +405,7 @@ def time_index_sharded(device, n_queries: int, n_cand: int, k: int, ws: int, ran
     from pkg.modelling.distributed import QueryShardedBruteForceIndex
 
     qidx = QueryShardedBruteForceIndex(k, None, C)
-    qidx.search_owned(Q[:4096 * ws])  # warm
+    qidx.search_owned(Q)  # warm
     torch.cuda.synchronize()
     torch.distributed.barrier()
     torch.cuda.synchronize()

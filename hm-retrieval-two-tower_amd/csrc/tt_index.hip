@@ -211,7 +211,7 @@ __global__ void query_prep_kernel(const float* __restrict__ q, int64_t ldq, int6
     ss = __builtin_fmaf(x0, x0, __builtin_fmaf(x1, x1, ss));
     nz = nz || x0 != 0.0f || x1 != 0.0f;
     neg = neg || x0 < 0.0f || x1 < 0.0f;
-    reinterpret_cast<unsigned*>(qb + r * D)[e2] = pack_bf16x2(x0, x1);
+    if (qb) reinterpret_cast<unsigned*>(qb + r * D)[e2] = pack_bf16x2(x0, x1);
   }
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) ss += __shfl_xor(ss, m, kWave);
@@ -232,16 +232,17 @@ struct ScreenArgs {
   const void* index;
   const __bf16* qb;   // [nq_pad, D]
   int64_t nq;         // real queries in this chunk
-  int64_t n;          // real candidates (rows >= n are zero padding)
-  int64_t n_pad;
+  int64_t row0;       // candidate rows [row0, row1) of the image are screened
+  int64_t row1;
   int S;              // candidate splits
   int NS;             // sample tiles per split (0: keep every score)
   int jsel;           // tau = jsel-th largest of a query's 64 bins
   int cap;            // entries per (query, split, lane half) list
-  unsigned index_offset;
-  uint2* buf;         // [nq_pad][S][2][cap] (score bits, index_offset + candidate)
+  unsigned index_offset;  // id of image row r = index_offset + r
+  uint2* buf;         // [nq_pad][S][2][cap] (score bits, id)
   int* count;         // [nq_pad][S][2]; -1 = list overflowed
-  float* tau;         // [nq_pad][S]
+  float* tau_split;   // sample pass output [nq_pad][S]
+  const float* tau;   // scan pass input [nq_pad]: keep s~ > tau[q]
 };
 
 // s_waitcnt with only the vector-memory counter constrained (gfx9 encoding).
@@ -304,10 +305,11 @@ __global__ void __launch_bounds__(kSThreads) screen_kernel(const ScreenArgs a) {
   const int split = static_cast<int>(blockIdx.x % a.S);
   const int64_t q0 = static_cast<int64_t>(blockIdx.x / a.S) * kQPerWG + wave * kQPerWave + l32;
   const int64_t q1 = q0 + 32;
-  const int ntiles = static_cast<int>(a.n_pad / kCTile);
+  const int t0 = static_cast<int>(a.row0 / kCTile);
+  const int ntiles = static_cast<int>((a.row1 + kCTile - 1) / kCTile) - t0;
   const int per = (ntiles + a.S - 1) / a.S;
-  const int tb = split * per;
-  const int nt = max(min(ntiles, tb + per) - tb, 0);
+  const int tb = t0 + split * per;
+  const int nt = max(min(ntiles - split * per, per), 0);
   const int ns = min(a.NS, nt);
   const __bf16* crow = index_rows(a.index);
   const bool my_pieces = wave * PPW < PIECES;  // D = 32: waves 4..7 stage nothing
@@ -354,11 +356,14 @@ __global__ void __launch_bounds__(kSThreads) screen_kernel(const ScreenArgs a) {
     const int swz = (row * CH / 16) % CH;
     return *reinterpret_cast<const bf16x8*>(B + row * RB + ((ch ^ swz) << 4));
   };
-  auto mask_pad = [&](f32x16& acc, int64_t cfirst) {  // rows past n (last tile only)
+  auto mask_pad = [&](f32x16& acc, int64_t cfirst) {  // rows outside [row0, row1) (edge tiles only)
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
-      if (cfirst + (r & 3) + 8 * (r >> 2) >= a.n) acc[r] = -INFINITY;
+    for (int r = 0; r < 16; ++r) {
+      const int64_t c = cfirst + (r & 3) + 8 * (r >> 2);
+      if (c < a.row0 || c >= a.row1) acc[r] = -INFINITY;
+    }
   };
+  auto edge = [&](int64_t cbase) { return cbase < a.row0 || cbase + kCTile > a.row1; };
   auto advance = [&](int u) {  // (sample) tile u consumed: wait for u + 1, barrier
     if (u + 1 < nv) wait_tiles(min(u + kStages - 1, nv - 1) - (u + 1));
     __builtin_amdgcn_s_barrier();
@@ -390,7 +395,7 @@ __global__ void __launch_bounds__(kSThreads) screen_kernel(const ScreenArgs a) {
           c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bq0[s], c0, 0, 0, 0);
           c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bq1[s], c1, 0, 0, 0);
         }
-        if (cbase + kCTile > a.n) {
+        if (edge(cbase)) {
           mask_pad(c0, cbase + 32 * t + 4 * h);
           mask_pad(c1, cbase + 32 * t + 4 * h);
         }
@@ -404,17 +409,17 @@ __global__ void __launch_bounds__(kSThreads) screen_kernel(const ScreenArgs a) {
       }
       advance(u);
     }
-    const float t0 = ns > 0 ? bins_select(b0a, b0b, a.jsel) : -INFINITY;
-    const float t1 = ns > 0 ? bins_select(b1a, b1b, a.jsel) : -INFINITY;
+    const float tq0 = ns > 0 ? bins_select(b0a, b0b, a.jsel) : -INFINITY;
+    const float tq1 = ns > 0 ? bins_select(b1a, b1b, a.jsel) : -INFINITY;
     if (h == 0) {
-      a.tau[q0 * a.S + split] = t0;
-      a.tau[q1 * a.S + split] = t1;
+      a.tau_split[q0 * a.S + split] = tq0;
+      a.tau_split[q1 * a.S + split] = tq1;
     }
   }
   if constexpr (!SAMPLE) {
   // the estimate of the sample pass; queries past nq keep nothing
-  float tau0 = q0 < a.nq ? a.tau[q0 * a.S + split] : INFINITY;
-  float tau1 = q1 < a.nq ? a.tau[q1 * a.S + split] : INFINITY;
+  float tau0 = q0 < a.nq ? a.tau[q0] : INFINITY;
+  float tau1 = q1 < a.nq ? a.tau[q1] : INFINITY;
 
   // ---- phase 2: every tile of the split once, keep s~ > tau -----------------
   const int64_t lst0 = ((q0 * a.S + split) * 2 + h) * static_cast<int64_t>(a.cap);
@@ -483,7 +488,7 @@ __global__ void __launch_bounds__(kSThreads) screen_kernel(const ScreenArgs a) {
       p0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[s], bq0[s], p0, 0, 0, 0);
       p1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[s], bq1[s], p1, 0, 0, 0);
     }
-    if (cbase + kCTile > a.n) {
+    if (edge(cbase)) {
       mask_pad(p0, cbase + 32 * t + 4 * h);
       mask_pad(p1, cbase + 32 * t + 4 * h);
     }
@@ -539,6 +544,105 @@ __global__ void __launch_bounds__(kSThreads) screen_kernel(const ScreenArgs a) {
   }
 }
 
+// tau[q] = min over the splits' estimates (the lowest is the safest: more
+// entries, fewer failed certificates).
+__global__ void tau_min_kernel(const float* __restrict__ tau_split, int S, int64_t nq, float* __restrict__ tau) {
+  const int64_t q = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (q >= nq) return;
+  float t = tau_split[q * S];
+  for (int s = 1; s < S; ++s) t = fminf(t, tau_split[q * S + s]);
+  tau[q] = t;
+}
+
+// ---- CSR packing of a chunk's lists (candidate-sharded search) -------------
+// n_q = sum of the query's 2S list counts (-1 if one overflowed); offsets are
+// an exclusive scan over the whole call, carried across chunks in *total.
+constexpr int kPackBlock = 1024;
+
+__global__ void __launch_bounds__(kPackBlock) pack_count_kernel(const int* __restrict__ count, int nl, int64_t nq,
+                                                               int* __restrict__ local, int64_t* __restrict__ bsum) {
+  __shared__ int64_t sh[kPackBlock];
+  const int64_t q = blockIdx.x * static_cast<int64_t>(kPackBlock) + threadIdx.x;
+  int64_t n = 0;
+  if (q < nq) {
+    int v = 0;
+    bool ovf = false;
+    for (int j = 0; j < nl; ++j) {
+      const int c = count[q * nl + j];
+      ovf = ovf || c < 0;
+      v += c < 0 ? 0 : c;
+    }
+    n = ovf ? 0 : v;
+    local[q] = ovf ? -1 : v;  // count (offset written below)
+  }
+  sh[threadIdx.x] = n;
+  __syncthreads();
+  for (int off = 1; off < kPackBlock; off <<= 1) {  // inclusive Hillis-Steele scan
+    const int64_t x = threadIdx.x >= off ? sh[threadIdx.x - off] : 0;
+    __syncthreads();
+    sh[threadIdx.x] += x;
+    __syncthreads();
+  }
+  if (q < nq) local[nq + q] = static_cast<int>(sh[threadIdx.x] - n);  // exclusive, within the block
+  if (threadIdx.x == kPackBlock - 1) bsum[blockIdx.x] = sh[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(kPackBlock) pack_scan_kernel(int64_t* __restrict__ bsum, int nb,
+                                                              int64_t* __restrict__ total, int64_t* __restrict__ off_end) {
+  __shared__ int64_t sh[kPackBlock];
+  const int64_t base = *total;
+  int64_t carry = 0;
+  for (int b0 = 0; b0 < nb; b0 += kPackBlock) {
+    const int b = b0 + threadIdx.x;
+    const int64_t v = b < nb ? bsum[b] : 0;
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    for (int off = 1; off < kPackBlock; off <<= 1) {
+      const int64_t x = threadIdx.x >= off ? sh[threadIdx.x - off] : 0;
+      __syncthreads();
+      sh[threadIdx.x] += x;
+      __syncthreads();
+    }
+    if (b < nb) bsum[b] = base + carry + sh[threadIdx.x] - v;  // exclusive block base
+    carry += sh[kPackBlock - 1];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    *total = base + carry;
+    *off_end = base + carry;
+  }
+}
+
+// One wave per query: copies its lists to entries[offset..) (int64 = id << 32
+// | score bits); a query that would pass `cap` is reported with count -1.
+__global__ void __launch_bounds__(256) pack_copy_kernel(const uint2* __restrict__ buf, const int* __restrict__ count,
+                                                       int nl, int lcap, int64_t nq, const int* __restrict__ local,
+                                                       const int64_t* __restrict__ bsum, int64_t cap,
+                                                       int64_t* __restrict__ entries, int* __restrict__ counts_out,
+                                                       int64_t* __restrict__ offsets_out) {
+  const int64_t q = blockIdx.x * 4ll + threadIdx.x / kWave;
+  if (q >= nq) return;
+  const int lane = lane_id();
+  int n = local[q];
+  const int64_t start = bsum[q / kPackBlock] + local[nq + q];
+  if (n >= 0 && start + n > cap) n = -1;
+  if (lane == 0) {
+    counts_out[q] = n;
+    offsets_out[q] = start;
+  }
+  if (n <= 0) return;
+  int64_t dst = start;
+  for (int j = 0; j < nl; ++j) {
+    const int c = count[q * nl + j];
+    const uint2* src = buf + (q * nl + j) * static_cast<int64_t>(lcap);
+    for (int i = lane; i < c; i += kWave) {
+      const uint2 e = src[i];
+      entries[dst + i] = static_cast<int64_t>((static_cast<uint64_t>(e.y) << 32) | e.x);
+    }
+    dst += c;
+  }
+}
+
 // ---- finalize ------------------------------------------------------------
 // Exact score: k-ordered fmaf chain over the fp32 rows (dim real columns).
 // qs is the query row in LDS (broadcast reads); the candidate row is loaded in
@@ -572,23 +676,25 @@ __device__ __forceinline__ float exact_score(const float* __restrict__ qs, const
   return acc;
 }
 
-// Lists of one query: `nseg` segments; segment j starts at
-// buf + seg_base(q, j) and holds count[q * nseg + j] entries (-1: overflowed);
-// its screen kept s~ > tau[q * tau_per_q + j / seg_per_tau].
+// Lists of one query: `nseg` segments; segment j of query q holds
+// count[q * cq + j * cj] entries (-1: overflowed) starting at
+// buf + (q * nseg + j) * cap (region form) or at off[q * cq + j * cj] (CSR
+// form, cap == 0, entries as int64 = id << 32 | score bits, the same bytes as
+// uint2 {score bits, id}); their screens kept s~ > tau[q].
 struct Lists {
   const uint2* buf;
   const int* count;
   const float* tau;
   int nseg;
-  int cap;          // region form: segment j of query q at (q * nseg + j) * cap
-  const int64_t* off;  // CSR form (cap == 0): segment j of query q at off[q * nseg + j]
-  int tau_per_q;
-  int seg_per_tau;
+  int cap;
+  const int64_t* off;
+  int64_t cq;
+  int64_t cj;
 };
 
+__device__ __forceinline__ int seg_count(const Lists& L, int64_t q, int j) { return L.count[q * L.cq + j * L.cj]; }
 __device__ __forceinline__ const uint2* seg_ptr(const Lists& L, int64_t q, int j) {
-  const int64_t i = q * L.nseg + j;
-  return L.buf + (L.cap ? i * L.cap : L.off[i]);
+  return L.cap ? L.buf + (q * L.nseg + j) * static_cast<int64_t>(L.cap) : L.buf + L.off[q * L.cq + j * L.cj];
 }
 
 // Radix select with 8-bit digits and an LDS histogram (one wave) over keys
@@ -794,13 +900,13 @@ __global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
   const float m = a.qmarg[q];
   bool fail = false;
   int ntot = 0;
-  float tmax = -INFINITY;
+  float tmax;
   for (int j = 0; j < Ls.nseg; ++j) {
-    const int c = Ls.count[q * Ls.nseg + j];
+    const int c = seg_count(Ls, q, j);
     fail = fail || c < 0;
     ntot += c;
   }
-  for (int j = 0; j < Ls.nseg; j += Ls.seg_per_tau) tmax = fmaxf(tmax, Ls.tau[q * Ls.tau_per_q + j / Ls.seg_per_tau]);
+  tmax = Ls.tau[q];
   fail = fail || ntot < K;
   float X = -INFINITY;
   if (!fail) {
@@ -808,7 +914,7 @@ __global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
     const Kth r = radix_select(
         [&](unsigned prefix, unsigned hi_mask, int shift) {
           for (int j = 0; j < Ls.nseg; ++j) {
-            const int c = Ls.count[q * Ls.nseg + j];
+            const int c = seg_count(Ls, q, j);
             const uint2* e = seg_ptr(Ls, q, j);
             for (int i = lane; i < c; i += kWave) {
               const unsigned key = float_order_key(__uint_as_float(e[i].x));
@@ -831,7 +937,7 @@ __global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
   if (!fail) {
     for (int e = lane; e < a.dim; e += kWave) qs[e] = a.q[q * a.ldq + e];
     for (int j = 0; j < Ls.nseg && !fail; ++j) {
-      const int c = Ls.count[q * Ls.nseg + j];
+      const int c = seg_count(Ls, q, j);
       const uint2* e = seg_ptr(Ls, q, j);
       for (int i0 = 0; i0 < c; i0 += kWave) {
         const int i = i0 + lane;
@@ -1033,11 +1139,12 @@ struct SearchPlan {
   int64_t chunk;
 };
 
-// R = target list entries per query over the whole candidate set (~3k), split
-// evenly over `parts` = S splits x `shards` ranks screening disjoint ranges.
-SearchPlan plan_search(int64_t nq, int64_t n_cand, int k, int shards) {
+// R = target list entries per query over the whole candidate set (3k + 100),
+// split evenly over the S splits x `shards` ranks screening disjoint ranges;
+// each split estimates its share and the query keeps the lowest estimate.
+SearchPlan plan_search(int64_t nq, int64_t n_rows, int k, int shards) {
   SearchPlan p{};
-  const int64_t ntiles = ceil_div(n_cand, kCTile);
+  const int64_t ntiles = ceil_div(n_rows, kCTile) + 1;  // + 1: a range need not start on a tile
   p.P = next_pow2(k < 2 ? 2 : k);
   p.k = k;
   p.parts = 8192 / k < 1 ? 1 : (8192 / k > 64 ? 64 : 8192 / k);
@@ -1066,7 +1173,8 @@ SearchPlan plan_search(int64_t nq, int64_t n_cand, int k, int shards) {
     p.jsel = j < 1 ? 1 : (j > 64 ? 64 : j);
     mu = R / 2.0;
   }
-  p.cap = next_pow2(static_cast<int>(3.0 * mu) + 64);
+  // the lowest of S (x shards) estimates lands lower than each: room for it
+  p.cap = next_pow2(static_cast<int>(3.0 * mu * (p.S > 1 ? 2.0 : 1.0)) + 64);
   const size_t per_query = static_cast<size_t>(p.S) * 2 * p.cap * sizeof(uint2);
   int64_t chunk = static_cast<int64_t>(kListBudget / per_query) / kQPerWG * kQPerWG;
   if (chunk < kQPerWG) chunk = kQPerWG;
@@ -1081,36 +1189,110 @@ struct SearchWs {
   float* qmarg;
   uint2* buf;
   int* count;
+  float* tau_split;
   float* tau;
   int* fail_count;  // [0] failures, then the fallback's ctrl words
   int* fail_list;
   uint2* fb_scratch;
   int* fb_scratch_n;
+  int* pack_local;  // [2][chunk]
+  int64_t* pack_bsum;
+  int64_t* pack_total;
 };
 
-SearchWs carve_search(Carver& cv, int D, const SearchPlan& p) {
+SearchWs carve_search(Carver& cv, int D, const SearchPlan& p, bool lists, bool finalize) {
   const int64_t nq_pad = p.chunk;
-  SearchWs w;
+  SearchWs w{};
   w.qb = cv.take<__bf16>(nq_pad * D);
   w.qflags = cv.take<int>(nq_pad);
   w.qmarg = cv.take<float>(nq_pad);
-  w.buf = cv.take<uint2>(nq_pad * p.S * 2 * static_cast<int64_t>(p.cap));
-  w.count = cv.take<int>(nq_pad * p.S * 2);
-  w.tau = cv.take<float>(nq_pad * p.S);
-  w.fail_count = cv.take<int>(2 + kFbSlots);
-  w.fail_list = cv.take<int>(nq_pad);
-  w.fb_scratch = cv.take<uint2>(static_cast<int64_t>(kFbSlots) * p.parts * p.k);
-  w.fb_scratch_n = cv.take<int>(static_cast<int64_t>(kFbSlots) * p.parts);
+  if (lists) {
+    w.buf = cv.take<uint2>(nq_pad * p.S * 2 * static_cast<int64_t>(p.cap));
+    w.count = cv.take<int>(nq_pad * p.S * 2);
+    w.tau_split = cv.take<float>(nq_pad * p.S);
+    w.tau = cv.take<float>(nq_pad);
+    w.pack_local = cv.take<int>(2 * nq_pad);
+    w.pack_bsum = cv.take<int64_t>(ceil_div(nq_pad, kPackBlock));
+    w.pack_total = cv.take<int64_t>(1);
+  }
+  if (finalize) {
+    w.fail_count = cv.take<int>(2 + kFbSlots);
+    w.fail_list = cv.take<int>(nq_pad);
+    w.fb_scratch = cv.take<uint2>(static_cast<int64_t>(kFbSlots) * p.parts * p.k);
+    w.fb_scratch_n = cv.take<int>(static_cast<int64_t>(kFbSlots) * p.parts);
+  }
   return w;
 }
 
 template <int D>
-void launch_screen(const ScreenArgs& sa, int64_t nq_pad, hipStream_t st) {
+void launch_pass(const ScreenArgs& sa, int64_t nq_pad, bool sample, hipStream_t st) {
   const dim3 grid((nq_pad / kQPerWG) * sa.S), block(kSThreads);
-  hipLaunchKernelGGL((screen_kernel<D, true>), grid, block, 0, st, sa);
-  probe_begin(TT_PROBE_INDEX_SCREEN, st);
-  hipLaunchKernelGGL((screen_kernel<D, false>), grid, block, 0, st, sa);
-  probe_end(TT_PROBE_INDEX_SCREEN, st);
+  if (sample) {
+    hipLaunchKernelGGL((screen_kernel<D, true>), grid, block, 0, st, sa);
+  } else {
+    probe_begin(TT_PROBE_INDEX_SCREEN, st);
+    hipLaunchKernelGGL((screen_kernel<D, false>), grid, block, 0, st, sa);
+    probe_end(TT_PROBE_INDEX_SCREEN, st);
+  }
+}
+
+int run_pass(int D, const ScreenArgs& sa, int64_t nq_pad, bool sample, hipStream_t st) {
+  switch (D) {
+    case 32: launch_pass<32>(sa, nq_pad, sample, st); break;
+    case 64: launch_pass<64>(sa, nq_pad, sample, st); break;
+    default: launch_pass<128>(sa, nq_pad, sample, st); break;
+  }
+  TT_CHECK_LAUNCH();
+  return TT_OK;
+}
+
+int run_prep(const float* q, int64_t ldq, int64_t nq, int dim, int D, const void* index, const SearchWs& w,
+             bool with_rows, hipStream_t st) {
+  const int64_t nq_pad = round_up(nq, kQPerWG);
+  hipLaunchKernelGGL(query_prep_kernel, dim3(ceil_div(nq_pad, 4)), dim3(256), 0, st, q, ldq, nq, dim, nq_pad, D, index,
+                     with_rows ? w.qb : nullptr, w.qflags, w.qmarg);
+  TT_CHECK_LAUNCH();
+  return TT_OK;
+}
+
+// sample pass + min over the splits -> tau[0..nq)
+int run_estimate(int D, const void* index, int64_t row0, int64_t row1, int64_t nq, const SearchPlan& p,
+                 const SearchWs& w, float* tau, hipStream_t st) {
+  const int64_t nq_pad = round_up(nq, kQPerWG);
+  ScreenArgs sa{index, w.qb, nq, row0, row1, p.S, p.NS, p.jsel, p.cap, 0u, nullptr, nullptr, w.tau_split, nullptr};
+  if (int rc = run_pass(D, sa, nq_pad, true, st)) return rc;
+  hipLaunchKernelGGL(tau_min_kernel, dim3(ceil_div(nq, 256)), dim3(256), 0, st, w.tau_split, p.S, nq, tau);
+  TT_CHECK_LAUNCH();
+  return TT_OK;
+}
+
+int run_scan(int D, const void* index, int64_t row0, int64_t row1, int64_t nq, const SearchPlan& p, const SearchWs& w,
+             const float* tau, unsigned index_offset, hipStream_t st) {
+  const int64_t nq_pad = round_up(nq, kQPerWG);
+  ScreenArgs sa{index, w.qb, nq, row0, row1, p.S, p.NS, p.jsel, p.cap, index_offset, w.buf, w.count, nullptr, tau};
+  return run_pass(D, sa, nq_pad, false, st);
+}
+
+int run_finalize(const FinalArgs& fa, const FallbackArgs& fb, int64_t nq, const SearchPlan& p, hipStream_t st) {
+  const size_t shm = final_lds_bytes(p.L, p.P);
+  if (shm > 65536)
+    TT_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(finalize_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(shm)));
+  const size_t fshm = fallback_lds_bytes(p.L, p.P, p.parts, p.k);
+  if (fshm > 65536)
+    TT_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fallback_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(fshm)));
+  probe_begin(TT_PROBE_INDEX_FINALIZE, st);
+  hipLaunchKernelGGL(finalize_kernel, dim3(nq), dim3(kWave), shm, st, fa);
+  probe_end(TT_PROBE_INDEX_FINALIZE, st);
+  TT_CHECK_LAUNCH();
+  hipLaunchKernelGGL(fallback_kernel, dim3(kFbGrid), dim3(kFbWaves * kWave), fshm, st, fb);
+  TT_CHECK_LAUNCH();
+  return TT_OK;
+}
+
+inline bool is_vec4(const float* cand, int64_t ldc, int dim) {
+  return reinterpret_cast<uintptr_t>(cand) % 16 == 0 && ldc % 4 == 0 && dim % 4 == 0;
 }
 
 }  // namespace
@@ -1147,7 +1329,7 @@ extern "C" size_t tt_bruteforce_workspace_size(int64_t n_queries, int64_t n_cand
   if (n_queries < 1 || n_cand < 1 || k < 1 || pick_dpad(dim) == 0) return 0;
   const SearchPlan p = plan_search(n_queries, n_cand, k, 1);
   Carver cv(nullptr, 0);
-  carve_search(cv, pick_dpad(dim), p);
+  carve_search(cv, pick_dpad(dim), p, true, true);
   return cv.used();
 }
 
@@ -1170,47 +1352,166 @@ extern "C" int tt_bruteforce_search(const void* index, const float* cand, int64_
   const int D = pick_dpad(dim);
   const SearchPlan p = plan_search(n_queries, n_cand, k, 1);
   Carver cv(workspace, workspace_bytes);
-  SearchWs w = carve_search(cv, D, p);
+  SearchWs w = carve_search(cv, D, p, true, true);
   if (!workspace || cv.used() > workspace_bytes)
     return fail(TT_ERR_WORKSPACE, "tt_bruteforce_search: workspace %zu < required %zu", workspace_bytes, cv.used());
   hipStream_t st = to_stream(stream);
-  const int64_t n_pad = round_up(n_cand, kCTile);
-  const size_t shm = final_lds_bytes(p.L, p.P);
-  if (shm > 65536)
-    TT_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(finalize_kernel),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(shm)));
-  const size_t fshm = fallback_lds_bytes(p.L, p.P, p.parts, k);
-  if (fshm > 65536)
-    TT_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fallback_kernel),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(fshm)));
-  const int vec4 = (reinterpret_cast<uintptr_t>(cand) % 16 == 0 && ldc % 4 == 0 && dim % 4 == 0) ? 1 : 0;
+  const int vec4 = is_vec4(cand, ldc, dim) ? 1 : 0;
   for (int64_t q0 = 0; q0 < n_queries; q0 += p.chunk) {
     const int64_t nq = (n_queries - q0 < p.chunk) ? n_queries - q0 : p.chunk;
-    const int64_t nq_pad = round_up(nq, kQPerWG);
+    const float* qc = queries + q0 * ldq;
     TT_CHECK_HIP(hipMemsetAsync(w.fail_count, 0, (2 + kFbSlots) * sizeof(int), st));
-    hipLaunchKernelGGL(query_prep_kernel, dim3(ceil_div(nq_pad, 4)), dim3(256), 0, st, queries + q0 * ldq, ldq, nq,
-                       dim, nq_pad, D, index, w.qb, w.qflags, w.qmarg);
-    TT_CHECK_LAUNCH();
-    ScreenArgs sa{index, w.qb, nq, n_cand, n_pad, p.S, p.NS, p.jsel, p.cap, static_cast<unsigned>(index_offset),
-                  w.buf, w.count, w.tau};
-    switch (D) {
-      case 32: launch_screen<32>(sa, nq_pad, st); break;
-      case 64: launch_screen<64>(sa, nq_pad, st); break;
-      default: launch_screen<128>(sa, nq_pad, st); break;
-    }
-    TT_CHECK_LAUNCH();
-    Lists ls{w.buf, w.count, w.tau, 2 * p.S, p.cap, nullptr, p.S, 2};
-    FinalArgs fa{queries + q0 * ldq, ldq, cand, ldc, n_cand, index_offset, index_offset, dim, k, p.L, p.P, vec4,
+    if (int rc = run_prep(qc, ldq, nq, dim, D, index, w, true, st)) return rc;
+    if (int rc = run_estimate(D, index, 0, n_cand, nq, p, w, w.tau, st)) return rc;
+    if (int rc = run_scan(D, index, 0, n_cand, nq, p, w, w.tau, static_cast<unsigned>(index_offset), st)) return rc;
+    Lists ls{w.buf, w.count, w.tau, 2 * p.S, p.cap, nullptr, 2 * p.S, 1};
+    FinalArgs fa{qc, ldq, cand, ldc, n_cand, index_offset, index_offset, dim, k, p.L, p.P, vec4,
                  nq, w.qflags, w.qmarg, ls, out_scores + q0 * k, out_idx + q0 * k, w.fail_count, w.fail_list};
-    probe_begin(TT_PROBE_INDEX_FINALIZE, st);
-    hipLaunchKernelGGL(finalize_kernel, dim3(nq), dim3(kWave), shm, st, fa);
-    probe_end(TT_PROBE_INDEX_FINALIZE, st);
-    TT_CHECK_LAUNCH();
-    FallbackArgs fb{queries + q0 * ldq, ldq, cand, ldc, n_cand, index_offset, dim, k, p.L, p.P, p.parts, vec4,
+    FallbackArgs fb{qc, ldq, cand, ldc, n_cand, index_offset, dim, k, p.L, p.P, p.parts, vec4,
                     w.fail_count, w.fail_list, w.fail_count + 1, w.fb_scratch, w.fb_scratch_n,
                     out_scores + q0 * k, out_idx + q0 * k};
-    hipLaunchKernelGGL(fallback_kernel, dim3(kFbGrid), dim3(kFbWaves * kWave), fshm, st, fb);
+    if (int rc = run_finalize(fa, fb, nq, p, st)) return rc;
+  }
+  return TT_OK;
+}
+
+// ---- candidate-sharded search (ShardedBruteForceIndex) ----------------------
+namespace {
+int check_range(const char* fn, const void* index, int64_t row0, int64_t row1, int32_t dim, int32_t k,
+                int32_t shards, int64_t n_queries) {
+  TT_REQUIRE(index, "%s: NULL index", fn);
+  TT_REQUIRE(row0 >= 0 && row1 > row0 && row1 < (1ll << 31), "%s: bad row range [%lld, %lld)", fn,
+             static_cast<long long>(row0), static_cast<long long>(row1));
+  if (pick_dpad(dim) == 0) return fail(TT_ERR_UNSUPPORTED, "%s: dim=%d > 128", fn, dim);
+  TT_REQUIRE(k >= 1 && k <= 4000, "%s: k=%d out of range", fn, k);
+  TT_REQUIRE(shards >= 1, "%s: shards must be >= 1", fn);
+  TT_REQUIRE(n_queries >= 0, "%s: negative n_queries", fn);
+  return TT_OK;
+}
+}  // namespace
+
+extern "C" size_t tt_bruteforce_shard_workspace_size(int64_t n_queries, int64_t row0, int64_t row1, int32_t dim,
+                                                     int32_t k, int32_t shards) {
+  if (n_queries < 1 || row1 <= row0 || k < 1 || shards < 1 || pick_dpad(dim) == 0) return 0;
+  const SearchPlan p = plan_search(n_queries, row1 - row0, k, shards);
+  Carver cv(nullptr, 0);
+  carve_search(cv, pick_dpad(dim), p, true, false);
+  return cv.used();
+}
+
+extern "C" int64_t tt_bruteforce_shard_capacity(int64_t n_queries, int64_t row0, int64_t row1, int32_t k,
+                                                int32_t shards) {
+  if (n_queries < 1 || row1 <= row0 || k < 1 || shards < 1) return 0;
+  // expected entries per query on this shard ~ (3k + 100) / shards, lower
+  // estimates (the minimum over the shards) keep up to ~2x as many
+  const int64_t per = (6 * static_cast<int64_t>(k) + 200) / shards + 64;
+  const int64_t rows = row1 - row0;
+  return n_queries * (per < rows ? per : rows);
+}
+
+extern "C" int tt_bruteforce_shard_estimate(const void* index, int64_t row0, int64_t row1, const float* queries,
+                                            int64_t ldq, int64_t n_queries, int32_t dim, int32_t k, int32_t shards,
+                                            float* tau, void* workspace, size_t workspace_bytes, tt_stream_t stream) {
+  clear_error();
+  if (int rc = check_range("tt_bruteforce_shard_estimate", index, row0, row1, dim, k, shards, n_queries)) return rc;
+  if (n_queries == 0) return TT_OK;
+  TT_REQUIRE(queries && tau && ldq >= dim, "tt_bruteforce_shard_estimate: NULL queries/tau or bad ldq");
+  const int D = pick_dpad(dim);
+  const SearchPlan p = plan_search(n_queries, row1 - row0, k, shards);
+  Carver cv(workspace, workspace_bytes);
+  SearchWs w = carve_search(cv, D, p, true, false);
+  if (!workspace || cv.used() > workspace_bytes)
+    return fail(TT_ERR_WORKSPACE, "tt_bruteforce_shard_estimate: workspace %zu < required %zu", workspace_bytes,
+                cv.used());
+  hipStream_t st = to_stream(stream);
+  for (int64_t q0 = 0; q0 < n_queries; q0 += p.chunk) {
+    const int64_t nq = (n_queries - q0 < p.chunk) ? n_queries - q0 : p.chunk;
+    if (int rc = run_prep(queries + q0 * ldq, ldq, nq, dim, D, index, w, true, st)) return rc;
+    if (int rc = run_estimate(D, index, row0, row1, nq, p, w, tau + q0, st)) return rc;
+  }
+  return TT_OK;
+}
+
+extern "C" int tt_bruteforce_shard_screen(const void* index, int64_t row0, int64_t row1, const float* queries,
+                                          int64_t ldq, int64_t n_queries, int32_t dim, int32_t k, int32_t shards,
+                                          const float* tau, int64_t* entries, int64_t entries_cap, int32_t* counts,
+                                          int64_t* offsets, void* workspace, size_t workspace_bytes,
+                                          tt_stream_t stream) {
+  clear_error();
+  if (int rc = check_range("tt_bruteforce_shard_screen", index, row0, row1, dim, k, shards, n_queries)) return rc;
+  TT_REQUIRE(offsets, "tt_bruteforce_shard_screen: NULL offsets");
+  hipStream_t st = to_stream(stream);
+  if (n_queries == 0) {
+    TT_CHECK_HIP(hipMemsetAsync(offsets, 0, sizeof(int64_t), st));
+    return TT_OK;
+  }
+  TT_REQUIRE(queries && tau && counts && ldq >= dim, "tt_bruteforce_shard_screen: NULL queries/tau/counts or bad ldq");
+  TT_REQUIRE(entries || entries_cap == 0, "tt_bruteforce_shard_screen: NULL entries");
+  const int D = pick_dpad(dim);
+  const SearchPlan p = plan_search(n_queries, row1 - row0, k, shards);
+  Carver cv(workspace, workspace_bytes);
+  SearchWs w = carve_search(cv, D, p, true, false);
+  if (!workspace || cv.used() > workspace_bytes)
+    return fail(TT_ERR_WORKSPACE, "tt_bruteforce_shard_screen: workspace %zu < required %zu", workspace_bytes,
+                cv.used());
+  TT_CHECK_HIP(hipMemsetAsync(w.pack_total, 0, sizeof(int64_t), st));
+  for (int64_t q0 = 0; q0 < n_queries; q0 += p.chunk) {
+    const int64_t nq = (n_queries - q0 < p.chunk) ? n_queries - q0 : p.chunk;
+    if (int rc = run_prep(queries + q0 * ldq, ldq, nq, dim, D, index, w, true, st)) return rc;
+    if (int rc = run_scan(D, index, row0, row1, nq, p, w, tau + q0, 0u, st)) return rc;
+    const int nl = 2 * p.S;
+    const int nb = static_cast<int>(ceil_div(nq, kPackBlock));
+    hipLaunchKernelGGL(pack_count_kernel, dim3(nb), dim3(kPackBlock), 0, st, w.count, nl, nq, w.pack_local,
+                       w.pack_bsum);
+    TT_CHECK_LAUNCH();
+    hipLaunchKernelGGL(pack_scan_kernel, dim3(1), dim3(kPackBlock), 0, st, w.pack_bsum, nb, w.pack_total,
+                       offsets + n_queries);
+    TT_CHECK_LAUNCH();
+    hipLaunchKernelGGL(pack_copy_kernel, dim3(ceil_div(nq, 4)), dim3(256), 0, st, w.buf, w.count, nl, p.cap, nq,
+                       w.pack_local, w.pack_bsum, entries_cap, entries, counts + q0, offsets + q0);
     TT_CHECK_LAUNCH();
   }
   return TT_OK;
+}
+
+extern "C" size_t tt_bruteforce_finalize_workspace_size(int64_t n_queries, int32_t dim, int32_t k) {
+  if (n_queries < 1 || k < 1 || pick_dpad(dim) == 0) return 0;
+  SearchPlan p = plan_search(n_queries, 1 << 20, k, 1);
+  p.chunk = round_up(n_queries, kQPerWG);
+  Carver cv(nullptr, 0);
+  carve_search(cv, pick_dpad(dim), p, false, true);
+  return cv.used();
+}
+
+extern "C" int tt_bruteforce_finalize(const void* index, const float* cand, int64_t ldc, int64_t n_cand, int32_t dim,
+                                      const float* queries, int64_t ldq, int64_t n_queries, int32_t k,
+                                      int32_t num_sources, const int64_t* entries, const int32_t* counts,
+                                      const int64_t* offsets, const float* tau, float* out_scores, int32_t* out_idx,
+                                      void* workspace, size_t workspace_bytes, tt_stream_t stream) {
+  clear_error();
+  TT_REQUIRE(index && cand, "tt_bruteforce_finalize: NULL index/cand");
+  TT_REQUIRE(n_cand >= 1 && dim >= 1 && ldc >= dim && ldq >= dim, "tt_bruteforce_finalize: bad shapes");
+  if (pick_dpad(dim) == 0) return fail(TT_ERR_UNSUPPORTED, "tt_bruteforce_finalize: dim=%d > 128", dim);
+  TT_REQUIRE(k >= 1 && k <= n_cand && k <= 4000, "tt_bruteforce_finalize: bad k=%d", k);
+  TT_REQUIRE(num_sources >= 1, "tt_bruteforce_finalize: num_sources must be >= 1");
+  TT_REQUIRE(n_queries >= 0, "tt_bruteforce_finalize: negative n_queries");
+  if (n_queries == 0) return TT_OK;
+  TT_REQUIRE(queries && counts && offsets && tau && out_scores && out_idx, "tt_bruteforce_finalize: NULL argument");
+  const int D = pick_dpad(dim);
+  SearchPlan p = plan_search(n_queries, 1 << 20, k, 1);
+  p.chunk = round_up(n_queries, kQPerWG);
+  Carver cv(workspace, workspace_bytes);
+  SearchWs w = carve_search(cv, D, p, false, true);
+  if (!workspace || cv.used() > workspace_bytes)
+    return fail(TT_ERR_WORKSPACE, "tt_bruteforce_finalize: workspace %zu < required %zu", workspace_bytes, cv.used());
+  hipStream_t st = to_stream(stream);
+  const int vec4 = is_vec4(cand, ldc, dim) ? 1 : 0;
+  TT_CHECK_HIP(hipMemsetAsync(w.fail_count, 0, (2 + kFbSlots) * sizeof(int), st));
+  if (int rc = run_prep(queries, ldq, n_queries, dim, D, index, w, false, st)) return rc;
+  Lists ls{reinterpret_cast<const uint2*>(entries), counts, tau, num_sources, 0, offsets, 1, n_queries};
+  FinalArgs fa{queries, ldq, cand, ldc, n_cand, 0, 0, dim, k, p.L, p.P, vec4,
+               n_queries, w.qflags, w.qmarg, ls, out_scores, out_idx, w.fail_count, w.fail_list};
+  FallbackArgs fb{queries, ldq, cand, ldc, n_cand, 0, dim, k, p.L, p.P, p.parts, vec4,
+                  w.fail_count, w.fail_list, w.fail_count + 1, w.fb_scratch, w.fb_scratch_n, out_scores, out_idx};
+  return run_finalize(fa, fb, n_queries, p, st);
 }

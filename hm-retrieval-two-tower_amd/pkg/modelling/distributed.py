@@ -35,7 +35,7 @@ import torch.distributed as dist
 
 logger = logging.getLogger(__name__)
 
-__all__ = ["IndexOps", "ShardedBruteForceIndex", "QueryShardedBruteForceIndex", "DataParallelTrainStep", "shard_range", "all_gather_cat",
+__all__ = ["IndexOps", "ShardIndexOps", "ShardedBruteForceIndex", "QueryShardedBruteForceIndex", "DataParallelTrainStep", "shard_range", "all_gather_cat",
            "EmbeddingOps", "ShardedTables", "ShardedTrainStep"]
 
 
@@ -74,9 +74,90 @@ class IndexOps:
                         hip_ops.topk_merge)
 
 
+@dataclass
+class ShardIndexOps:
+    """Kernels of the candidate-sharded search (tt.h: tt_bruteforce_build,
+    tt_bruteforce_shard_estimate / _screen, tt_bruteforce_finalize).
+    Injectable so the orchestration below runs on CPU over gloo in the tests
+    (oracle.shard_*); the defaults are libtt."""
+    build: Callable[[torch.Tensor], Any]
+    estimate: Callable[..., torch.Tensor]
+    screen: Callable[..., Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]
+    finalize: Callable[..., Tuple[torch.Tensor, torch.Tensor]]
+
+    @staticmethod
+    def hip() -> "ShardIndexOps":
+        from pkg.modelling import hip_ops
+
+        return ShardIndexOps(hip_ops.bruteforce_build, hip_ops.bruteforce_shard_estimate,
+                             hip_ops.bruteforce_shard_screen, hip_ops.bruteforce_finalize)
+
+
+def _staged(group) -> bool:
+    """gloo moves host tensors only: device tensors go through the host."""
+    return dist.get_backend(group) == "gloo"
+
+
+def _all_reduce_min(t: torch.Tensor, group) -> None:
+    if _staged(group) and t.is_cuda:
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.MIN, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+
+
+def _a2a_any(out: torch.Tensor, inp: torch.Tensor, out_splits: List[int], in_splits: List[int], group) -> torch.Tensor:
+    if _staged(group) and inp.is_cuda:
+        h = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(h, inp.cpu(), out_splits, in_splits, group=group)
+        out.copy_(h)
+        return out
+    return _a2a(out, inp, out_splits, in_splits, group)
+
+
+def _all_gather_any(t: torch.Tensor, group) -> torch.Tensor:
+    if _staged(group) and t.is_cuda:
+        return all_gather_cat(t.cpu(), group).to(t.device)
+    return all_gather_cat(t, group)
+
+
+def _gather_query_blocks(s: torch.Tensor, i: torch.Tensor, Q: int, world: int, group) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Rank-ordered concatenation of the per-rank query blocks
+    shard_range(Q, world, r) of (scores, indices) [block, k] -> [Q, k]."""
+    k = s.shape[1]
+    per = -(-Q // world)
+    pad_s = torch.full((per, k), float("-inf"), dtype=s.dtype, device=s.device)
+    pad_i = torch.full((per, k), -1, dtype=i.dtype, device=i.device)
+    pad_s[:s.shape[0]] = s
+    pad_i[:i.shape[0]] = i
+    all_s, all_i = _all_gather_any(pad_s, group), _all_gather_any(pad_i, group)
+    blocks = [shard_range(Q, world, r) for r in range(world)]
+    return (torch.cat([all_s[r, :e - b] for r, (b, e) in enumerate(blocks)]),
+            torch.cat([all_i[r, :e - b] for r, (b, e) in enumerate(blocks)]))
+
+
 class ShardedBruteForceIndex:
     """
-    Candidate-sharded brute-force index.
+    Candidate-sharded brute-force index (north star: "shards the
+    candidate matrix across the 8 GPUs").  BruteForceIndex.call
+    (brute_force.py:76-83) with the SCORING of the candidate rows split over
+    the ranks: rank g screens rows shard_range(N, G, g) for every query.
+
+    Protocol per search (tt.h, tt_bruteforce_shard_*):
+      1. each rank estimates, per query, the score at rank ~(3k+100)/G of its
+         rows; one all_reduce(MIN) of those [Q] floats gives a common tau;
+      2. each rank keeps its screened scores s~ > tau[q] (bf16 MFMA screen),
+         packed per query (CSR);
+      3. all_to_all: the lists of query block r (shard_range(Q, G, r)) go to
+         rank r — sizes first, then the entries (Q·~(3k+100)·8 B in total);
+      4. the owner certifies each query against the bf16 error bound,
+         rescores the surviving candidates with the exact fp32 chain and
+         returns the exact top-k (or scans the query exactly).
+    The result equals one top_k over all candidates bit for bit.  Every rank
+    keeps the full fp32 candidate matrix (105,542 x 128 = 54 MB of 288 GB):
+    the exact rescoring of step 4 may need any row; only the scoring is
+    sharded.
 
     Parameters
     ----------
@@ -84,61 +165,77 @@ class ShardedBruteForceIndex:
         Results per query.
     query_model: callable
         Query feature dict -> [B, E] embeddings (replicated on every rank).
-    local_candidates: [n_local, E] tensor
-        This rank's shard of the candidate matrix (rows shard_range(N, world, rank)).
-    index_offset: int
-        Global row of the shard's first candidate.
-    local_identifiers: optional identifiers of the local rows.
+    candidates: [N, E] tensor
+        The whole candidate matrix (replicated); this rank scores rows
+        shard_range(N, world, rank).
+    identifiers: optional identifiers of the N rows.
     """
 
-    def __init__(self, k: int, query_model, local_candidates: torch.Tensor, index_offset: int,
-                 local_identifiers=None, group=None, ops: Optional[IndexOps] = None):
+    def __init__(self, k: int, query_model, candidates: torch.Tensor, identifiers=None, group=None,
+                 ops: Optional[ShardIndexOps] = None):
         self.k = int(k)
         self.query_model = query_model
         self.group = group
-        self.ops = ops or IndexOps.hip()
+        self.ops = ops or ShardIndexOps.hip()
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        self.cand = local_candidates.contiguous()
-        self.offset = int(index_offset)
-        n_local = torch.tensor([self.cand.shape[0]], dtype=torch.int64, device=self.cand.device)
-        sizes = [torch.zeros_like(n_local) for _ in range(self.world)]
-        dist.all_gather(sizes, n_local, group=group)
-        self.shard_sizes = [int(s.item()) for s in sizes]
-        if min(self.shard_sizes) < self.k:
-            raise ValueError(f"every shard needs >= k={self.k} candidates, got {self.shard_sizes}")
-        self.num_candidates = sum(self.shard_sizes)
+        self.cand = candidates.contiguous()
+        self.num_candidates = int(self.cand.shape[0])
+        if self.num_candidates < self.k:
+            raise ValueError(f"need >= k={self.k} candidates, got {self.num_candidates}")
+        self.rows = shard_range(self.num_candidates, self.world, self.rank)
+        if self.rows[1] <= self.rows[0]:
+            raise ValueError(f"{self.world} shards for {self.num_candidates} candidates leave rank {self.rank} empty")
         self.image = self.ops.build(self.cand)
-        self.local_identifiers = local_identifiers
-
-    def search(self, query_embeddings: torch.Tensor, k: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
-        """Global (scores [Q,k], indices [Q,k]) on every rank."""
-        k = k or self.k
-        s, i = self.ops.search(self.image, self.cand, query_embeddings.contiguous(), k, self.offset)
-        all_s = all_gather_cat(s, self.group)
-        all_i = all_gather_cat(i, self.group)
-        return self.ops.merge(all_s, all_i, k)
+        self.identifiers = identifiers
 
     def search_owned(self, query_embeddings: torch.Tensor, k: Optional[int] = None
                      ) -> Tuple[Tuple[int, int], torch.Tensor, torch.Tensor]:
-        """Global top-k of this rank's query block only: ((begin, end), scores
-        [end-begin, k], indices).  Query block r = shard_range(Q, world, r).
-        One all_to_all moves each shard's lists for block r to rank r, so a
-        rank receives Q/G·G·k entries instead of the all-gather's Q·G·k, and
-        the merge work is split over the ranks too."""
+        """Exact global top-k of this rank's query block: ((begin, end),
+        scores [end-begin, k], indices [end-begin, k] int32)."""
         k = k or self.k
-        Q = int(query_embeddings.shape[0])
-        s, i = self.ops.search(self.image, self.cand, query_embeddings.contiguous(), k, self.offset)
-        blocks = [shard_range(Q, self.world, r) for r in range(self.world)]
-        in_splits = [(e - b) * k for b, e in blocks]
+        if k > self.num_candidates:
+            raise ValueError(f"k={k} exceeds the number of candidates {self.num_candidates}")
+        q = query_embeddings.contiguous()
+        Q, G = int(q.shape[0]), self.world
+        r0, r1 = self.rows
+        tau = self.ops.estimate(self.image, q, r0, r1, k, G)
+        if G > 1:
+            _all_reduce_min(tau, self.group)
+        entries, counts, offsets = self.ops.screen(self.image, q, r0, r1, k, G, tau)
+        blocks = [shard_range(Q, G, r) for r in range(G)]
+        starts = torch.tensor([b for b, _ in blocks] + [Q], dtype=torch.int64, device=offsets.device)
+        cap = int(entries.shape[0])
+        bnd = [min(int(x), cap) for x in offsets[starts].cpu().tolist()]  # the search's one host sync
+        in_splits = [bnd[r + 1] - bnd[r] for r in range(G)]
         mb, me = blocks[self.rank]
-        out_splits = [(me - mb) * k] * self.world
-        rs = torch.empty(self.world, me - mb, k, dtype=s.dtype, device=s.device)
-        ri = torch.empty(self.world, me - mb, k, dtype=i.dtype, device=i.device)
-        _a2a(rs.reshape(-1), s.reshape(-1), out_splits, in_splits, self.group)
-        _a2a(ri.reshape(-1), i.reshape(-1), out_splits, in_splits, self.group)
-        ms, mi = self.ops.merge(rs, ri, k)
-        return (mb, me), ms, mi
+        nb = me - mb
+        if G > 1:
+            sz = torch.tensor(in_splits, dtype=torch.int64, device=entries.device)
+            rsz = torch.empty_like(sz)
+            _a2a_any(rsz, sz, [1] * G, [1] * G, self.group)
+            out_splits = [int(x) for x in rsz.cpu().tolist()]
+            recv = torch.empty(sum(out_splits), dtype=torch.int64, device=entries.device)
+            _a2a_any(recv, entries[:bnd[G]], out_splits, in_splits, self.group)
+            rc = torch.empty(G * nb, dtype=torch.int32, device=counts.device)
+            _a2a_any(rc, counts, [nb] * G, [e - b for b, e in blocks], self.group)
+            rc = rc.view(G, nb)
+        else:
+            out_splits, recv, rc = in_splits, entries, counts.view(1, Q)
+        base = torch.tensor([0] + list(np.cumsum(out_splits[:-1])), dtype=torch.int64, device=rc.device)
+        cl = rc.clamp(min=0).to(torch.int64)
+        off = (torch.cumsum(cl, 1) - cl + base.view(G, 1)).contiguous()
+        s, i = self.ops.finalize(self.image, self.cand, q[mb:me].contiguous(), k, recv, rc.contiguous(), off,
+                                 tau[mb:me].contiguous())
+        return (mb, me), s, i
+
+    def search(self, query_embeddings: torch.Tensor, k: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Global (scores [Q,k], indices [Q,k]) on every rank (blocks all-gathered)."""
+        Q = int(query_embeddings.shape[0])
+        _, s, i = self.search_owned(query_embeddings, k)
+        if self.world == 1:
+            return s, i
+        return _gather_query_blocks(s, i, Q, self.world, self.group)
 
     def __call__(self, queries: Dict[str, Any]):
         with torch.no_grad():
@@ -183,20 +280,9 @@ class QueryShardedBruteForceIndex:
 
     def search(self, query_embeddings: torch.Tensor, k: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
         """Global (scores [Q,k], indices [Q,k]) on every rank (blocks all-gathered)."""
-        k = k or self.k
         Q = int(query_embeddings.shape[0])
-        (b, e), s, i = self.search_owned(query_embeddings, k)
-        per = -(-Q // self.world)
-        pad_s = torch.full((per, k), float("-inf"), dtype=s.dtype, device=s.device)
-        pad_i = torch.full((per, k), -1, dtype=i.dtype, device=i.device)
-        pad_s[:e - b] = s
-        pad_i[:e - b] = i
-        all_s, all_i = all_gather_cat(pad_s, self.group), all_gather_cat(pad_i, self.group)
-        rows = [all_s[r, :hi - lo] for r, (lo, hi) in enumerate(shard_range(Q, self.world, r)
-                                                                 for r in range(self.world))]
-        rows_i = [all_i[r, :hi - lo] for r, (lo, hi) in enumerate(shard_range(Q, self.world, r)
-                                                                   for r in range(self.world))]
-        return torch.cat(rows), torch.cat(rows_i)
+        _, s, i = self.search_owned(query_embeddings, k)
+        return _gather_query_blocks(s, i, Q, self.world, self.group)
 
     def __call__(self, queries: Dict[str, Any]):
         with torch.no_grad():

@@ -40,19 +40,47 @@ def _oracle_ops():
     return IndexOps(build=lambda c: None, search=search, merge=merge)
 
 
+def _shard_oracle_ops(tau_mode="estimate"):
+    """The candidate-sharded protocol's kernels restated on CPU
+    (oracle.shard_*).  tau_mode "inf": every screen keeps nothing, so every
+    query must reach the owner's exact fallback; "rank0_high": rank 0's
+    estimate is far too high, so the all_reduce(MIN) must save the lists."""
+    from oracle import oracle
+    from pkg.modelling.distributed import ShardIndexOps
+
+    def estimate(img, q, r0, r1, k, shards):
+        t = oracle.shard_estimate(q.numpy(), img[r0:r1], k, shards)
+        if tau_mode == "inf":
+            t[:] = np.inf
+        elif tau_mode == "rank0_high" and dist.get_rank() == 0:
+            t[:] = 1e30
+        return torch.from_numpy(t)
+
+    def screen(img, q, r0, r1, k, shards, tau):
+        e, cnt, off = oracle.shard_screen(q.numpy(), img[r0:r1], r0, tau.numpy())
+        return torch.from_numpy(e), torch.from_numpy(cnt), torch.from_numpy(off)
+
+    def finalize(img, cand, q, k, entries, counts, offsets, tau):
+        s, i = oracle.shard_finalize(q.numpy(), cand.numpy(), k, entries.numpy(), counts.numpy(), offsets.numpy(),
+                                     tau.numpy())
+        return torch.from_numpy(s), torch.from_numpy(i)
+
+    return ShardIndexOps(build=lambda c: c.numpy(), estimate=estimate, screen=screen, finalize=finalize)
+
+
 def _index_worker(rank, world, port, q, c, k, out):
     _init(rank, world, port)
-    from pkg.modelling.distributed import QueryShardedBruteForceIndex, ShardedBruteForceIndex, shard_range
+    from pkg.modelling.distributed import QueryShardedBruteForceIndex, ShardedBruteForceIndex
 
     qidx = QueryShardedBruteForceIndex(k, None, torch.from_numpy(c), ops=_oracle_ops())
     qs_s, qs_i = qidx.search(torch.from_numpy(q))
     out[("q", rank)] = (qs_s.numpy(), qs_i.numpy())
 
-    b, e = shard_range(c.shape[0], world, rank)
-    idx = ShardedBruteForceIndex(k, None, torch.from_numpy(c[b:e]), b, ops=_oracle_ops())
-    s, i = idx.search(torch.from_numpy(q))
-    blk, os_, oi = idx.search_owned(torch.from_numpy(q))
-    out[rank] = (s.numpy(), i.numpy(), idx.num_candidates, blk, os_.numpy(), oi.numpy())
+    for mode in ("estimate", "inf", "rank0_high"):
+        idx = ShardedBruteForceIndex(k, None, torch.from_numpy(c), ops=_shard_oracle_ops(mode))
+        s, i = idx.search(torch.from_numpy(q))
+        blk, os_, oi = idx.search_owned(torch.from_numpy(q))
+        out[(mode, rank)] = (s.numpy(), i.numpy(), idx.num_candidates, blk, os_.numpy(), oi.numpy())
     dist.destroy_process_group()
 
 
@@ -65,21 +93,24 @@ def test_sharded_index_equals_unsharded(world):
     c[100:140] = c[99]  # cross-shard ties must resolve by global index
     q = np.maximum(rng.standard_normal((20, 16)), 0).astype(np.float32)
     q[3] = 0.0
+    q[7] = rng.standard_normal(16).astype(np.float32)  # mixed signs: the absolute screen bound
     k = 25
     out = mp.Manager().dict()
     mp.spawn(_index_worker, args=(world, _free_port(), q, c, k, out), nprocs=world, join=True)
     rs, ri, _ = oracle.bruteforce_topk(q, c, k)
-    covered = []
+    for mode in ("estimate", "inf", "rank0_high"):
+        covered = []
+        for r in range(world):
+            s, i, n, (b, e), os_, oi = out[(mode, r)]
+            assert n == 301
+            assert np.array_equal(i, ri) and np.array_equal(s, rs), mode
+            # search_owned: this rank's query block only, same global lists
+            assert np.array_equal(oi, ri[b:e]) and np.array_equal(os_, rs[b:e]), mode
+            covered += list(range(b, e))
+        assert covered == list(range(q.shape[0]))
     for r in range(world):
-        s, i, n, (b, e), os_, oi = out[r]
-        assert n == 301
-        assert np.array_equal(i, ri) and np.array_equal(s, rs)
-        # search_owned: this rank's query block only, same global lists
-        assert np.array_equal(oi, ri[b:e]) and np.array_equal(os_, rs[b:e])
-        covered += list(range(b, e))
         qs_s, qs_i = out[("q", r)]  # query-sharded: every rank holds the full answer
         assert np.array_equal(qs_i, ri) and np.array_equal(qs_s, rs)
-    assert covered == list(range(q.shape[0]))
 
 
 class _Dense:
