@@ -12,9 +12,15 @@ random-init weights (no dataset/checkpoint download).  A step is one full
 train_step (gather, towers, fused in-batch CE fwd+bwd, MLP backward, dense
 + sparse Adagrad), replayed as a hipGraph; inputs are resident in HBM.
 
-N>1 (torchrun, one process per GPU, RCCL): weak scaling, each rank runs the
-same C3 step on its own batch of 16384 with per-replica in-batch negatives
-(the reference's train_step under data parallelism).  The large tables
+N>1 (torchrun, one process per GPU, RCCL), default --negatives global: the
+C3 step itself (global batch 16384, the reference's loss over the WHOLE
+batch, two_tower_model.py:113-122) split over the ranks — 16384/N rows per
+rank, candidate embeddings + logq all-gathered, each rank's rows scored
+against all 16384 candidates, query embeddings + lse all-gathered for the
+dC of each rank's candidates (ShardedTrainStep
+global_negatives): strong scaling, value = 16384 x steps / max-over-ranks
+time.  --negatives replica: weak scaling, each rank its own batch of 16384
+with per-replica negatives (a labelled variant).  The large tables
 (customer, postal, article) are row-sharded over the ranks (all_to_all of
 requested rows forward, of per-row gradient sums backward, Adagrad on the
 owner); small tables, MLP gradients and the loss share one all_reduce
@@ -166,12 +172,12 @@ def time_train(args, model, data, device, ws):
     from pkg.modelling.models.two_tower_model import GraphedTrainStep
     from pkg.modelling.distributed import ShardedTrainStep
 
-    B = args.batch
+    B = local_batch(args, ws)
     pool = [data.batch(B) for _ in range(4)]
     torch.cuda.synchronize()
     if ws > 1 or args.train_mode == "sharded":
         # large tables (customer, postal, article) row-sharded over the ranks
-        step = ShardedTrainStep(model, shard_min_rows=100_000)
+        step = ShardedTrainStep(model, shard_min_rows=100_000, global_negatives=args.negatives == "global")
         # routing (ids only) runs two batches ahead on a side stream
         run = lambda i: step(pool[i % len(pool)], ahead=[pool[(i + 1) % len(pool)], pool[(i + 2) % len(pool)]])
     else:
@@ -204,6 +210,16 @@ def time_train(args, model, data, device, ws):
         print("host ms/step by phase:", {k: round(v / args.steps * 1e3, 3)
                                          for k, v in step.host_times.items()}, file=sys.stderr)  # timed steps only
     return dt, loss
+
+
+def local_batch(args, ws: int) -> int:
+    """Rows per rank: the global batch split over the ranks (global
+    negatives), or a full batch per rank (per-replica negatives)."""
+    if ws > 1 and args.negatives == "global":
+        if args.batch % ws:
+            raise SystemExit(f"--batch {args.batch} must split evenly over {ws} ranks")
+        return args.batch // ws
+    return args.batch
 
 
 def time_inbatch_kernel(model, data, device, B: int, reps: int = 20):
@@ -511,6 +527,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--train-mode", choices=("auto", "sharded"), default="auto",
                     help="sharded: run the N>1 row-sharded step (ShardedTrainStep) even on one rank")
+    ap.add_argument("--negatives", choices=("global", "replica"), default="global",
+                    help="N>1: global = the C3 batch split over the ranks with negatives from the whole batch "
+                         "(strong scaling); replica = a batch per rank with per-replica negatives (weak scaling)")
     ap.add_argument("--index-mode", choices=("auto", "sharded"), default="auto",
                     help="sharded: run the N>1 candidate-sharded index (search_owned) even on one rank")
     args = ap.parse_args()
@@ -538,7 +557,8 @@ def main():
     flops, ms_rows, ms_cols, ms_entry = time_inbatch_kernel(model, data, device, B)
     gather = time_gather(model, data, device, B)
     dt, loss = time_train(args, model, data, device, ws)
-    pairs = ws * B * args.steps
+    global_neg = ws > 1 and args.negatives == "global"
+    pairs = (B if global_neg else ws * B) * args.steps
     value = pairs / dt
     ms_per_step = dt / args.steps * 1e3
 
@@ -552,16 +572,18 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if global_neg else "weak",
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic (H&M-shaped ids, Zipf; random-init weights)",
         "config": {
             "workload": "C3: main.py schema @ emb 128, towers [256]->128, logQ in-batch softmax, Adagrad, batch 16384"
-                        + (" per replica, per-replica in-batch negatives; customer/postal/article tables row-sharded "
-                           "over the ranks (all_to_all), small tables and MLP replicated (all_reduce)"
-                           if ws > 1 else ""),
-            "global_batch": ws * B,
+                        + ((f" split over {ws} ranks ({B // ws} rows each), in-batch negatives from the whole batch "
+                            "(all_gather of C, logq, Q, lse)" if global_neg else
+                            " per replica, per-replica in-batch negatives (labelled variant)")
+                           + "; customer/postal/article tables row-sharded over the ranks (all_to_all), small tables "
+                             "and MLP replicated (all_reduce)" if ws > 1 else ""),
+            "global_batch": B if global_neg else ws * B,
             "parallelism": f"dp{ws}",
         },
         "final_loss": loss,

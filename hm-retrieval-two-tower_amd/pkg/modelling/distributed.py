@@ -35,7 +35,7 @@ import torch.distributed as dist
 
 logger = logging.getLogger(__name__)
 
-__all__ = ["IndexOps", "ShardIndexOps", "ShardedBruteForceIndex", "QueryShardedBruteForceIndex", "DataParallelTrainStep", "shard_range", "all_gather_cat",
+__all__ = ["IndexOps", "ShardIndexOps", "BatchComm", "ShardedBruteForceIndex", "QueryShardedBruteForceIndex", "DataParallelTrainStep", "shard_range", "all_gather_cat",
            "EmbeddingOps", "ShardedTables", "ShardedTrainStep"]
 
 
@@ -419,8 +419,52 @@ class EmbeddingOps:
 
 
 def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits: List[int], in_splits: List[int], group) -> torch.Tensor:
+    if _staged(group) and inp.is_cuda:  # gloo: through the host
+        h = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(h, inp.cpu(), out_splits, in_splits, group=group)
+        out.copy_(h)
+        return out
     dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
     return out
+
+
+def _all_reduce_sum(t: torch.Tensor, group) -> None:
+    if _staged(group) and t.is_cuda:
+        h = t.cpu()
+        dist.all_reduce(h, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, group=group)
+
+
+class BatchComm:
+    """all_gather / reduce_scatter of equal per-rank blocks along dim 0, for
+    the global-negatives loss (losses.global_inbatch_grads): RCCL
+    all_gather_into_tensor / reduce_scatter_tensor; over gloo (CPU tests, or
+    several ranks sharing one GPU) through the host."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world == 1:
+            return t
+        out = _all_gather_any(t.contiguous(), self.group)
+        return out.reshape((self.world * t.shape[0],) + tuple(t.shape[1:]))
+
+    def reduce_scatter(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world == 1:
+            return t
+        n = t.shape[0] // self.world
+        if _staged(self.group):  # gloo has no reduce_scatter: sum everywhere, keep this rank's block
+            h = t.detach().cpu().contiguous()
+            dist.all_reduce(h, group=self.group)
+            return h[self.rank * n:(self.rank + 1) * n].to(t.device)
+        out = torch.empty((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.reduce_scatter_tensor(out, t.contiguous(), group=self.group)
+        return out
 
 
 class _Route:
@@ -576,7 +620,7 @@ class ShardedTables:
         per = (rows + W - 1) // W
         mine = torch.zeros(per, self.dim, dtype=torch.float32, device=self.shard[name].device)
         mine[:self.shard[name].shape[0]] = self.shard[name]
-        parts = all_gather_cat(mine, self.group)
+        parts = _all_gather_any(mine, self.group)
         full = torch.empty(rows, self.dim, dtype=torch.float32, device=mine.device)
         for r in range(W):
             n = len(range(r, rows, W))
@@ -627,11 +671,23 @@ class ShardedTrainStep:
     own process group while this step computes, so its host sync does not
     stall the compute stream.
 
+    global_negatives=True (the reference's semantics, two_tower_model.py:
+    113-122: every query row's negatives are the candidates of the GLOBAL
+    batch): the towers run on this rank's rows, the candidate embeddings and
+    logq are all-gathered, the rows pass scores this rank's queries against
+    all of them (positive of local row i = global column rank*b + i); the
+    query embeddings and their lse are all-gathered and the cols pass scores
+    all of them against this rank's candidates (dC of its columns).  The
+    loss and every gradient are those of the global batch (tests:
+    test_distributed_gloo global loss, test_distributed_gpu step).  The
+    collectives sit inside the captured middle with RCCL; False keeps
+    per-replica negatives (a labelled variant).
+
     Adagrad (the reference's optimizer, main.py:100-101) only.
     """
 
     def __init__(self, model, shard_min_rows: int = 100_000, group=None, ops: Optional[EmbeddingOps] = None,
-                 use_graph: bool = True):
+                 use_graph: bool = True, global_negatives: bool = False):
         from pkg.modelling.optimizer_factory import Adagrad
 
         opt = model.optimizer
@@ -642,7 +698,13 @@ class ShardedTrainStep:
         self.ops = ops or EmbeddingOps.hip()
         self.world = dist.get_world_size(group)
         self.lr, self.eps, self.init = opt.learning_rate, opt.epsilon, opt.initial_accumulator_value
-        self.use_graph = use_graph
+        self.global_negatives = bool(global_negatives)
+        self.comm = BatchComm(group) if self.global_negatives else None
+        # the global-negatives middle holds collectives: captured with RCCL
+        # (eager fallback if capture fails; TT_EAGER_COLLECTIVES=1 forces
+        # eager), never over gloo (host staging synchronises)
+        self.use_graph = use_graph and not (self.global_negatives and self.world > 1 and (
+            _staged(group) or os.environ.get("TT_EAGER_COLLECTIVES") == "1"))
         big: Dict[str, torch.Tensor] = {}
         self.small: Dict[Any, Any] = {}
         for tower in model.towers:
@@ -773,7 +835,15 @@ class ShardedTrainStep:
             widths.append(layer.output_dim)
         anchors = [layer._anchor for layer in layers]
         qi, ci = _ShardedGatherFn.apply(self, calls, self._B, widths, *anchors)
-        loss = m.tower_loss(qi, ci, m.candidate_logq(x))
+        if self.global_negatives:
+            from pkg.modelling.losses import global_towers_inbatch_softmax_xent
+
+            if m.loss.reduction != "sum":
+                raise NotImplementedError("global negatives: the reference's SUM reduction only")
+            loss = global_towers_inbatch_softmax_xent(qi, ci, m.query_tower.dense, m.candidate_tower.dense,
+                                                      self.comm, m.candidate_logq(x))
+        else:
+            loss = m.tower_loss(qi, ci, m.candidate_logq(x))
         for t in m.towers:
             t.dense.flat.grad = None
         if getattr(self, "_one", None) is None:
@@ -880,7 +950,7 @@ class ShardedTrainStep:
         if rt is not None:
             self.tables.apply_routed(rt, self._g_req, self.lr, self.eps)
         tm = self._tick("apply", tm)
-        dist.all_reduce(self._bucket, group=self.group)
+        _all_reduce_sum(self._bucket, self.group)
         off = 0
         for ti, t in enumerate(m.towers):
             n = t.dense.flat.numel()

@@ -17,7 +17,8 @@ import torch
 
 from pkg.modelling import hip_ops
 
-__all__ = ["InBatchSoftmaxCrossEntropy", "inbatch_softmax_xent", "towers_inbatch_softmax_xent", "TOWER_C_SCOPE"]
+__all__ = ["InBatchSoftmaxCrossEntropy", "inbatch_softmax_xent", "towers_inbatch_softmax_xent",
+           "global_inbatch_grads", "global_towers_inbatch_softmax_xent", "TOWER_C_SCOPE"]
 
 
 class _InBatchXent(torch.autograd.Function):
@@ -95,6 +96,65 @@ class _TowersInBatchXent(torch.autograd.Function):
             ctx.on_tower(0, gqi, gflat_q)
         main.wait_stream(side)
         return gqi, gci, gflat_q, gflat_c, None, None, None, None, None
+
+
+def global_inbatch_grads(q: torch.Tensor, c: torch.Tensor, logq: Optional[torch.Tensor], comm,
+                         rows=None, cols=None):
+    """This rank's share of the in-batch loss over the GLOBAL batch
+    (two_tower_model.py:113-122 with the batch split over the ranks: row i's
+    negatives are every candidate of every rank).  q, c: this rank's [b, E]
+    rows (global rows rank*b ...); comm: all_gather over the ranks (equal b
+    everywhere).  Returns (row_loss [b], dq [b, E], dc [b, E]): the loss
+    terms of this rank's rows, d loss / d q of its rows, and d (global loss)
+    / d c of its candidates.  The rows pass scores the local queries against
+    all candidates; the cols pass scores all queries (with their lse) against
+    the local candidates, so every gradient is summed inside one kernel in a
+    fixed order (no cross-rank reduction of partial sums)."""
+    rows = rows or hip_ops.inbatch_rows
+    cols = cols or hip_ops.inbatch_cols
+    b = q.shape[0]
+    off = comm.rank * b
+    C = comm.all_gather(c)                                     # [G b, E]
+    L = comm.all_gather(logq) if logq is not None else None   # [G b]
+    lse, row_loss, dq = rows(q, C, L, pos_offset=off)
+    Qa = comm.all_gather(q)                                    # [G b, E]
+    lse_a = comm.all_gather(lse)                               # [G b]
+    dc = cols(Qa, lse_a, c, logq, pos_offset=off)              # local columns, every row
+    return row_loss, dq, dc
+
+
+class _GlobalTowersInBatchXent(torch.autograd.Function):
+    """_TowersInBatchXent with global in-batch negatives (global_inbatch_grads):
+    the returned loss is this rank's rows' share; the step sums it (and the
+    gradients) over the ranks."""
+
+    @staticmethod
+    def forward(ctx, qi, ci, flat_q, flat_c, logq, stack_q, stack_c, scale, comm):
+        qa = stack_q.forward_acts(qi, flat_q)
+        ca = stack_c.forward_acts(ci, flat_c)
+        row_loss, dq, dc = global_inbatch_grads(qa[-1], ca[-1], logq, comm)
+        ctx.stacks = (stack_q, stack_c)
+        ctx.nq = len(qa)
+        ctx.scale = scale
+        ctx.save_for_backward(flat_q, flat_c, dq, dc, *qa, *ca)
+        return hip_ops.loss_sum(row_loss, scale)
+
+    @staticmethod
+    def backward(ctx, g):
+        flat_q, flat_c, dq, dc, *acts = ctx.saved_tensors
+        qa, ca = acts[:ctx.nq], acts[ctx.nq:]
+        s = (g * ctx.scale if ctx.scale != 1.0 else g).reshape(1).float().contiguous()
+        stack_q, stack_c = ctx.stacks
+        gci, gflat_c = stack_c.backward_acts(ca, flat_c, dc, s, ctx.needs_input_grad[1])
+        gqi, gflat_q = stack_q.backward_acts(qa, flat_q, dq, s, ctx.needs_input_grad[0])
+        return gqi, gci, gflat_q, gflat_c, None, None, None, None, None
+
+
+def global_towers_inbatch_softmax_xent(qi: torch.Tensor, ci: torch.Tensor, stack_q, stack_c, comm,
+                                       logq: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """towers_inbatch_softmax_xent with the negatives of every rank (SUM
+    reduction, the reference's runner.py:78-83)."""
+    return _GlobalTowersInBatchXent.apply(qi, ci, stack_q.flat, stack_c.flat, logq, stack_q, stack_c, 1.0, comm)
 
 
 def towers_inbatch_softmax_xent(qi: torch.Tensor, ci: torch.Tensor, stack_q, stack_c,

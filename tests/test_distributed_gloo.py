@@ -283,3 +283,56 @@ def test_sharded_tables_match_unsharded_adagrad(world):
         ref[k] = np.where(touched[:, None], upd, ref[k])
         for r in range(world):
             np.testing.assert_allclose(out[r][1][k], ref[k], rtol=0, atol=2e-6)
+
+
+def _global_loss_worker(rank, world, port, q, c, logq, out):
+    _init(rank, world, port)
+    from oracle import oracle
+    from pkg.modelling.distributed import BatchComm
+    from pkg.modelling.losses import global_inbatch_grads
+
+    def rows(qq, C, L, pos_offset):
+        r = oracle.inbatch_softmax_xent(qq.numpy(), C.numpy(), None if L is None else L.numpy(), pos_offset)
+        return torch.from_numpy(r["lse"]), torch.from_numpy(r["row_loss"]), torch.from_numpy(r["dq"])
+
+    def cols(Qa, lse, cl, L, pos_offset):  # all rows (with their lse) against the local columns
+        S = Qa.numpy() @ cl.numpy().T - (0.0 if L is None else L.numpy()[None, :])
+        P = np.exp(S - lse.numpy()[:, None])
+        P[pos_offset + np.arange(cl.shape[0]), np.arange(cl.shape[0])] -= 1.0
+        return torch.from_numpy(P.T @ Qa.numpy())
+
+    b = q.shape[0] // world
+    sl = slice(rank * b, (rank + 1) * b)
+    row_loss, dq, dc = global_inbatch_grads(torch.from_numpy(q[sl]), torch.from_numpy(c[sl]),
+                                            torch.from_numpy(logq[sl]), BatchComm(), rows, cols)
+    out[rank] = (row_loss.numpy(), dq.numpy(), dc.numpy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_global_negatives_loss_equals_full_batch(world):
+    """Global in-batch negatives split over the ranks (all_gather of the
+    candidates and logq, rows pass with the positive at rank*b + i, cols pass
+    share reduce-scattered) equal the reference loss over the whole batch
+    (two_tower_model.py:113-122): every row's loss term, dQ, and dC.
+    (The CPU ops restate the rows / cols passes; comm is the real gloo one.)"""
+    from oracle import oracle
+
+    rng = np.random.default_rng(1)
+    B, E = 12 * world, 8
+    q = rng.standard_normal((B, E))
+    c = rng.standard_normal((B, E))
+    logq = np.log(rng.dirichlet(np.ones(B)))
+    ref = oracle.inbatch_softmax_xent(q, c, logq)
+    out = mp.Manager().dict()
+    mp.spawn(_global_loss_worker, args=(world, _free_port(), q, c, logq, out), nprocs=world, join=True)
+    b = B // world
+    total = 0.0
+    for r in range(world):
+        rl, dq, dc = out[r]
+        sl = slice(r * b, (r + 1) * b)
+        np.testing.assert_allclose(rl, ref["row_loss"][sl], rtol=1e-12)
+        np.testing.assert_allclose(dq, ref["dq"][sl], rtol=1e-10, atol=1e-12)
+        np.testing.assert_allclose(dc, ref["dc"][sl], rtol=1e-10, atol=1e-12)
+        total += rl.sum()
+    assert abs(total - ref["loss"]) <= 1e-10 * abs(ref["loss"])
