@@ -679,8 +679,9 @@ class ShardedTrainStep:
     query embeddings and their lse are all-gathered and the cols pass scores
     all of them against this rank's candidates (dC of its columns).  The
     loss and every gradient are those of the global batch (tests:
-    test_distributed_gloo global loss, test_distributed_gpu step).  The
-    collectives sit inside the captured middle with RCCL; False keeps
+    test_distributed_gloo global loss, test_distributed_gpu step).  With
+    world > 1 that middle runs eagerly by default (its collectives are not
+    captured into the hipGraph; TT_GRAPH_COLLECTIVES=1 opts in).  False keeps
     per-replica negatives (a labelled variant).
 
     Adagrad (the reference's optimizer, main.py:100-101) only.
@@ -700,11 +701,11 @@ class ShardedTrainStep:
         self.lr, self.eps, self.init = opt.learning_rate, opt.epsilon, opt.initial_accumulator_value
         self.global_negatives = bool(global_negatives)
         self.comm = BatchComm(group) if self.global_negatives else None
-        # the global-negatives middle holds collectives: captured with RCCL
-        # (eager fallback if capture fails; TT_EAGER_COLLECTIVES=1 forces
-        # eager), never over gloo (host staging synchronises)
+        # the global-negatives middle holds collectives: it runs eagerly unless
+        # TT_GRAPH_COLLECTIVES=1 asks to capture them with RCCL (never over
+        # gloo, whose host staging synchronises)
         self.use_graph = use_graph and not (self.global_negatives and self.world > 1 and (
-            _staged(group) or os.environ.get("TT_EAGER_COLLECTIVES") == "1"))
+            _staged(group) or os.environ.get("TT_GRAPH_COLLECTIVES") != "1"))
         big: Dict[str, torch.Tensor] = {}
         self.small: Dict[Any, Any] = {}
         for tower in model.towers:
