@@ -451,6 +451,49 @@ def time_index_sharded(device, n_queries: int, n_cand: int, k: int, ws: int, ran
     return res
 
 
+def time_pipeline(model, data, device, rows: int, B: int, encode_n: int = 2_000_000):
+    """modelling_runner's training input path at scale: `rows` synthetic
+    H&M-shaped examples encoded into an HBM-resident DeviceDataset, one epoch
+    of TwoTowerModel.fit (one hipGraph replay per batch: device batch take +
+    train step; the partial last batch eager), timed after a first epoch
+    that captures the graph.  Plus the host StringLookup rate of libtt's
+    native vocabulary on 64-hex-char customer ids (H&M's id format)."""
+    from pkg.modelling.dataset import DeviceDataset
+    from pkg.schema.vocab import NativeVocab
+
+    cols = {}
+    for s in range(0, rows, 1 << 20):
+        b = data.batch(min(1 << 20, rows - s))
+        for k, v in b.items():
+            cols.setdefault(k, []).append(v.cpu().numpy())
+    cols = {k: np.concatenate(v) for k, v in cols.items()}
+    ds = DeviceDataset(cols, B, shuffle_size=100_000, seed=0, device=device)
+    model.fit(ds, epochs=1, use_graph=True)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    model.fit(ds, epochs=1, use_graph=True)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t
+    del ds
+    rng = np.random.default_rng(0)
+    vocab = np.array([f"{x:016x}{x ^ 0x5bd1e995:016x}" * 2
+                      for x in rng.integers(0, 2**62, HM_VOCAB["customer_id"]).tolist()])
+    nv = NativeVocab(vocab)
+    import pyarrow as pa
+
+    vals = pa.array(vocab[rng.integers(0, len(vocab), encode_n)])
+    nv.encode(vals[:1000])
+    t = time.perf_counter()
+    nv.encode(vals)
+    enc_dt = time.perf_counter() - t
+    return {"rows": rows, "batch": B, "shuffle_size": 100_000, "epoch_seconds": dt, "rows_per_s": rows / dt,
+            "note": "fit over an HBM-resident DeviceDataset: tt_batch_take + train step replayed as one hipGraph "
+                    "per batch, partial last batch eager, one host sync per epoch",
+            "encode": {"values": encode_n, "vocab": len(vocab), "seconds": enc_dt, "values_per_s": encode_n / enc_dt,
+                       "threads": os.cpu_count() if os.cpu_count() and os.cpu_count() < 64 else 64,
+                       "note": "libtt tt_vocab_encode (host hash StringLookup) of 64-char hex ids, Arrow input"}}
+
+
 def cpu_baseline(seconds_budget: float = 20.0):
     """oracle.CpuTwoTower (numpy fp32 restatement of the same train step) on
     host cores, same schema and batch, timed over whole steps until ~budget."""
@@ -524,6 +567,8 @@ def main():
     ap.add_argument("--fused-apply", action="store_true",
                     help="apply each tower's Adagrad inside the backward (TwoTowerModel fused_optimizer_apply)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pipeline-rows", type=int, default=10_000_000,
+                    help="rows of the device-resident input-pipeline leg (0 skips it; N=1 only)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--train-mode", choices=("auto", "sharded"), default="auto",
                     help="sharded: run the N>1 row-sharded step (ShardedTrainStep) even on one rank")
@@ -609,6 +654,9 @@ def main():
         result["index"] = time_index(device, args.index_queries, HM_VOCAB["article_id"], 100)
     elif not args.no_index:
         result["index"] = time_index_sharded(device, args.index_queries, HM_VOCAB["article_id"], 100, ws, rank)
+    if ws == 1 and args.pipeline_rows > 0:
+        result["pipeline"] = time_pipeline(model, data, device, args.pipeline_rows, B)
+        result["pipeline"]["vs_train_step_rate"] = result["pipeline"]["rows_per_s"] / value
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:

@@ -198,6 +198,14 @@ _PROTOS = {
     ),
     "tt_topk_merge": (c_int32, [c_void_p, c_void_p, c_int32, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
     "tt_recall_hits": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, POINTER(c_int32), c_int32, c_void_p, c_void_p]),
+    "tt_vocab_create": (c_int32, [c_void_p, c_void_p, c_int64, POINTER(c_void_p)]),
+    "tt_vocab_size": (c_int64, [c_void_p]),
+    "tt_vocab_encode": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int32]),
+    "tt_vocab_destroy": (c_int32, [c_void_p]),
+    "tt_batch_take": (
+        c_int32,
+        [c_void_p, c_int64, c_int32, c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_int64, c_void_p,
+         c_void_p]),
 }
 
 EXPORTED_SYMBOLS = tuple(_PROTOS.keys())

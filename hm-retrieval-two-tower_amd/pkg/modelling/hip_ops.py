@@ -721,3 +721,25 @@ def recall_hits(true_ids: torch.Tensor, cand_ids: torch.Tensor, ks: Sequence[int
     ks_arr = (ctypes.c_int32 * len(ks))(*[int(k) for k in ks])
     check(lib().tt_recall_hits(true_ids.data_ptr(), cand_ids.data_ptr(), B, K, ks_arr, len(ks), hits.data_ptr(),
                                _stream()))
+
+
+def batch_take(src: torch.Tensor, perm: torch.Tensor, cursor: torch.Tensor, out: torch.Tensor,
+               advance: bool = True, status: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out[c, b] = src[c, perm[cursor + b]] for the 32-bit word columns of an
+    HBM-resident dataset (tt_batch_take); cursor (device int64 [1]) advances by
+    the batch when `advance`.  Graph-capturable: nothing is read on the host."""
+    _req(src, "src", torch.int32, 2)
+    _req(perm, "perm", torch.int64, 1)
+    _req(cursor, "cursor", torch.int64, 1)
+    _req(out, "out", torch.int32, 2)
+    if src.shape[0] != out.shape[0]:
+        raise ValueError(f"src has {src.shape[0]} columns, out {out.shape[0]}")
+    if perm.numel() != src.shape[1]:
+        raise ValueError(f"perm has {perm.numel()} entries for {src.shape[1]} rows")
+    if status is not None:
+        _req(status, "status", torch.int32, 1)
+    check(lib().tt_batch_take(src.data_ptr(), _row_major(src, "src"), src.shape[0], perm.data_ptr(), src.shape[1],
+                              cursor.data_ptr(), out.shape[1], int(bool(advance)), out.data_ptr(),
+                              _row_major(out, "out"), status.data_ptr() if status is not None else None,
+                              _stream()))
+    return out

@@ -108,3 +108,16 @@ class BruteForceIndex(AbstractKerasModel):
             "identifiers": ident.cpu() if isinstance(ident, torch.Tensor)
             else torch.as_tensor(np.arange(len(ident))),
         }
+
+    def save(self, model_path: str) -> None:
+        """Candidates, identifiers, k and the query tower (pkg.modelling.export):
+        a loaded index answers raw queries on its own (brute_force.py:108-114)."""
+        from pkg.modelling import export
+
+        export.save_index(self, model_path[:-3] if model_path.endswith(".pt") else model_path)
+
+    @classmethod
+    def load(cls, model_path: str, device: Optional[torch.device] = None) -> "BruteForceIndex":
+        from pkg.modelling import export
+
+        return export.load_index(model_path[:-3] if model_path.endswith(".pt") else model_path, device)

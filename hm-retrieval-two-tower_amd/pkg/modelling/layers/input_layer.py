@@ -141,8 +141,14 @@ class InputLayer:
             out[f.name] = torch.as_tensor(f.encode(x[f.name]), device=self.device)
         return out
 
-    def _ids(self, v) -> torch.Tensor:
-        t = v if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v))
+    def _ids(self, v, feature: Optional[Feature] = None) -> torch.Tensor:
+        if not isinstance(v, torch.Tensor):
+            a = np.asarray(v)
+            # raw values (the reference's tf.string inputs): StringLookup on the host
+            if feature is not None and a.dtype.kind in "OUS":
+                return torch.as_tensor(feature.encode(a), device=self.device)
+            v = a
+        t = v if isinstance(v, torch.Tensor) else torch.as_tensor(v)
         t = t.reshape(-1)
         if t.dtype != torch.int32:
             t = t.to(torch.int32)
@@ -161,7 +167,7 @@ class InputLayer:
             segments.append((v, None, len(segments)))
         ids_by_call = []
         for f, off in zip(self.categorical_features, self.column_offsets()):
-            ids = self._ids(x[f.name])
+            ids = self._ids(x[f.name], f)
             batch = ids.numel() if batch is None else batch
             if ids.numel() != batch:
                 raise ValueError(f"feature {f.name} has {ids.numel()} rows, expected {batch}")

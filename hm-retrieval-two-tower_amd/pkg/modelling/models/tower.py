@@ -255,6 +255,18 @@ class Tower(AbstractKerasModel):
         sd["dense.flat"] = self.dense.flat.detach().cpu()
         return sd
 
+    def save(self, model_path: str) -> None:
+        """Weights (.pt), architecture (.json), vocabularies (.npz)."""
+        from pkg.modelling import export
+
+        export.save_tower(self, model_path[:-3] if model_path.endswith(".pt") else model_path)
+
+    @classmethod
+    def load(cls, model_path: str, device: Optional[torch.device] = None) -> "Tower":
+        from pkg.modelling import export
+
+        return export.load_tower(model_path[:-3] if model_path.endswith(".pt") else model_path, device)
+
     def load_state_dict(self, sd: Dict[str, torch.Tensor]) -> None:
         for t in self.input_layer.tables():
             t.weight.copy_(sd[f"tables.{t.name}"].to(t.weight.device))

@@ -214,6 +214,10 @@ class TwoTowerModel(AbstractKerasModel):
             use_graph: bool = False) -> Dict[str, List[float]]:
         """Train for `epochs` passes; returns {"loss": [mean batch loss per epoch]}
         (Keras' loss metric is the running mean over the epoch's batches)."""
+        from pkg.modelling.dataset import DeviceDataset
+
+        if use_graph and isinstance(dataset, DeviceDataset) and dataset.fn is None and dataset.batch_size:
+            return self._fit_device(dataset, epochs, callbacks)
         history: Dict[str, List[float]] = {"loss": []}
         graphed: Optional[GraphedTrainStep] = None
         for epoch in range(epochs):
@@ -234,6 +238,41 @@ class TwoTowerModel(AbstractKerasModel):
             mean = float(total.item()) / max(n, 1)
             history["loss"].append(mean)
             logger.info(f"epoch {epoch + 1}/{epochs}: loss {mean:.6f} over {n} batches")
+            for cb in callbacks or []:
+                if callable(cb):
+                    cb(epoch, {"loss": mean})
+        return history
+
+    def _fit_device(self, ds, epochs: int, callbacks) -> Dict[str, List[float]]:
+        """fit over an HBM-resident DeviceDataset: each full batch is one replay
+        of a graph that takes the batch on the device and trains on it; the
+        partial last batch runs eagerly.  One host sync per epoch (the loss)."""
+        history: Dict[str, List[float]] = {"loss": []}
+        B, nfull = int(ds.batch_size), ds.full_batches
+        rem = ds.num_rows - nfull * B
+        graphed = getattr(self, "_device_fit_graph", None)
+        if graphed is not None and (graphed.source is not ds or graphed.model is not self):
+            graphed = None
+        for epoch in range(epochs):
+            ds.begin_epoch()
+            todo = nfull
+            if todo and graphed is None:
+                graphed = GraphedTrainStep(self, None, warmup=1, source=ds)  # warm-up = this epoch's batch 0
+                self._device_fit_graph = graphed
+                todo -= 1
+            elif graphed is not None:
+                graphed.loss_total.zero_()
+            for _ in range(todo):
+                graphed.graph.replay()
+            total = graphed.loss_total.clone() if graphed is not None else torch.zeros(
+                (), dtype=torch.float64, device=self.device)
+            if rem:
+                total += self.train_step(ds.view(ds.take(rem)))["loss"].double()
+            ds.check_status()
+            n = nfull + (1 if rem else 0)
+            mean = float(total.item()) / max(n, 1)
+            history["loss"].append(mean)
+            logger.info(f"epoch {epoch + 1}/{epochs}: loss {mean:.6f} over {n} batches (device-resident, graphed)")
             for cb in callbacks or []:
                 if callable(cb):
                     cb(epoch, {"loss": mean})
@@ -264,14 +303,23 @@ class TwoTowerModel(AbstractKerasModel):
     def save(self, model_path: str) -> None:
         """Save the two-tower model and each tower separately in the
         two_tower / query_tower / candidate_tower entries of the model
-        directory (two_tower_model.py:176-205), as weights-only checkpoints."""
+        directory (two_tower_model.py:176-205): weights (.pt, weights-only),
+        architecture (.json) and vocabularies (.npz) — pkg.modelling.export."""
+        from pkg.modelling import export
+
         base = os.path.dirname(model_path)
         os.makedirs(base or ".", exist_ok=True)
-        for name, obj in (("two_tower", self), ("query_tower", self.query_tower),
-                          ("candidate_tower", self.candidate_tower)):
-            path = os.path.join(base, name + ".pt")
-            logging.info(f"Saving {name} at path: {path}")
-            torch.save(obj.state_dict(), path)
+        logging.info(f"Saving two_tower, query_tower, candidate_tower under {base or '.'}")
+        export.save_two_tower(self, os.path.join(base, "two_tower"))
+        export.save_tower(self.query_tower, os.path.join(base, "query_tower"))
+        export.save_tower(self.candidate_tower, os.path.join(base, "candidate_tower"))
+
+    @classmethod
+    def load(cls, model_path: str, device: Optional[torch.device] = None) -> "TwoTowerModel":
+        """The model saved by save(model_path) (compile() it again to train)."""
+        from pkg.modelling import export
+
+        return export.load_two_tower(os.path.join(os.path.dirname(model_path), "two_tower"), device)
 
 
 class GraphedTrainStep:
@@ -285,32 +333,60 @@ class GraphedTrainStep:
     are real optimisation steps on the example batch.  Requires an optimizer
     whose kernels do not depend on the host step count (Adagrad)."""
 
-    def __init__(self, model: TwoTowerModel, example_batch: Dict[str, Any], warmup: int = 2):
+    def __init__(self, model: TwoTowerModel, example_batch: Optional[Dict[str, Any]], warmup: int = 2,
+                 source=None):
+        """source: a pkg.modelling.dataset.DeviceDataset whose next batch is
+        taken on the device inside the graph (tt_batch_take, cursor in device
+        memory) — every replay then trains on the dataset's next batch and
+        adds its loss to `loss_total` (fp64, device) with no host work."""
         from pkg.modelling.optimizer_factory import Adagrad
 
         if not isinstance(model.optimizer, Adagrad):
             raise ValueError("graph capture needs the Adagrad optimizer (Adam's coefficients depend on the step)")
         self.model = model
-        ex = {k: self._to_dev(v, model.device).reshape(-1) for k, v in example_batch.items()}
-        self.int_keys = sorted(k for k, v in ex.items() if v.dtype != torch.float32)
-        self.float_keys = sorted(k for k, v in ex.items() if v.dtype == torch.float32)
-        self.batch_size = next(iter(ex.values())).shape[0]
+        self.source = source
+        if source is not None:
+            if not source.batch_size:
+                raise ValueError("a graphed DeviceDataset source needs a batch_size")
+            self.int_keys, self.float_keys = list(source.int_keys), list(source.float_keys)
+            self.batch_size = int(source.batch_size)
+            ex = None
+        else:
+            ex = {k: self._to_dev(v, model.device).reshape(-1) for k, v in example_batch.items()}
+            self.int_keys = sorted(k for k, v in ex.items() if v.dtype != torch.float32)
+            self.float_keys = sorted(k for k, v in ex.items() if v.dtype == torch.float32)
+            self.batch_size = next(iter(ex.values())).shape[0]
         B = self.batch_size
-        self._ibuf = torch.empty(max(len(self.int_keys), 1), B, dtype=torch.int32, device=model.device)
-        self._fbuf = torch.empty(max(len(self.float_keys), 1), B, dtype=torch.float32, device=model.device)
+        K, F = len(self.int_keys), len(self.float_keys)
+        # one [K + F, B] buffer of 32-bit words: int rows first, then float rows
+        # (the DeviceDataset layout, so one take launch fills the whole batch)
+        self._wbuf = torch.empty(max(K + F, 1), B, dtype=torch.int32, device=model.device)
+        self._ibuf = self._wbuf[:K] if K else torch.empty(1, B, dtype=torch.int32, device=model.device)
+        self._fbuf = (self._wbuf[K:K + F].view(torch.float32) if F
+                      else torch.empty(1, B, dtype=torch.float32, device=model.device))
         self.static = {k: self._ibuf[i] for i, k in enumerate(self.int_keys)}
         self.static.update({k: self._fbuf[i] for i, k in enumerate(self.float_keys)})
-        self.load(ex)
+        self.loss_total = torch.zeros((), dtype=torch.float64, device=model.device)
+        if ex is not None:
+            self.load(ex)
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for _ in range(max(warmup, 1)):
-                out = model.train_step(self.static)
+                out = self._step()
             self.warmup_out = {k: v.clone() for k, v in out.items()}
         torch.cuda.current_stream().wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            self.out = model.train_step(self.static)
+            self.out = self._step()
+
+    def _step(self) -> Dict[str, torch.Tensor]:
+        if self.source is not None:
+            self.source.take(self.batch_size, out=self._wbuf)
+        out = self.model.train_step(self.static)
+        if self.source is not None:
+            self.loss_total += out["loss"].double()
+        return out
 
     @staticmethod
     def _to_dev(v, device):

@@ -7,7 +7,10 @@ the test set BEFORE the epoch's training (runner.py:99-103), fit one epoch,
 save model and index; finally re-log the last recall (runner.py:107).
 
 Datasets are this framework's encoded shards (pkg.modelling.dataset) found in
-the directories of the settings' *_tfrecord_path fields.  If a shard carries
+the directories of the settings' *_tfrecord_path fields.  On the GPU they are
+loaded into HBM once (DeviceDataset: batches assembled on the device) and
+training replays one hipGraph per batch (take + train step); use_graph=False
+or device_resident=False select the eager / host-batched paths.  If a shard carries
 "__raw__<candidate_col>" (integer codes of the raw candidate ids), those are
 used as index identifiers and recall ground truth, so OOV candidates that
 share embedding row 0 remain distinct, as raw string ids are in the
@@ -21,7 +24,7 @@ import os
 import torch
 
 from pkg.etl.transformations import date_filter, load_dataframe
-from pkg.modelling.dataset import EncodedDataset
+from pkg.modelling.dataset import DeviceDataset, EncodedDataset
 from pkg.modelling.indices.brute_force import BruteForceIndex
 from pkg.modelling.indices.static_index import StaticIndex
 from pkg.modelling.losses import CategoricalCrossentropy
@@ -36,19 +39,20 @@ logger = logging.getLogger(__name__)
 RAW_PREFIX = "__raw__"
 
 
-def modelling_runner(settings: Settings, use_graph: bool = False):
+def modelling_runner(settings: Settings, use_graph: bool = True, device_resident: bool = True):
     """Train a Two-Tower Model and evaluate it (runner.py:18-108)."""
     logger.info("--- Modelling Starting ---")
     schema = Schema.load_from_filepath(settings.schema_filepath)
     tc = schema.training_config
     cand_col = settings.candidate_col_name
     raw_col = RAW_PREFIX + cand_col
-    train_ds = EncodedDataset.load(os.path.dirname(settings.train_data_tfrecord_path), tc.train_batch_size,
-                                   tc.shuffle_size)
-    test_ds = EncodedDataset.load(os.path.dirname(settings.test_data_tfrecord_path), tc.test_batch_size)
+    resident = device_resident and torch.cuda.is_available()
+    loader = DeviceDataset.load if resident else EncodedDataset.load
+    train_ds = loader(os.path.dirname(settings.train_data_tfrecord_path), tc.train_batch_size, tc.shuffle_size)
+    test_ds = loader(os.path.dirname(settings.test_data_tfrecord_path), tc.test_batch_size)
     test_ds = test_ds.map(lambda x: ({f.name: x[f.name] for f in schema.query_features},
                                      x[raw_col] if raw_col in x else x[cand_col]))
-    candidate_ds = EncodedDataset.load(os.path.dirname(settings.candidate_tfrecord_path), tc.candidate_batch_size)
+    candidate_ds = loader(os.path.dirname(settings.candidate_tfrecord_path), tc.candidate_batch_size)
 
     model = TwoTowerModel.create_from_schema(schema, cand_col)
     optimizer = OptimizerFactory.get_optimizer(tc.optimizer_name, tc.optimizer_kwargs)

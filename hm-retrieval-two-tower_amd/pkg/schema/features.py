@@ -79,6 +79,7 @@ class Feature:
                 raise TypeError(f"Got embedding size, dtype must be tf.string got {dtype}")
         self.embedding_size = embedding_size
         self._lookup: Optional[Dict[str, int]] = None
+        self._native = None
         self._init_vocab(vocab)
 
         if max_vocab_size:
@@ -102,6 +103,7 @@ class Feature:
                 self.vocab = None
                 self.is_built = False
         self._lookup = None
+        self._native = None
 
     def set_vocab_from_dataframe(self, df: pd.DataFrame) -> None:
         """
@@ -118,6 +120,7 @@ class Feature:
         self.vocab = np.array([str(x) for x in vocab])
         self.is_built = True
         self._lookup = None
+        self._native = None
 
     # ---- id encoding (StringLookup) -------------------------------------
     @property
@@ -134,21 +137,27 @@ class Feature:
             self._lookup = {v: i + 1 for i, v in enumerate(self.vocab)}
         return self._lookup
 
-    def encode(self, values: Sequence) -> np.ndarray:
-        """Strings (or anything str()-able) -> int32 rows; OOV -> 0."""
-        table = self.lookup_table()
-        flat = np.asarray(values, dtype=object).reshape(-1)
-        out = np.empty(flat.shape[0], dtype=np.int32)
-        for i, v in enumerate(flat):
-            if isinstance(v, bytes):
-                v = v.decode()
-            out[i] = table.get(str(v), 0)
-        return out
+    def encode(self, values: Sequence, num_threads: int = 0) -> np.ndarray:
+        """Strings (or anything str()-able) -> int32 rows; OOV -> 0.  Runs in
+        libtt's multi-threaded host hash lookup (pkg.schema.vocab), built once
+        per vocabulary."""
+        if self.vocab is None:
+            raise ValueError(f"feature {self.name} has no vocab")
+        if self._native is None:
+            from pkg.schema.vocab import NativeVocab
+
+            self._native = NativeVocab(self.vocab)
+        return self._native.encode(values, num_threads)
 
     def __getstate__(self):
         state = dict(self.__dict__)
         state["_lookup"] = None
+        state["_native"] = None
         return state
+
+    def __setstate__(self, state):
+        state.setdefault("_native", None)
+        self.__dict__.update(state)
 
     def __repr__(self) -> str:
         return (f"Feature({self.name!r}, {self.dtype}, {self.feature_family}, "

@@ -429,6 +429,37 @@ int tt_recall_hits(const int32_t* true_ids, const int32_t* cand_ids,
                    int64_t batch, int32_t k_total, const int32_t* ks_host,
                    int32_t num_ks, int64_t* hits, tt_stream_t stream);
 
+
+/* ------------------------------------------------------------------------ *
+ * K15  Input pipeline.
+ * Replaces the TFRecord dataset (pkg/modelling/tfrecord_dataset.py:59-98)
+ * and the per-batch StringLookup (pkg/modelling/layers/input_layer.py:33-36).
+ *
+ * Host vocabulary (CPU only, no device memory): strings are passed as an
+ * Arrow-style arena — `data` bytes and `offsets[n + 1]` (int64, value i is
+ * data[offsets[i] .. offsets[i+1])).  vocab[i] -> row i + 1, any other value
+ * -> row 0 (StringLookup num_oov_indices=1); a value listed twice maps to its
+ * last row.  tt_vocab_create copies the arena; `num_threads` <= 0 uses every
+ * hardware thread (at most 64).
+ * ------------------------------------------------------------------------ */
+int tt_vocab_create(const char* data, const int64_t* offsets, int64_t n, void** out_vocab);
+int64_t tt_vocab_size(const void* vocab);
+int tt_vocab_encode(const void* vocab, const char* data, const int64_t* offsets, int64_t n,
+                    int32_t* out_rows, int32_t num_threads);
+int tt_vocab_destroy(void* vocab);
+
+/* Device batch assembly from an HBM-resident dataset of 32-bit words
+ * (int32 rows / float32 values), column-major `src[ncols][src_ld]`:
+ *   dst[c * dst_ld + b] = src[c * src_ld + perm[*cursor + b]],  b < batch,
+ * then (advance != 0) *cursor += batch.  perm (int64 [n_rows]) is the
+ * epoch's example order (the reference's shuffle buffer), cursor an int64 in
+ * device memory, so the call can be captured in a replayed graph.  A position
+ * or permutation entry outside [0, n_rows) writes zero words and ORs 1 into
+ * *status (optional device int32). */
+int tt_batch_take(const void* src, int64_t src_ld, int32_t ncols, const int64_t* perm, int64_t n_rows,
+                  int64_t* cursor, int64_t batch, int32_t advance, void* dst, int64_t dst_ld,
+                  int32_t* status, tt_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
