@@ -277,6 +277,92 @@ def pmc_traffic(kernel: str):
     return None
 
 
+def _graph_time(fn, reps: int) -> float:
+    """ms per call of fn, `reps` calls replayed from one hipGraph between HIP
+    events on the current stream (no host overhead between launches)."""
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(graph, stream=side):
+            for _ in range(reps):
+                fn()
+    torch.cuda.current_stream().wait_stream(side)
+    graph.replay()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    graph.replay()
+    e1.record(stream)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def time_gather_uniform(model, device, B: int, reps: int = 50, c5_rows: int = 100_000_000, c5_batch: int = 65536):
+    """The gather with no cache help: (1) the C3 step's both-tower launch with
+    UNIFORM ids over every table (the 1.37M-row customer table alone is 702 MB,
+    far beyond the 256 MB Infinity Cache); (2) BASELINE configs[4]'s 100M x 128
+    fp32 table (51.2 GB) gathered at batch 65,536 with uniform ids."""
+    from pkg.modelling import hip_ops
+
+    g = torch.Generator(device=device)
+    g.manual_seed(7)
+    launches, nbytes = [], 0
+    for tower in (model.query_tower, model.candidate_tower):
+        layer = tower.input_layer
+        segs = []
+        for f in layer.numerical_features:
+            segs.append((torch.zeros(B, device=device), None, len(segs)))
+            nbytes += B * 8
+        for f, off in zip(layer.categorical_features, layer.column_offsets()):
+            w = layer.embedding_layers[f.name].weight
+            ids = torch.randint(0, w.shape[0], (B,), generator=g, device=device, dtype=torch.int32)
+            segs.append((w, ids, off))
+            nbytes += B * (4 + 8 * w.shape[1])
+        launches.append((segs, torch.empty(B, layer.output_dim, device=device)))
+    with torch.no_grad():
+        ms = _graph_time(lambda: hip_ops.gather_multi(launches, B), reps)
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    out = {"kernel": "gather_grouped_kernel, C3 step shapes, uniform ids", "bound": "hbm", "achieved": gbs,
+           "peak": MI355X_HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / MI355X_HBM_PEAK_GBS,
+           "algorithmic_bytes_per_launch": nbytes, "ms_per_launch": ms}
+    if c5_rows:
+        table = torch.empty(c5_rows, 128, device=device)  # 51.2 GB; contents irrelevant to the rate
+        ids = torch.randint(0, c5_rows, (c5_batch,), generator=g, device=device, dtype=torch.int32)
+        o = torch.empty(c5_batch, 128, device=device)
+        with torch.no_grad():
+            ms5 = _graph_time(lambda: hip_ops.gather_grouped([(table, ids, 0)], c5_batch, o), reps)
+        nb5 = c5_batch * (4 + 8 * 128)
+        out["c5_100m_table"] = {"rows": c5_rows, "dim": 128, "batch": c5_batch, "ms_per_launch": ms5,
+                                "achieved": nb5 / (ms5 * 1e-3) / 1e9, "unit": "GB/s",
+                                "frac": nb5 / (ms5 * 1e-3) / 1e9 / MI355X_HBM_PEAK_GBS,
+                                "algorithmic_bytes_per_launch": nb5}
+        del table
+        torch.cuda.empty_cache()
+    return out
+
+
+def rocprof_avg_ms(kernel: str):
+    """Average duration (ms) of `kernel` in the newest committed rocprofv3
+    --stats summary (profiles/*_bench_kernel_stats.csv), or None."""
+    import csv
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_bench_kernel_stats.csv")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        for r in csv.DictReader(f):
+            if kernel in r["Name"]:
+                return {"ms": float(r["AverageNs"]) * 1e-6, "calls": int(r["Calls"]),
+                        "source": os.path.relpath(files[-1], ROOT)}
+    return None
+
+
 def time_gather(model, data, device, B: int, reps: int = 50):
     """K2+K3 gather of both towers' inputs for one step's batch in one
     tt_gather_multi launch (as the train step issues it), HIP events on the
@@ -567,6 +653,8 @@ def main():
     ap.add_argument("--fused-apply", action="store_true",
                     help="apply each tower's Adagrad inside the backward (TwoTowerModel fused_optimizer_apply)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-uniform-gather", action="store_true",
+                    help="skip the uniform-id gather legs (C3 shapes and the 100M-row C5 table)")
     ap.add_argument("--pipeline-rows", type=int, default=10_000_000,
                     help="rows of the device-resident input-pipeline leg (0 skips it; N=1 only)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
@@ -601,6 +689,8 @@ def main():
     # kernel-level timings on the unsharded model, before the train step takes its tables
     flops, ms_rows, ms_cols, ms_entry = time_inbatch_kernel(model, data, device, B)
     gather = time_gather(model, data, device, B)
+    if ws == 1 and not args.no_uniform_gather:
+        gather["uniform_ids"] = time_gather_uniform(model, device, B)
     dt, loss = time_train(args, model, data, device, ws)
     global_neg = ws > 1 and args.negatives == "global"
     pairs = (B if global_neg else ws * B) * args.steps
@@ -650,6 +740,12 @@ def main():
         },
         "gather_roofline": gather,
     }
+    rp = rocprof_avg_ms("inbatch_pass_kernel<128, 0>")
+    if rp is not None:
+        # the profiler's dispatch timestamps (no event overhead around each launch)
+        a_rp = flops / (rp["ms"] * 1e-3) / 1e12
+        result["roofline"]["rocprof"] = {"ms_per_launch": rp["ms"], "calls": rp["calls"], "achieved": a_rp,
+                                         "frac": a_rp / MI355X_BF16_DENSE_TFLOPS, "source": rp["source"]}
     if ws == 1 and args.index_mode == "auto" and not args.no_index:
         result["index"] = time_index(device, args.index_queries, HM_VOCAB["article_id"], 100)
     elif not args.no_index:

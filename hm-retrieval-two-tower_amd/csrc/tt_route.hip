@@ -185,7 +185,7 @@ int plan_route(const tt_route_lookup* lookups, int32_t num, int64_t batch, int32
   size_t sb = 0;
   unsigned long long* kp = nullptr;
   uint32_t* vp = nullptr;
-  hipError_t e = rocprim::radix_sort_pairs(nullptr, sb, kp, kp, vp, vp, static_cast<unsigned>(p->total), 0,
+  hipError_t e = rocprim::radix_sort_pairs<SortConfig>(nullptr, sb, kp, kp, vp, vp, static_cast<unsigned>(p->total), 0,
                                            p->end_bit, nullptr, false);
   p->sort_bytes = (e == hipSuccess) ? sb : static_cast<size_t>(p->total) * 24 + (size_t(4) << 20);
   return TT_OK;
@@ -224,7 +224,7 @@ extern "C" size_t tt_route_workspace_size(int32_t num_lookups, int64_t batch, in
   size_t sb = 0;
   unsigned long long* kp = nullptr;
   uint32_t* vp = nullptr;
-  hipError_t e = rocprim::radix_sort_pairs(nullptr, sb, kp, kp, vp, vp, static_cast<unsigned>(p.total), 0,
+  hipError_t e = rocprim::radix_sort_pairs<SortConfig>(nullptr, sb, kp, kp, vp, vp, static_cast<unsigned>(p.total), 0,
                                            p.end_bit, nullptr, false);
   p.sort_bytes = (e == hipSuccess) ? sb : static_cast<size_t>(p.total) * 24 + (size_t(4) << 20);
   Carver cv(nullptr, 0);
@@ -260,7 +260,7 @@ extern "C" int tt_route_requests(const tt_route_lookup* lookups, int32_t num_loo
   hipLaunchKernelGGL(route_keys_kernel, dim3(static_cast<unsigned>(ceil_div(p.total, 256))), dim3(256), 0, st, a);
   TT_CHECK_LAUNCH();
   size_t sb = p.sort_bytes;
-  TT_CHECK_HIP(rocprim::radix_sort_pairs(w.sort_tmp, sb, w.keys_in, w.keys, w.vals_in, w.vals,
+  TT_CHECK_HIP(rocprim::radix_sort_pairs<SortConfig>(w.sort_tmp, sb, w.keys_in, w.keys, w.vals_in, w.vals,
                                          static_cast<unsigned>(p.total), 0, p.end_bit, st, false));
   const unsigned nb = static_cast<unsigned>(ceil_div(p.total, kScanThreads));
   TT_CHECK_HIP(hipMemsetAsync(counts, 0, static_cast<size_t>(world) * sizeof(long long), st));

@@ -509,7 +509,7 @@ int make_plan(const tt_sparse_table* tables, int cnt, int64_t batch, const float
   j.fp1 = h1;
   size_t sb = 0;
   uint32_t* np = nullptr;
-  hipError_t e = rocprim::radix_sort_pairs(nullptr, sb, np, np, np, np, static_cast<unsigned>(base), 0, p->end_bit,
+  hipError_t e = rocprim::radix_sort_pairs<SortConfig>(nullptr, sb, np, np, np, np, static_cast<unsigned>(base), 0, p->end_bit,
                                            nullptr, false);
   // rocPRIM picks its config from the device; on a host without one (size
   // queries only) use a bound: a key/value ping-pong copy plus 4 MiB.
@@ -607,7 +607,7 @@ int run_sparse(const tt_sparse_table* tables, int32_t num_tables, int64_t batch,
       hipLaunchKernelGGL(build_keys_kernel, dim3(ceil_div(p.total, kThreads)), dim3(kThreads), 0, st, j, p.total);
       TT_CHECK_LAUNCH();
       size_t sb = p.sort_bytes;
-      TT_CHECK_HIP(rocprim::radix_sort_pairs(w.sort_tmp, sb, w.keys_in, w.keys, w.vals_in, w.vals,
+      TT_CHECK_HIP(rocprim::radix_sort_pairs<SortConfig>(w.sort_tmp, sb, w.keys_in, w.keys, w.vals_in, w.vals,
                                              static_cast<unsigned>(p.total), 0, p.end_bit, st, false));
     }
     if (stage == kStageSort) continue;

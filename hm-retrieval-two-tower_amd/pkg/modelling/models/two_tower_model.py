@@ -35,6 +35,9 @@ __all__ = ["TwoTowerModel", "GraphedTrainStep", "LOGQ_KEY"]
 # Optional batch entry carrying per-example log p(candidate) computed from raw
 # ids at encoding time (exact even for ids outside a truncated vocab).
 LOGQ_KEY = "__logq__"
+# where the embedding update's id sort may start: after the whole forward
+# ("loss") or as soon as the batch's ids are gathered ("gather")
+SORT_AFTER = os.environ.get("TT_SORT_AFTER", "loss")
 
 
 class TwoTowerModel(AbstractKerasModel):
@@ -140,6 +143,18 @@ class TwoTowerModel(AbstractKerasModel):
             call = self._logq_call(x)  # rides in the towers' gather launch
             qi, ci = InputLayer.gather_many([self.query_tower.input_layer, self.candidate_tower.input_layer], [q, c],
                                             extra=[call] if call is not None else ())
+            self._sort_issued = False
+            if training and qi.is_cuda:
+                # the embedding update's id sort needs only these ids
+                self._ids_ready = torch.cuda.Event()
+                self._ids_ready.record()
+                if (SORT_AFTER == "early" and getattr(self, "_in_train_step", False)
+                        and hasattr(self.optimizer, "prepare") and getattr(self, "_on_tower", None) is None):
+                    # issued (and so captured) right here: a graph replays nodes
+                    # in capture order, so a sort captured after the backward
+                    # starts after it even when only the ids gate it
+                    self.optimizer.prepare(self.towers, after=self._ids_ready)
+                    self._sort_issued = True
             logq = call[1].view(-1) if call is not None else self.candidate_logq(x)
             return self.tower_loss(qi, ci, logq)
 
@@ -176,17 +191,22 @@ class TwoTowerModel(AbstractKerasModel):
             raise RuntimeError("call compile(optimizer=...) before training")
         fused = self.fused_optimizer_apply and isinstance(self.optimizer, Adagrad) and self.device.type == "cuda"
         self._on_tower = self._apply_tower if fused else None
+        self._in_train_step = True
         try:
             loss = self.compute_loss(data, training=True)
         finally:
             self._on_tower = None
+            self._in_train_step = False
         fwd_done = None
         if fused:
             # one id sort per tower on a side stream, before the backward needs it
             self.optimizer.prepare_towers(self.towers, ["", TOWER_C_SCOPE])
-        elif hasattr(self.optimizer, "prepare") and loss.is_cuda:
-            fwd_done = torch.cuda.Event()
-            fwd_done.record()
+        elif hasattr(self.optimizer, "prepare") and loss.is_cuda and not getattr(self, "_sort_issued", False):
+            if SORT_AFTER == "gather" and getattr(self, "_ids_ready", None) is not None:
+                fwd_done = self._ids_ready
+            else:
+                fwd_done = torch.cuda.Event()
+                fwd_done.record()
         for t in self.towers:
             t.dense.flat.grad = None
         if getattr(self, "_one", None) is None or self._one.device != loss.device:
