@@ -1,0 +1,481 @@
+// K4 (tower MLP), row-streaming form: C = epi(maskA(A) . B) for a tall fp32
+// activation A [M, K] and a small weight operand B [K, N] (K, N <= 288),
+// the shape of every Dense-layer GEMM of the towers except the weight
+// gradients (/root/reference/pkg/modelling/models/tower.py:41-49):
+//   forward   h = relu(x W + b)                       B = W,   epi bias + relu
+//   backward  g_in = (g_out * relu'(y) * s) W^T        B = W^T, maskA = relu'(y) * s,
+//             (optionally * relu'(x) for the layer below: epi cmask)
+//
+// Precision: bf16x3 on v_mfma_f32_32x32x16_bf16 with fp32 accumulation:
+// a = a_hi + a_lo, b = b_hi + b_lo (hi = bf16(x), lo = bf16(x - hi)),
+// a_lo b_hi + a_hi b_lo + a_hi b_hi — every product to ~2^-17 relative,
+// i.e. fp32-faithful (the model-level parity tests hold the fp32 tolerance).
+//
+// Layout (MI355X): B is tiny and read by every workgroup, so it is split
+// ONCE per call into a bf16 hi/lo image already in MFMA B-fragment order
+// (tt_mlp_pack): one wave's fragment for (k-step, 32-column block, plane) is
+// 1 KiB contiguous, so each wave loads its fragments straight from L2 into
+// VGPRs with fully coalesced 16-B-per-lane loads, 3 k-steps ahead.  A is
+// streamed once: 64 rows per workgroup (256 workgroups fill the 256 CUs at
+// M = 16384), 64-deep fp32 stages loaded row-contiguous by range-checked
+// buffer loads two stages ahead (rows past M and depths past K read as 0),
+// masked, split into hi/lo and written to a double-buffered XOR-swizzled LDS
+// tile, read back as A fragments with conflict-free ds_read_b128.  The main
+// loop is branch-free (the image is zero-padded to whole stages and to 4
+// column blocks per wave row), so the compiler's vmcnt waits are exact.
+// 4 waves; wave w computes rows 0..63 x the 32-column blocks w, w+4, w+8
+// (each B fragment is loaded by exactly one wave of the workgroup).
+#include <type_traits>
+
+#include "tt_common.h"
+
+namespace tt {
+namespace {
+
+constexpr int kMlpThreads = 256;
+constexpr int kMlpBM = 64;       // rows per workgroup
+constexpr int kMlpBK = 64;       // depth per A stage (4 MFMA k-steps)
+constexpr int kMlpMaxCB = 3;     // 32-column blocks per wave (N <= 384)
+
+
+struct MlpArgs {
+  const float* A;
+  int64_t lda;
+  const float* amask;  // A := (amask > 0) ? A * s : 0   (HAS_MASK)
+  int64_t ldam;
+  const float* scale;  // device scalar s (NULL: 1)
+  const __bf16* img;   // B image [KSp][NBp][2][64][8]
+  int64_t M;
+  int K, N, KSp, NBp;
+  const float* bias;   // epilogue + bias[n] (NULL: none)
+  int relu;
+  const float* cmask;  // epilogue: C := (cmask > 0) ? C : 0 (NULL: none)
+  int64_t ldcm;
+  float* C;
+  int64_t ldc;
+  float* parts;        // optional [gridDim.x][N]: per-workgroup column sums of C
+};
+
+// Raw buffer resource over `bytes` bytes: loads past the end return 0.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mlp_desc(const void* base, uint64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0,
+                                           static_cast<int>(bytes > 0x7fffffffull ? 0x7fffffffu : bytes),
+                                           0x00020000);
+}
+
+__device__ __forceinline__ f32x4 mlp_load4(__amdgpu_buffer_rsrc_t d, unsigned voff) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(d, voff, 0, 0));
+}
+
+__device__ __forceinline__ unsigned bf16_bits(float v) {
+  return static_cast<unsigned>(__builtin_bit_cast(unsigned short, static_cast<__bf16>(v)));
+}
+__device__ __forceinline__ float bf16_val(unsigned bits) { return __uint_as_float(bits << 16); }
+
+// LDS A tile: plane p, row r (0..63), 16-B chunk c (0..7) of the 64-deep stage
+// at byte (p * 64 + r) * 128 + ((c ^ ((r >> 1) & 7)) << 4): the 16 lanes of
+// one ds_read_b128 cycle (16 consecutive rows, one chunk) cover all 64 banks.
+__device__ __forceinline__ int a_lds_off(int plane, int row, int chunk) {
+  return ((plane * kMlpBM + row) << 7) + ((chunk ^ ((row >> 1) & 7)) << 4);
+}
+
+template <int NCB, bool HAS_MASK>
+__global__ void __launch_bounds__(kMlpThreads) mlp_rows_kernel(const MlpArgs a) {
+  // A stages (2 x 2 planes x 64 rows x 128 B = 32 KiB), then the output tile
+  // [64][NCB * 128 + 4] fp32 of the epilogue (<= 97 KiB)
+  constexpr int OUT_LD = NCB * 128 + 4;
+  constexpr int SMEM = kMlpBM * OUT_LD * 4 > 2 * 2 * kMlpBM * 128 ? kMlpBM * OUT_LD * 4 : 2 * 2 * kMlpBM * 128;
+  __shared__ __attribute__((aligned(16))) char smem_raw[SMEM];
+  char (*smem)[2 * kMlpBM * 128] = reinterpret_cast<char (*)[2 * kMlpBM * 128]>(smem_raw);
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int lane = lane_id();
+  const int l32 = lane & 31, h = lane >> 5;
+  const int64_t m0 = static_cast<int64_t>(blockIdx.x) * kMlpBM;
+  const float s = a.scale ? *a.scale : 1.0f;
+
+  // ---- A stages: thread -> rows qrow + 16 u (u < 4), depths qk .. qk + 3 ------
+  // (16 threads per row: 256 contiguous bytes per row per stage)
+  const int qrow = tid >> 4, qk = (tid & 15) * 4;
+  const __amdgpu_buffer_rsrc_t da = mlp_desc(a.A + m0 * a.lda, static_cast<uint64_t>(a.M - m0) * a.lda * 4);
+  const __amdgpu_buffer_rsrc_t dm = mlp_desc(HAS_MASK ? a.amask + m0 * a.ldam : a.A, static_cast<uint64_t>(a.M - m0) * a.ldam * 4);
+  f32x4 ra[2][4], rm[2][4];
+  auto fetch_a = [&](int k0, auto slot_c) {
+    constexpr int SL = decltype(slot_c)::value;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int row = qrow + 16 * u;
+      ra[SL][u] = mlp_load4(da, static_cast<unsigned>((row * a.lda + k0 + qk) * 4));
+      if constexpr (HAS_MASK) rm[SL][u] = mlp_load4(dm, static_cast<unsigned>((row * a.ldam + k0 + qk) * 4));
+    }
+  };
+  auto stash_a = [&](int k0, auto slot_c, int buf) {
+    constexpr int SL = decltype(slot_c)::value;
+    char* base = smem[buf];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int row = qrow + 16 * u;
+      unsigned hb[4], lb[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = (k0 + qk + e < a.K) ? ra[SL][u][e] : 0.0f;  // depths past K (or a ragged row's tail)
+        if constexpr (HAS_MASK) v = (rm[SL][u][e] > 0.0f) ? v * s : 0.0f;
+        hb[e] = bf16_bits(v);
+        lb[e] = bf16_bits(v - bf16_val(hb[e]));
+      }
+      const int chunk = qk >> 3, half = (qk >> 2) & 1;
+      *reinterpret_cast<uint2*>(base + a_lds_off(0, row, chunk) + 8 * half) =
+          make_uint2(hb[0] | (hb[1] << 16), hb[2] | (hb[3] << 16));
+      *reinterpret_cast<uint2*>(base + a_lds_off(1, row, chunk) + 8 * half) =
+          make_uint2(lb[0] | (lb[1] << 16), lb[2] | (lb[3] << 16));
+    }
+  };
+
+  // ---- B fragments: k-step ks, block i (column block wave + 4 i), plane p ----
+  const bf16x8* img = reinterpret_cast<const bf16x8*>(a.img) + lane;
+  const int64_t kstride = static_cast<int64_t>(a.NBp) * 2 * 64;  // bf16x8 per k-step
+  bf16x8 bq[4][NCB][2];  // k-step ks in slot ks % 4 (static under the 2-stage unroll)
+  auto load_b = [&](int ks, auto slot_c) {
+    constexpr int SL = decltype(slot_c)::value;
+    const int kc = ks < a.KSp ? ks : a.KSp - 1;  // past the end: a harmless re-read
+#pragma unroll
+    for (int i = 0; i < NCB; ++i) {
+      const bf16x8* p = img + kc * kstride + ((wave + 4 * i) * 2) * 64;
+      bq[SL][i][0] = p[0];
+      bq[SL][i][1] = p[64];
+    }
+  };
+
+  f32x16 acc[2][NCB];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int i = 0; i < NCB; ++i) acc[rb][i] = f32x16{};
+
+  const int nstage = (a.K + kMlpBK - 1) / kMlpBK;  // KSp = 4 nstage
+  const int ks_end = (a.K + 15) / 16;               // k-steps holding data
+  load_b(0, std::integral_constant<int, 0>());
+  load_b(1, std::integral_constant<int, 1>());
+  load_b(2, std::integral_constant<int, 2>());
+  fetch_a(0, std::integral_constant<int, 0>());
+  fetch_a(kMlpBK, std::integral_constant<int, 1>());
+  stash_a(0, std::integral_constant<int, 0>(), 0);
+  __syncthreads();
+  // stage st (parity PAR): A of stage st + 1 sits in ra[1 - PAR], stage st + 2
+  // is fetched into ra[PAR]; k-steps 4 st .. 4 st + 3 use B slots 0..3 and
+  // prefetch k-steps 4 st + 3 .. 4 st + 6.
+  auto stage = [&](int st, auto par_c) {
+    constexpr int PAR = decltype(par_c)::value;
+    fetch_a((st + 2) * kMlpBK, std::integral_constant<int, PAR>());
+    const char* base = smem[PAR];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int ks = 4 * st + kk;
+      if (kk == 0) load_b(ks + 3, std::integral_constant<int, 3>());
+      if (kk == 1) load_b(ks + 3, std::integral_constant<int, 0>());
+      if (kk == 2) load_b(ks + 3, std::integral_constant<int, 1>());
+      if (kk == 3) load_b(ks + 3, std::integral_constant<int, 2>());
+      if (ks >= ks_end) continue;  // the zero padding of the last stage (uniform)
+      bf16x8 ah[2], al[2];
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        const int row = 32 * rb + l32, chunk = 2 * kk + h;
+        ah[rb] = *reinterpret_cast<const bf16x8*>(base + a_lds_off(0, row, chunk));
+        al[rb] = *reinterpret_cast<const bf16x8*>(base + a_lds_off(1, row, chunk));
+      }
+#pragma unroll
+      for (int i = 0; i < NCB; ++i)
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          acc[rb][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[rb], bq[kk][i][0], acc[rb][i], 0, 0, 0);
+          acc[rb][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[rb], bq[kk][i][1], acc[rb][i], 0, 0, 0);
+          acc[rb][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[rb], bq[kk][i][0], acc[rb][i], 0, 0, 0);
+        }
+    }
+    if (st + 1 < nstage) {
+      stash_a((st + 1) * kMlpBK, std::integral_constant<int, 1 - PAR>(), 1 - PAR);
+      __syncthreads();
+    }
+  };
+  for (int st = 0; st < nstage; st += 2) {
+    stage(st, std::integral_constant<int, 0>());
+    if (st + 1 < nstage) stage(st + 1, std::integral_constant<int, 1>());
+  }
+
+  // ---- epilogue: lane (l32, h), register r -> row (r & 3) + 8 (r >> 2) + 4 h, column l32
+  // acc (+ bias, relu) -> LDS tile [64][OUT_LD] (column = 32 cb + l32 of this
+  // wave's blocks, in block order cb = wave + 4 i), then row-contiguous vector
+  // stores of C with the epilogue mask read the same way (coalesced).
+  __syncthreads();  // every wave is done reading the A stages
+  float* tile = reinterpret_cast<float*>(smem_raw);
+#pragma unroll
+  for (int i = 0; i < NCB; ++i) {
+    const int col = (wave + 4 * i) * 32 + l32;
+    const float b = (a.bias && col < a.N) ? a.bias[col] : 0.0f;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float v = acc[rb][i][r] + b;
+        if (a.relu) v = v > 0.0f ? v : 0.0f;
+        tile[(32 * rb + (r & 3) + 8 * (r >> 2) + 4 * h) * OUT_LD + col] = v;
+      }
+  }
+  __syncthreads();
+  const int64_t rows = a.M - m0 < kMlpBM ? a.M - m0 : kMlpBM;
+  float* C = a.C + m0 * a.ldc;
+  const float* cm = a.cmask ? a.cmask + m0 * a.ldcm : nullptr;
+  // 16-B stores of whole rows; a ragged N writes its row's padding columns
+  // (zeros: the image is zero there) when the row pitch has room for them
+  const int n4 = (a.N + 3) / 4 * 4;
+  const bool v4 = (a.ldc % 4 == 0) && (a.ldc >= n4) && (reinterpret_cast<uintptr_t>(a.C) % 16 == 0) &&
+                  (!cm || ((a.N % 4 == 0) && (a.ldcm % 4 == 0) && (reinterpret_cast<uintptr_t>(a.cmask) % 16 == 0)));
+  if (v4) {
+    const int per_row = n4 / 4;
+    for (int idx = tid; idx < rows * per_row; idx += kMlpThreads) {
+      const int row = idx / per_row, c4 = (idx - row * per_row) * 4;
+      f32x4 v = *reinterpret_cast<const f32x4*>(tile + row * OUT_LD + c4);
+      if (cm) {
+        const f32x4 mk = *reinterpret_cast<const f32x4*>(cm + row * a.ldcm + c4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = mk[e] > 0.0f ? v[e] : 0.0f;
+        if (a.parts) *reinterpret_cast<f32x4*>(tile + row * OUT_LD + c4) = v;  // masked, for the column sums
+      }
+      *reinterpret_cast<f32x4*>(C + row * a.ldc + c4) = v;
+    }
+  } else {
+    for (int idx = tid; idx < rows * a.N; idx += kMlpThreads) {
+      const int row = idx / a.N, c = idx - row * a.N;
+      float v = tile[row * OUT_LD + c];
+      if (cm && !(cm[row * a.ldcm + c] > 0.0f)) v = 0.0f;
+      if (cm && a.parts) tile[row * OUT_LD + c] = v;
+      C[row * a.ldc + c] = v;
+    }
+  }
+  if (a.parts == nullptr) return;
+  // column sums (the bias gradient of the layer below when C is its masked
+  // output gradient): this workgroup's rows in order; mlp_colsum_kernel then
+  // adds the workgroups' partials in workgroup order (deterministic).
+  __syncthreads();
+  for (int c = tid; c < a.N; c += kMlpThreads) {
+    float sum = 0.0f;
+    for (int row = 0; row < rows; ++row) sum += tile[row * OUT_LD + c];  // already masked
+    a.parts[static_cast<int64_t>(blockIdx.x) * a.N + c] = sum;
+  }
+}
+
+// out[c] = sum over b of parts[b][c] in b order; 64 columns x 16 row groups
+// per block, the 16 group sums added in order in LDS.
+__global__ void __launch_bounds__(1024) mlp_colsum_kernel(const float* __restrict__ parts, int nblk, int N,
+                                                          float* __restrict__ out) {
+  __shared__ float red[16][65];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int grp = threadIdx.x >> 6;
+  const int per = (nblk + 15) / 16;
+  float sum = 0.0f;
+  if (c < N) {
+    const int b1 = min(nblk, (grp + 1) * per);
+    for (int b = grp * per; b < b1; ++b) sum += parts[static_cast<int64_t>(b) * N + c];
+  }
+  red[grp][threadIdx.x & 63] = sum;
+  __syncthreads();
+  if (grp == 0 && c < N) {
+    float t = red[0][threadIdx.x];
+#pragma unroll
+    for (int g = 1; g < 16; ++g) t += red[g][threadIdx.x];
+    out[c] = t;
+  }
+}
+
+// One thread per (k-step, column block, lane): 8 hi + 8 lo bf16 of
+// B[k = 16 ks + 8 (lane >> 5) + j][n = 32 cb + (lane & 31)], j < 8, zero padded.
+// trans: B = W^T with W [N, K] row-major (B[k][n] = W[n * ldw + k]).
+__global__ void __launch_bounds__(256) mlp_pack_kernel(const float* __restrict__ w, int64_t ldw, int K, int N,
+                                                       int trans, int KS, int NB, __bf16* __restrict__ img) {
+  const int64_t t = blockIdx.x * 256ll + threadIdx.x;
+  if (t >= static_cast<int64_t>(KS) * NB * 64) return;
+  const int lane = static_cast<int>(t & 63);
+  const int cb = static_cast<int>((t >> 6) % NB);
+  const int ks = static_cast<int>((t >> 6) / NB);
+  const int n = 32 * cb + (lane & 31);
+  unsigned hb[8], lb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 16 * ks + 8 * (lane >> 5) + j;
+    const float v = (k < K && n < N) ? (trans ? w[static_cast<int64_t>(n) * ldw + k] : w[static_cast<int64_t>(k) * ldw + n])
+                                     : 0.0f;
+    hb[j] = bf16_bits(v);
+    lb[j] = bf16_bits(v - bf16_val(hb[j]));
+  }
+  u32x4 hv, lv;
+  hv.x = hb[0] | (hb[1] << 16); hv.y = hb[2] | (hb[3] << 16); hv.z = hb[4] | (hb[5] << 16); hv.w = hb[6] | (hb[7] << 16);
+  lv.x = lb[0] | (lb[1] << 16); lv.y = lb[2] | (lb[3] << 16); lv.z = lb[4] | (lb[5] << 16); lv.w = lb[6] | (lb[7] << 16);
+  const int64_t base = ((static_cast<int64_t>(ks) * NB + cb) * 2) * 64 + lane;
+  reinterpret_cast<u32x4*>(img)[base] = hv;        // plane 0: hi
+  reinterpret_cast<u32x4*>(img)[base + 64] = lv;   // plane 1: lo
+}
+
+// image k-steps padded to whole 64-deep stages, column blocks to 4 per wave row
+struct PackJob {
+  const float* w;
+  int64_t ldw;
+  int K, N, trans, KS, NB;
+  __bf16* img;
+  int64_t first;  // first thread of this job
+};
+constexpr int kMaxPackJobs = 8;
+struct PackJobs {
+  PackJob j[kMaxPackJobs];
+  int n;
+};
+
+__global__ void __launch_bounds__(256) mlp_pack_many_kernel(const PackJobs jobs, int64_t total) {
+  const int64_t t = blockIdx.x * 256ll + threadIdx.x;
+  if (t >= total) return;
+  int q = 0;
+  while (q + 1 < jobs.n && t >= jobs.j[q + 1].first) ++q;
+  const PackJob& J = jobs.j[q];
+  const int64_t u = t - J.first;
+  const int lane = static_cast<int>(u & 63);
+  const int cb = static_cast<int>((u >> 6) % J.NB);
+  const int ks = static_cast<int>((u >> 6) / J.NB);
+  const int n = 32 * cb + (lane & 31);
+  unsigned hb[8], lb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 16 * ks + 8 * (lane >> 5) + j;
+    const float v = (k < J.K && n < J.N) ? (J.trans ? J.w[static_cast<int64_t>(n) * J.ldw + k]
+                                                    : J.w[static_cast<int64_t>(k) * J.ldw + n])
+                                         : 0.0f;
+    hb[j] = bf16_bits(v);
+    lb[j] = bf16_bits(v - bf16_val(hb[j]));
+  }
+  u32x4 hv, lv;
+  hv.x = hb[0] | (hb[1] << 16); hv.y = hb[2] | (hb[3] << 16); hv.z = hb[4] | (hb[5] << 16); hv.w = hb[6] | (hb[7] << 16);
+  lv.x = lb[0] | (lb[1] << 16); lv.y = lb[2] | (lb[3] << 16); lv.z = lb[4] | (lb[5] << 16); lv.w = lb[6] | (lb[7] << 16);
+  const int64_t base = ((static_cast<int64_t>(ks) * J.NB + cb) * 2) * 64 + lane;
+  reinterpret_cast<u32x4*>(J.img)[base] = hv;
+  reinterpret_cast<u32x4*>(J.img)[base + 64] = lv;
+}
+
+inline int mlp_ks(int K) { return (K + 63) / 64 * 4; }
+inline int mlp_nb(int N) { return (N + 127) / 128 * 4; }
+
+}  // namespace
+}  // namespace tt
+
+using namespace tt;
+
+extern "C" size_t tt_mlp_pack_bytes(int32_t K, int32_t N) {
+  if (K < 1 || N < 1) return 0;
+  return static_cast<size_t>(mlp_ks(K)) * mlp_nb(N) * 2 * 64 * 8 * sizeof(__bf16);
+}
+
+extern "C" int tt_mlp_pack(const float* w, int64_t ldw, int32_t K, int32_t N, int32_t trans, void* img,
+                           size_t img_bytes, tt_stream_t stream) {
+  clear_error();
+  TT_REQUIRE(w && img, "tt_mlp_pack: NULL pointer");
+  TT_REQUIRE(K >= 1 && N >= 1, "tt_mlp_pack: bad K/N");
+  TT_REQUIRE(ldw >= (trans ? K : N), "tt_mlp_pack: ldw too small");
+  TT_REQUIRE(img_bytes >= tt_mlp_pack_bytes(K, N), "tt_mlp_pack: image too small");
+  const int KS = mlp_ks(K), NB = mlp_nb(N);
+  const int64_t threads = static_cast<int64_t>(KS) * NB * 64;
+  hipLaunchKernelGGL(mlp_pack_kernel, dim3(ceil_div(threads, 256)), dim3(256), 0, to_stream(stream), w, ldw, K, N,
+                     trans ? 1 : 0, KS, NB, static_cast<__bf16*>(img));
+  TT_CHECK_LAUNCH();
+  return TT_OK;
+}
+
+extern "C" int tt_mlp_pack_many(const tt_mlp_pack_job* jobs, int32_t num_jobs, tt_stream_t stream) {
+  clear_error();
+  TT_REQUIRE(jobs && num_jobs >= 1 && num_jobs <= kMaxPackJobs, "tt_mlp_pack_many: 1..%d jobs", kMaxPackJobs);
+  PackJobs pj{};
+  pj.n = num_jobs;
+  int64_t total = 0;
+  for (int i = 0; i < num_jobs; ++i) {
+    const tt_mlp_pack_job& j = jobs[i];
+    TT_REQUIRE(j.w && j.img && j.K >= 1 && j.N >= 1, "tt_mlp_pack_many: job %d: bad w/img/K/N", i);
+    TT_REQUIRE(j.ldw >= (j.trans ? j.K : j.N), "tt_mlp_pack_many: job %d: ldw too small", i);
+    TT_REQUIRE(j.img_bytes >= tt_mlp_pack_bytes(j.K, j.N), "tt_mlp_pack_many: job %d: image too small", i);
+    PackJob& J = pj.j[i];
+    J.w = j.w;
+    J.ldw = j.ldw;
+    J.K = j.K;
+    J.N = j.N;
+    J.trans = j.trans ? 1 : 0;
+    J.KS = mlp_ks(j.K);
+    J.NB = mlp_nb(j.N);
+    J.img = static_cast<__bf16*>(j.img);
+    J.first = total;
+    total += static_cast<int64_t>(J.KS) * J.NB * 64;
+  }
+  hipLaunchKernelGGL(mlp_pack_many_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, to_stream(stream), pj, total);
+  TT_CHECK_LAUNCH();
+  return TT_OK;
+}
+
+extern "C" size_t tt_mlp_rows_workspace_size(int64_t M, int32_t N) {
+  if (M < 0 || N < 1) return 0;
+  return static_cast<size_t>(ceil_div(M, kMlpBM)) * N * sizeof(float);
+}
+
+extern "C" int tt_mlp_rows(const float* A, int64_t lda, const float* amask, int64_t ldam, const float* scale,
+                           int64_t M, int32_t K, const void* img, int32_t N, const float* bias, int32_t relu,
+                           const float* cmask, int64_t ldcm, float* C, int64_t ldc, float* colsum, void* workspace,
+                           size_t workspace_bytes, tt_stream_t stream) {
+  clear_error();
+  TT_REQUIRE(A && img && C, "tt_mlp_rows: NULL A/img/C");
+  TT_REQUIRE(M >= 0 && K >= 1 && N >= 1, "tt_mlp_rows: bad M/K/N");
+  const int NB = mlp_nb(N);
+  TT_REQUIRE(NB <= 4 * kMlpMaxCB, "tt_mlp_rows: N=%d > %d unsupported", N, 32 * 4 * kMlpMaxCB);
+  TT_REQUIRE(M * lda < (int64_t(1) << 30) && (!amask || M * ldam < (int64_t(1) << 30)),
+             "tt_mlp_rows: operand too large for 32-bit buffer offsets");
+  TT_REQUIRE(lda >= K && ldc >= N && (!amask || ldam >= K) && (!cmask || ldcm >= N),
+             "tt_mlp_rows: leading dimension too small");
+  if (M == 0) return TT_OK;
+  MlpArgs a{};
+  a.A = A;
+  a.lda = lda;
+  a.amask = amask;
+  a.ldam = ldam;
+  a.scale = scale;
+  a.img = static_cast<const __bf16*>(img);
+  a.M = M;
+  a.K = K;
+  a.N = N;
+  a.KSp = mlp_ks(K);
+  a.NBp = NB;
+  a.bias = bias;
+  a.relu = relu ? 1 : 0;
+  a.cmask = cmask;
+  a.ldcm = ldcm;
+  a.C = C;
+  a.ldc = ldc;
+  if (colsum) {
+    TT_REQUIRE(workspace && workspace_bytes >= tt_mlp_rows_workspace_size(M, N),
+               "tt_mlp_rows: colsum needs a workspace of tt_mlp_rows_workspace_size bytes");
+    a.parts = static_cast<float*>(workspace);
+  }
+  TT_REQUIRE(reinterpret_cast<uintptr_t>(A) % 16 == 0 && lda % 4 == 0 &&
+                 (!amask || (reinterpret_cast<uintptr_t>(amask) % 16 == 0 && ldam % 4 == 0)),
+             "tt_mlp_rows: A / amask rows must be 16-B aligned (ld %% 4 == 0)");
+  const dim3 grid(static_cast<unsigned>(ceil_div(M, kMlpBM)));
+  hipStream_t st = to_stream(stream);
+  const int ncb = NB / 4;
+  if (amask) {
+    if (ncb == 1) hipLaunchKernelGGL((mlp_rows_kernel<1, true>), grid, dim3(kMlpThreads), 0, st, a);
+    else if (ncb == 2) hipLaunchKernelGGL((mlp_rows_kernel<2, true>), grid, dim3(kMlpThreads), 0, st, a);
+    else hipLaunchKernelGGL((mlp_rows_kernel<3, true>), grid, dim3(kMlpThreads), 0, st, a);
+  } else {
+    if (ncb == 1) hipLaunchKernelGGL((mlp_rows_kernel<1, false>), grid, dim3(kMlpThreads), 0, st, a);
+    else if (ncb == 2) hipLaunchKernelGGL((mlp_rows_kernel<2, false>), grid, dim3(kMlpThreads), 0, st, a);
+    else hipLaunchKernelGGL((mlp_rows_kernel<3, false>), grid, dim3(kMlpThreads), 0, st, a);
+  }
+  TT_CHECK_LAUNCH();
+  if (colsum) {
+    hipLaunchKernelGGL(mlp_colsum_kernel, dim3(ceil_div(N, 64)), dim3(1024), 0, st, a.parts,
+                       static_cast<int>(grid.x), N, colsum);
+  }
+  TT_CHECK_LAUNCH();
+  return TT_OK;
+}

@@ -20,6 +20,7 @@ __all__ = [
     "RowTable",
     "SparseTable",
     "RouteLookup",
+    "MlpPackJob",
     "MAX_SEGMENTS",
     "MAX_SOURCES",
     "lib",
@@ -79,6 +80,18 @@ class RouteLookup(ctypes.Structure):
         ("ids", c_void_p),
         ("num_rows", c_int64),
         ("tag", c_int32),
+    ]
+
+
+class MlpPackJob(ctypes.Structure):
+    _fields_ = [
+        ("w", c_void_p),
+        ("ldw", c_int64),
+        ("K", c_int32),
+        ("N", c_int32),
+        ("trans", c_int32),
+        ("img", c_void_p),
+        ("img_bytes", c_size_t),
     ]
 
 
@@ -202,6 +215,14 @@ _PROTOS = {
     "tt_vocab_size": (c_int64, [c_void_p]),
     "tt_vocab_encode": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int32]),
     "tt_vocab_destroy": (c_int32, [c_void_p]),
+    "tt_mlp_pack_bytes": (c_size_t, [c_int32, c_int32]),
+    "tt_mlp_pack": (c_int32, [c_void_p, c_int64, c_int32, c_int32, c_int32, c_void_p, c_size_t, c_void_p]),
+    "tt_mlp_pack_many": (c_int32, [c_void_p, c_int32, c_void_p]),
+    "tt_mlp_rows_workspace_size": (c_size_t, [c_int64, c_int32]),
+    "tt_mlp_rows": (
+        c_int32,
+        [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_int32, c_void_p, c_int32,
+         c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_size_t, c_void_p]),
     "tt_batch_take": (
         c_int32,
         [c_void_p, c_int64, c_int32, c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_int64, c_void_p,

@@ -743,3 +743,70 @@ def batch_take(src: torch.Tensor, perm: torch.Tensor, cursor: torch.Tensor, out:
                               _row_major(out, "out"), status.data_ptr() if status is not None else None,
                               _stream()))
     return out
+
+
+def mlp_pack(w: torch.Tensor, trans: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """bf16 hi/lo MFMA-fragment image of B = w ([K, N]) or B = w^T (trans:
+    w is [N, K]) for mlp_rows (tt_mlp_pack)."""
+    _req(w, "w", torch.float32, 2)
+    K, N = (w.shape[1], w.shape[0]) if trans else (w.shape[0], w.shape[1])
+    nbytes = lib().tt_mlp_pack_bytes(K, N)
+    if out is None:
+        out = torch.empty(nbytes, dtype=torch.uint8, device=w.device)
+    if out.numel() < nbytes:
+        raise ValueError(f"image buffer of {out.numel()} B < {nbytes} B")
+    check(lib().tt_mlp_pack(w.data_ptr(), _row_major(w, "w"), K, N, int(bool(trans)), out.data_ptr(), out.numel(),
+                            _stream()))
+    out.mlp_kn = (K, N)
+    return out
+
+
+def mlp_pack_many(jobs: Sequence[Tuple[torch.Tensor, bool, torch.Tensor]]) -> None:
+    """Several mlp_pack images in one launch: jobs of (w, trans, image buffer)."""
+    arr = (_native.MlpPackJob * len(jobs))()
+    for i, (w, trans, img) in enumerate(jobs):
+        _req(w, "w", torch.float32, 2)
+        K, N = (w.shape[1], w.shape[0]) if trans else (w.shape[0], w.shape[1])
+        arr[i].w, arr[i].ldw, arr[i].K, arr[i].N = w.data_ptr(), _row_major(w, "w"), K, N
+        arr[i].trans, arr[i].img, arr[i].img_bytes = int(bool(trans)), img.data_ptr(), img.numel()
+    check(lib().tt_mlp_pack_many(arr, len(jobs), _stream()))
+
+
+def mlp_rows(a: torch.Tensor, img: torch.Tensor, k: int, n: int, out: torch.Tensor, *,
+             amask: Optional[torch.Tensor] = None, scale: Optional[torch.Tensor] = None,
+             bias: Optional[torch.Tensor] = None, relu: bool = False,
+             cmask: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out[M, n] = epi(maskA(a[:, :k]) . B) with B packed by mlp_pack (tt_mlp_rows);
+    colsum (a contiguous [n] tensor): also the column sums of out."""
+    _req(a, "a", torch.float32, 2)
+    _req(out, "out", torch.float32, 2)
+    M = a.shape[0]
+    if a.shape[1] < k or out.shape[0] != M or out.shape[1] < n:
+        raise ValueError(f"mlp_rows: a {tuple(a.shape)}, out {tuple(out.shape)}, k={k}, n={n}")
+    for t, nm in ((amask, "amask"), (cmask, "cmask")):
+        if t is not None:
+            _req(t, nm, torch.float32, 2)
+            if t.shape[0] != M:
+                raise ValueError(f"{nm} has {t.shape[0]} rows, expected {M}")
+    if amask is not None and amask.shape[1] < k:
+        raise ValueError("amask narrower than k")
+    if cmask is not None and cmask.shape[1] < n:
+        raise ValueError("cmask narrower than n")
+    if bias is not None and (bias.dtype != torch.float32 or bias.numel() < n or not bias.is_contiguous()):
+        raise ValueError("bias must be a contiguous fp32 vector of >= n entries")
+    ws = None
+    if colsum is not None:
+        if colsum.dtype != torch.float32 or colsum.numel() != n or not colsum.is_contiguous():
+            raise ValueError("colsum must be a contiguous fp32 [n] tensor")
+        ws = Workspace.get(lib().tt_mlp_rows_workspace_size(M, n), a.device, "mlp_colsum")
+    check(lib().tt_mlp_rows(a.data_ptr(), _row_major(a, "a"),
+                            amask.data_ptr() if amask is not None else None,
+                            _row_major(amask, "amask") if amask is not None else 0,
+                            scale.data_ptr() if scale is not None else None, M, k, img.data_ptr(), n,
+                            bias.data_ptr() if bias is not None else None, int(bool(relu)),
+                            cmask.data_ptr() if cmask is not None else None,
+                            _row_major(cmask, "cmask") if cmask is not None else 0, out.data_ptr(),
+                            _row_major(out, "out"), colsum.data_ptr() if colsum is not None else None,
+                            ws.data_ptr() if ws is not None else None, ws.numel() if ws is not None else 0,
+                            _stream()))
+    return out

@@ -6,9 +6,16 @@ zero bias, relu on every layer including the last (tower.py:45,48), so the
 joint embeddings are non-negative.  All kernels and biases of a tower live in
 ONE flat fp32 buffer (views per layer; each layer's bias right after its
 kernel), so its gradient is one contiguous tensor and the dense optimizer
-step is a single tt_dense_* launch.  Two GEMM backends (DenseStack.backend):
-  * "hipblaslt" (default): torch fp32 GEMMs (bias + relu in the forward
-    GEMM's epilogue); libtt's tt_relu_bias_grad for the ReluGrad/BiasAddGrad
+step is a single tt_dense_* launch.  Three GEMM backends (DenseStack.backend,
+default from $TT_TOWER_BACKEND, else "mlp"):
+  * "mlp" (default): libtt's tt_mlp_rows (bf16x3 MFMA, fp32-faithful) for the
+    forward GEMMs (bias + relu epilogue) and the input-gradient GEMMs (the
+    layer below's ReluGrad mask and BiasAddGrad column sums fused into the
+    epilogue); one tt_mlp_pack_many launch per tower per step packs its
+    weight images; the weight gradients stay hipBLASLt split-K +
+    tt_sum_slices, the top layer's ReluGrad/BiasAddGrad tt_relu_bias_grad;
+  * "hipblaslt": torch fp32 GEMMs (bias + relu in the forward GEMM's
+    epilogue); libtt's tt_relu_bias_grad for the ReluGrad/BiasAddGrad
     pair and tt_sum_slices for the split-K weight gradient;
   * "tt": libtt's tt_gemm on bf16 MFMA (GEMM_BF16X3 hi/lo split =
     fp32-faithful, or GEMM_BF16): bias + relu fused into the forward
@@ -17,6 +24,7 @@ step is a single tt_dense_* launch.  Two GEMM backends (DenseStack.backend):
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -110,19 +118,50 @@ class DenseStack:
         self.flat = flat.to(device).requires_grad_(True)
         self.out_dim = fan_in
         # GEMM backend: "hipblaslt" (torch fp32 GEMMs + libtt relu/bias-grad and
-        # split-K reduction) or "tt" (libtt tt_gemm, bf16 MFMA; `precision`
-        # GEMM_BF16X3 = fp32-faithful hi/lo split, GEMM_BF16 = plain bf16)
-        self.backend = "hipblaslt"
+        # split-K reduction), "mlp" (libtt tt_mlp_rows, bf16x3 MFMA, for the
+        # forward and input-gradient GEMMs; weight gradients as "hipblaslt"),
+        # or "tt" (libtt tt_gemm, bf16 MFMA; `precision` GEMM_BF16X3 =
+        # fp32-faithful hi/lo split, GEMM_BF16 = plain bf16)
+        self.backend = os.environ.get("TT_TOWER_BACKEND", "mlp")
         self.precision = hip_ops.GEMM_BF16X3
 
     def params(self, flat: Optional[torch.Tensor] = None):
         f = self.flat if flat is None else flat
         return [(f[w:w + fi * fo].view(fi, fo), f[b:b + fo]) for w, fi, fo, b in self.layout]
 
+    def _pack_images(self, flat: torch.Tensor) -> Dict[Tuple[str, int], torch.Tensor]:
+        """Every layer's packed bf16 hi/lo weight images, forward ("f": B = W)
+        and transposed ("t": B = W^T, the input-gradient GEMMs), in ONE
+        tt_mlp_pack_many launch into buffers owned by the stack (fixed
+        addresses: graph-capturable).  Packed at the start of each forward,
+        so they always match `flat`."""
+        imgs = self.__dict__.setdefault("_images", {})
+        jobs = []
+        for li, (w, _) in enumerate(self.params(flat)):
+            for kind, trans in (("f", False), ("t", True)):
+                K, N = (w.shape[1], w.shape[0]) if trans else (w.shape[0], w.shape[1])
+                nbytes = hip_ops.lib().tt_mlp_pack_bytes(K, N)
+                buf = imgs.get((kind, li))
+                if buf is None or buf.numel() < nbytes or buf.device != w.device:
+                    buf = imgs[(kind, li)] = torch.empty(nbytes, dtype=torch.uint8, device=w.device)
+                jobs.append((w, trans, buf))
+        for i in range(0, len(jobs), 8):
+            hip_ops.mlp_pack_many(jobs[i:i + 8])
+        return imgs
+
     def forward_acts(self, x: torch.Tensor, flat: torch.Tensor) -> List[torch.Tensor]:
         """[x, h_1, ..., h_L] with h_l = relu(h_{l-1} W_l + b_l)."""
         if self.backend == "tt":
             return self._forward_tt(x, flat)
+        if self.backend == "mlp":
+            imgs = self._pack_images(flat)
+            acts = [x]
+            h = x
+            for li, (w, b) in enumerate(self.params(flat)):
+                out = torch.empty(h.shape[0], w.shape[1], dtype=torch.float32, device=h.device)
+                h = hip_ops.mlp_rows(h, imgs[("f", li)], w.shape[0], w.shape[1], out, bias=b, relu=True)
+                acts.append(h)
+            return acts
         acts = [x]
         h = x
         for w, b in self.params(flat):
@@ -139,6 +178,8 @@ class DenseStack:
         inplace: gout may be overwritten."""
         if self.backend == "tt":
             return self._backward_tt(acts, flat, gout, gscale, need_input_grad)
+        if self.backend == "mlp":
+            return self._backward_mlp(acts, flat, gout, gscale, need_input_grad, inplace)
         gflat = torch.empty_like(flat)
         params = self.params(flat)
         gparams = self.params(gflat)
@@ -154,6 +195,34 @@ class DenseStack:
                 # fast path only where it picks the better kernel (ragged output widths)
                 g = _mm_fast_fp32(g, w.t()) if w.shape[0] % 64 else torch.mm(g, w.t())
         return (g if need_input_grad else None), gflat
+
+    def _backward_mlp(self, acts: List[torch.Tensor], flat: torch.Tensor, gout: torch.Tensor,
+                      gscale: Optional[torch.Tensor], need_input_grad: bool, inplace: bool):
+        """"mlp" backend.  Top layer: G_L = relu'(h_L) * s * gout and db_L by
+        one tt_relu_bias_grad.  Per layer l from the top: [dW_l] = h_{l-1}^T G_l
+        (hipBLASLt split-K + tt_sum_slices), then ONE tt_mlp_rows for the layer
+        below: G_{l-1} = (G_l W_l^T) * relu'(h_{l-1}) with db_{l-1} = colsum
+        G_{l-1} in its epilogue (the ReluGrad / BiasAddGrad pair fused), or the
+        input gradient dx = G_1 W_1^T (16-B padded rows, returned as a view)."""
+        gflat = torch.empty_like(flat)
+        params = self.params(flat)
+        gparams = self.params(gflat)
+        imgs = self.__dict__["_images"]  # packed by this step's forward (same flat)
+        L = len(params)
+        g, _ = hip_ops.relu_bias_grad(gout, acts[L], gscale, out=gout if inplace else None, db=gparams[L - 1][1])
+        for li in range(L - 1, -1, -1):
+            w = params[li][0]
+            _splitk_mm_tn(acts[li], g, gparams[li][0])
+            if li == 0 and not need_input_grad:
+                return None, gflat
+            fi, fo = w.shape
+            ld = (fi + 3) // 4 * 4  # 16-B rows for the kernel's vector stores
+            out = torch.empty(g.shape[0], ld, dtype=torch.float32, device=g.device)[:, :fi]
+            if li > 0:
+                g = hip_ops.mlp_rows(g, imgs[("t", li)], fo, fi, out, cmask=acts[li], colsum=gparams[li - 1][1])
+            else:
+                g = hip_ops.mlp_rows(g, imgs[("t", li)], fo, fi, out)
+        return g, gflat
 
     def _forward_tt(self, x: torch.Tensor, flat: torch.Tensor) -> List[torch.Tensor]:
         """libtt backend: one tt_gemm per layer (bias + relu in the epilogue)."""

@@ -460,6 +460,40 @@ int tt_batch_take(const void* src, int64_t src_ld, int32_t ncols, const int64_t*
                   int64_t* cursor, int64_t batch, int32_t advance, void* dst, int64_t dst_ld,
                   int32_t* status, tt_stream_t stream);
 
+/* ------------------------------------------------------------------------ *
+ * K4  Tower MLP, row-streaming GEMM (Dense layers, pkg/modelling/models/
+ * tower.py:41-49): C[M, N] = epi(maskA(A) . B) for a tall fp32 activation
+ * A [M, K] and a small weight operand B [K, N] (N <= 384), on bf16x3 MFMA
+ * (fp32-faithful: a_lo b_hi + a_hi b_lo + a_hi b_hi, fp32 accumulation).
+ *   maskA (amask != NULL):  A := (amask > 0) ? A * (*scale) : 0   (ReluGrad)
+ *   epilogue:  + bias[n] (bias != NULL), relu (relu != 0), then
+ *              C := (cmask > 0) ? C : 0 (cmask != NULL)
+ * B is first packed by tt_mlp_pack into a bf16 hi/lo image in MFMA fragment
+ * order (img_bytes >= tt_mlp_pack_bytes(K, N)); trans != 0 packs B = W^T of a
+ * row-major W [N, K] (the input-gradient GEMMs).  scale is a device scalar.
+ * ------------------------------------------------------------------------ */
+size_t tt_mlp_pack_bytes(int32_t K, int32_t N);
+int tt_mlp_pack(const float* w, int64_t ldw, int32_t K, int32_t N, int32_t trans, void* img, size_t img_bytes,
+                tt_stream_t stream);
+/* Up to 8 packs in one launch (a tower's forward and transposed images). */
+typedef struct {
+  const float* w;
+  int64_t ldw;
+  int32_t K, N, trans;
+  void* img;
+  size_t img_bytes;
+} tt_mlp_pack_job;
+int tt_mlp_pack_many(const tt_mlp_pack_job* jobs, int32_t num_jobs, tt_stream_t stream);
+/* colsum != NULL: also colsum[n] = sum_m C[m][n] (the bias gradient of the
+ * layer below, BiasAddGrad): per-workgroup partial sums in the epilogue, then
+ * one small launch adds them in workgroup order (deterministic); needs a
+ * caller workspace of tt_mlp_rows_workspace_size(M, N) bytes. */
+size_t tt_mlp_rows_workspace_size(int64_t M, int32_t N);
+int tt_mlp_rows(const float* A, int64_t lda, const float* amask, int64_t ldam, const float* scale, int64_t M,
+                int32_t K, const void* img, int32_t N, const float* bias, int32_t relu, const float* cmask,
+                int64_t ldcm, float* C, int64_t ldc, float* colsum, void* workspace, size_t workspace_bytes,
+                tt_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

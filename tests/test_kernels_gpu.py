@@ -581,3 +581,41 @@ def test_sparse_adagrad_mostly_invalid_ids_bitexact(cuda):
                            0.05, 1e-7)
     assert np.array_equal(tw.cpu().numpy(), ref_w)
     assert np.array_equal(ta.cpu().numpy(), ref_acc)
+
+
+@pytest.mark.parametrize("M,K,N", [(16384, 258, 256), (16384, 256, 128), (16384, 128, 256), (16384, 256, 258),
+                                   (16384, 200, 256), (1000, 37, 64), (1, 5, 3), (130, 300, 384), (64, 64, 32)])
+def test_mlp_rows_vs_torch_fp64(cuda, M, K, N):
+    """tt_mlp_rows (bf16x3 MFMA, the tower MLP's forward and input-gradient
+    GEMMs) against a torch fp64 reference of the same op: C = relu(A B + b)
+    and C = ((mask(A) > 0) A s) B^T masked by cmask; fp32-faithful bound
+    2e-5 relative in norm (bf16x3 products are exact to ~2^-17)."""
+    g = torch.Generator(device=cuda)
+    g.manual_seed(M * 7 + K * 3 + N)
+    lda = (K + 3) // 4 * 4
+    A = torch.randn(M, lda, generator=g, device=cuda)[:, :K]
+    W = torch.randn(K, N, generator=g, device=cuda) * K ** -0.5
+    b = torch.randn(N, generator=g, device=cuda) * 0.1
+    ldc = (N + 3) // 4 * 4
+    out = torch.full((M, ldc), float("nan"), device=cuda)[:, :N]
+    hip_ops.mlp_rows(A, hip_ops.mlp_pack(W), K, N, out, bias=b, relu=True)
+    ref = torch.relu(A.double() @ W.double() + b.double())
+    assert torch.isfinite(out).all()
+    assert float((out.double() - ref).norm() / ref.norm().clamp_min(1e-30)) < 2e-5
+    # backward form: B = W'^T of a row-major W' [N, K], masked A and output
+    Wt = torch.randn(N, K, generator=g, device=cuda) * K ** -0.5
+    Am = torch.randn(M, lda, generator=g, device=cuda)[:, :K]
+    Cm = torch.randn(M, N + 4, generator=g, device=cuda)[:, :N] if N % 4 == 0 else None
+    s = torch.full((1,), 0.75, device=cuda)
+    out2 = torch.empty(M, ldc, device=cuda)[:, :N]
+    cs = torch.empty(N, device=cuda)
+    img = torch.empty(hip_ops.lib().tt_mlp_pack_bytes(K, N), dtype=torch.uint8, device=cuda)
+    hip_ops.mlp_pack_many([(Wt, True, img)])
+    for _ in range(2):  # the in-launch reduction's counter is left ready for the next call
+        hip_ops.mlp_rows(A, img, K, N, out2, amask=Am, scale=s, cmask=Cm, colsum=cs)
+    ref2 = ((A.double() * (Am > 0).double() * 0.75) @ Wt.double().t())
+    if Cm is not None:
+        ref2 = ref2 * (Cm > 0).double()
+    assert float((out2.double() - ref2).norm() / ref2.norm().clamp_min(1e-30)) < 2e-5
+    # colsum = the column sums of the written output, summed in workgroup order
+    assert torch.allclose(cs.double(), out2.double().sum(0), rtol=1e-5, atol=1e-5 * float(out2.abs().sum(0).max()))

@@ -113,7 +113,8 @@ def _cpu_mirror(m):
 
 
 @pytest.mark.parametrize("zipf,backend,precision", [(True, "hipblaslt", None), (False, "hipblaslt", None),
-                                                    (True, "tt", "x3"), (False, "tt", "x3"), (True, "tt", "bf16")])
+                                                    (True, "tt", "x3"), (False, "tt", "x3"), (True, "tt", "bf16"),
+                                                    (True, "mlp", None), (False, "mlp", None)])
 def test_train_steps_match_cpu_restatement(cuda, zipf, backend, precision):
     """First step: every parameter update within 1e-2 rel of the fp32 CPU
     restatement (bf16 MFMA operands in the fused loss give ~1e-3 per-example
@@ -121,7 +122,8 @@ def test_train_steps_match_cpu_restatement(cuda, zipf, backend, precision):
     loss trajectory over 3 steps within 1e-3 rel (parameters themselves drift
     apart: lr 0.05 on a 0.1 accumulator moves embeddings by about their own
     scale every step, so any rounding difference is amplified).  Both tower
-    GEMM backends: hipBLASLt fp32 and libtt tt_gemm (bf16x3 and plain bf16)."""
+    GEMM backends: hipBLASLt fp32, libtt tt_gemm (bf16x3 and plain bf16) and
+    libtt tt_mlp_rows (bf16x3) for the forward / input-gradient GEMMs."""
     m = _small_model(cuda)
     for t in (m.query_tower, m.candidate_tower):
         t.dense.backend = backend
