@@ -287,6 +287,248 @@ __global__ void __launch_bounds__(1024) mlp_colsum_kernel(const float* __restric
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Weight gradient of a Dense layer (the tape's MatMul for the kernel and
+// BiasAddGrad for the bias, tower.py:41-49):
+//   [dW; db] = [A | 1]^T . Gm    (A [M, Ka] activations, Gm [M, N] the
+//   layer's output gradient, optionally Gm = (gmask > 0) ? G * s : 0 — the
+//   ReluGrad of the layer's own relu folded into the load)
+// The output [Ka + 1, N] is exactly the flat parameter layout (kernel rows
+// then the bias row).  Reduction over the M batch rows, split over S
+// workgroups (blockIdx.x = split): each writes its partial [Ka + 1, N] and
+// mlp_sum_parts_kernel adds them in split order (deterministic).
+// MFMA view: C[i][j] += A'[i][k] B[k][j] with A' = [A | 1]^T (i = activation
+// column, k = batch row), B = Gm.  Both operands need 8 consecutive BATCH
+// rows per lane, so the staged fp32 rows are split hi/lo and written
+// TRANSPOSED into LDS (column-major: 32 batch rows of one column = 64 B,
+// XOR-swizzled 16-B chunks), then read as conflict-free ds_read_b128
+// fragments.  8 waves (two per SIMD); for N <= 256 (8 column blocks) wave w
+// owns column block w and every 32-row block of Ka + 1 (<= 9: Ka <= 287);
+// for N <= 128 (4 column blocks) waves w and w + 4 share column block w,
+// rows blocks 0-4 and 5-8.
+constexpr int kWgThreads = 512;
+constexpr int kWgBK = 16;      // batch rows per stage (one MFMA k-step)
+constexpr int kWgMaxIB = 9;    // 32-row blocks of Ka + 1 (Ka + 1 <= 288)
+
+struct WgradArgs {
+  const float* A;
+  int64_t lda;
+  const float* G;
+  int64_t ldg;
+  const float* gmask;  // (MASK) Gm = (gmask > 0) ? G * s : 0
+  int64_t ldgm;
+  const float* scale;
+  int64_t M;
+  int Ka, N, IB;       // IB = ceil((Ka + 1) / 32)
+  int64_t rows_per_split;
+  float* parts;        // [S][(Ka + 1) * N]
+  int avec;            // A rows 16-B aligned (float4 loads)
+};
+
+// transposed LDS tile: plane p, column c, 16-B chunk q (8 batch rows) of the
+// 16-row stage (32 B per column); the 16 lanes of one ds_read_b128 cycle
+// (16 consecutive columns, one chunk) hit 16 distinct 4-bank groups
+__device__ __forceinline__ int wt_off(int ncols, int plane, int col, int chunk) {
+  return ((plane * ncols + col) << 5) + ((chunk ^ ((col >> 3) & 1)) << 4);
+}
+
+template <int NJ, bool MASK>
+__global__ void __launch_bounds__(kWgThreads) mlp_wgrad_kernel(const WgradArgs a) {
+  constexpr int AC = kWgMaxIB * 32;   // A' columns staged (zero beyond Ka + 1)
+  constexpr int GC = NJ * 32;         // G columns staged (N rounded up to NJ column blocks)
+  constexpr int IMAX = NJ == 8 ? kWgMaxIB : (kWgMaxIB + 1) / 2;  // row blocks per wave
+  constexpr int STAGE_BYTES = 2 * (AC + GC) * 32;
+  __shared__ __attribute__((aligned(16))) char smem[2][STAGE_BYTES];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int lane = lane_id();
+  const int l32 = lane & 31, h = lane >> 5;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * a.rows_per_split;
+  int64_t r1 = r0 + a.rows_per_split;
+  if (r1 > a.M) r1 = a.M;
+  const int nstage = r1 > r0 ? static_cast<int>((r1 - r0 + kWgBK - 1) / kWgBK) : 0;
+  const float s = a.scale ? *a.scale : 1.0f;
+
+  // staging units: (row pair p of 16, column quad c) of A' (AC / 4 quads) then G (GC / 4)
+  constexpr int RP = kWgBK / 2;  // row pairs per stage
+  constexpr int AQ = AC / 4, GQ = GC / 4, UNITS = RP * (AQ + GQ);
+  constexpr int UPT = (UNITS + kWgThreads - 1) / kWgThreads;
+  // two stages of staged rows in registers: stage st + 2 is loaded while
+  // stage st is computed (slot = stage parity, static under the 2x unroll)
+  f32x4 va[2][UPT][2];
+  f32x4 vm[2][MASK ? UPT : 1][2];
+  // branch-free staging loads (range-checked buffer loads: rows past the
+  // split and past M read as 0), so the compiler's vmcnt waits are exact and
+  // the two-stage prefetch really overlaps
+  const __amdgpu_buffer_rsrc_t dA = mlp_desc(a.A + r0 * a.lda, static_cast<uint64_t>(r1 - r0) * a.lda * 4);
+  const __amdgpu_buffer_rsrc_t dG = mlp_desc(a.G + r0 * a.ldg, static_cast<uint64_t>(r1 - r0) * a.ldg * 4);
+  const __amdgpu_buffer_rsrc_t dM =
+      mlp_desc(MASK ? a.gmask + r0 * a.ldgm : a.G, static_cast<uint64_t>(r1 - r0) * (MASK ? a.ldgm : a.ldg) * 4);
+  auto fetch = [&](int st, auto slot_c) {
+    constexpr int SL = decltype(slot_c)::value;
+#pragma unroll
+    for (int u = 0; u < UPT; ++u) {
+      int unit = tid + u * kWgThreads;
+      unit = unit < UNITS ? unit : UNITS - 1;  // (the tail slots re-load a valid unit, unused)
+      // A units then G units; RP * AQ is a multiple of 64, so a wave is all A or all G
+      static_assert((RP * AQ) % 64 == 0, "A/G boundary on a wave edge");
+      const bool isg = __builtin_amdgcn_readfirstlane(unit >= RP * AQ ? 1 : 0) != 0;
+      const int uu = isg ? unit - RP * AQ : unit;
+      const int pr = uu % RP, c = (uu / RP) * 4;
+#pragma unroll
+      for (int e2 = 0; e2 < 2; ++e2) {
+        const int lrow = st * kWgBK + 2 * pr + e2;  // row inside the split
+        const int64_t ld = isg ? a.ldg : a.lda;
+        const f32x4 x4 = mlp_load4(isg ? dG : dA, static_cast<unsigned>((lrow * ld + c) * 4));
+        const bool live = r0 + lrow < r1;
+        const int lim = isg ? a.N : a.Ka;
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int col = c + e;
+          v[e] = col < lim ? x4[e] : ((!isg && col == a.Ka && live) ? 1.0f : 0.0f);
+        }
+        va[SL][u][e2] = v;
+        if constexpr (MASK) {
+          const f32x4 m4 = mlp_load4(dM, static_cast<unsigned>((lrow * a.ldgm + c) * 4));
+          vm[SL][u][e2] = m4;
+        }
+      }
+    }
+  };
+  auto stash = [&](int buf, auto slot_c) {
+    constexpr int SL = decltype(slot_c)::value;
+    char* base = smem[buf];
+#pragma unroll
+    for (int u = 0; u < UPT; ++u) {
+      const int unit = tid + u * kWgThreads;
+      if (unit < UNITS) {
+      const bool isg = unit >= RP * AQ;
+      const int uu = isg ? unit - RP * AQ : unit;
+      const int pr = uu % RP, c = (uu / RP) * 4;
+      char* tb = base + (isg ? 2 * AC * 32 : 0);
+      const int ncols = isg ? GC : AC;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float x0 = va[SL][u][0][e], x1 = va[SL][u][1][e];
+        if constexpr (MASK) {
+          if (isg) {
+            x0 = vm[SL][u][0][e] > 0.0f ? x0 * s : 0.0f;
+            x1 = vm[SL][u][1][e] > 0.0f ? x1 * s : 0.0f;
+          }
+        }
+        const unsigned h0 = bf16_bits(x0), h1 = bf16_bits(x1);
+        const unsigned l0 = bf16_bits(x0 - bf16_val(h0)), l1 = bf16_bits(x1 - bf16_val(h1));
+        const int col = c + e, k = 2 * pr;  // rows k, k + 1 of the stage
+        *reinterpret_cast<unsigned*>(tb + wt_off(ncols, 0, col, k >> 3) + (k & 7) * 2) = h0 | (h1 << 16);
+        *reinterpret_cast<unsigned*>(tb + wt_off(ncols, 1, col, k >> 3) + (k & 7) * 2) = l0 | (l1 << 16);
+      }
+      }
+    }
+  };
+
+  const int jb = wave % NJ;
+  const int ib0 = NJ == 8 ? 0 : (wave / NJ) * IMAX;  // first row block of this wave
+  f32x16 acc[IMAX];
+#pragma unroll
+  for (int i = 0; i < IMAX; ++i) acc[i] = f32x16{};
+
+  using Z = std::integral_constant<int, 0>;
+  using O = std::integral_constant<int, 1>;
+  if (nstage > 0) {
+    fetch(0, Z());
+    if (nstage > 1) fetch(1, O());
+    stash(0, Z());
+    __syncthreads();
+  }
+  auto stage = [&](int st, auto par_c) {
+    constexpr int PAR = decltype(par_c)::value;
+    if (st + 2 < nstage) fetch(st + 2, par_c);  // the slot stage st came from
+    const char* base = smem[PAR];
+    const char* gb = base + 2 * AC * 32;
+    {
+      const int chunk = h;
+      const int gcol = 32 * jb + l32;
+      const bf16x8 bh = *reinterpret_cast<const bf16x8*>(gb + wt_off(GC, 0, gcol, chunk));
+      const bf16x8 bl = *reinterpret_cast<const bf16x8*>(gb + wt_off(GC, 1, gcol, chunk));
+#pragma unroll
+      for (int i = 0; i < IMAX; ++i) {
+        if (ib0 + i < a.IB) {  // uniform; no `break`, so the loop unrolls and acc stays in registers
+          const int col = 32 * (ib0 + i) + l32;
+          const bf16x8 ah = *reinterpret_cast<const bf16x8*>(base + wt_off(AC, 0, col, chunk));
+          const bf16x8 al = *reinterpret_cast<const bf16x8*>(base + wt_off(AC, 1, col, chunk));
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[i], 0, 0, 0);
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[i], 0, 0, 0);
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[i], 0, 0, 0);
+        }
+      }
+    }
+    if (st + 1 < nstage) {
+      __syncthreads();  // everyone is done reading the other buffer (read one stage ago)
+      stash(1 - PAR, std::integral_constant<int, 1 - PAR>());
+      __syncthreads();
+    }
+  };
+  for (int st = 0; st < nstage; st += 2) {
+    stage(st, Z());
+    if (st + 1 < nstage) stage(st + 1, O());
+  }
+
+  // partial [Ka + 1, N] of this split: lane (l32, h), register r -> row
+  // 32 (ib0 + i) + (r & 3) + 8 (r >> 2) + 4 h, column 32 jb + l32
+  const int rows_out = a.Ka + 1;
+  float* P = a.parts + static_cast<int64_t>(blockIdx.x) * rows_out * a.N;
+  const int n = 32 * jb + l32;
+#pragma unroll
+  for (int i = 0; i < IMAX; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = 32 * (ib0 + i) + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (ib0 + i < a.IB && n < a.N && row < rows_out) P[static_cast<int64_t>(row) * a.N + n] = acc[i][r];
+    }
+  }
+}
+
+// out[e] = sum over splits of parts[sp][e] (deterministic): a block covers 64
+// float4 of the output; group g of 16 adds splits [g S/16, (g+1) S/16) in
+// order (their loads all in flight), then the 16 group sums are added in
+// group order.  len % 4 == 0.
+__global__ void __launch_bounds__(1024) mlp_sum_parts_kernel(const float* __restrict__ parts, int S, int64_t len,
+                                                             float* __restrict__ out) {
+  __shared__ f32x4 red[16][64];
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int64_t e4 = (blockIdx.x * 64ll + lane) * 4;
+  const int per = (S + 15) / 16;
+  const int s0 = grp * per, s1 = min(S, s0 + per);
+  f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (e4 < len) {
+    f32x4 v[8];
+    for (int sb = s0; sb < s1; sb += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (sb + u < s1) v[u] = *reinterpret_cast<const f32x4*>(parts + (sb + u) * len + e4);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (sb + u < s1) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[q] += v[u][q];
+        }
+    }
+  }
+  red[grp][lane] = acc;
+  __syncthreads();
+  if (grp == 0 && e4 < len) {
+    f32x4 t = red[0][lane];
+    for (int g = 1; g < 16; ++g) {
+      const f32x4 r = red[g][lane];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) t[q] += r[q];
+    }
+    *reinterpret_cast<f32x4*>(out + e4) = t;
+  }
+}
+
 // One thread per (k-step, column block, lane): 8 hi + 8 lo bf16 of
 // B[k = 16 ks + 8 (lane >> 5) + j][n = 32 cb + (lane & 31)], j < 8, zero padded.
 // trans: B = W^T with W [N, K] row-major (B[k][n] = W[n * ldw + k]).
@@ -476,6 +718,69 @@ extern "C" int tt_mlp_rows(const float* A, int64_t lda, const float* amask, int6
     hipLaunchKernelGGL(mlp_colsum_kernel, dim3(ceil_div(N, 64)), dim3(1024), 0, st, a.parts,
                        static_cast<int>(grid.x), N, colsum);
   }
+  TT_CHECK_LAUNCH();
+  return TT_OK;
+}
+
+// splits of the batch reduction: ~128+ rows each, at most 64 (partials stay
+// <= 64 x (Ka + 1) x N floats)
+#ifndef TT_WGRAD_MAX_SPLITS
+#define TT_WGRAD_MAX_SPLITS 64
+#endif
+static int wgrad_splits(int64_t M) {
+  int64_t S = M / 128;
+  if (S > TT_WGRAD_MAX_SPLITS) S = TT_WGRAD_MAX_SPLITS;
+  if (S < 1) S = 1;
+  return static_cast<int>(S);
+}
+
+extern "C" size_t tt_mlp_wgrad_workspace_size(int64_t M, int32_t Ka, int32_t N) {
+  if (M < 0 || Ka < 0 || N < 1) return 0;
+  return static_cast<size_t>(wgrad_splits(M)) * (Ka + 1) * N * sizeof(float);
+}
+
+extern "C" int tt_mlp_wgrad(const float* A, int64_t lda, const float* G, int64_t ldg, const float* gmask,
+                            int64_t ldgm, const float* scale, int64_t M, int32_t Ka, int32_t N, float* dwb,
+                            void* workspace, size_t workspace_bytes, tt_stream_t stream) {
+  clear_error();
+  TT_REQUIRE(A && G && dwb, "tt_mlp_wgrad: NULL A/G/dwb");
+  TT_REQUIRE(M >= 0 && Ka >= 1 && Ka + 1 <= kWgMaxIB * 32, "tt_mlp_wgrad: Ka=%d outside [1, %d]", Ka,
+             kWgMaxIB * 32 - 1);
+  TT_REQUIRE(N >= 1 && N <= 256 && N % 4 == 0, "tt_mlp_wgrad: N=%d must be a multiple of 4 in [4, 256]", N);
+  TT_REQUIRE(lda >= Ka && ldg >= N && (!gmask || ldgm >= N), "tt_mlp_wgrad: leading dimension too small");
+  TT_REQUIRE(ldg % 4 == 0 && reinterpret_cast<uintptr_t>(G) % 16 == 0 &&
+                 (!gmask || (ldgm % 4 == 0 && reinterpret_cast<uintptr_t>(gmask) % 16 == 0)),
+             "tt_mlp_wgrad: G / gmask rows must be 16-B aligned");
+  const int S = wgrad_splits(M);
+  TT_REQUIRE(workspace && workspace_bytes >= tt_mlp_wgrad_workspace_size(M, Ka, N),
+             "tt_mlp_wgrad: workspace %zu < %zu", workspace_bytes, tt_mlp_wgrad_workspace_size(M, Ka, N));
+  WgradArgs a{};
+  a.A = A;
+  a.lda = lda;
+  a.G = G;
+  a.ldg = ldg;
+  a.gmask = gmask;
+  a.ldgm = ldgm;
+  a.scale = scale;
+  a.M = M;
+  a.Ka = Ka;
+  a.N = N;
+  a.IB = (Ka + 1 + 31) / 32;
+  a.rows_per_split = round_up(ceil_div(M > 0 ? M : 1, S), kWgBK);
+  a.parts = static_cast<float*>(workspace);
+  a.avec = (lda % 4 == 0 && reinterpret_cast<uintptr_t>(A) % 16 == 0) ? 1 : 0;
+  hipStream_t st = to_stream(stream);
+  const dim3 grid(static_cast<unsigned>(S));
+  if (N <= 128) {
+    if (gmask) hipLaunchKernelGGL((mlp_wgrad_kernel<4, true>), grid, dim3(kWgThreads), 0, st, a);
+    else hipLaunchKernelGGL((mlp_wgrad_kernel<4, false>), grid, dim3(kWgThreads), 0, st, a);
+  } else {
+    if (gmask) hipLaunchKernelGGL((mlp_wgrad_kernel<8, true>), grid, dim3(kWgThreads), 0, st, a);
+    else hipLaunchKernelGGL((mlp_wgrad_kernel<8, false>), grid, dim3(kWgThreads), 0, st, a);
+  }
+  TT_CHECK_LAUNCH();
+  const int64_t len = static_cast<int64_t>(Ka + 1) * N;
+  hipLaunchKernelGGL(mlp_sum_parts_kernel, dim3(ceil_div(len, 256)), dim3(1024), 0, st, a.parts, S, len, dwb);
   TT_CHECK_LAUNCH();
   return TT_OK;
 }

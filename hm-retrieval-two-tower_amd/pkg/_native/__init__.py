@@ -223,6 +223,11 @@ _PROTOS = {
         c_int32,
         [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_int32, c_void_p, c_int32,
          c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "tt_mlp_wgrad_workspace_size": (c_size_t, [c_int64, c_int32, c_int32]),
+    "tt_mlp_wgrad": (
+        c_int32,
+        [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int32, c_int32, c_void_p,
+         c_void_p, c_size_t, c_void_p]),
     "tt_batch_take": (
         c_int32,
         [c_void_p, c_int64, c_int32, c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_int64, c_void_p,

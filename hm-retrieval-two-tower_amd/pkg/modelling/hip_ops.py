@@ -810,3 +810,27 @@ def mlp_rows(a: torch.Tensor, img: torch.Tensor, k: int, n: int, out: torch.Tens
                             ws.data_ptr() if ws is not None else None, ws.numel() if ws is not None else 0,
                             _stream()))
     return out
+
+
+def mlp_wgrad(a: torch.Tensor, g: torch.Tensor, dwb: torch.Tensor, *, gmask: Optional[torch.Tensor] = None,
+              scale: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dwb [Ka + 1, N] = [a | 1]^T . Gm (weight gradient rows then the bias
+    gradient row), Gm = g or (gmask > 0) ? g * scale : 0 (tt_mlp_wgrad)."""
+    _req(a, "a", torch.float32, 2)
+    _req(g, "g", torch.float32, 2)
+    _req(dwb, "dwb", torch.float32, 2)
+    M, Ka = a.shape
+    N = g.shape[1]
+    if g.shape[0] != M or tuple(dwb.shape) != (Ka + 1, N) or not dwb.is_contiguous():
+        raise ValueError(f"mlp_wgrad: a {tuple(a.shape)}, g {tuple(g.shape)}, dwb {tuple(dwb.shape)}")
+    if gmask is not None:
+        _req(gmask, "gmask", torch.float32, 2)
+        if tuple(gmask.shape) != (M, N):
+            raise ValueError("gmask must match g")
+    ws = Workspace.get(lib().tt_mlp_wgrad_workspace_size(M, Ka, N), a.device, "mlp_wgrad")
+    check(lib().tt_mlp_wgrad(a.data_ptr(), _row_major(a, "a"), g.data_ptr(), _row_major(g, "g"),
+                             gmask.data_ptr() if gmask is not None else None,
+                             _row_major(gmask, "gmask") if gmask is not None else 0,
+                             scale.data_ptr() if scale is not None else None, M, Ka, N, dwb.data_ptr(), ws.data_ptr(),
+                             ws.numel(), _stream()))
+    return dwb

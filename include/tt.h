@@ -493,6 +493,16 @@ int tt_mlp_rows(const float* A, int64_t lda, const float* amask, int64_t ldam, c
                 int32_t K, const void* img, int32_t N, const float* bias, int32_t relu, const float* cmask,
                 int64_t ldcm, float* C, int64_t ldc, float* colsum, void* workspace, size_t workspace_bytes,
                 tt_stream_t stream);
+/* Weight + bias gradient of a Dense layer (the tape's MatMul and BiasAddGrad):
+ * dwb[Ka + 1, N] = [A | 1]^T . Gm, Gm = G, or (gmask > 0) ? G * (*scale) : 0
+ * (gmask != NULL: the layer's own ReluGrad).  dwb row-major with ld N — the
+ * flat parameter layout of kernel [Ka, N] followed by bias [N].  bf16x3 MFMA,
+ * batch split over workgroups, partials added in split order (deterministic;
+ * workspace of tt_mlp_wgrad_workspace_size bytes).  Ka + 1 <= 288, N <= 256. */
+size_t tt_mlp_wgrad_workspace_size(int64_t M, int32_t Ka, int32_t N);
+int tt_mlp_wgrad(const float* A, int64_t lda, const float* G, int64_t ldg, const float* gmask, int64_t ldgm,
+                 const float* scale, int64_t M, int32_t Ka, int32_t N, float* dwb, void* workspace,
+                 size_t workspace_bytes, tt_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -619,3 +619,29 @@ def test_mlp_rows_vs_torch_fp64(cuda, M, K, N):
     assert float((out2.double() - ref2).norm() / ref2.norm().clamp_min(1e-30)) < 2e-5
     # colsum = the column sums of the written output, summed in workgroup order
     assert torch.allclose(cs.double(), out2.double().sum(0), rtol=1e-5, atol=1e-5 * float(out2.abs().sum(0).max()))
+
+
+@pytest.mark.parametrize("M,Ka,N,masked", [(16384, 258, 256, False), (16384, 256, 128, True), (16384, 200, 256, False),
+                                           (1000, 37, 64, True), (1, 5, 4, False), (130, 287, 256, True),
+                                           (4099, 64, 100, False)])
+def test_mlp_wgrad_vs_torch_fp64(cuda, M, Ka, N, masked):
+    """tt_mlp_wgrad (bf16x3 MFMA, the Dense layers' weight + bias gradient):
+    [dW; db] = [A | 1]^T Gm, Gm = G or relu'(gmask) * s * G, against torch
+    fp64; fp32-faithful bound 2e-5 relative in norm; run twice, bit-identical
+    (the split partials are added in split order)."""
+    g = torch.Generator(device=cuda)
+    g.manual_seed(M + 3 * Ka + 7 * N)
+    A = torch.randn(M, (Ka + 3) // 4 * 4, generator=g, device=cuda)[:, :Ka]
+    ldg = (N + 3) // 4 * 4
+    G = torch.randn(M, ldg, generator=g, device=cuda)[:, :N]
+    Gm = torch.randn(M, ldg, generator=g, device=cuda)[:, :N] if masked else None
+    s = torch.full((1,), 1.5, device=cuda)
+    out = torch.full((Ka + 1, N), float("nan"), device=cuda)
+    hip_ops.mlp_wgrad(A, G, out, gmask=Gm, scale=s if masked else None)
+    Gd = G.double() * ((Gm > 0).double() * 1.5 if masked else 1.0)
+    ref = torch.cat([A.double(), torch.ones(M, 1, dtype=torch.float64, device=cuda)], 1).t() @ Gd
+    assert torch.isfinite(out).all()
+    assert float((out.double() - ref).norm() / ref.norm()) < 2e-5
+    again = torch.empty_like(out)
+    hip_ops.mlp_wgrad(A, G, again, gmask=Gm, scale=s if masked else None)
+    assert torch.equal(out, again)

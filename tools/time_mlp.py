@@ -80,5 +80,23 @@ for K1 in (258, 200):
     tp = [gtime(lambda: torch._addmm_activation(b1, Xv, W1)), gtime(lambda: torch._addmm_activation(b2, H1, W2)),
           gtime(lambda: torch.mm(G2, W2.t())), gtime(lambda: torch.mm(G1, W1.t()))]
     tpk = gtime(lambda: (hip_ops.mlp_pack(W1, out=img1), hip_ops.mlp_pack(W2, out=img2)))
+    dwb1 = torch.empty(K1 + 1, 256, device=dev)
+    dwb2 = torch.empty(257, 128, device=dev)
+    hip_ops.mlp_wgrad(Xv, G1, dwb1)
+    hip_ops.mlp_wgrad(H1, G2, dwb2, gmask=E, scale=s)
+    torch.cuda.synchronize()
+    r1 = torch.cat([Xd, torch.ones(M, 1, dtype=torch.float64, device=dev)], 1).t() @ G1.double()
+    r2 = torch.cat([H1.double(), torch.ones(M, 1, dtype=torch.float64, device=dev)], 1).t() @ (
+        G2.double() * (E > 0).double() * 0.5)
+    print(f"K1={K1} wgrad1 rel {rel(dwb1, r1):.2e} wgrad2 rel {rel(dwb2, r2):.2e}")
+    tw1 = gtime(lambda: hip_ops.mlp_wgrad(Xv, G1, dwb1))
+    tw2 = gtime(lambda: hip_ops.mlp_wgrad(H1, G2, dwb2, gmask=E, scale=s))
+    part1 = torch.empty(16, K1, 256, device=dev)
+    part2 = torch.empty(16, 256, 128, device=dev)
+    tb1 = gtime(lambda: hip_ops.sum_slices(torch.bmm(Xv.reshape(16, M // 16, K1).transpose(1, 2),
+                                                     G1.view(16, M // 16, 256), out=part1), dwb1[:K1]))
+    tb2 = gtime(lambda: hip_ops.sum_slices(torch.bmm(H1.view(16, M // 16, 256).transpose(1, 2),
+                                                     G2.view(16, M // 16, 128), out=part2), dwb2[:256]))
+    print(f"K1={K1} us wgrad tt: dW1 {tw1:.1f} dW2(+mask) {tw2:.1f} | torch bmm+sum_slices: {tb1:.1f} {tb2:.1f}")
     print(f"K1={K1} us tt: fwd1 {t[0]:.1f} fwd2 {t[1]:.1f} dx2 {t[2]:.1f} dx1 {t[3]:.1f} | "
           f"torch: {tp[0]:.1f} {tp[1]:.1f} {tp[2]:.1f} {tp[3]:.1f} | pack x2 {tpk:.1f}")
