@@ -704,8 +704,9 @@ class ShardedTrainStep:
         # the global-negatives middle holds collectives: it runs eagerly unless
         # TT_GRAPH_COLLECTIVES=1 asks to capture them with RCCL (never over
         # gloo, whose host staging synchronises)
-        self.use_graph = use_graph and not (self.global_negatives and self.world > 1 and (
-            _staged(group) or os.environ.get("TT_GRAPH_COLLECTIVES") != "1"))
+        self.use_graph = use_graph and os.environ.get("TT_SHARDED_EAGER") != "1" and not (
+            self.global_negatives and self.world > 1 and (
+                _staged(group) or os.environ.get("TT_GRAPH_COLLECTIVES") != "1"))
         big: Dict[str, torch.Tensor] = {}
         self.small: Dict[Any, Any] = {}
         for tower in model.towers:
