@@ -10,12 +10,14 @@
 //       acc += g*g;  w -= lr*g / (sqrt(acc) + eps)
 //
 // MI355X design (every stage uses the whole GPU):
-//  1. keys   — one launch over all tables' lookups builds 32-bit keys
-//     (table index | row id) and values (lookup index); each table's region is
-//     padded to a multiple of kBlock with an "invalid" id that sorts last.
-//  2. sort   — one stable LSD radix sort of all tables' (key, value) pairs
-//     (rocPRIM onesweep, only the key bits in use), so each table's lookups
-//     come out grouped by row id in increasing batch position.
+//  1+2. keys + sort — every table's lookups become 32-bit keys (table index |
+//     row id) with the lookup index as value, each table's region padded to a
+//     multiple of kBlock with an "invalid" id that sorts last, sorted stably so
+//     each table's lookups come out grouped by row id in increasing batch
+//     position.  Default: ONE launch, one workgroup per table sorting its
+//     region in LDS (region_sort_kernel; regions of <= 16384 lookups, or any
+//     size for tables of <= 255 rows).  Otherwise (or TT_SPARSE_SORT=device):
+//     a key-build launch + one rocPRIM radix sort over the key bits in use.
 //  3. blocks — one (sub-)wave per kBlock consecutive sorted lookups of a
 //     table, lanes over embedding columns (coalesced row reads): sequential
 //     fp32 sums of each segment piece; a segment that starts and ends inside
@@ -32,6 +34,8 @@
 // rounded fp32 divide/sqrt) so results match the CPU restatement bit for bit.
 // (HIP's __fsqrt_rn maps to the approximate native sqrt on this toolchain.)
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "tt_common.h"
@@ -162,6 +166,258 @@ __global__ void __launch_bounds__(kThreads) build_keys_kernel(const Job j, int t
     }
     j.hdr->fp0 = j.fp0;
     j.hdr->fp1 = j.fp1;
+  }
+}
+
+// 1+2 fused for regions of at most kLdsSortMax lookups: one workgroup per
+// table builds its region's keys straight into LDS and sorts them there by a
+// stable LSD radix sort over the bits the table's row ids use (8-bit digits at
+// most), then writes the same sorted (key, value) arrays the rocPRIM path
+// writes.  The table index is the key's high part and each table owns its
+// region, so sorting the regions one by one equals the global sort.  One
+// launch on one CU per table instead of a key build and a multi-launch device
+// sort: it runs beside the backward without taking the chip.
+//   LDS: row key per original position (u32), position ping-pong (u16) and the
+//   per-wave digit counts [digit][wave].  Each wave owns a contiguous slice of
+//   the current order; ranks inside a 64-lane tile come from 8 ballots (lanes
+//   with equal digits), so the scatter keeps the order: stable.
+constexpr int kLdsSortMax = 16384;
+constexpr int kLsThreads = 1024;
+constexpr int kLsWaves = kLsThreads / kWave;
+constexpr int kLsTiles = kLdsSortMax / kLsWaves / kWave;  // 64-lane tiles per wave at the maximum
+constexpr int kLsLdsBytes = kLdsSortMax * 4 + 2 * kLdsSortMax * 2 + 256 * kLsWaves * 4;
+
+// row key of region position i: the row id, or nr for invalid ids and padding
+// One region's descriptor in registers (a reference into the kernel's
+// by-value Job indexed by blockIdx.x made the compiler copy the whole Job to
+// scratch).
+struct Region {
+  const int32_t *ids0, *ids1, *ids2, *ids3;  // no array: a dynamically indexed one lands in scratch
+  int64_t batch;
+  uint32_t* keys;  // sorted outputs, offset to this region
+  uint32_t* vals;
+  int n;           // valid lookups
+  uint32_t nr;     // rows: row key of invalid ids and padding
+  uint32_t khi;    // table index << id_bits
+  uint32_t invalid;
+};
+
+__device__ __forceinline__ int source_of(const Region& R, int64_t i) {  // i / batch for i < 4 * batch
+  return (i >= R.batch) + (i >= 2 * R.batch) + (i >= 3 * R.batch);
+}
+
+// row key of region position i: the row id, or nr for invalid ids and padding
+// Branch-free (padding positions load ids[0][0] and discard it), so a caller's
+// unrolled loads all issue before the first wait.
+__device__ __forceinline__ uint32_t region_key(const Region& R, int i) {
+  const bool valid = i < R.n;
+  const int iv = valid ? i : 0;
+  const int s = source_of(R, iv);
+  const int b = iv - s * static_cast<int>(R.batch);
+  const int32_t* ids = R.ids0;
+  ids = s >= 1 ? R.ids1 : ids;
+  ids = s >= 2 ? R.ids2 : ids;
+  ids = s >= 3 ? R.ids3 : ids;
+  const int32_t r = ids[b];
+  return (valid && r >= 0 && static_cast<uint32_t>(r) < R.nr) ? static_cast<uint32_t>(r) : R.nr;
+}
+
+// row keys of one source's positions [s*batch, (s+1)*batch) into LDS, 16
+// independent id loads in flight per thread (the source's pointer is uniform
+// and written out per call: a select among the four made the compiler index
+// them from scratch)
+template <typename KT>
+__device__ __forceinline__ void stage_source(const Region& R, const int32_t* __restrict__ ids, int s, KT* dst) {
+  const int nb = static_cast<int>(R.batch);
+  for (int base = 0; base < nb; base += 16 * kLsThreads) {
+    int32_t r[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int b = base + u * kLsThreads + static_cast<int>(threadIdx.x);
+      r[u] = ids[b < nb ? b : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int b = base + u * kLsThreads + static_cast<int>(threadIdx.x);
+      const uint32_t k = (r[u] >= 0 && static_cast<uint32_t>(r[u]) < R.nr) ? static_cast<uint32_t>(r[u]) : R.nr;
+      if (b < nb) dst[s * nb + b] = static_cast<KT>(k);
+    }
+  }
+}
+
+// row keys of positions [0, n) into LDS (padding past the lookups: nr)
+template <typename KT>
+__device__ __forceinline__ void stage_keys(const Region& R, int n, KT* dst) {
+  stage_source(R, R.ids0, 0, dst);
+  if (R.n > R.batch) stage_source(R, R.ids1, 1, dst);
+  if (R.n > 2 * R.batch) stage_source(R, R.ids2, 2, dst);
+  if (R.n > 3 * R.batch) stage_source(R, R.ids3, 3, dst);
+  for (int i = R.n + static_cast<int>(threadIdx.x); i < n; i += kLsThreads) dst[i] = static_cast<KT>(R.nr);
+}
+
+// sorted (key, value) at output slot `out` of region position ps with row key k
+__device__ __forceinline__ void region_store(const Region& R, int out, uint32_t ps, uint32_t k) {
+  uint32_t val = 0xFFFFFFFFu;  // padding and invalid ids keep no gradient offset
+  if (k < R.nr) {
+    const uint32_t s = static_cast<uint32_t>(source_of(R, ps));
+    val = (s << kSrcShift) | static_cast<uint32_t>(ps - s * R.batch);
+  }
+  R.keys[out] = R.khi | (k < R.nr ? k : R.invalid);
+  R.vals[out] = val;
+}
+
+// lanes of this wave holding the same digit (among the `act` lanes): one
+// ballot per digit bit, each lane keeping the lanes that agree with its bit
+__device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool act) {
+  const uint64_t a = __ballot(act);
+  uint32_t lo = static_cast<uint32_t>(a), hi = static_cast<uint32_t>(a >> 32);
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const uint32_t bit = (d >> b) & 1u;
+    const uint64_t bal = __ballot(bit);
+    const uint32_t flip = bit - 1u;  // 0 when the bit is set, all ones when clear
+    lo &= static_cast<uint32_t>(bal) ^ flip;
+    hi &= static_cast<uint32_t>(bal >> 32) ^ flip;
+  }
+  return act ? (static_cast<uint64_t>(hi) << 32 | lo) : 0;
+}
+
+// hist[digit][wave] counts -> exclusive offsets in (digit, wave) order
+__device__ __forceinline__ void scan_digit_counts(uint32_t* hist, uint32_t* wsum) {
+  const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
+  __syncthreads();
+  uint32_t h[4], run = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    h[u] = hist[4 * tid + u];
+    run += h[u];
+  }
+  uint32_t inc = run;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, kWave);
+    if (lane >= o) inc += y;
+  }
+  if (lane == kWave - 1) wsum[w] = inc;
+  __syncthreads();
+  uint32_t ex = inc - run;
+  for (int v = 0; v < w; ++v) ex += wsum[v];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    hist[4 * tid + u] = ex;
+    ex += h[u];
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(kLsThreads) region_sort_kernel(const Job j) {
+  extern __shared__ __attribute__((aligned(16))) char lsm[];
+  uint32_t* lkey = reinterpret_cast<uint32_t*>(lsm);
+  uint16_t* const pbuf0 = reinterpret_cast<uint16_t*>(lsm + kLdsSortMax * 4);
+  uint16_t* const pbuf1 = pbuf0 + kLdsSortMax;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(lsm + kLdsSortMax * 8);  // [256 digits][kLsWaves]
+  __shared__ uint32_t wsum[kLsWaves];
+  const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
+  Region R;
+  int n;
+  {
+    const TableDesc& T = j.t[blockIdx.x];
+    R.ids0 = T.ids[0];
+    R.ids1 = T.ids[1];
+    R.ids2 = T.ids[2];
+    R.ids3 = T.ids[3];
+    R.batch = j.batch;
+    R.keys = const_cast<uint32_t*>(j.keys) + T.base;
+    R.vals = const_cast<uint32_t*>(j.vals) + T.base;
+    R.n = T.n;
+    R.nr = static_cast<uint32_t>(T.num_rows);
+    R.khi = static_cast<uint32_t>(blockIdx.x) << j.id_bits;
+    R.invalid = (1u << j.id_bits) - 1u;
+    n = T.n_pad;
+  }
+  const uint32_t nr = R.nr;
+  if (blockIdx.x == 0 && tid == 0) {  // stamp the workspace with this call's fingerprint
+    if (j.hdr->magic != kHdrMagic) {
+      j.hdr->error = 0u;
+      j.hdr->magic = kHdrMagic;
+    }
+    j.hdr->fp0 = j.fp0;
+    j.hdr->fp1 = j.fp1;
+  }
+  const int bits = 32 - __builtin_clz(nr);  // row keys lie in [0, nr]
+  const int per = ((n + kLsWaves - 1) / kLsWaves + kWave - 1) / kWave * kWave;
+  const int wbeg = w * per, wend = min(n, wbeg + per);
+  const uint64_t lt = (uint64_t(1) << lane) - 1u;
+  for (int e = tid; e < 256 * kLsWaves; e += kLsThreads) hist[e] = 0u;
+  if (bits <= 8) {
+    // small table: ONE counting pass on the whole key (any region size); the
+    // keys are staged in LDS as bytes when they fit, else re-read from the ids
+    uint8_t* k8 = reinterpret_cast<uint8_t*>(lsm);
+    const bool staged = n <= kLdsSortMax * 8;
+    if (staged) stage_keys(R, n, k8);
+    __syncthreads();
+    for (int i = wbeg + lane; i < wend; i += kWave)  // counts only: order-free LDS atomics
+      atomicAdd(&hist[(staged ? k8[i] : region_key(R, i)) * kLsWaves + w], 1u);
+    scan_digit_counts(hist, wsum);
+    for (int t0 = wbeg; t0 < wend; t0 += kWave) {
+      const int i = t0 + lane;
+      const bool act = i < wend;
+      const uint32_t d = act ? (staged ? k8[i] : region_key(R, i)) : 0u;
+      const uint64_t m = digit_peers(d, act);
+      if (act) {
+        uint32_t* slot = &hist[d * kLsWaves + w];
+        const uint32_t off = *slot;
+        region_store(R, static_cast<int>(off + __builtin_popcountll(m & lt)), static_cast<uint32_t>(i), d);
+        if (__builtin_ctzll(m) == lane) *slot = off + __builtin_popcountll(m);
+      }
+    }
+    return;
+  }
+  // n <= kLdsSortMax (host-checked): keys in LDS, LSD passes of <= 8 bits
+  stage_keys(R, n, lkey);
+  for (int i = tid; i < n; i += kLsThreads) pbuf0[i] = static_cast<uint16_t>(i);
+  const int passes = (bits + 7) / 8;
+  const int width = (bits + passes - 1) / passes;
+  const uint32_t dmask = (1u << width) - 1u;
+  int cur = 0;
+  for (int p = 0; p < passes; ++p) {
+    const int sh = p * width;
+    if (p > 0)
+      for (int e = tid; e < 256 * kLsWaves; e += kLsThreads) hist[e] = 0u;
+    __syncthreads();
+    uint16_t pos[kLsTiles];
+    uint32_t dig[kLsTiles];
+    const uint16_t* src = cur ? pbuf1 : pbuf0;
+    uint16_t* dst = cur ? pbuf0 : pbuf1;
+#pragma unroll
+    for (int q = 0; q < kLsTiles; ++q) {
+      const int i = wbeg + q * kWave + lane;
+      pos[q] = 0;
+      dig[q] = 0;
+      if (i < wend) {
+        pos[q] = src[i];
+        dig[q] = (lkey[pos[q]] >> sh) & dmask;
+        atomicAdd(&hist[dig[q] * kLsWaves + w], 1u);  // counts only: order-free
+      }
+    }
+    scan_digit_counts(hist, wsum);
+    const bool last = p == passes - 1;
+#pragma unroll
+    for (int q = 0; q < kLsTiles; ++q) {
+      if (wbeg + q * kWave < wend) {  // wave-uniform
+        const uint64_t m = digit_peers(dig[q], wbeg + q * kWave + lane < wend);
+        if (m != 0) {
+          uint32_t* slot = &hist[dig[q] * kLsWaves + w];
+          const uint32_t off = *slot;
+          const uint32_t o = off + __builtin_popcountll(m & lt);
+          if (last) region_store(R, static_cast<int>(o), pos[q], lkey[pos[q]]);
+          else dst[o] = pos[q];
+          if (__builtin_ctzll(m) == lane) *slot = off + __builtin_popcountll(m);
+        }
+      }
+    }
+    cur ^= 1;
+    __syncthreads();  // the scatter is complete before hist is cleared / the order read
   }
 }
 
@@ -572,6 +828,16 @@ size_t tables_ws_bytes(const tt_sparse_table* tables, int32_t num_tables, int64_
   return total;
 }
 
+// TT_SPARSE_SORT=device forces the key build + rocPRIM sort for every call
+// (the LDS region sort is used when every region fits, by default).
+bool use_lds_sort() {
+  static const bool v = [] {
+    const char* e = std::getenv("TT_SPARSE_SORT");
+    return !(e && std::strcmp(e, "device") == 0);
+  }();
+  return v;
+}
+
 // Stages: the key build + sort depends only on the ids, so a caller may run
 // it early on a side stream (kStageSort) and the gradient-dependent block/join
 // pass later (kStageApply) with the same tables, batch and workspace.
@@ -604,11 +870,21 @@ int run_sparse(const tt_sparse_table* tables, int32_t num_tables, int64_t batch,
     j.dense_dim = dense_dim;
     j.hdr = w.hdr;
     if (stage != kStageApply) {
-      hipLaunchKernelGGL(build_keys_kernel, dim3(ceil_div(p.total, kThreads)), dim3(kThreads), 0, st, j, p.total);
-      TT_CHECK_LAUNCH();
-      size_t sb = p.sort_bytes;
-      TT_CHECK_HIP(rocprim::radix_sort_pairs<SortConfig>(w.sort_tmp, sb, w.keys_in, w.keys, w.vals_in, w.vals,
-                                             static_cast<unsigned>(p.total), 0, p.end_bit, st, false));
+      bool lds = use_lds_sort();
+      for (int i = 0; i < cnt && lds; ++i) lds = j.t[i].n_pad <= kLdsSortMax || bits_for(j.t[i].num_rows) <= 8;
+      if (lds) {
+        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(region_sort_kernel),
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, kLsLdsBytes);
+        TT_CHECK_HIP(attr);
+        hipLaunchKernelGGL(region_sort_kernel, dim3(cnt), dim3(kLsThreads), kLsLdsBytes, st, j);
+        TT_CHECK_LAUNCH();
+      } else {
+        hipLaunchKernelGGL(build_keys_kernel, dim3(ceil_div(p.total, kThreads)), dim3(kThreads), 0, st, j, p.total);
+        TT_CHECK_LAUNCH();
+        size_t sb = p.sort_bytes;
+        TT_CHECK_HIP(rocprim::radix_sort_pairs<SortConfig>(w.sort_tmp, sb, w.keys_in, w.keys, w.vals_in, w.vals,
+                                               static_cast<unsigned>(p.total), 0, p.end_bit, st, false));
+      }
     }
     if (stage == kStageSort) continue;
     const int blocks = static_cast<int>(ceil_div(p.waves, kThreads / kWave));

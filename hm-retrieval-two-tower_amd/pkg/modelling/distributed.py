@@ -937,7 +937,10 @@ class ShardedTrainStep:
         if self._graph is None and self.use_graph and self._calls >= 1 and cur is not None:
             try:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                # thread_local: the process group's watchdog thread polls its
+                # events during the capture; in the default global mode that
+                # poll invalidates the capture and the watchdog aborts the process
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
                     self._middle()
                 self._graph = g
             except Exception as e:  # keep training eagerly (still the HIP kernels)

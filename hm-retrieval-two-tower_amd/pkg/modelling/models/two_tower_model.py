@@ -207,6 +207,11 @@ class TwoTowerModel(AbstractKerasModel):
             else:
                 fwd_done = torch.cuda.Event()
                 fwd_done.record()
+        if fwd_done is not None and SORT_AFTER == "mid":
+            # captured between the forward and the backward: launched before the
+            # backward's nodes, ordered after the forward only
+            self.optimizer.prepare(self.towers, after=fwd_done)
+            fwd_done = None
         for t in self.towers:
             t.dense.flat.grad = None
         if getattr(self, "_one", None) is None or self._one.device != loss.device:
@@ -397,7 +402,9 @@ class GraphedTrainStep:
             self.warmup_out = {k: v.clone() for k, v in out.items()}
         torch.cuda.current_stream().wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        # thread_local: other host threads (a process group's watchdog, the
+        # dataset's order prefetch) may query events while this thread captures
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self.out = self._step()
 
     def _step(self) -> Dict[str, torch.Tensor]:

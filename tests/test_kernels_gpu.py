@@ -564,13 +564,42 @@ def test_route_requests_match_torch_restatement(cuda, world):
     assert torch.equal(tags, et) and torch.equal(lrows, er) and torch.equal(tids, eids)
 
 
-def test_sparse_adagrad_mostly_invalid_ids_bitexact(cuda):
+@pytest.mark.parametrize("rows,sources,B", [(255, 2, 20000), (256, 1, 16384), (256, 2, 9000), (1, 1, 100),
+                                             (1371980, 1, 16384), (40, 3, 5000)])
+def test_sparse_adagrad_sort_paths_bitexact(cuda, rows, sources, B):
+    """The embedding update's id sort takes one of three paths per call: the
+    single-pass LDS counting sort (tables of <= 255 rows, any region size),
+    the multi-pass LDS radix sort (regions <= 16384 lookups), or the key build
+    + device radix sort (anything else).  Each is bit-exact vs the restatement
+    (rows = 256 x 18000 lookups takes the device path)."""
+    rng = np.random.default_rng(rows + B)
+    D = 8
+    w = rng.uniform(-0.05, 0.05, (rows, D)).astype(np.float32)
+    acc = np.full((rows, D), 0.1, np.float32)
+    ids = [zipf_ids(rng, B, rows) for _ in range(sources)]
+    ids[0][::97] = -3
+    grad = rng.standard_normal((B, D * sources)).astype(np.float32)
+    ref_w, ref_acc = w.copy(), acc.copy()
+    oracle.sparse_adagrad(ref_w, ref_acc, np.concatenate(ids),
+                          np.concatenate([grad[:, D * s:D * (s + 1)] for s in range(sources)]), 0.05, 1e-7)
+    tw, ta = _t(w, cuda), _t(acc, cuda)
+    hip_ops.sparse_adagrad([dict(table=tw, slot0=ta, ids=[_t(i, cuda) for i in ids],
+                                 grad_col_offset=[D * s for s in range(sources)])], B, _t(grad, cuda), 0.05, 1e-7)
+    assert np.array_equal(tw.cpu().numpy(), ref_w)
+    assert np.array_equal(ta.cpu().numpy(), ref_acc)
+
+
+@pytest.mark.parametrize("n", [16384, 16385, 20000])
+def test_sparse_adagrad_mostly_invalid_ids_bitexact(cuda, n):
     """Lookups whose ids are mostly outside the table (the owner-side update
-    of a sharded step marks other tables' requests -1) leave only the valid
-    rows updated, bit-exact against the restatement."""
+    of a sharded step marks other tables' requests -1, or ids past the last
+    row) leave only the valid rows updated, bit-exact against the restatement.
+    n = 16384 is the largest region the LDS region sort takes; 16385 and 20000
+    go through the key build + device radix sort."""
     rng = np.random.default_rng(11)
-    n, V, D = 20000, 3000, 128
+    V, D = 3000, 128
     ids = np.where(rng.random(n) < 0.7, -1, zipf_ids(rng, n, V)).astype(np.int32)
+    ids[rng.random(n) < 0.05] = V + 7
     grad = rng.standard_normal((n, D)).astype(np.float32)
     w = rng.uniform(-0.05, 0.05, (V, D)).astype(np.float32)
     acc = np.full((V, D), 0.1, np.float32)
