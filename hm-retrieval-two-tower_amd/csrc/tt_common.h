@@ -83,6 +83,14 @@ __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
 
+// Workgroup barrier for LDS hand-offs only: this wave's LDS operations are
+// complete (lgkmcnt(0)), global loads stay in flight.  __syncthreads() also
+// waits vmcnt(0), which drains every prefetch a pipelined loop has issued.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // vmcnt(63) expcnt(7) lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+}
+
 // Sum over the 64 lanes of a wave (every lane receives the total).
 __device__ __forceinline__ int wave_sum_i32(int v) {
 #pragma unroll

@@ -27,6 +27,8 @@
 // (each B fragment is loaded by exactly one wave of the workgroup).
 #include <type_traits>
 
+#include <cstdlib>
+
 #include "tt_common.h"
 
 namespace tt {
@@ -65,6 +67,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mlp_desc(const void* base, uin
 
 __device__ __forceinline__ f32x4 mlp_load4(__amdgpu_buffer_rsrc_t d, unsigned voff) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(d, voff, 0, 0));
+}
+// voff per lane (loop-invariant), soff uniform (e.g. the stage's row offset)
+__device__ __forceinline__ f32x4 mlp_load4s(__amdgpu_buffer_rsrc_t d, unsigned voff, unsigned soff) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(d, voff, soff, 0));
 }
 
 __device__ __forceinline__ unsigned bf16_bits(float v) {
@@ -295,21 +301,25 @@ __global__ void __launch_bounds__(1024) mlp_colsum_kernel(const float* __restric
 //   layer's output gradient, optionally Gm = (gmask > 0) ? G * s : 0 — the
 //   ReluGrad of the layer's own relu folded into the load)
 // The output [Ka + 1, N] is exactly the flat parameter layout (kernel rows
-// then the bias row).  Reduction over the M batch rows, split over S
-// workgroups (blockIdx.x = split): each writes its partial [Ka + 1, N] and
-// mlp_sum_parts_kernel adds them in split order (deterministic).
+// then the bias row).  Grid = S batch splits x CG column groups of 64: each
+// workgroup reduces its split's rows for ALL Ka + 1 rows of the output and
+// one 64-column group, writes that slice of its split's partial [Ka + 1, N],
+// and mlp_sum_parts_kernel adds the partials in split order (deterministic).
+// The CG workgroups of one split sit on one XCD (blockIdx % 8 picks the XCD),
+// so the split's A rows they all stage come from that XCD's L2.
 // MFMA view: C[i][j] += A'[i][k] B[k][j] with A' = [A | 1]^T (i = activation
 // column, k = batch row), B = Gm.  Both operands need 8 consecutive BATCH
 // rows per lane, so the staged fp32 rows are split hi/lo and written
-// TRANSPOSED into LDS (column-major: 32 batch rows of one column = 64 B,
+// TRANSPOSED into LDS (column-major: 16 batch rows of one column = 32 B,
 // XOR-swizzled 16-B chunks), then read as conflict-free ds_read_b128
-// fragments.  8 waves (two per SIMD); for N <= 256 (8 column blocks) wave w
-// owns column block w and every 32-row block of Ka + 1 (<= 9: Ka <= 287);
-// for N <= 128 (4 column blocks) waves w and w + 4 share column block w,
-// rows blocks 0-4 and 5-8.
+// fragments.  8 waves: wave w owns column block (w & 1) of the group and the
+// 32-row blocks (w >> 1) + 4 t of Ka + 1 (<= 9 blocks: Ka <= 287).
 constexpr int kWgThreads = 512;
 constexpr int kWgBK = 16;      // batch rows per stage (one MFMA k-step)
 constexpr int kWgMaxIB = 9;    // 32-row blocks of Ka + 1 (Ka + 1 <= 288)
+constexpr int kWgCols = 64;    // output columns per workgroup
+constexpr int kWgIMax = 3;     // row blocks per wave
+constexpr int kWgDepth = 4;    // stages of loads in flight
 
 struct WgradArgs {
   const float* A;
@@ -321,171 +331,200 @@ struct WgradArgs {
   const float* scale;
   int64_t M;
   int Ka, N, IB;       // IB = ceil((Ka + 1) / 32)
+  int CG, S;           // column groups, splits
   int64_t rows_per_split;
   float* parts;        // [S][(Ka + 1) * N]
-  int avec;            // A rows 16-B aligned (float4 loads)
 };
 
 // transposed LDS tile: plane p, column c, 16-B chunk q (8 batch rows) of the
-// 16-row stage (32 B per column); the 16 lanes of one ds_read_b128 cycle
-// (16 consecutive columns, one chunk) hit 16 distinct 4-bank groups
+// 16-row stage, 48 B per column (32 used): 12-word column stride, so the 16
+// lanes of one ds_read_b128 cycle (16 consecutive columns) hit 16 distinct
+// 4-bank groups, and the staging writes (8 row pairs x columns 4 apart per
+// instruction) spread over the banks (a 32-B stride put every 8th column on
+// the same 8 banks: 56 % of the LDS cycles were conflicts)
+constexpr int kWtColBytes = 48;
 __device__ __forceinline__ int wt_off(int ncols, int plane, int col, int chunk) {
-  return ((plane * ncols + col) << 5) + ((chunk ^ ((col >> 3) & 1)) << 4);
+  return (plane * ncols + col) * kWtColBytes + (chunk << 4);
 }
 
-template <int NJ, bool MASK>
+template <bool MASK>
 __global__ void __launch_bounds__(kWgThreads) mlp_wgrad_kernel(const WgradArgs a) {
   constexpr int AC = kWgMaxIB * 32;   // A' columns staged (zero beyond Ka + 1)
-  constexpr int GC = NJ * 32;         // G columns staged (N rounded up to NJ column blocks)
-  constexpr int IMAX = NJ == 8 ? kWgMaxIB : (kWgMaxIB + 1) / 2;  // row blocks per wave
-  constexpr int STAGE_BYTES = 2 * (AC + GC) * 32;
-  __shared__ __attribute__((aligned(16))) char smem[2][STAGE_BYTES];
+  constexpr int GC = kWgCols;         // G columns staged (this group's)
+  constexpr int STAGE_BYTES = 2 * (AC + GC) * kWtColBytes;
+  extern __shared__ __attribute__((aligned(16))) char wsm[];  // 2 stage buffers (dynamic: > 64 KiB)
+  char* const smem[2] = {wsm, wsm + STAGE_BYTES};
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
   const int lane = lane_id();
   const int l32 = lane & 31, h = lane >> 5;
-  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * a.rows_per_split;
+  // blockIdx -> (split, column group); XCD-grouped when S % 8 == 0
+  int split, cg;
+  {
+    const int b = blockIdx.x;
+    if (a.S % 8 == 0) {
+      const int q = b >> 3;
+      cg = q % a.CG;
+      split = (q / a.CG) * 8 + (b & 7);
+    } else {
+      cg = b % a.CG;
+      split = b / a.CG;
+    }
+  }
+  const int c0 = cg * GC;  // first output column of the group
+  const int64_t r0 = static_cast<int64_t>(split) * a.rows_per_split;
   int64_t r1 = r0 + a.rows_per_split;
   if (r1 > a.M) r1 = a.M;
   const int nstage = r1 > r0 ? static_cast<int>((r1 - r0 + kWgBK - 1) / kWgBK) : 0;
   const float s = a.scale ? *a.scale : 1.0f;
 
-  // staging units: (row pair p of 16, column quad c) of A' (AC / 4 quads) then G (GC / 4)
+  // staging units: (row pair p of 16, column quad c).  A' has RP * AQ = 576
+  // units: every thread one, threads < 64 (wave 0) a second; G has RP * GQ
+  // = 128 units, on threads 256..383 (waves 4, 5).  Roles are per wave, so
+  // each load names ONE buffer descriptor (a per-lane choice between two made
+  // the compiler emit waterfall loops that drained every load).
   constexpr int RP = kWgBK / 2;  // row pairs per stage
-  constexpr int AQ = AC / 4, GQ = GC / 4, UNITS = RP * (AQ + GQ);
-  constexpr int UPT = (UNITS + kWgThreads - 1) / kWgThreads;
-  // two stages of staged rows in registers: stage st + 2 is loaded while
-  // stage st is computed (slot = stage parity, static under the 2x unroll)
-  f32x4 va[2][UPT][2];
-  f32x4 vm[2][MASK ? UPT : 1][2];
-  // branch-free staging loads (range-checked buffer loads: rows past the
-  // split and past M read as 0), so the compiler's vmcnt waits are exact and
-  // the two-stage prefetch really overlaps
+  constexpr int AQ = AC / 4, GQ = GC / 4;
+  static_assert(RP * AQ == kWgThreads + 64 && RP * GQ == 128, "unit split below assumes Ka+1 <= 288, 64 G columns");
+  const bool a2 = tid < 64;                        // second A unit (wave 0)
+  const bool gu = tid >= 256 && tid < 256 + 128;   // G unit (waves 4, 5)
+  const int ua0 = tid, ua1 = kWgThreads + tid, ug = tid - 256;
+  // load-side units: every thread issues the same loads (threads without a
+  // second A unit / a G unit re-load lines their wave already fetches, L1
+  // hits), so the loop has no load branches and the compiler's vmcnt waits
+  // stay exact across the kWgDepth stages in flight
+  const int la1 = a2 ? ua1 : ua0, lg = tid & 127;
+  // kWgDepth stages of staged rows in registers: stage st + kWgDepth is
+  // loaded while stage st is computed (slot = st % kWgDepth, static under the
+  // unroll), raw (column limits applied by stash, so no load is waited on early)
+  f32x4 va0[kWgDepth][2], va1[kWgDepth][2], vg[kWgDepth][2];
+  f32x4 vm[kWgDepth][MASK ? 2 : 1];
+  // range-checked buffer loads: rows past the split and past M read as 0
   const __amdgpu_buffer_rsrc_t dA = mlp_desc(a.A + r0 * a.lda, static_cast<uint64_t>(r1 - r0) * a.lda * 4);
   const __amdgpu_buffer_rsrc_t dG = mlp_desc(a.G + r0 * a.ldg, static_cast<uint64_t>(r1 - r0) * a.ldg * 4);
   const __amdgpu_buffer_rsrc_t dM =
       mlp_desc(MASK ? a.gmask + r0 * a.ldgm : a.G, static_cast<uint64_t>(r1 - r0) * (MASK ? a.ldgm : a.ldg) * 4);
+  // per-lane byte offsets inside a stage (loop-invariant); the stage's row
+  // offset goes in the scalar soffset
+  const unsigned lda4 = static_cast<unsigned>(a.lda) * 4, ldg4 = static_cast<unsigned>(a.ldg) * 4,
+                 ldm4 = static_cast<unsigned>(MASK ? a.ldgm : a.ldg) * 4;
+  const unsigned oa0 = 2 * (ua0 % RP) * lda4 + (ua0 / RP) * 16;
+  const unsigned oa1 = 2 * (la1 % RP) * lda4 + (la1 / RP) * 16;
+  const unsigned og = 2 * (lg % RP) * ldg4 + (c0 + (lg / RP) * 4) * 4;
+  const unsigned om = 2 * (lg % RP) * ldm4 + (c0 + (lg / RP) * 4) * 4;
   auto fetch = [&](int st, auto slot_c) {
     constexpr int SL = decltype(slot_c)::value;
+    const unsigned sa = static_cast<unsigned>(st * kWgBK) * lda4, sg = static_cast<unsigned>(st * kWgBK) * ldg4,
+                   sm = static_cast<unsigned>(st * kWgBK) * ldm4;
 #pragma unroll
-    for (int u = 0; u < UPT; ++u) {
-      int unit = tid + u * kWgThreads;
-      unit = unit < UNITS ? unit : UNITS - 1;  // (the tail slots re-load a valid unit, unused)
-      // A units then G units; RP * AQ is a multiple of 64, so a wave is all A or all G
-      static_assert((RP * AQ) % 64 == 0, "A/G boundary on a wave edge");
-      const bool isg = __builtin_amdgcn_readfirstlane(unit >= RP * AQ ? 1 : 0) != 0;
-      const int uu = isg ? unit - RP * AQ : unit;
-      const int pr = uu % RP, c = (uu / RP) * 4;
-#pragma unroll
-      for (int e2 = 0; e2 < 2; ++e2) {
-        const int lrow = st * kWgBK + 2 * pr + e2;  // row inside the split
-        const int64_t ld = isg ? a.ldg : a.lda;
-        const f32x4 x4 = mlp_load4(isg ? dG : dA, static_cast<unsigned>((lrow * ld + c) * 4));
-        const bool live = r0 + lrow < r1;
-        const int lim = isg ? a.N : a.Ka;
-        f32x4 v;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int col = c + e;
-          v[e] = col < lim ? x4[e] : ((!isg && col == a.Ka && live) ? 1.0f : 0.0f);
-        }
-        va[SL][u][e2] = v;
-        if constexpr (MASK) {
-          const f32x4 m4 = mlp_load4(dM, static_cast<unsigned>((lrow * a.ldgm + c) * 4));
-          vm[SL][u][e2] = m4;
-        }
-      }
+    for (int e2 = 0; e2 < 2; ++e2) {
+      va0[SL][e2] = mlp_load4s(dA, oa0 + e2 * lda4, sa);
+      va1[SL][e2] = mlp_load4s(dA, oa1 + e2 * lda4, sa);
+      vg[SL][e2] = mlp_load4s(dG, og + e2 * ldg4, sg);
+      if constexpr (MASK) vm[SL][e2] = mlp_load4s(dM, om + e2 * ldm4, sm);
     }
   };
-  auto stash = [&](int buf, auto slot_c) {
+  // one unit's 2 rows x 4 columns -> hi / lo bf16 planes of the transposed tile
+  auto put = [&](char* tb, int ncols, int pr, int c, int gc, int lim, bool isg, int st, const f32x4* v,
+                 const f32x4* m) {
+    const bool live0 = r0 + st * kWgBK + 2 * pr < r1, live1 = r0 + st * kWgBK + 2 * pr + 1 < r1;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int col = gc + e;
+      const bool ones = !isg && col == a.Ka;  // the bias row of A' = [A | 1]^T
+      float x0 = col < lim ? v[0][e] : ((ones && live0) ? 1.0f : 0.0f);
+      float x1 = col < lim ? v[1][e] : ((ones && live1) ? 1.0f : 0.0f);
+      if (MASK && isg) {
+        x0 = m[0][e] > 0.0f ? x0 * s : 0.0f;
+        x1 = m[1][e] > 0.0f ? x1 * s : 0.0f;
+      }
+      const unsigned h0 = bf16_bits(x0), h1 = bf16_bits(x1);
+      const unsigned l0 = bf16_bits(x0 - bf16_val(h0)), l1 = bf16_bits(x1 - bf16_val(h1));
+      const int tcol = c + e, k = 2 * pr;  // tile column; rows k, k + 1 of the stage
+      *reinterpret_cast<unsigned*>(tb + wt_off(ncols, 0, tcol, k >> 3) + (k & 7) * 2) = h0 | (h1 << 16);
+      *reinterpret_cast<unsigned*>(tb + wt_off(ncols, 1, tcol, k >> 3) + (k & 7) * 2) = l0 | (l1 << 16);
+    }
+  };
+  auto stash = [&](int st, int buf, auto slot_c) {
     constexpr int SL = decltype(slot_c)::value;
     char* base = smem[buf];
-#pragma unroll
-    for (int u = 0; u < UPT; ++u) {
-      const int unit = tid + u * kWgThreads;
-      if (unit < UNITS) {
-      const bool isg = unit >= RP * AQ;
-      const int uu = isg ? unit - RP * AQ : unit;
-      const int pr = uu % RP, c = (uu / RP) * 4;
-      char* tb = base + (isg ? 2 * AC * 32 : 0);
-      const int ncols = isg ? GC : AC;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float x0 = va[SL][u][0][e], x1 = va[SL][u][1][e];
-        if constexpr (MASK) {
-          if (isg) {
-            x0 = vm[SL][u][0][e] > 0.0f ? x0 * s : 0.0f;
-            x1 = vm[SL][u][1][e] > 0.0f ? x1 * s : 0.0f;
-          }
-        }
-        const unsigned h0 = bf16_bits(x0), h1 = bf16_bits(x1);
-        const unsigned l0 = bf16_bits(x0 - bf16_val(h0)), l1 = bf16_bits(x1 - bf16_val(h1));
-        const int col = c + e, k = 2 * pr;  // rows k, k + 1 of the stage
-        *reinterpret_cast<unsigned*>(tb + wt_off(ncols, 0, col, k >> 3) + (k & 7) * 2) = h0 | (h1 << 16);
-        *reinterpret_cast<unsigned*>(tb + wt_off(ncols, 1, col, k >> 3) + (k & 7) * 2) = l0 | (l1 << 16);
-      }
-      }
-    }
+    put(base, AC, ua0 % RP, (ua0 / RP) * 4, (ua0 / RP) * 4, a.Ka, false, st, va0[SL], nullptr);
+    if (a2) put(base, AC, ua1 % RP, (ua1 / RP) * 4, (ua1 / RP) * 4, a.Ka, false, st, va1[SL], nullptr);
+    if (gu) put(base + 2 * AC * kWtColBytes, GC, lg % RP, (lg / RP) * 4, c0 + (lg / RP) * 4, a.N, true, st, vg[SL],
+                MASK ? vm[SL] : nullptr);
   };
 
-  const int jb = wave % NJ;
-  const int ib0 = NJ == 8 ? 0 : (wave / NJ) * IMAX;  // first row block of this wave
-  f32x16 acc[IMAX];
+  const int jl = wave & 1;    // column block inside the group
+  const int ig = wave >> 1;   // row blocks ig, ig + 4, ig + 8
+  f32x16 acc[kWgIMax];
 #pragma unroll
-  for (int i = 0; i < IMAX; ++i) acc[i] = f32x16{};
+  for (int i = 0; i < kWgIMax; ++i) acc[i] = f32x16{};
 
-  using Z = std::integral_constant<int, 0>;
-  using O = std::integral_constant<int, 1>;
   if (nstage > 0) {
-    fetch(0, Z());
-    if (nstage > 1) fetch(1, O());
-    stash(0, Z());
-    __syncthreads();
+    fetch(0, std::integral_constant<int, 0>());
+    fetch(1, std::integral_constant<int, 1>());
+    fetch(2, std::integral_constant<int, 2>());
+    fetch(3, std::integral_constant<int, 3>());
+    stash(0, 0, std::integral_constant<int, 0>());
+    lds_barrier();
   }
-  auto stage = [&](int st, auto par_c) {
-    constexpr int PAR = decltype(par_c)::value;
-    if (st + 2 < nstage) fetch(st + 2, par_c);  // the slot stage st came from
+  // stage st: buffer st % 2, register slot st % kWgDepth
+  auto stage = [&](int st, auto slot_c) {
+    constexpr int SLOT = decltype(slot_c)::value;
+    constexpr int PAR = SLOT & 1;
+    constexpr int NEXT = (SLOT + 1) % kWgDepth;
+    fetch(st + kWgDepth, slot_c);  // the slot stage st came from (past the split: zeros, unused)
     const char* base = smem[PAR];
-    const char* gb = base + 2 * AC * 32;
+    const char* gb = base + 2 * AC * kWtColBytes;
     {
       const int chunk = h;
-      const int gcol = 32 * jb + l32;
+      const int gcol = 32 * jl + l32;
       const bf16x8 bh = *reinterpret_cast<const bf16x8*>(gb + wt_off(GC, 0, gcol, chunk));
       const bf16x8 bl = *reinterpret_cast<const bf16x8*>(gb + wt_off(GC, 1, gcol, chunk));
+      // row blocks past Ka + 1 multiply zero fragments (the tile is zero
+      // there): no branches, and the three products of a block are issued
+      // one block apart (independent accumulators back to back)
+      bf16x8 ah[kWgIMax], al[kWgIMax];
 #pragma unroll
-      for (int i = 0; i < IMAX; ++i) {
-        if (ib0 + i < a.IB) {  // uniform; no `break`, so the loop unrolls and acc stays in registers
-          const int col = 32 * (ib0 + i) + l32;
-          const bf16x8 ah = *reinterpret_cast<const bf16x8*>(base + wt_off(AC, 0, col, chunk));
-          const bf16x8 al = *reinterpret_cast<const bf16x8*>(base + wt_off(AC, 1, col, chunk));
-          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[i], 0, 0, 0);
-          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[i], 0, 0, 0);
-          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[i], 0, 0, 0);
-        }
+      for (int i = 0; i < kWgIMax; ++i) {
+        const int col = min(32 * (ig + 4 * i), AC - 32) + l32;
+        ah[i] = *reinterpret_cast<const bf16x8*>(base + wt_off(AC, 0, col, chunk));
+        al[i] = *reinterpret_cast<const bf16x8*>(base + wt_off(AC, 1, col, chunk));
       }
+#pragma unroll
+      for (int i = 0; i < kWgIMax; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh, acc[i], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < kWgIMax; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl, acc[i], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < kWgIMax; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh, acc[i], 0, 0, 0);
     }
-    if (st + 1 < nstage) {
-      __syncthreads();  // everyone is done reading the other buffer (read one stage ago)
-      stash(1 - PAR, std::integral_constant<int, 1 - PAR>());
-      __syncthreads();
-    }
+    lds_barrier();  // everyone is done reading the other buffer (read one stage ago)
+    stash(st + 1, 1 - PAR, std::integral_constant<int, NEXT>());
+    lds_barrier();
   };
-  for (int st = 0; st < nstage; st += 2) {
-    stage(st, Z());
-    if (st + 1 < nstage) stage(st + 1, O());
+  // branch-free body: every stage fetches, computes and stashes (stages past
+  // the split read zeros, which add nothing), so vmcnt waits stay exact; the
+  // stage count is rounded up to the 4x unroll
+  static_assert(kWgDepth == 4, "the stage loop below is unrolled 4x");
+  for (int st = 0; st < nstage; st += 4) {
+    stage(st, std::integral_constant<int, 0>());
+    stage(st + 1, std::integral_constant<int, 1>());
+    stage(st + 2, std::integral_constant<int, 2>());
+    stage(st + 3, std::integral_constant<int, 3>());
   }
 
-  // partial [Ka + 1, N] of this split: lane (l32, h), register r -> row
-  // 32 (ib0 + i) + (r & 3) + 8 (r >> 2) + 4 h, column 32 jb + l32
+  // this group's slice of the split's partial [Ka + 1, N]: lane (l32, h),
+  // register r -> row 32 ib + (r & 3) + 8 (r >> 2) + 4 h, column c0 + 32 jl + l32
   const int rows_out = a.Ka + 1;
-  float* P = a.parts + static_cast<int64_t>(blockIdx.x) * rows_out * a.N;
-  const int n = 32 * jb + l32;
+  float* P = a.parts + static_cast<int64_t>(split) * rows_out * a.N;
+  const int n = c0 + 32 * jl + l32;
 #pragma unroll
-  for (int i = 0; i < IMAX; ++i) {
+  for (int i = 0; i < kWgIMax; ++i) {
+    const int ib = ig + 4 * i;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int row = 32 * (ib0 + i) + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (ib0 + i < a.IB && n < a.N && row < rows_out) P[static_cast<int64_t>(row) * a.N + n] = acc[i][r];
+      const int row = 32 * ib + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (ib < a.IB && n < a.N && row < rows_out) P[static_cast<int64_t>(row) * a.N + n] = acc[i][r];
     }
   }
 }
@@ -722,21 +761,26 @@ extern "C" int tt_mlp_rows(const float* A, int64_t lda, const float* amask, int6
   return TT_OK;
 }
 
-// splits of the batch reduction: ~128+ rows each, at most 64 (partials stay
-// <= 64 x (Ka + 1) x N floats)
-#ifndef TT_WGRAD_MAX_SPLITS
-#define TT_WGRAD_MAX_SPLITS 64
-#endif
-static int wgrad_splits(int64_t M) {
-  int64_t S = M / 128;
-  if (S > TT_WGRAD_MAX_SPLITS) S = TT_WGRAD_MAX_SPLITS;
+// splits of the batch reduction: enough (split, column group) workgroups to
+// fill the chip, >= 64 rows each; a multiple of 8 when there are >= 8 (the
+// XCD grouping)
+static int wgrad_splits(int64_t M, int N) {
+  const int cg = (N + kWgCols - 1) / kWgCols;
+  static const int64_t target = [] {  // TT_WGRAD_WGS: workgroups to aim for (default one per CU)
+    const char* e = std::getenv("TT_WGRAD_WGS");
+    return static_cast<int64_t>(e ? std::atoi(e) : 256);
+  }();
+  int64_t S = target / cg;
+  if (S > 128) S = 128;
+  const int64_t by_rows = M / 64;
+  if (S > by_rows) S = by_rows >= 8 ? by_rows / 8 * 8 : by_rows;
   if (S < 1) S = 1;
   return static_cast<int>(S);
 }
 
 extern "C" size_t tt_mlp_wgrad_workspace_size(int64_t M, int32_t Ka, int32_t N) {
   if (M < 0 || Ka < 0 || N < 1) return 0;
-  return static_cast<size_t>(wgrad_splits(M)) * (Ka + 1) * N * sizeof(float);
+  return static_cast<size_t>(wgrad_splits(M, N)) * (Ka + 1) * N * sizeof(float);
 }
 
 extern "C" int tt_mlp_wgrad(const float* A, int64_t lda, const float* G, int64_t ldg, const float* gmask,
@@ -751,7 +795,7 @@ extern "C" int tt_mlp_wgrad(const float* A, int64_t lda, const float* G, int64_t
   TT_REQUIRE(ldg % 4 == 0 && reinterpret_cast<uintptr_t>(G) % 16 == 0 &&
                  (!gmask || (ldgm % 4 == 0 && reinterpret_cast<uintptr_t>(gmask) % 16 == 0)),
              "tt_mlp_wgrad: G / gmask rows must be 16-B aligned");
-  const int S = wgrad_splits(M);
+  const int S = wgrad_splits(M, N);
   TT_REQUIRE(workspace && workspace_bytes >= tt_mlp_wgrad_workspace_size(M, Ka, N),
              "tt_mlp_wgrad: workspace %zu < %zu", workspace_bytes, tt_mlp_wgrad_workspace_size(M, Ka, N));
   WgradArgs a{};
@@ -766,18 +810,21 @@ extern "C" int tt_mlp_wgrad(const float* A, int64_t lda, const float* G, int64_t
   a.Ka = Ka;
   a.N = N;
   a.IB = (Ka + 1 + 31) / 32;
+  a.CG = (N + kWgCols - 1) / kWgCols;
+  a.S = S;
   a.rows_per_split = round_up(ceil_div(M > 0 ? M : 1, S), kWgBK);
   a.parts = static_cast<float*>(workspace);
-  a.avec = (lda % 4 == 0 && reinterpret_cast<uintptr_t>(A) % 16 == 0) ? 1 : 0;
   hipStream_t st = to_stream(stream);
-  const dim3 grid(static_cast<unsigned>(S));
-  if (N <= 128) {
-    if (gmask) hipLaunchKernelGGL((mlp_wgrad_kernel<4, true>), grid, dim3(kWgThreads), 0, st, a);
-    else hipLaunchKernelGGL((mlp_wgrad_kernel<4, false>), grid, dim3(kWgThreads), 0, st, a);
-  } else {
-    if (gmask) hipLaunchKernelGGL((mlp_wgrad_kernel<8, true>), grid, dim3(kWgThreads), 0, st, a);
-    else hipLaunchKernelGGL((mlp_wgrad_kernel<8, false>), grid, dim3(kWgThreads), 0, st, a);
-  }
+  const dim3 grid(static_cast<unsigned>(S * a.CG));
+  constexpr int shm = 2 * 2 * (kWgMaxIB * 32 + kWgCols) * kWtColBytes;
+  static const hipError_t attr_t = hipFuncSetAttribute(reinterpret_cast<const void*>(mlp_wgrad_kernel<true>),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, shm);
+  static const hipError_t attr_f = hipFuncSetAttribute(reinterpret_cast<const void*>(mlp_wgrad_kernel<false>),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, shm);
+  TT_CHECK_HIP(attr_t);
+  TT_CHECK_HIP(attr_f);
+  if (gmask) hipLaunchKernelGGL((mlp_wgrad_kernel<true>), grid, dim3(kWgThreads), shm, st, a);
+  else hipLaunchKernelGGL((mlp_wgrad_kernel<false>), grid, dim3(kWgThreads), shm, st, a);
   TT_CHECK_LAUNCH();
   const int64_t len = static_cast<int64_t>(Ka + 1) * N;
   hipLaunchKernelGGL(mlp_sum_parts_kernel, dim3(ceil_div(len, 256)), dim3(1024), 0, st, a.parts, S, len, dwb);

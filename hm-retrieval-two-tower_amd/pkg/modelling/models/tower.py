@@ -38,6 +38,26 @@ from pkg.modelling.models.abstract_keras_model import AbstractKerasModel, Tensor
 __all__ = ["Tower", "DenseStack"]
 
 
+# weight-gradient side streams of the "mlp" backend (losses.WGRAD_STREAM)
+_WGRAD_STREAMS = {}
+# the "mlp" backend's weight gradients: "blas" (default: hipBLASLt split-K +
+# tt_sum_slices, with the separate ReluGrad / bias-gradient launches) or "tt"
+# (tt_mlp_wgrad: no vendor GEMM and no glue launch in the step, but the C3
+# step measured 0.609 vs 0.595 ms — its split partials and the activation
+# re-reads of its column groups keep it HBM-bound at 28-30 us per layer)
+WGRAD_KERNEL = os.environ.get("TT_WGRAD", "blas")
+
+
+def _wgrad_stream(cur: torch.cuda.Stream) -> torch.cuda.Stream:
+    """The weight-gradient stream of the tower whose backward runs now, one per
+    device and workspace scope (query / candidate tower): created by the first
+    (eager) step, never inside a graph capture, whose stream is a fresh one."""
+    key = (cur.device.index, hip_ops.Workspace._scope)
+    if key not in _WGRAD_STREAMS:
+        _WGRAD_STREAMS[key] = torch.cuda.Stream(device=cur.device)
+    return _WGRAD_STREAMS[key]
+
+
 def _splitk_mm_tn(a: torch.Tensor, g: torch.Tensor, out: torch.Tensor, splits: int = 16) -> None:
     """out = a^T g for tall a [B, fin], g [B, fout] (the weight gradient).
     hipBLASLt runs this skinny, K=B-long product on a handful of tiles; a
@@ -170,16 +190,19 @@ class DenseStack:
         return acts
 
     def backward_acts(self, acts: List[torch.Tensor], flat: torch.Tensor, gout: torch.Tensor,
-                      gscale: Optional[torch.Tensor], need_input_grad: bool, inplace: bool = True):
+                      gscale: Optional[torch.Tensor], need_input_grad: bool, inplace: bool = True,
+                      joins: Optional[List[torch.cuda.Stream]] = None):
         """(d x, d flat) from the saved activations.  hipBLASLt backend, per
         layer: one tt_relu_bias_grad (relu mask x the incoming gradient, times
         gscale on the top layer, and the bias gradient), the weight gradient
         (split-K GEMM + tt_sum_slices) and the input gradient (GEMM).
-        inplace: gout may be overwritten."""
+        inplace: gout may be overwritten.  joins ("mlp" backend, GPU): the weight
+        gradients run on a side stream appended to this list, which the caller
+        must make its stream wait on before using d flat."""
         if self.backend == "tt":
             return self._backward_tt(acts, flat, gout, gscale, need_input_grad)
         if self.backend == "mlp":
-            return self._backward_mlp(acts, flat, gout, gscale, need_input_grad, inplace)
+            return self._backward_mlp(acts, flat, gout, gscale, need_input_grad, inplace, joins)
         gflat = torch.empty_like(flat)
         params = self.params(flat)
         gparams = self.params(gflat)
@@ -197,31 +220,89 @@ class DenseStack:
         return (g if need_input_grad else None), gflat
 
     def _backward_mlp(self, acts: List[torch.Tensor], flat: torch.Tensor, gout: torch.Tensor,
-                      gscale: Optional[torch.Tensor], need_input_grad: bool, inplace: bool):
+                      gscale: Optional[torch.Tensor], need_input_grad: bool, inplace: bool,
+                      joins: Optional[List[torch.cuda.Stream]] = None):
         """"mlp" backend.  Top layer: G_L = relu'(h_L) * s * gout and db_L by
         one tt_relu_bias_grad.  Per layer l from the top: [dW_l] = h_{l-1}^T G_l
         (hipBLASLt split-K + tt_sum_slices), then ONE tt_mlp_rows for the layer
         below: G_{l-1} = (G_l W_l^T) * relu'(h_{l-1}) with db_{l-1} = colsum
         G_{l-1} in its epilogue (the ReluGrad / BiasAddGrad pair fused), or the
         input gradient dx = G_1 W_1^T (16-B padded rows, returned as a view)."""
+        if WGRAD_KERNEL == "tt" and gout.is_cuda and self._wgrad_fits(gout):
+            return self._backward_mlp_tt(acts, flat, gout, gscale, need_input_grad)
         gflat = torch.empty_like(flat)
         params = self.params(flat)
         gparams = self.params(gflat)
         imgs = self.__dict__["_images"]  # packed by this step's forward (same flat)
         L = len(params)
         g, _ = hip_ops.relu_bias_grad(gout, acts[L], gscale, out=gout if inplace else None, db=gparams[L - 1][1])
+        # joins given: the weight gradients (hipBLASLt) leave the input-gradient
+        # chain (which gates the embedding update) for a stream of their own,
+        # each started as soon as its G_l exists.  That stream never feeds back
+        # into this one: the CALLER joins it from the capture's origin stream (a
+        # captured branch that waits on a sub-branch it forked crashes
+        # hipGraph instantiation on this ROCm).
+        cur = torch.cuda.current_stream(g.device) if (joins is not None and g.is_cuda) else None
+        ws = _wgrad_stream(cur) if cur is not None else None
+        dx = None
         for li in range(L - 1, -1, -1):
             w = params[li][0]
-            _splitk_mm_tn(acts[li], g, gparams[li][0])
+            if ws is not None:
+                ws.wait_stream(cur)
+                with torch.cuda.stream(ws):
+                    _splitk_mm_tn(acts[li], g, gparams[li][0])
+                    g.record_stream(ws)
+            else:
+                _splitk_mm_tn(acts[li], g, gparams[li][0])
             if li == 0 and not need_input_grad:
-                return None, gflat
+                break
             fi, fo = w.shape
             ld = (fi + 3) // 4 * 4  # 16-B rows for the kernel's vector stores
             out = torch.empty(g.shape[0], ld, dtype=torch.float32, device=g.device)[:, :fi]
             if li > 0:
                 g = hip_ops.mlp_rows(g, imgs[("t", li)], fo, fi, out, cmask=acts[li], colsum=gparams[li - 1][1])
             else:
-                g = hip_ops.mlp_rows(g, imgs[("t", li)], fo, fi, out)
+                dx = g = hip_ops.mlp_rows(g, imgs[("t", li)], fo, fi, out)
+        if ws is not None:
+            joins.append(ws)
+        return dx, gflat
+
+    def _wgrad_fits(self, gout: torch.Tensor) -> bool:
+        """tt_mlp_wgrad's shape contract: N % 4 == 0, N <= 256, Ka + 1 <= 288,
+        16-B aligned gradient rows."""
+        if gout.stride(1) != 1 or gout.stride(0) % 4 or gout.data_ptr() % 16:
+            return False
+        return all(fo % 4 == 0 and fo <= 256 and fi + 1 <= 288 for _, fi, fo, _ in self.layout)
+
+    def _backward_mlp_tt(self, acts: List[torch.Tensor], flat: torch.Tensor, gout: torch.Tensor,
+                         gscale: Optional[torch.Tensor], need_input_grad: bool):
+        """"mlp" backend, every GEMM hand-written.  Per layer l from the top:
+        [dW_l; db_l] = [h_{l-1} | 1]^T G_l by ONE tt_mlp_wgrad straight into
+        the flat gradient (the top layer's G_L = relu'(h_L) * s * gout is formed
+        inside its loads), then ONE tt_mlp_rows for the layer below:
+        G_{l-1} = (G_l W_l^T) * relu'(h_{l-1}) (the top layer's relu mask and
+        scale applied to its A loads), or the input gradient dx = G_1 W_1^T.
+        No ReluGrad / BiasAddGrad / split-K glue launches remain.  gout is not
+        modified."""
+        gflat = torch.empty_like(flat)
+        imgs = self.__dict__["_images"]  # packed by this step's forward (same flat)
+        L = len(self.layout)
+        g = gout
+        for li in range(L - 1, -1, -1):
+            w_off, fi, fo, _ = self.layout[li]
+            dwb = gflat[w_off:w_off + (fi + 1) * fo].view(fi + 1, fo)
+            top = li == L - 1
+            if top:
+                hip_ops.mlp_wgrad(acts[li], gout, dwb, gmask=acts[L], scale=gscale)
+            else:
+                hip_ops.mlp_wgrad(acts[li], g, dwb)
+            if li == 0 and not need_input_grad:
+                return None, gflat
+            ld = (fi + 3) // 4 * 4  # 16-B rows for the kernel's vector stores
+            out = torch.empty(g.shape[0], ld, dtype=torch.float32, device=g.device)[:, :fi]
+            g = hip_ops.mlp_rows(g, imgs[("t", li)], fo, fi, out,
+                                 amask=acts[L] if top else None, scale=gscale if top else None,
+                                 cmask=acts[li] if li > 0 else None)
         return g, gflat
 
     def _forward_tt(self, x: torch.Tensor, flat: torch.Tensor) -> List[torch.Tensor]:

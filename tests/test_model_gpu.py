@@ -114,8 +114,9 @@ def _cpu_mirror(m):
 
 @pytest.mark.parametrize("zipf,backend,precision", [(True, "hipblaslt", None), (False, "hipblaslt", None),
                                                     (True, "tt", "x3"), (False, "tt", "x3"), (True, "tt", "bf16"),
-                                                    (True, "mlp", None), (False, "mlp", None)])
-def test_train_steps_match_cpu_restatement(cuda, zipf, backend, precision):
+                                                    (True, "mlp", None), (False, "mlp", None),
+                                                    (True, "mlp", "wgrad_tt"), (False, "mlp", "wgrad_tt")])
+def test_train_steps_match_cpu_restatement(cuda, zipf, backend, precision, monkeypatch):
     """First step: every parameter update within 1e-2 rel of the fp32 CPU
     restatement (bf16 MFMA operands in the fused loss give ~1e-3 per-example
     gradient error, amplified where a batch-summed gradient cancels).  Then the
@@ -124,7 +125,12 @@ def test_train_steps_match_cpu_restatement(cuda, zipf, backend, precision):
     scale every step, so any rounding difference is amplified).  Both tower
     GEMM backends: hipBLASLt fp32, libtt tt_gemm (bf16x3 and plain bf16) and
     libtt tt_mlp_rows (bf16x3) for the forward / input-gradient GEMMs."""
+    from pkg.modelling.models import tower as tower_mod
+
     m = _small_model(cuda)
+    if precision == "wgrad_tt":  # "mlp" backend with tt_mlp_wgrad: no vendor GEMM in the step
+        monkeypatch.setattr(tower_mod, "WGRAD_KERNEL", "tt")
+        precision = None
     for t in (m.query_tower, m.candidate_tower):
         t.dense.backend = backend
         if precision:
