@@ -477,16 +477,37 @@ __global__ void __launch_bounds__(256) combine_rows_kernel(
   const int64_t i = blockIdx.x * (256ll / LPR) + threadIdx.x / LPR;
   const int sub = threadIdx.x % LPR;
   if (i >= n_rows) return;
+  // splits in groups of 4 whose loads are all issued before any is used
+  // (index clamped, weight 0 past nsplit); splits added in order as before
   float M = -1.0e30f;
-  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, part_m[s * n_stat_pad + i]);
+  for (int s0 = 0; s0 < nsplit; s0 += 4) {
+    float m[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) m[u] = part_m[min(s0 + u, nsplit - 1) * n_stat_pad + i];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) M = fmaxf(M, m[u]);
+  }
   float L = 0.0f;
   f32x4 o = {0.0f, 0.0f, 0.0f, 0.0f};
-  for (int s = 0; s < nsplit; ++s) {
-    const float w = expf(part_m[s * n_stat_pad + i] - M);
-    L += part_l[s * n_stat_pad + i] * w;
-    const f32x4 ps = *reinterpret_cast<const f32x4*>(part_o + (s * n_stat_pad + i) * D + 4 * sub);
+  for (int s0 = 0; s0 < nsplit; s0 += 4) {
+    float m[4], l[4];
+    f32x4 ps[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) o[u] += ps[u] * w;
+    for (int u = 0; u < 4; ++u) {
+      const int64_t sr = min(s0 + u, nsplit - 1) * n_stat_pad + i;
+      m[u] = part_m[sr];
+      l[u] = part_l[sr];
+      ps[u] = *reinterpret_cast<const f32x4*>(part_o + sr * D + 4 * sub);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (s0 + u < nsplit) {
+        const float w = expf(m[u] - M);
+        L += l[u] * w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] += ps[u][e] * w;
+      }
+    }
   }
   const float lse = M + logf(L);
   const float inv = 1.0f / L;
@@ -525,10 +546,17 @@ __global__ void __launch_bounds__(256) combine_cols_kernel(const float* __restri
   const float scale = logq ? expf(-logq[j]) : 1.0f;
   const int64_t pos = j + pos_offset;
   f32x4 o = {0.0f, 0.0f, 0.0f, 0.0f};
-  for (int s = 0; s < nsplit; ++s) {
-    const f32x4 ps = *reinterpret_cast<const f32x4*>(part_o + (s * n_stat_pad + j) * D + 4 * sub);
+  for (int s0 = 0; s0 < nsplit; s0 += 4) {  // 4 splits' loads in flight, added in order
+    f32x4 ps[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) o[u] += ps[u];
+    for (int u = 0; u < 4; ++u)
+      ps[u] = *reinterpret_cast<const f32x4*>(part_o + (min(s0 + u, nsplit - 1) * n_stat_pad + j) * D + 4 * sub);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (s0 + u < nsplit) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] += ps[u][e];
+      }
   }
 #pragma unroll
   for (int u = 0; u < 4; ++u) {

@@ -200,7 +200,7 @@ __global__ void __launch_bounds__(kMlpThreads) mlp_rows_kernel(const MlpArgs a) 
     }
     if (st + 1 < nstage) {
       stash_a((st + 1) * kMlpBK, std::integral_constant<int, 1 - PAR>(), 1 - PAR);
-      __syncthreads();
+      lds_barrier();  // LDS hand-off only: the A / B prefetches stay in flight
     }
   };
   for (int st = 0; st < nstage; st += 2) {
