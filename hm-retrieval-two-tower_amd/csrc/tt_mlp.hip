@@ -766,9 +766,13 @@ extern "C" int tt_mlp_rows(const float* A, int64_t lda, const float* amask, int6
 // XCD grouping)
 static int wgrad_splits(int64_t M, int N) {
   const int cg = (N + kWgCols - 1) / kWgCols;
-  static const int64_t target = [] {  // TT_WGRAD_WGS: workgroups to aim for (default one per CU)
+  // TT_WGRAD_WGS: workgroups to aim for.  Default 128 (half the CUs): in the
+  // train step the two towers' backward chains run side by side, and one
+  // workgroup per CU (256) starved the other tower (step 0.631 vs 0.617 ms)
+  // although it is the faster kernel alone (28 vs 44 us)
+  static const int64_t target = [] {
     const char* e = std::getenv("TT_WGRAD_WGS");
-    return static_cast<int64_t>(e ? std::atoi(e) : 256);
+    return static_cast<int64_t>(e ? std::atoi(e) : 128);
   }();
   int64_t S = target / cg;
   if (S > 128) S = 128;
