@@ -67,7 +67,14 @@ __global__ void __launch_bounds__(1024) column_total_kernel(const float* __restr
   const int b0 = i * chunk, b1 = min(b0 + chunk, nblk);
   float acc = 0.0f;
   if (c < cols)
-    for (int b = b0; b < b1; ++b) acc += part[static_cast<int64_t>(b) * cols + c];
+    for (int bb = b0; bb < b1; bb += 16) {  // 16 loads in flight (index clamped), added in order
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = part[static_cast<int64_t>(min(bb + u, b1 - 1)) * cols + c];
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (bb + u < b1) acc += v[u];
+    }
   red[i][threadIdx.x & 63] = acc;
   __syncthreads();
   if (i == 0 && c < cols) {

@@ -281,7 +281,14 @@ __global__ void __launch_bounds__(1024) mlp_colsum_kernel(const float* __restric
   float sum = 0.0f;
   if (c < N) {
     const int b1 = min(nblk, (grp + 1) * per);
-    for (int b = grp * per; b < b1; ++b) sum += parts[static_cast<int64_t>(b) * N + c];
+    for (int bb = grp * per; bb < b1; bb += 16) {  // 16 loads in flight (index clamped), added in order
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = parts[static_cast<int64_t>(min(bb + u, b1 - 1)) * N + c];
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (bb + u < b1) sum += v[u];
+    }
   }
   red[grp][threadIdx.x & 63] = sum;
   __syncthreads();
