@@ -185,7 +185,10 @@ constexpr int kLdsSortMax = 16384;
 constexpr int kLsThreads = 1024;
 constexpr int kLsWaves = kLsThreads / kWave;
 constexpr int kLsTiles = kLdsSortMax / kLsWaves / kWave;  // 64-lane tiles per wave at the maximum
-constexpr int kLsLdsBytes = kLdsSortMax * 4 + 2 * kLdsSortMax * 2 + 256 * kLsWaves * 4;
+// digit counts [256 digits][kLsWaves] at a row stride of kLsWaves + 1 words, so
+// the distinct digits of one wave's lanes fall in distinct LDS banks
+constexpr int kHistStride = kLsWaves + 1;
+constexpr int kLsLdsBytes = kLdsSortMax * 4 + 2 * kLdsSortMax * 2 + 256 * kHistStride * 4;
 
 // row key of region position i: the row id, or nr for invalid ids and padding
 // One region's descriptor in registers (a reference into the kernel's
@@ -267,12 +270,14 @@ __device__ __forceinline__ void region_store(const Region& R, int out, uint32_t 
 }
 
 // lanes of this wave holding the same digit (among the `act` lanes): one
-// ballot per digit bit, each lane keeping the lanes that agree with its bit
-__device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool act) {
+// ballot per digit bit (d < 2^nbits, nbits <= 8, wave-uniform), each lane
+// keeping the lanes that agree with its bit
+__device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool act, int nbits) {
   const uint64_t a = __ballot(act);
   uint32_t lo = static_cast<uint32_t>(a), hi = static_cast<uint32_t>(a >> 32);
 #pragma unroll
   for (int b = 0; b < 8; ++b) {
+    if (b >= nbits) break;
     const uint32_t bit = (d >> b) & 1u;
     const uint64_t bal = __ballot(bit);
     const uint32_t flip = bit - 1u;  // 0 when the bit is set, all ones when clear
@@ -282,6 +287,15 @@ __device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool act) {
   return act ? (static_cast<uint64_t>(hi) << 32 | lo) : 0;
 }
 
+// word of (digit, wave) entry L = digit * kLsWaves + wave of the padded histogram
+__device__ __forceinline__ int hist_word(int L) { return (L / kLsWaves) * kHistStride + L % kLsWaves; }
+
+// one wave's count of a tile: the lowest lane of each digit adds its peers
+// (distinct digits, distinct words; the wave's own tiles run in order)
+__device__ __forceinline__ void count_peers(uint32_t* hist, uint32_t d, uint64_t m, int w) {
+  if (m != 0 && __builtin_ctzll(m) == static_cast<int>(lane_id())) hist[d * kHistStride + w] += __builtin_popcountll(m);
+}
+
 // hist[digit][wave] counts -> exclusive offsets in (digit, wave) order
 __device__ __forceinline__ void scan_digit_counts(uint32_t* hist, uint32_t* wsum) {
   const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
@@ -289,7 +303,7 @@ __device__ __forceinline__ void scan_digit_counts(uint32_t* hist, uint32_t* wsum
   uint32_t h[4], run = 0;
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
-    h[u] = hist[4 * tid + u];
+    h[u] = hist[hist_word(4 * tid + u)];
     run += h[u];
   }
   uint32_t inc = run;
@@ -304,7 +318,7 @@ __device__ __forceinline__ void scan_digit_counts(uint32_t* hist, uint32_t* wsum
   for (int v = 0; v < w; ++v) ex += wsum[v];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
-    hist[4 * tid + u] = ex;
+    hist[hist_word(4 * tid + u)] = ex;
     ex += h[u];
   }
   __syncthreads();
@@ -315,7 +329,7 @@ __global__ void __launch_bounds__(kLsThreads) region_sort_kernel(const Job j) {
   uint32_t* lkey = reinterpret_cast<uint32_t*>(lsm);
   uint16_t* const pbuf0 = reinterpret_cast<uint16_t*>(lsm + kLdsSortMax * 4);
   uint16_t* const pbuf1 = pbuf0 + kLdsSortMax;
-  uint32_t* hist = reinterpret_cast<uint32_t*>(lsm + kLdsSortMax * 8);  // [256 digits][kLsWaves]
+  uint32_t* hist = reinterpret_cast<uint32_t*>(lsm + kLdsSortMax * 8);  // [256 digits][kHistStride]
   __shared__ uint32_t wsum[kLsWaves];
   const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
   Region R;
@@ -348,7 +362,7 @@ __global__ void __launch_bounds__(kLsThreads) region_sort_kernel(const Job j) {
   const int per = ((n + kLsWaves - 1) / kLsWaves + kWave - 1) / kWave * kWave;
   const int wbeg = w * per, wend = min(n, wbeg + per);
   const uint64_t lt = (uint64_t(1) << lane) - 1u;
-  for (int e = tid; e < 256 * kLsWaves; e += kLsThreads) hist[e] = 0u;
+  for (int e = tid; e < 256 * kHistStride; e += kLsThreads) hist[e] = 0u;
   if (bits <= 8) {
     // small table: ONE counting pass on the whole key (any region size); the
     // keys are staged in LDS as bytes when they fit, else re-read from the ids
@@ -356,16 +370,20 @@ __global__ void __launch_bounds__(kLsThreads) region_sort_kernel(const Job j) {
     const bool staged = n <= kLdsSortMax * 8;
     if (staged) stage_keys(R, n, k8);
     __syncthreads();
-    for (int i = wbeg + lane; i < wend; i += kWave)  // counts only: order-free LDS atomics
-      atomicAdd(&hist[(staged ? k8[i] : region_key(R, i)) * kLsWaves + w], 1u);
+    for (int t0 = wbeg; t0 < wend; t0 += kWave) {  // counts: peers per tile, no LDS atomics
+      const int i = t0 + lane;
+      const bool act = i < wend;
+      const uint32_t d = act ? (staged ? k8[i] : region_key(R, i)) : 0u;
+      count_peers(hist, d, digit_peers(d, act, bits), w);
+    }
     scan_digit_counts(hist, wsum);
     for (int t0 = wbeg; t0 < wend; t0 += kWave) {
       const int i = t0 + lane;
       const bool act = i < wend;
       const uint32_t d = act ? (staged ? k8[i] : region_key(R, i)) : 0u;
-      const uint64_t m = digit_peers(d, act);
+      const uint64_t m = digit_peers(d, act, bits);
       if (act) {
-        uint32_t* slot = &hist[d * kLsWaves + w];
+        uint32_t* slot = &hist[d * kHistStride + w];
         const uint32_t off = *slot;
         region_store(R, static_cast<int>(off + __builtin_popcountll(m & lt)), static_cast<uint32_t>(i), d);
         if (__builtin_ctzll(m) == lane) *slot = off + __builtin_popcountll(m);
@@ -383,10 +401,11 @@ __global__ void __launch_bounds__(kLsThreads) region_sort_kernel(const Job j) {
   for (int p = 0; p < passes; ++p) {
     const int sh = p * width;
     if (p > 0)
-      for (int e = tid; e < 256 * kLsWaves; e += kLsThreads) hist[e] = 0u;
+      for (int e = tid; e < 256 * kHistStride; e += kLsThreads) hist[e] = 0u;
     __syncthreads();
     uint16_t pos[kLsTiles];
     uint32_t dig[kLsTiles];
+    uint64_t peer[kLsTiles];  // lanes of the tile with the same digit, reused by the scatter
     const uint16_t* src = cur ? pbuf1 : pbuf0;
     uint16_t* dst = cur ? pbuf0 : pbuf1;
 #pragma unroll
@@ -397,7 +416,14 @@ __global__ void __launch_bounds__(kLsThreads) region_sort_kernel(const Job j) {
       if (i < wend) {
         pos[q] = src[i];
         dig[q] = (lkey[pos[q]] >> sh) & dmask;
-        atomicAdd(&hist[dig[q] * kLsWaves + w], 1u);  // counts only: order-free
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kLsTiles; ++q) {
+      peer[q] = 0;
+      if (wbeg + q * kWave < wend) {  // wave-uniform
+        peer[q] = digit_peers(dig[q], wbeg + q * kWave + lane < wend, width);
+        count_peers(hist, dig[q], peer[q], w);
       }
     }
     scan_digit_counts(hist, wsum);
@@ -405,9 +431,9 @@ __global__ void __launch_bounds__(kLsThreads) region_sort_kernel(const Job j) {
 #pragma unroll
     for (int q = 0; q < kLsTiles; ++q) {
       if (wbeg + q * kWave < wend) {  // wave-uniform
-        const uint64_t m = digit_peers(dig[q], wbeg + q * kWave + lane < wend);
+        const uint64_t m = peer[q];
         if (m != 0) {
-          uint32_t* slot = &hist[dig[q] * kLsWaves + w];
+          uint32_t* slot = &hist[dig[q] * kHistStride + w];
           const uint32_t off = *slot;
           const uint32_t o = off + __builtin_popcountll(m & lt);
           if (last) region_store(R, static_cast<int>(o), pos[q], lkey[pos[q]]);
