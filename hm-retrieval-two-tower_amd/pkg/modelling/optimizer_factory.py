@@ -109,6 +109,13 @@ class Adagrad(_Optimizer):
             done.record(side)
             self._tower_prep[id(tower)] = ([id(s["table"]) for s in specs], batch, done, key)
 
+    def apply_dense(self, tower, flat_grad: torch.Tensor) -> None:
+        """Tower's dense Adagrad step alone, on the current stream (the same
+        update _apply makes from flat.grad)."""
+        flat = tower.dense.flat
+        (acc,) = self._slot(flat, 1, self.initial_accumulator_value)
+        hip_ops.dense_adagrad(flat.data, acc, flat_grad, self.learning_rate, self.epsilon)
+
     def apply_tower(self, tower, input_grad: Optional[torch.Tensor], flat_grad: torch.Tensor) -> None:
         """Tower's dense Adagrad step and its tables' sparse step, on the current
         stream and workspace scope (the ones prepare_towers used for it)."""

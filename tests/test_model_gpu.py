@@ -235,6 +235,31 @@ def test_fused_optimizer_apply_bit_identical_to_unfused(cuda):
     b.optimizer.check_status(cuda)
 
 
+def test_dense_early_bit_identical_to_dense_after_join(cuda, monkeypatch):
+    """The default step applies each tower's dense (MLP) Adagrad inside the
+    backward on the tower's stream (TT_DENSE_EARLY); with it off the dense
+    step runs after the join.  Tables, accumulators, MLP buffers and losses
+    are bit-identical at ragged batch sizes, and apply_gradients is left with
+    only the embedding update (no dense update applied twice)."""
+    from pkg.modelling.models import two_tower_model as ttm
+
+    a, b = _small_model(cuda, seed=5), _small_model(cuda, seed=5)
+    rng = np.random.default_rng(4)
+    for i, B in enumerate((512, 37, 256, 1)):
+        x = _batch(cuda, rng, B, True)
+        monkeypatch.setattr(ttm, "DENSE_EARLY", False)
+        la = a.train_step(x)["loss"]
+        monkeypatch.setattr(ttm, "DENSE_EARLY", True)
+        lb = b.train_step(x)["loss"]
+        assert b._dense_done == set() and all(t.dense.flat.grad is None for t in b.towers)
+        assert torch.equal(la, lb), (i, B)
+        sa, sb = _state(a), _state(b)
+        for k in sa:
+            assert torch.equal(sa[k], sb[k]), (i, B, k)
+    a.optimizer.check_status(cuda)
+    b.optimizer.check_status(cuda)
+
+
 def test_stale_presorted_workspace_is_reported_not_applied(cuda):
     """A presorted sparse apply whose workspace holds another call's sorted
     keys applies nothing and is reported by tt_sparse_status (TTError), the
