@@ -17,6 +17,7 @@ void clear_error();
 // Timing probes armed by tt_probe_arm (no-ops unless armed).
 void probe_begin(int kernel, hipStream_t st);
 void probe_end(int kernel, hipStream_t st);
+int probe_reps(int kernel);  // launches to issue between the armed events (1 unless armed with reps)
 
 #define TT_REQUIRE(cond, ...)                                  \
   do {                                                         \

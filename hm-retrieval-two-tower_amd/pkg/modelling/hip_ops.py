@@ -34,6 +34,7 @@ __all__ = [
     "inbatch_cols",
     "inbatch_fused",
     "probe_arm",
+    "probe_arm_repeat",
     "route_requests",
     "route_owner",
     "bruteforce_build",
@@ -512,6 +513,15 @@ def probe_arm(kernel: int, start: "torch.cuda.Event", stop: "torch.cuda.Event") 
         if not ev.cuda_event:  # torch creates the HIP event on first record
             ev.record()
     check(lib().tt_probe_arm(kernel, start.cuda_event, stop.cuda_event))
+
+
+def probe_arm_repeat(kernel: int, start: "torch.cuda.Event", stop: "torch.cuda.Event", reps: int) -> None:
+    """As probe_arm, and the armed in-batch pass is launched `reps` times back
+    to back between the events (tt_probe_arm_repeat)."""
+    for ev in (start, stop):
+        if not ev.cuda_event:
+            ev.record()
+    check(lib().tt_probe_arm_repeat(kernel, start.cuda_event, stop.cuda_event, int(reps)))
 
 
 def _opt_ptr(t: Optional[torch.Tensor], name: str, n: int) -> Optional[int]:

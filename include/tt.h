@@ -55,6 +55,11 @@ enum {
   TT_PROBE_COUNT = 4
 };
 int tt_probe_arm(int32_t kernel, void* ev_start, void* ev_stop);
+/* As tt_probe_arm, and the armed launch is issued `reps` (>= 1) times back to
+ * back between the two events (in-batch passes only: they are idempotent), so
+ * the per-launch time is (stop - start) / reps without one event pair per
+ * launch.  Other kernels ignore reps. */
+int tt_probe_arm_repeat(int32_t kernel, void* ev_start, void* ev_stop, int32_t reps);
 
 /* ------------------------------------------------------------------------ *
  * K2+K3  Grouped embedding gather + concat.
