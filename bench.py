@@ -484,9 +484,10 @@ def time_index(device, n_queries: int, n_cand: int, k: int, E: int = 128, check:
 def time_index_sharded(device, n_queries: int, n_cand: int, k: int, ws: int, rank: int, E: int = 128,
                        check: int = 256):
     """configs[3] candidate-sharded over the ranks (ShardedBruteForceIndex):
-    rank r owns candidate rows shard_range(N, G, r) and searches every query;
-    one all_to_all hands each query block's per-shard lists to its owner,
-    which merges them (tt_topk_merge).  Strong scaling: Q and N fixed.  QPS =
+    rank r holds only candidate rows shard_range(N, G, r) and computes their
+    exact top-k for every query (tt_bruteforce_search, global indices); one
+    all_to_all hands each query block's per-shard lists to its owner, which
+    merges them (tt_topk_merge).  Strong scaling: Q and N fixed.  QPS =
     Q / max-over-ranks wall time of search_owned, barrier + sync both sides.
     Beside it, `query_sharded`: the same queries split over the ranks against
     replicated candidates (QueryShardedBruteForceIndex, no exchange)."""
@@ -498,7 +499,7 @@ def time_index_sharded(device, n_queries: int, n_cand: int, k: int, ws: int, ran
     g.manual_seed(2)
     Q = torch.relu(torch.randn(n_queries, E, generator=g, device=device))
     Q[::100] = 0.0
-    idx = ShardedBruteForceIndex(k, None, C)
+    idx = ShardedBruteForceIndex.from_full(k, None, C)  # a copy of this rank's rows only
     idx.search_owned(Q)  # warm: code + full-size workspaces, outside the timed region
     torch.cuda.synchronize()
     torch.distributed.barrier()

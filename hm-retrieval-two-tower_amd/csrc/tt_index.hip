@@ -554,95 +554,6 @@ __global__ void tau_min_kernel(const float* __restrict__ tau_split, int S, int64
   tau[q] = t;
 }
 
-// ---- CSR packing of a chunk's lists (candidate-sharded search) -------------
-// n_q = sum of the query's 2S list counts (-1 if one overflowed); offsets are
-// an exclusive scan over the whole call, carried across chunks in *total.
-constexpr int kPackBlock = 1024;
-
-__global__ void __launch_bounds__(kPackBlock) pack_count_kernel(const int* __restrict__ count, int nl, int64_t nq,
-                                                               int* __restrict__ local, int64_t* __restrict__ bsum) {
-  __shared__ int64_t sh[kPackBlock];
-  const int64_t q = blockIdx.x * static_cast<int64_t>(kPackBlock) + threadIdx.x;
-  int64_t n = 0;
-  if (q < nq) {
-    int v = 0;
-    bool ovf = false;
-    for (int j = 0; j < nl; ++j) {
-      const int c = count[q * nl + j];
-      ovf = ovf || c < 0;
-      v += c < 0 ? 0 : c;
-    }
-    n = ovf ? 0 : v;
-    local[q] = ovf ? -1 : v;  // count (offset written below)
-  }
-  sh[threadIdx.x] = n;
-  __syncthreads();
-  for (int off = 1; off < kPackBlock; off <<= 1) {  // inclusive Hillis-Steele scan
-    const int64_t x = threadIdx.x >= off ? sh[threadIdx.x - off] : 0;
-    __syncthreads();
-    sh[threadIdx.x] += x;
-    __syncthreads();
-  }
-  if (q < nq) local[nq + q] = static_cast<int>(sh[threadIdx.x] - n);  // exclusive, within the block
-  if (threadIdx.x == kPackBlock - 1) bsum[blockIdx.x] = sh[threadIdx.x];
-}
-
-__global__ void __launch_bounds__(kPackBlock) pack_scan_kernel(int64_t* __restrict__ bsum, int nb,
-                                                              int64_t* __restrict__ total, int64_t* __restrict__ off_end) {
-  __shared__ int64_t sh[kPackBlock];
-  const int64_t base = *total;
-  int64_t carry = 0;
-  for (int b0 = 0; b0 < nb; b0 += kPackBlock) {
-    const int b = b0 + threadIdx.x;
-    const int64_t v = b < nb ? bsum[b] : 0;
-    sh[threadIdx.x] = v;
-    __syncthreads();
-    for (int off = 1; off < kPackBlock; off <<= 1) {
-      const int64_t x = threadIdx.x >= off ? sh[threadIdx.x - off] : 0;
-      __syncthreads();
-      sh[threadIdx.x] += x;
-      __syncthreads();
-    }
-    if (b < nb) bsum[b] = base + carry + sh[threadIdx.x] - v;  // exclusive block base
-    carry += sh[kPackBlock - 1];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    *total = base + carry;
-    *off_end = base + carry;
-  }
-}
-
-// One wave per query: copies its lists to entries[offset..) (int64 = id << 32
-// | score bits); a query that would pass `cap` is reported with count -1.
-__global__ void __launch_bounds__(256) pack_copy_kernel(const uint2* __restrict__ buf, const int* __restrict__ count,
-                                                       int nl, int lcap, int64_t nq, const int* __restrict__ local,
-                                                       const int64_t* __restrict__ bsum, int64_t cap,
-                                                       int64_t* __restrict__ entries, int* __restrict__ counts_out,
-                                                       int64_t* __restrict__ offsets_out) {
-  const int64_t q = blockIdx.x * 4ll + threadIdx.x / kWave;
-  if (q >= nq) return;
-  const int lane = lane_id();
-  int n = local[q];
-  const int64_t start = bsum[q / kPackBlock] + local[nq + q];
-  if (n >= 0 && start + n > cap) n = -1;
-  if (lane == 0) {
-    counts_out[q] = n;
-    offsets_out[q] = start;
-  }
-  if (n <= 0) return;
-  int64_t dst = start;
-  for (int j = 0; j < nl; ++j) {
-    const int c = count[q * nl + j];
-    const uint2* src = buf + (q * nl + j) * static_cast<int64_t>(lcap);
-    for (int i = lane; i < c; i += kWave) {
-      const uint2 e = src[i];
-      entries[dst + i] = static_cast<int64_t>((static_cast<uint64_t>(e.y) << 32) | e.x);
-    }
-    dst += c;
-  }
-}
-
 // ---- finalize ------------------------------------------------------------
 // Exact score: k-ordered fmaf chain over the fp32 rows (dim real columns).
 // qs is the query row in LDS (broadcast reads); the candidate row is loaded in
@@ -1195,9 +1106,6 @@ struct SearchWs {
   int* fail_list;
   uint2* fb_scratch;
   int* fb_scratch_n;
-  int* pack_local;  // [2][chunk]
-  int64_t* pack_bsum;
-  int64_t* pack_total;
 };
 
 SearchWs carve_search(Carver& cv, int D, const SearchPlan& p, bool lists, bool finalize) {
@@ -1211,9 +1119,6 @@ SearchWs carve_search(Carver& cv, int D, const SearchPlan& p, bool lists, bool f
     w.count = cv.take<int>(nq_pad * p.S * 2);
     w.tau_split = cv.take<float>(nq_pad * p.S);
     w.tau = cv.take<float>(nq_pad);
-    w.pack_local = cv.take<int>(2 * nq_pad);
-    w.pack_bsum = cv.take<int64_t>(ceil_div(nq_pad, kPackBlock));
-    w.pack_total = cv.take<int64_t>(1);
   }
   if (finalize) {
     w.fail_count = cv.take<int>(2 + kFbSlots);
@@ -1373,145 +1278,4 @@ extern "C" int tt_bruteforce_search(const void* index, const float* cand, int64_
     if (int rc = run_finalize(fa, fb, nq, p, st)) return rc;
   }
   return TT_OK;
-}
-
-// ---- candidate-sharded search (ShardedBruteForceIndex) ----------------------
-namespace {
-int check_range(const char* fn, const void* index, int64_t row0, int64_t row1, int32_t dim, int32_t k,
-                int32_t shards, int64_t n_queries) {
-  TT_REQUIRE(index, "%s: NULL index", fn);
-  TT_REQUIRE(row0 >= 0 && row1 > row0 && row1 < (1ll << 31), "%s: bad row range [%lld, %lld)", fn,
-             static_cast<long long>(row0), static_cast<long long>(row1));
-  if (pick_dpad(dim) == 0) return fail(TT_ERR_UNSUPPORTED, "%s: dim=%d > 128", fn, dim);
-  TT_REQUIRE(k >= 1 && k <= 4000, "%s: k=%d out of range", fn, k);
-  TT_REQUIRE(shards >= 1, "%s: shards must be >= 1", fn);
-  TT_REQUIRE(n_queries >= 0, "%s: negative n_queries", fn);
-  return TT_OK;
-}
-}  // namespace
-
-extern "C" size_t tt_bruteforce_shard_workspace_size(int64_t n_queries, int64_t row0, int64_t row1, int32_t dim,
-                                                     int32_t k, int32_t shards) {
-  if (n_queries < 1 || row1 <= row0 || k < 1 || shards < 1 || pick_dpad(dim) == 0) return 0;
-  const SearchPlan p = plan_search(n_queries, row1 - row0, k, shards);
-  Carver cv(nullptr, 0);
-  carve_search(cv, pick_dpad(dim), p, true, false);
-  return cv.used();
-}
-
-extern "C" int64_t tt_bruteforce_shard_capacity(int64_t n_queries, int64_t row0, int64_t row1, int32_t k,
-                                                int32_t shards) {
-  if (n_queries < 1 || row1 <= row0 || k < 1 || shards < 1) return 0;
-  // expected entries per query on this shard ~ (3k + 100) / shards, lower
-  // estimates (the minimum over the shards) keep up to ~2x as many
-  const int64_t per = (6 * static_cast<int64_t>(k) + 200) / shards + 64;
-  const int64_t rows = row1 - row0;
-  return n_queries * (per < rows ? per : rows);
-}
-
-extern "C" int tt_bruteforce_shard_estimate(const void* index, int64_t row0, int64_t row1, const float* queries,
-                                            int64_t ldq, int64_t n_queries, int32_t dim, int32_t k, int32_t shards,
-                                            float* tau, void* workspace, size_t workspace_bytes, tt_stream_t stream) {
-  clear_error();
-  if (int rc = check_range("tt_bruteforce_shard_estimate", index, row0, row1, dim, k, shards, n_queries)) return rc;
-  if (n_queries == 0) return TT_OK;
-  TT_REQUIRE(queries && tau && ldq >= dim, "tt_bruteforce_shard_estimate: NULL queries/tau or bad ldq");
-  const int D = pick_dpad(dim);
-  const SearchPlan p = plan_search(n_queries, row1 - row0, k, shards);
-  Carver cv(workspace, workspace_bytes);
-  SearchWs w = carve_search(cv, D, p, true, false);
-  if (!workspace || cv.used() > workspace_bytes)
-    return fail(TT_ERR_WORKSPACE, "tt_bruteforce_shard_estimate: workspace %zu < required %zu", workspace_bytes,
-                cv.used());
-  hipStream_t st = to_stream(stream);
-  for (int64_t q0 = 0; q0 < n_queries; q0 += p.chunk) {
-    const int64_t nq = (n_queries - q0 < p.chunk) ? n_queries - q0 : p.chunk;
-    if (int rc = run_prep(queries + q0 * ldq, ldq, nq, dim, D, index, w, true, st)) return rc;
-    if (int rc = run_estimate(D, index, row0, row1, nq, p, w, tau + q0, st)) return rc;
-  }
-  return TT_OK;
-}
-
-extern "C" int tt_bruteforce_shard_screen(const void* index, int64_t row0, int64_t row1, const float* queries,
-                                          int64_t ldq, int64_t n_queries, int32_t dim, int32_t k, int32_t shards,
-                                          const float* tau, int64_t* entries, int64_t entries_cap, int32_t* counts,
-                                          int64_t* offsets, void* workspace, size_t workspace_bytes,
-                                          tt_stream_t stream) {
-  clear_error();
-  if (int rc = check_range("tt_bruteforce_shard_screen", index, row0, row1, dim, k, shards, n_queries)) return rc;
-  TT_REQUIRE(offsets, "tt_bruteforce_shard_screen: NULL offsets");
-  hipStream_t st = to_stream(stream);
-  if (n_queries == 0) {
-    TT_CHECK_HIP(hipMemsetAsync(offsets, 0, sizeof(int64_t), st));
-    return TT_OK;
-  }
-  TT_REQUIRE(queries && tau && counts && ldq >= dim, "tt_bruteforce_shard_screen: NULL queries/tau/counts or bad ldq");
-  TT_REQUIRE(entries || entries_cap == 0, "tt_bruteforce_shard_screen: NULL entries");
-  const int D = pick_dpad(dim);
-  const SearchPlan p = plan_search(n_queries, row1 - row0, k, shards);
-  Carver cv(workspace, workspace_bytes);
-  SearchWs w = carve_search(cv, D, p, true, false);
-  if (!workspace || cv.used() > workspace_bytes)
-    return fail(TT_ERR_WORKSPACE, "tt_bruteforce_shard_screen: workspace %zu < required %zu", workspace_bytes,
-                cv.used());
-  TT_CHECK_HIP(hipMemsetAsync(w.pack_total, 0, sizeof(int64_t), st));
-  for (int64_t q0 = 0; q0 < n_queries; q0 += p.chunk) {
-    const int64_t nq = (n_queries - q0 < p.chunk) ? n_queries - q0 : p.chunk;
-    if (int rc = run_prep(queries + q0 * ldq, ldq, nq, dim, D, index, w, true, st)) return rc;
-    if (int rc = run_scan(D, index, row0, row1, nq, p, w, tau + q0, 0u, st)) return rc;
-    const int nl = 2 * p.S;
-    const int nb = static_cast<int>(ceil_div(nq, kPackBlock));
-    hipLaunchKernelGGL(pack_count_kernel, dim3(nb), dim3(kPackBlock), 0, st, w.count, nl, nq, w.pack_local,
-                       w.pack_bsum);
-    TT_CHECK_LAUNCH();
-    hipLaunchKernelGGL(pack_scan_kernel, dim3(1), dim3(kPackBlock), 0, st, w.pack_bsum, nb, w.pack_total,
-                       offsets + n_queries);
-    TT_CHECK_LAUNCH();
-    hipLaunchKernelGGL(pack_copy_kernel, dim3(ceil_div(nq, 4)), dim3(256), 0, st, w.buf, w.count, nl, p.cap, nq,
-                       w.pack_local, w.pack_bsum, entries_cap, entries, counts + q0, offsets + q0);
-    TT_CHECK_LAUNCH();
-  }
-  return TT_OK;
-}
-
-extern "C" size_t tt_bruteforce_finalize_workspace_size(int64_t n_queries, int32_t dim, int32_t k) {
-  if (n_queries < 1 || k < 1 || pick_dpad(dim) == 0) return 0;
-  SearchPlan p = plan_search(n_queries, 1 << 20, k, 1);
-  p.chunk = round_up(n_queries, kQPerWG);
-  Carver cv(nullptr, 0);
-  carve_search(cv, pick_dpad(dim), p, false, true);
-  return cv.used();
-}
-
-extern "C" int tt_bruteforce_finalize(const void* index, const float* cand, int64_t ldc, int64_t n_cand, int32_t dim,
-                                      const float* queries, int64_t ldq, int64_t n_queries, int32_t k,
-                                      int32_t num_sources, const int64_t* entries, const int32_t* counts,
-                                      const int64_t* offsets, const float* tau, float* out_scores, int32_t* out_idx,
-                                      void* workspace, size_t workspace_bytes, tt_stream_t stream) {
-  clear_error();
-  TT_REQUIRE(index && cand, "tt_bruteforce_finalize: NULL index/cand");
-  TT_REQUIRE(n_cand >= 1 && dim >= 1 && ldc >= dim && ldq >= dim, "tt_bruteforce_finalize: bad shapes");
-  if (pick_dpad(dim) == 0) return fail(TT_ERR_UNSUPPORTED, "tt_bruteforce_finalize: dim=%d > 128", dim);
-  TT_REQUIRE(k >= 1 && k <= n_cand && k <= 4000, "tt_bruteforce_finalize: bad k=%d", k);
-  TT_REQUIRE(num_sources >= 1, "tt_bruteforce_finalize: num_sources must be >= 1");
-  TT_REQUIRE(n_queries >= 0, "tt_bruteforce_finalize: negative n_queries");
-  if (n_queries == 0) return TT_OK;
-  TT_REQUIRE(queries && counts && offsets && tau && out_scores && out_idx, "tt_bruteforce_finalize: NULL argument");
-  const int D = pick_dpad(dim);
-  SearchPlan p = plan_search(n_queries, 1 << 20, k, 1);
-  p.chunk = round_up(n_queries, kQPerWG);
-  Carver cv(workspace, workspace_bytes);
-  SearchWs w = carve_search(cv, D, p, false, true);
-  if (!workspace || cv.used() > workspace_bytes)
-    return fail(TT_ERR_WORKSPACE, "tt_bruteforce_finalize: workspace %zu < required %zu", workspace_bytes, cv.used());
-  hipStream_t st = to_stream(stream);
-  const int vec4 = is_vec4(cand, ldc, dim) ? 1 : 0;
-  TT_CHECK_HIP(hipMemsetAsync(w.fail_count, 0, (2 + kFbSlots) * sizeof(int), st));
-  if (int rc = run_prep(queries, ldq, n_queries, dim, D, index, w, false, st)) return rc;
-  Lists ls{reinterpret_cast<const uint2*>(entries), counts, tau, num_sources, 0, offsets, 1, n_queries};
-  FinalArgs fa{queries, ldq, cand, ldc, n_cand, 0, 0, dim, k, p.L, p.P, vec4,
-               n_queries, w.qflags, w.qmarg, ls, out_scores, out_idx, w.fail_count, w.fail_list};
-  FallbackArgs fb{queries, ldq, cand, ldc, n_cand, 0, dim, k, p.L, p.P, p.parts, vec4,
-                  w.fail_count, w.fail_list, w.fail_count + 1, w.fb_scratch, w.fb_scratch_n, out_scores, out_idx};
-  return run_finalize(fa, fb, n_queries, p, st);
 }

@@ -3,11 +3,12 @@
 SURVEY §8e.  Two pieces the reference's call sites shard naturally:
 
 * ShardedBruteForceIndex — BruteForceIndex with the candidate matrix
-  row-sharded over the ranks.  Each rank scores the (replicated) queries
-  against its shard with tt_bruteforce_search, indices offset by the shard's
-  first global row; the per-shard sorted top-k lists are all-gathered and
-  merged with tt_topk_merge (score desc, global index asc), which equals
-  tf.math.top_k over the unsharded scores (brute_force.py:76-81).
+  row-sharded over the ranks: each rank holds only its block of rows and
+  computes the exact top-k of its shard (tt_bruteforce_search, indices offset
+  by the block's first global row); the per-shard lists of each query block
+  go to its owner (all_to_all) and are merged with tt_topk_merge (score desc,
+  global index asc), which equals tf.math.top_k over the unsharded scores
+  (brute_force.py:76-81).
 
 * DataParallelTrainStep — the reference's train_step
   (two_tower_model.py:94-130) replicated per GPU the way a data-parallel
@@ -35,7 +36,7 @@ import torch.distributed as dist
 
 logger = logging.getLogger(__name__)
 
-__all__ = ["IndexOps", "ShardIndexOps", "BatchComm", "ShardedBruteForceIndex", "QueryShardedBruteForceIndex", "DataParallelTrainStep", "shard_range", "all_gather_cat",
+__all__ = ["IndexOps", "BatchComm", "ShardedBruteForceIndex", "QueryShardedBruteForceIndex", "DataParallelTrainStep", "shard_range", "all_gather_cat",
            "EmbeddingOps", "ShardedTables", "ShardedTrainStep"]
 
 
@@ -61,6 +62,10 @@ def shard_range(n: int, world: int, rank: int) -> Tuple[int, int]:
 
 @dataclass
 class IndexOps:
+    """Kernels of the sharded indices (tt.h: tt_bruteforce_build,
+    tt_bruteforce_search with a global index offset, tt_topk_merge).
+    Injectable so the orchestration below runs on CPU over gloo in the tests
+    (oracle.bruteforce_topk / topk_merge); the defaults are libtt."""
     build: Callable[[torch.Tensor], Any]
     search: Callable[..., Tuple[torch.Tensor, torch.Tensor]]
     merge: Callable[[torch.Tensor, torch.Tensor, int], Tuple[torch.Tensor, torch.Tensor]]
@@ -74,46 +79,9 @@ class IndexOps:
                         hip_ops.topk_merge)
 
 
-@dataclass
-class ShardIndexOps:
-    """Kernels of the candidate-sharded search (tt.h: tt_bruteforce_build,
-    tt_bruteforce_shard_estimate / _screen, tt_bruteforce_finalize).
-    Injectable so the orchestration below runs on CPU over gloo in the tests
-    (oracle.shard_*); the defaults are libtt."""
-    build: Callable[[torch.Tensor], Any]
-    estimate: Callable[..., torch.Tensor]
-    screen: Callable[..., Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]
-    finalize: Callable[..., Tuple[torch.Tensor, torch.Tensor]]
-
-    @staticmethod
-    def hip() -> "ShardIndexOps":
-        from pkg.modelling import hip_ops
-
-        return ShardIndexOps(hip_ops.bruteforce_build, hip_ops.bruteforce_shard_estimate,
-                             hip_ops.bruteforce_shard_screen, hip_ops.bruteforce_finalize)
-
-
 def _staged(group) -> bool:
     """gloo moves host tensors only: device tensors go through the host."""
     return dist.get_backend(group) == "gloo"
-
-
-def _all_reduce_min(t: torch.Tensor, group) -> None:
-    if _staged(group) and t.is_cuda:
-        h = t.cpu()
-        dist.all_reduce(h, op=dist.ReduceOp.MIN, group=group)
-        t.copy_(h)
-    else:
-        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
-
-
-def _a2a_any(out: torch.Tensor, inp: torch.Tensor, out_splits: List[int], in_splits: List[int], group) -> torch.Tensor:
-    if _staged(group) and inp.is_cuda:
-        h = torch.empty(out.shape, dtype=out.dtype)
-        dist.all_to_all_single(h, inp.cpu(), out_splits, in_splits, group=group)
-        out.copy_(h)
-        return out
-    return _a2a(out, inp, out_splits, in_splits, group)
 
 
 def _all_gather_any(t: torch.Tensor, group) -> torch.Tensor:
@@ -137,27 +105,31 @@ def _gather_query_blocks(s: torch.Tensor, i: torch.Tensor, Q: int, world: int, g
             torch.cat([all_i[r, :e - b] for r, (b, e) in enumerate(blocks)]))
 
 
+# index of a padding entry of a shard with fewer than k rows: sorts after
+# every real entry, -inf scores included (tt_topk_merge's (score, -index) key)
+PAD_INDEX = 0x7FFFFFFF
+
+
 class ShardedBruteForceIndex:
     """
-    Candidate-sharded brute-force index (SURVEY §8e, north star: "shards the
-    candidate matrix across the 8 GPUs").  BruteForceIndex.call
-    (brute_force.py:76-83) with the SCORING of the candidate rows split over
-    the ranks: rank g screens rows shard_range(N, G, g) for every query.
+    Candidate-sharded brute-force index (SURVEY §8e; north star: "shards the
+    candidate matrix across the 8 GPUs ... merges per-shard top-K").
+    BruteForceIndex.call (brute_force.py:75-83: matmul -> top_k -> gather)
+    with the candidate matrix row-sharded: rank g holds ONLY its contiguous
+    block C[b_g:e_g] (fp32 rows + their bf16 screening image), the blocks in
+    rank order.
 
-    Protocol per search (tt.h, tt_bruteforce_shard_*):
-      1. each rank estimates, per query, the score at rank ~(3k+100)/G of its
-         rows; one all_reduce(MIN) of those [Q] floats gives a common tau;
-      2. each rank keeps its screened scores s~ > tau[q] (bf16 MFMA screen),
-         packed per query (CSR);
-      3. all_to_all: the lists of query block r (shard_range(Q, G, r)) go to
-         rank r — sizes first, then the entries (Q·~(3k+100)·8 B in total);
-      4. the owner certifies each query against the bf16 error bound,
-         rescores the surviving candidates with the exact fp32 chain and
-         returns the exact top-k (or scans the query exactly).
-    The result equals one top_k over all candidates bit for bit.  Every rank
-    keeps the full fp32 candidate matrix (105,542 x 128 = 54 MB of 288 GB):
-    the exact rescoring of step 4 may need any row; only the scoring is
-    sharded.
+    Per search (queries replicated on every rank):
+      1. tt_bruteforce_search on the local rows with index_offset = b_g: the
+         exact top-k of the shard, indices global (ties -> lower index);
+      2. all_to_all: the lists of query block r (shard_range(Q, G, r)) go to
+         rank r — Q·k·8 B sent per rank, 1/G of it kept;
+      3. tt_topk_merge of the G lists -> the owner's exact global top-k.
+    Exact: a candidate of the global top-k outranks every other candidate of
+    its own shard that it beats globally, so it is in its shard's top-k; the
+    merge orders by the same (score desc, index asc) key top_k uses, and the
+    scores are the same fp32 chains wherever a row lives.  search() then
+    all-gathers the owners' blocks so every rank holds the whole answer.
 
     Parameters
     ----------
@@ -165,69 +137,81 @@ class ShardedBruteForceIndex:
         Results per query.
     query_model: callable
         Query feature dict -> [B, E] embeddings (replicated on every rank).
-    candidates: [N, E] tensor
-        The whole candidate matrix (replicated); this rank scores rows
-        shard_range(N, world, rank).
-    identifiers: optional identifiers of the N rows.
+    candidates: [n_g, E] tensor
+        THIS rank's rows; the global matrix is the rank-ordered concatenation
+        (ShardedBruteForceIndex.from_full slices it from a full matrix).
+    identifiers: optional identifiers of all N rows (small; replicated).
     """
 
     def __init__(self, k: int, query_model, candidates: torch.Tensor, identifiers=None, group=None,
-                 ops: Optional[ShardIndexOps] = None):
+                 ops: Optional[IndexOps] = None):
         self.k = int(k)
         self.query_model = query_model
         self.group = group
-        self.ops = ops or ShardIndexOps.hip()
+        self.ops = ops or IndexOps.hip()
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        self.cand = candidates.contiguous()
-        self.num_candidates = int(self.cand.shape[0])
+        self.shard = candidates.contiguous()
+        n = int(self.shard.shape[0])
+        sizes = _all_gather_any(torch.tensor([n], dtype=torch.int64, device=self.shard.device), group)
+        self.sizes = [int(x) for x in sizes.reshape(-1).cpu().tolist()]
+        self.offset = sum(self.sizes[:self.rank])
+        self.num_candidates = sum(self.sizes)
+        self.rows = (self.offset, self.offset + n)
+        if min(self.sizes) < 1:
+            raise ValueError(f"every rank needs >= 1 candidate row, got shard sizes {self.sizes}")
         if self.num_candidates < self.k:
             raise ValueError(f"need >= k={self.k} candidates, got {self.num_candidates}")
-        self.rows = shard_range(self.num_candidates, self.world, self.rank)
-        if self.rows[1] <= self.rows[0]:
-            raise ValueError(f"{self.world} shards for {self.num_candidates} candidates leave rank {self.rank} empty")
-        self.image = self.ops.build(self.cand)
+        if self.num_candidates >= 2 ** 31 - 64:
+            raise ValueError("global candidate indices must fit int32")
+        self.image = self.ops.build(self.shard)
         self.identifiers = identifiers
+
+    @classmethod
+    def from_full(cls, k: int, query_model, candidates: torch.Tensor, identifiers=None, group=None,
+                  ops: Optional[IndexOps] = None) -> "ShardedBruteForceIndex":
+        """This rank's block shard_range(N, G, rank) copied out of a full
+        matrix (which the caller may then free)."""
+        b, e = shard_range(int(candidates.shape[0]), dist.get_world_size(group), dist.get_rank(group))
+        return cls(k, query_model, candidates[b:e].clone(), identifiers, group, ops)
+
+    def search_shard(self, query_embeddings: torch.Tensor, k: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """This shard's exact top-k of every query, global indices, padded
+        with (-inf, PAD_INDEX) past its row count: ([Q, k], [Q, k] int32)."""
+        k = k or self.k
+        if k > self.num_candidates:
+            raise ValueError(f"k={k} exceeds the number of candidates {self.num_candidates}")
+        q = query_embeddings.contiguous()
+        kl = min(k, int(self.shard.shape[0]))
+        s, i = self.ops.search(self.image, self.shard, q, kl, self.offset)
+        if kl < k:
+            ps = torch.full((q.shape[0], k), float("-inf"), dtype=s.dtype, device=s.device)
+            pi = torch.full((q.shape[0], k), PAD_INDEX, dtype=i.dtype, device=i.device)
+            ps[:, :kl], pi[:, :kl] = s, i
+            s, i = ps, pi
+        return s, i
 
     def search_owned(self, query_embeddings: torch.Tensor, k: Optional[int] = None
                      ) -> Tuple[Tuple[int, int], torch.Tensor, torch.Tensor]:
         """Exact global top-k of this rank's query block: ((begin, end),
         scores [end-begin, k], indices [end-begin, k] int32)."""
         k = k or self.k
-        if k > self.num_candidates:
-            raise ValueError(f"k={k} exceeds the number of candidates {self.num_candidates}")
-        q = query_embeddings.contiguous()
-        Q, G = int(q.shape[0]), self.world
-        r0, r1 = self.rows
-        tau = self.ops.estimate(self.image, q, r0, r1, k, G)
-        if G > 1:
-            _all_reduce_min(tau, self.group)
-        entries, counts, offsets = self.ops.screen(self.image, q, r0, r1, k, G, tau)
+        Q, G = int(query_embeddings.shape[0]), self.world
+        s, i = self.search_shard(query_embeddings, k)
         blocks = [shard_range(Q, G, r) for r in range(G)]
-        starts = torch.tensor([b for b, _ in blocks] + [Q], dtype=torch.int64, device=offsets.device)
-        cap = int(entries.shape[0])
-        bnd = [min(int(x), cap) for x in offsets[starts].cpu().tolist()]  # the search's one host sync
-        in_splits = [bnd[r + 1] - bnd[r] for r in range(G)]
         mb, me = blocks[self.rank]
+        if G == 1:
+            return (mb, me), s, i
         nb = me - mb
-        if G > 1:
-            sz = torch.tensor(in_splits, dtype=torch.int64, device=entries.device)
-            rsz = torch.empty_like(sz)
-            _a2a_any(rsz, sz, [1] * G, [1] * G, self.group)
-            out_splits = [int(x) for x in rsz.cpu().tolist()]
-            recv = torch.empty(sum(out_splits), dtype=torch.int64, device=entries.device)
-            _a2a_any(recv, entries[:bnd[G]], out_splits, in_splits, self.group)
-            rc = torch.empty(G * nb, dtype=torch.int32, device=counts.device)
-            _a2a_any(rc, counts, [nb] * G, [e - b for b, e in blocks], self.group)
-            rc = rc.view(G, nb)
-        else:
-            out_splits, recv, rc = in_splits, entries, counts.view(1, Q)
-        base = torch.tensor([0] + list(np.cumsum(out_splits[:-1])), dtype=torch.int64, device=rc.device)
-        cl = rc.clamp(min=0).to(torch.int64)
-        off = (torch.cumsum(cl, 1) - cl + base.view(G, 1)).contiguous()
-        s, i = self.ops.finalize(self.image, self.cand, q[mb:me].contiguous(), k, recv, rc.contiguous(), off,
-                                 tau[mb:me].contiguous())
-        return (mb, me), s, i
+        in_splits = [(e - b) * k for b, e in blocks]
+        rs = torch.empty(G * nb * k, dtype=s.dtype, device=s.device)
+        ri = torch.empty(G * nb * k, dtype=i.dtype, device=i.device)
+        _a2a(rs, s.reshape(-1), [nb * k] * G, in_splits, self.group)
+        _a2a(ri, i.reshape(-1), [nb * k] * G, in_splits, self.group)
+        if nb == 0:
+            return (mb, me), s[:0], i[:0]
+        ms, mi = self.ops.merge(rs.view(G, nb, k), ri.view(G, nb, k), k)
+        return (mb, me), ms, mi
 
     def search(self, query_embeddings: torch.Tensor, k: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
         """Global (scores [Q,k], indices [Q,k]) on every rank (blocks all-gathered)."""
@@ -648,8 +632,8 @@ class _ShardedGatherFn(torch.autograd.Function):
 class ShardedTrainStep:
     """
     Data-parallel train step with the large embedding tables row-sharded
-    (ShardedTables) and the small ones replicated.  Per-replica in-batch
-    negatives, as DataParallelTrainStep.  Sparse work per rank stays ~constant
+    (ShardedTables) and the small ones replicated; in-batch negatives from
+    the global batch by default (below).  Sparse work per rank stays ~constant
     as ranks are added (each owner updates only its rows), unlike gathering
     every replica's sparse gradients.
 
@@ -679,16 +663,17 @@ class ShardedTrainStep:
     query embeddings and their lse are all-gathered and the cols pass scores
     all of them against this rank's candidates (dC of its columns).  The
     loss and every gradient are those of the global batch (tests:
-    test_distributed_gloo global loss, test_distributed_gpu step).  With
-    world > 1 that middle runs eagerly by default (its collectives are not
-    captured into the hipGraph; TT_GRAPH_COLLECTIVES=1 opts in).  False keeps
-    per-replica negatives (a labelled variant).
+    test_distributed_gloo global loss, test_distributed_gpu step).  This is
+    the default.  With world > 1 that middle runs eagerly unless its RCCL
+    collectives are captured into the hipGraph (TT_GRAPH_COLLECTIVES=1).
+    global_negatives=False keeps per-replica negatives (a labelled variant:
+    each rank's loss over its own batch).
 
     Adagrad (the reference's optimizer, main.py:100-101) only.
     """
 
     def __init__(self, model, shard_min_rows: int = 100_000, group=None, ops: Optional[EmbeddingOps] = None,
-                 use_graph: bool = True, global_negatives: bool = False):
+                 use_graph: bool = True, global_negatives: bool = True):
         from pkg.modelling.optimizer_factory import Adagrad
 
         opt = model.optimizer
@@ -975,6 +960,15 @@ class ShardedTrainStep:
             self._finish_routes(lambda k, step: step < now or len(upcoming) < 2)
         self._tick("prefetch", tm)
         return {"loss": loss}
+
+    def check_status(self) -> None:
+        """Raise if a shard's sparse apply since the last check refused keys
+        that were not its call's (tt_sparse_status); one stream sync.  Call it
+        once per epoch, like TwoTowerModel.fit does."""
+        if self.model.device.type == "cuda":
+            from pkg.modelling import hip_ops
+
+            hip_ops.sparse_status(self.model.device, "sparse", "")
 
     def _finish_routes(self, which) -> None:
         keep = []

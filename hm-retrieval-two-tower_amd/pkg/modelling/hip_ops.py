@@ -39,9 +39,6 @@ __all__ = [
     "route_owner",
     "bruteforce_build",
     "bruteforce_search",
-    "bruteforce_shard_estimate",
-    "bruteforce_shard_screen",
-    "bruteforce_finalize",
     "topk_merge",
     "recall_hits",
     "Workspace",
@@ -102,6 +99,17 @@ class Workspace:
     @classmethod
     def clear(cls) -> None:
         cls._bufs.clear()
+
+    @classmethod
+    def snapshot(cls) -> Dict[Tuple[int, str], int]:
+        """{key: device address} of every buffer now allocated.  A captured
+        hipGraph holds these addresses: it may be replayed only while
+        `unchanged(snapshot)` (no buffer it may use was regrown or cleared)."""
+        return {k: v.data_ptr() for k, v in cls._bufs.items()}
+
+    @classmethod
+    def unchanged(cls, snap: Dict[Tuple[int, str], int]) -> bool:
+        return all(k in cls._bufs and cls._bufs[k].data_ptr() == p for k, p in snap.items())
 
     class scope:  # noqa: N801 - context manager named like the operation
         def __init__(self, name: str):
@@ -626,83 +634,6 @@ def bruteforce_search(index: torch.Tensor, cand: torch.Tensor, queries: torch.Te
     check(L.tt_bruteforce_search(index.data_ptr(), cand.data_ptr(), ldc, n, d, queries.data_ptr(), ldq, nq, k,
                                  index_offset, out_s.data_ptr(), out_i.data_ptr(), ws.data_ptr(), ws.numel(),
                                  _stream()))
-    return out_s, out_i
-
-
-def bruteforce_shard_estimate(index: torch.Tensor, queries: torch.Tensor, row0: int, row1: int, k: int,
-                              shards: int) -> torch.Tensor:
-    """Candidate-sharded search step 1 (tt.h): per-query estimate tau [Q] of
-    the score at rank ~(3k+100)/shards among image rows [row0, row1)."""
-    _req(index, "index", torch.uint8, 1)
-    _req(queries, "queries", torch.float32, 2)
-    ldq = _row_major(queries, "queries")
-    nq, d = queries.shape
-    L = lib()
-    tau = torch.empty(nq, dtype=torch.float32, device=queries.device)
-    if nq == 0:
-        return tau
-    ws = Workspace.get(L.tt_bruteforce_shard_workspace_size(nq, row0, row1, d, k, shards), queries.device,
-                       "bruteforce_shard")
-    check(L.tt_bruteforce_shard_estimate(index.data_ptr(), row0, row1, queries.data_ptr(), ldq, nq, d, k, shards,
-                                         tau.data_ptr(), ws.data_ptr(), ws.numel(), _stream()))
-    return tau
-
-
-def bruteforce_shard_screen(index: torch.Tensor, queries: torch.Tensor, row0: int, row1: int, k: int, shards: int,
-                            tau: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-    """Step 2: (entries int64 [cap] = global row << 32 | screened-score bits,
-    counts int32 [Q] (-1 dropped), offsets int64 [Q+1]) of the scores > tau."""
-    _req(index, "index", torch.uint8, 1)
-    _req(queries, "queries", torch.float32, 2)
-    _req(tau, "tau", torch.float32, 1)
-    ldq = _row_major(queries, "queries")
-    nq, d = queries.shape
-    if tau.shape[0] != nq or not tau.is_contiguous():
-        raise ValueError("tau must be a contiguous [Q] tensor")
-    L = lib()
-    cap = max(int(L.tt_bruteforce_shard_capacity(max(nq, 1), row0, row1, k, shards)), 1)
-    entries = torch.empty(cap, dtype=torch.int64, device=queries.device)
-    counts = torch.empty(nq, dtype=torch.int32, device=queries.device)
-    offsets = torch.empty(nq + 1, dtype=torch.int64, device=queries.device)
-    ws = Workspace.get(L.tt_bruteforce_shard_workspace_size(max(nq, 1), row0, row1, d, k, shards), queries.device,
-                       "bruteforce_shard")
-    check(L.tt_bruteforce_shard_screen(index.data_ptr(), row0, row1, queries.data_ptr(), ldq, nq, d, k, shards,
-                                       tau.data_ptr(), entries.data_ptr(), cap, counts.data_ptr(), offsets.data_ptr(),
-                                       ws.data_ptr(), ws.numel(), _stream()))
-    return entries, counts, offsets
-
-
-def bruteforce_finalize(index: torch.Tensor, cand: torch.Tensor, queries: torch.Tensor, k: int,
-                        entries: torch.Tensor, counts: torch.Tensor, offsets: torch.Tensor,
-                        tau: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Step 4 (owner): exact top-k of `queries` from the screened lists of
-    G sources: counts int32 [G, Q], offsets int64 [G, Q] into entries."""
-    _req(index, "index", torch.uint8, 1)
-    _req(cand, "cand", torch.float32, 2)
-    _req(queries, "queries", torch.float32, 2)
-    _req(entries, "entries", torch.int64, 1)
-    _req(counts, "counts", torch.int32, 2)
-    _req(offsets, "offsets", torch.int64, 2)
-    _req(tau, "tau", torch.float32, 1)
-    ldc, ldq = _row_major(cand, "cand"), _row_major(queries, "queries")
-    n, d = cand.shape
-    nq = queries.shape[0]
-    G = counts.shape[0]
-    if tuple(counts.shape) != (G, nq) or tuple(offsets.shape) != (G, nq) or tau.shape[0] != nq:
-        raise ValueError("counts/offsets must be [G, Q] and tau [Q]")
-    if not (counts.is_contiguous() and offsets.is_contiguous() and tau.is_contiguous()):
-        raise ValueError("counts/offsets/tau must be contiguous")
-    if k > n:
-        raise ValueError(f"k={k} exceeds the number of candidates {n}")
-    L = lib()
-    out_s = torch.empty(nq, k, dtype=torch.float32, device=queries.device)
-    out_i = torch.empty(nq, k, dtype=torch.int32, device=queries.device)
-    if nq == 0:
-        return out_s, out_i
-    ws = Workspace.get(L.tt_bruteforce_finalize_workspace_size(nq, d, k), queries.device, "bruteforce_final")
-    check(L.tt_bruteforce_finalize(index.data_ptr(), cand.data_ptr(), ldc, n, d, queries.data_ptr(), ldq, nq, k, G,
-                                   entries.data_ptr(), counts.data_ptr(), offsets.data_ptr(), tau.data_ptr(),
-                                   out_s.data_ptr(), out_i.data_ptr(), ws.data_ptr(), ws.numel(), _stream()))
     return out_s, out_i
 
 

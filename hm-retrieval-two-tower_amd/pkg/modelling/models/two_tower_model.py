@@ -183,6 +183,15 @@ class TwoTowerModel(AbstractKerasModel):
             self.loss = loss
         if optimizer is not None:
             self.optimizer = optimizer
+            # a cached fit graph holds the old optimizer's slot addresses
+            self._device_fit_graph = None
+
+    def check_optimizer_status(self) -> None:
+        """Raise if a sparse apply since the last check refused stale or
+        foreign keys (tt_sparse_status; one stream sync)."""
+        check = getattr(self.optimizer, "check_status", None)
+        if check is not None and self.device.type == "cuda":
+            check(self.device)
 
     def train_step(self, data: Dict[str, Any]) -> Dict[str, torch.Tensor]:
         """One optimisation step on a batch of positive pairs; returns the
@@ -277,6 +286,7 @@ class TwoTowerModel(AbstractKerasModel):
                     out = self.train_step(batch)
                 total += out["loss"].double()
                 n += 1
+            self.check_optimizer_status()
             mean = float(total.item()) / max(n, 1)
             history["loss"].append(mean)
             logger.info(f"epoch {epoch + 1}/{epochs}: loss {mean:.6f} over {n} batches")
@@ -293,8 +303,8 @@ class TwoTowerModel(AbstractKerasModel):
         B, nfull = int(ds.batch_size), ds.full_batches
         rem = ds.num_rows - nfull * B
         graphed = getattr(self, "_device_fit_graph", None)
-        if graphed is not None and (graphed.source is not ds or graphed.model is not self):
-            graphed = None
+        if graphed is not None and not graphed.reusable(self, ds):
+            graphed = self._device_fit_graph = None
         for epoch in range(epochs):
             ds.begin_epoch()
             todo = nfull
@@ -311,6 +321,7 @@ class TwoTowerModel(AbstractKerasModel):
             if rem:
                 total += self.train_step(ds.view(ds.take(rem)))["loss"].double()
             ds.check_status()
+            self.check_optimizer_status()
             n = nfull + (1 if rem else 0)
             mean = float(total.item()) / max(n, 1)
             history["loss"].append(mean)
@@ -423,6 +434,17 @@ class GraphedTrainStep:
         # dataset's order prefetch) may query events while this thread captures
         with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self.out = self._step()
+        # what the captured pointers refer to (see reusable)
+        self.optimizer = model.optimizer
+        self.ws_snapshot = hip_ops.Workspace.snapshot()
+
+    def reusable(self, model: "TwoTowerModel", source=None) -> bool:
+        """True while a replay still trains `model` from `source` through the
+        buffers it was captured with: same optimizer object (its slots), no
+        libtt workspace regrown or cleared since the capture."""
+        return (self.model is model and self.source is source and self.optimizer is model.optimizer
+                and (source is None or int(source.batch_size) == self.batch_size)
+                and hip_ops.Workspace.unchanged(self.ws_snapshot))
 
     def _step(self) -> Dict[str, torch.Tensor]:
         if self.source is not None:

@@ -42,15 +42,21 @@ def _arrow_strings(values) -> pa.Array:
             arr = pa.array(a)
         elif a.dtype.kind in "iu":
             arr = pa.array(a).cast(pa.string())
-        else:
+        elif a.dtype.kind == "O":
             try:  # object arrays of str / bytes convert without a Python loop
                 arr = pa.array(a, from_pandas=False)
             except (pa.ArrowInvalid, pa.ArrowTypeError):
                 arr = None
-            if arr is None or not (pa.types.is_string(arr.type) or pa.types.is_large_string(arr.type)
-                                   or pa.types.is_binary(arr.type) or pa.types.is_large_binary(arr.type)):
+            if arr is None or arr.null_count or not (
+                    pa.types.is_string(arr.type) or pa.types.is_large_string(arr.type)
+                    or pa.types.is_binary(arr.type) or pa.types.is_large_binary(arr.type)):
+                # per element str(): None -> "None", as a str()-cast column reads
                 arr = pa.array([v.decode() if isinstance(v, bytes) else str(v) for v in a.tolist()],
                                type=pa.large_string())
+        else:
+            # floats / bools / other numpy scalars: str() of the numpy scalar
+            # itself (str(np.float32(0.1)) is "0.1"; tolist() would widen it)
+            arr = pa.array([str(v) for v in a], type=pa.large_string())
     if isinstance(arr, pa.ChunkedArray):
         arr = arr.combine_chunks()
     if pa.types.is_integer(arr.type):

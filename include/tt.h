@@ -363,56 +363,6 @@ int tt_bruteforce_search(const void* index, const float* cand, int64_t ldc,
                          int32_t* out_idx, void* workspace,
                          size_t workspace_bytes, tt_stream_t stream);
 
-/* Candidate-sharded search (ShardedBruteForceIndex).  Replaces
- * the same BruteForceIndex.call (brute_force.py:76-83) with the candidate
- * rows split over G ranks.  Every rank holds the full index image and the
- * fp32 candidates (the exact finalize may need any row); rank g SCORES only
- * rows [row0, row1):
- *  1. tt_bruteforce_shard_estimate: per query an estimate tau of the score at
- *     rank ~(3k+100)/G of the rows (NOT a bound); the caller all-reduces MIN
- *     over the ranks, so every rank screens with the same tau[q].
- *  2. tt_bruteforce_shard_screen: keeps s~ > tau[q] as int64 entries
- *     (global row << 32 | fp32 screened-score bits), packed per query in
- *     query order: counts[q] (-1: dropped, the owner falls back to an exact
- *     scan), offsets[q] into entries, offsets[n_queries] = total.  A query
- *     that would pass entries_cap is dropped (size with
- *     tt_bruteforce_shard_capacity).
- *  3. the caller moves each query block's entries to its owner rank
- *     (all_to_all), which calls
- *  4. tt_bruteforce_finalize on its queries with the lists of num_sources
- *     ranks: counts / offsets laid out [num_sources][n_queries] (offsets
- *     index `entries`); certifies the screen (the k-th largest screened
- *     score against tau), rescores with the exact fp32 chain and returns the
- *     exact top-k — bit-identical to tt_bruteforce_search over all rows. */
-size_t tt_bruteforce_shard_workspace_size(int64_t n_queries, int64_t row0,
-                                          int64_t row1, int32_t dim, int32_t k,
-                                          int32_t shards);
-int64_t tt_bruteforce_shard_capacity(int64_t n_queries, int64_t row0,
-                                     int64_t row1, int32_t k, int32_t shards);
-int tt_bruteforce_shard_estimate(const void* index, int64_t row0, int64_t row1,
-                                 const float* queries, int64_t ldq,
-                                 int64_t n_queries, int32_t dim, int32_t k,
-                                 int32_t shards, float* tau, void* workspace,
-                                 size_t workspace_bytes, tt_stream_t stream);
-int tt_bruteforce_shard_screen(const void* index, int64_t row0, int64_t row1,
-                               const float* queries, int64_t ldq,
-                               int64_t n_queries, int32_t dim, int32_t k,
-                               int32_t shards, const float* tau,
-                               int64_t* entries, int64_t entries_cap,
-                               int32_t* counts, int64_t* offsets,
-                               void* workspace, size_t workspace_bytes,
-                               tt_stream_t stream);
-size_t tt_bruteforce_finalize_workspace_size(int64_t n_queries, int32_t dim,
-                                             int32_t k);
-int tt_bruteforce_finalize(const void* index, const float* cand, int64_t ldc,
-                           int64_t n_cand, int32_t dim, const float* queries,
-                           int64_t ldq, int64_t n_queries, int32_t k,
-                           int32_t num_sources, const int64_t* entries,
-                           const int32_t* counts, const int64_t* offsets,
-                           const float* tau, float* out_scores,
-                           int32_t* out_idx, void* workspace,
-                           size_t workspace_bytes, tt_stream_t stream);
-
 /* Merge `num_lists` per-shard sorted top-k_in lists laid out
  * [num_lists][n_queries][k_in] into the global top-k_out with the same
  * order (score descending, index ascending on ties). */

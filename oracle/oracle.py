@@ -283,89 +283,6 @@ def topk_merge(scores: np.ndarray, idx: np.ndarray, k: int) -> Tuple[np.ndarray,
 
 
 # ---------------------------------------------------------------------------
-# Candidate-sharded search protocol (tt.h tt_bruteforce_shard_* /
-# tt_bruteforce_finalize, csrc/tt_index.hip): the same answer as
-# BruteForceIndex.call over all rows (brute_force.py:76-83).  Screened
-# scores here are bf16 products summed in fp64 and rounded once (the GPU's
-# MFMA order differs), both within the screen bound of the exact chain.
-SCREEN_EPS = np.float32(0.0087890625)  # 2^-7 + 2^-10 (tt_index.hip kEps)
-SCREEN_TINY = np.float32(1e-30)
-
-
-def bf16_round(x: np.ndarray) -> np.ndarray:
-    """Round-to-nearest-even to bf16, returned as float32 (finite inputs)."""
-    u = _f32(x).view(np.uint32).astype(np.uint64)
-    u = (u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000
-    return u.astype(np.uint32).view(np.float32)
-
-
-def screened_scores(q: np.ndarray, c: np.ndarray) -> np.ndarray:
-    return (bf16_round(q).astype(np.float64) @ bf16_round(c).astype(np.float64).T).astype(np.float32)
-
-
-def shard_estimate(q: np.ndarray, c_rows: np.ndarray, k: int, shards: int) -> np.ndarray:
-    """An estimate (any value is correct, its quality only sets the list
-    size): the screened score at rank ceil((3k+100)/shards) of the rows."""
-    s = screened_scores(q, c_rows)
-    r = min(int(np.ceil((3 * k + 100) / shards)), s.shape[1])
-    return np.sort(s, axis=1)[:, ::-1][:, r - 1].astype(np.float32)
-
-
-def shard_screen(q: np.ndarray, c_rows: np.ndarray, row0: int, tau: np.ndarray):
-    """(entries int64 = global row << 32 | score bits, counts int32 [Q],
-    offsets int64 [Q+1]) of the screened scores > tau[q], in query order."""
-    s = screened_scores(q, c_rows)
-    ents, counts = [], np.zeros(q.shape[0], np.int32)
-    for i in range(q.shape[0]):
-        j = np.nonzero(s[i] > tau[i])[0]
-        bits = s[i, j].view(np.uint32).astype(np.int64)
-        ents.append(((j.astype(np.int64) + row0) << 32) | bits)
-        counts[i] = len(j)
-    offsets = np.zeros(q.shape[0] + 1, np.int64)
-    offsets[1:] = np.cumsum(counts)
-    return (np.concatenate(ents) if ents else np.zeros(0, np.int64)), counts, offsets
-
-
-def shard_finalize(q: np.ndarray, c: np.ndarray, k: int, entries: np.ndarray, counts: np.ndarray,
-                   offsets: np.ndarray, tau: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
-    """Owner side: certify each query's screened lists (k-th largest screened
-    score sK: lb(sK) > ub(tau)), rescore the entries with ub >= lb(sK) by the
-    exact fp32 chain and take the top-k; an uncertified query is scanned
-    exactly.  counts / offsets are [G, Q]."""
-    q, c = _f32(q), _f32(c)
-    has_neg = bool((c < 0).any())
-    maxc = np.float32(np.sqrt((c.astype(np.float64) ** 2).sum(1)).max()) * np.float32(1 + 1e-5)
-    out_s = np.empty((q.shape[0], k), np.float32)
-    out_i = np.empty((q.shape[0], k), np.int32)
-    for i in range(q.shape[0]):
-        if not q[i].any():  # every score exactly 0: indices 0..k-1
-            out_s[i], out_i[i] = 0.0, np.arange(k)
-            continue
-        rel = not has_neg and bool((q[i] >= 0).all())
-        m = SCREEN_EPS * np.float32(np.linalg.norm(q[i].astype(np.float64)) * (1 + 1e-5)) * maxc + SCREEN_TINY
-        lb = (lambda x: x * (np.float32(1) - SCREEN_EPS) - SCREEN_TINY) if rel else (lambda x: x - m)
-        ub = (lambda x: x * (np.float32(1) + SCREEN_EPS) + SCREEN_TINY) if rel else (lambda x: x + m)
-        ok = bool((counts[:, i] >= 0).all())
-        if ok:
-            e = np.concatenate([entries[offsets[g, i]:offsets[g, i] + counts[g, i]] for g in range(counts.shape[0])])
-            ok = len(e) >= k
-        if ok:
-            sc = (e & 0xFFFFFFFF).astype(np.uint32).view(np.float32)
-            ids = (e >> 32).astype(np.int64)
-            X = lb(np.sort(sc)[::-1][k - 1])
-            ok = bool(X > ub(np.float32(tau[i])))
-        if ok:
-            keep = ids[ub(sc) >= X]
-            ex = fmaf_scores(q[i:i + 1], c[keep])[0] + np.float32(0.0)
-            order = np.lexsort((keep, -ex.astype(np.float64)))[:k]
-            out_s[i], out_i[i] = ex[order], keep[order]
-        else:
-            s_, i_, _ = bruteforce_topk(q[i:i + 1], c, k)
-            out_s[i], out_i[i] = s_[0], i_[0]
-    return out_s, out_i
-
-
-# ---------------------------------------------------------------------------
 # StaticIndex.call (static_index.py:37-55) and IndexRecall (index_recall.py:22-59)
 def static_index(candidates: Sequence, k: int, batch: int) -> np.ndarray:
     row = np.asarray(list(candidates)[:k])

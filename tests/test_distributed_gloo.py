@@ -40,47 +40,29 @@ def _oracle_ops():
     return IndexOps(build=lambda c: None, search=search, merge=merge)
 
 
-def _shard_oracle_ops(tau_mode="estimate"):
-    """The candidate-sharded protocol's kernels restated on CPU
-    (oracle.shard_*).  tau_mode "inf": every screen keeps nothing, so every
-    query must reach the owner's exact fallback; "rank0_high": rank 0's
-    estimate is far too high, so the all_reduce(MIN) must save the lists."""
-    from oracle import oracle
-    from pkg.modelling.distributed import ShardIndexOps
-
-    def estimate(img, q, r0, r1, k, shards):
-        t = oracle.shard_estimate(q.numpy(), img[r0:r1], k, shards)
-        if tau_mode == "inf":
-            t[:] = np.inf
-        elif tau_mode == "rank0_high" and dist.get_rank() == 0:
-            t[:] = 1e30
-        return torch.from_numpy(t)
-
-    def screen(img, q, r0, r1, k, shards, tau):
-        e, cnt, off = oracle.shard_screen(q.numpy(), img[r0:r1], r0, tau.numpy())
-        return torch.from_numpy(e), torch.from_numpy(cnt), torch.from_numpy(off)
-
-    def finalize(img, cand, q, k, entries, counts, offsets, tau):
-        s, i = oracle.shard_finalize(q.numpy(), cand.numpy(), k, entries.numpy(), counts.numpy(), offsets.numpy(),
-                                     tau.numpy())
-        return torch.from_numpy(s), torch.from_numpy(i)
-
-    return ShardIndexOps(build=lambda c: c.numpy(), estimate=estimate, screen=screen, finalize=finalize)
-
-
 def _index_worker(rank, world, port, q, c, k, out):
     _init(rank, world, port)
-    from pkg.modelling.distributed import QueryShardedBruteForceIndex, ShardedBruteForceIndex
+    from pkg.modelling.distributed import QueryShardedBruteForceIndex, ShardedBruteForceIndex, shard_range
 
     qidx = QueryShardedBruteForceIndex(k, None, torch.from_numpy(c), ops=_oracle_ops())
     qs_s, qs_i = qidx.search(torch.from_numpy(q))
     out[("q", rank)] = (qs_s.numpy(), qs_i.numpy())
 
-    for mode in ("estimate", "inf", "rank0_high"):
-        idx = ShardedBruteForceIndex(k, None, torch.from_numpy(c), ops=_shard_oracle_ops(mode))
+    # each rank is handed ONLY its rows: the even split, and a ragged split
+    # whose first shard has fewer rows than k (its list is padded)
+    N = c.shape[0]
+    ragged = [3] + [(N - 3) // (world - 1) + (1 if r < (N - 3) % (world - 1) else 0) for r in range(world - 1)]
+    for mode in ("even", "ragged"):
+        if mode == "even":
+            b, e = shard_range(N, world, rank)
+        else:
+            b = sum(ragged[:rank])
+            e = b + ragged[rank]
+        idx = ShardedBruteForceIndex(k, None, torch.from_numpy(c[b:e].copy()), ops=_oracle_ops())
         s, i = idx.search(torch.from_numpy(q))
         blk, os_, oi = idx.search_owned(torch.from_numpy(q))
-        out[(mode, rank)] = (s.numpy(), i.numpy(), idx.num_candidates, blk, os_.numpy(), oi.numpy())
+        out[(mode, rank)] = (s.numpy(), i.numpy(), idx.num_candidates, blk, os_.numpy(), oi.numpy(),
+                             idx.rows, int(idx.shard.shape[0]))
     dist.destroy_process_group()
 
 
@@ -93,21 +75,23 @@ def test_sharded_index_equals_unsharded(world):
     c[100:140] = c[99]  # cross-shard ties must resolve by global index
     q = np.maximum(rng.standard_normal((20, 16)), 0).astype(np.float32)
     q[3] = 0.0
-    q[7] = rng.standard_normal(16).astype(np.float32)  # mixed signs: the absolute screen bound
+    q[7] = rng.standard_normal(16).astype(np.float32)  # mixed signs
     k = 25
     out = mp.Manager().dict()
     mp.spawn(_index_worker, args=(world, _free_port(), q, c, k, out), nprocs=world, join=True)
     rs, ri, _ = oracle.bruteforce_topk(q, c, k)
-    for mode in ("estimate", "inf", "rank0_high"):
-        covered = []
+    for mode in ("even", "ragged"):
+        covered, rows = [], []
         for r in range(world):
-            s, i, n, (b, e), os_, oi = out[(mode, r)]
-            assert n == 301
+            s, i, n, (b, e), os_, oi, (r0, r1), held = out[(mode, r)]
+            assert n == 301 and held == r1 - r0 < 301  # no rank holds every row
+            rows.append((r0, r1))
             assert np.array_equal(i, ri) and np.array_equal(s, rs), mode
             # search_owned: this rank's query block only, same global lists
             assert np.array_equal(oi, ri[b:e]) and np.array_equal(os_, rs[b:e]), mode
             covered += list(range(b, e))
         assert covered == list(range(q.shape[0]))
+        assert rows[0][0] == 0 and rows[-1][1] == 301 and all(rows[j][1] == rows[j + 1][0] for j in range(world - 1))
     for r in range(world):
         qs_s, qs_i = out[("q", r)]  # query-sharded: every rank holds the full answer
         assert np.array_equal(qs_i, ri) and np.array_equal(qs_s, rs)

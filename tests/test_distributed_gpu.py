@@ -1,7 +1,8 @@
 """Candidate-sharded index on the GPU with the libtt kernels under real
-sharding: world 1, 2 and 3 processes on cuda:0 (gloo, collectives staged
-through the host), each rank screening its own candidate rows; every rank's
-answer must equal the single-GPU search bit for bit, and the oracle."""
+sharding: world 1, 2, 3 and 8 processes on cuda:0 (gloo, collectives staged
+through the host), each rank handed ONLY its block of candidate rows; every
+rank's answer must equal the single-GPU search bit for bit, and the oracle.
+The 8-way case is configs[3]'s layout (N = 105,542 H&M articles, top-100)."""
 import os
 import socket
 
@@ -30,23 +31,46 @@ def _worker(rank, world, port, c, q, k, out):
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "hm-retrieval-two-tower_amd")]
-    from pkg.modelling.distributed import ShardedBruteForceIndex
+    from pkg.modelling.distributed import ShardedBruteForceIndex, shard_range
 
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
-    idx = ShardedBruteForceIndex(k, None, torch.as_tensor(c, device=dev))
+    b, e = shard_range(c.shape[0], world, rank)
+    idx = ShardedBruteForceIndex(k, None, torch.as_tensor(c[b:e], device=dev))  # this rank's rows only
     s, i = idx.search(torch.as_tensor(q, device=dev))
-    (b, e), os_, oi = idx.search_owned(torch.as_tensor(q, device=dev))
+    (qb, qe), os_, oi = idx.search_owned(torch.as_tensor(q, device=dev))
     torch.cuda.synchronize()
-    out[rank] = (s.cpu().numpy(), i.cpu().numpy(), (b, e), os_.cpu().numpy(), oi.cpu().numpy(), idx.rows)
+    out[rank] = (s.cpu().numpy(), i.cpu().numpy(), (qb, qe), os_.cpu().numpy(), oi.cpu().numpy(), idx.rows,
+                 int(idx.shard.shape[0]), idx.num_candidates)
     dist.destroy_process_group()
+
+
+def _check_sharded(cuda, world, c, q, k):
+    from oracle import oracle
+    from pkg.modelling import hip_ops
+
+    N, Q = c.shape[0], q.shape[0]
+    tc = torch.as_tensor(c, device=cuda)
+    ref_s, ref_i = hip_ops.bruteforce_search(hip_ops.bruteforce_build(tc), tc, torch.as_tensor(q, device=cuda), k)
+    ref_s, ref_i = ref_s.cpu().numpy(), ref_i.cpu().numpy()
+    sel = np.arange(0, Q, 7)
+    os_, oi_, _ = oracle.bruteforce_topk(q[sel], c, k)
+    assert np.array_equal(ref_i[sel], oi_) and np.array_equal(ref_s[sel], os_)
+    del tc
+    out = mp.Manager().dict()
+    mp.spawn(_worker, args=(world, _free_port(), c, q, k, out), nprocs=world, join=True)
+    rows = []
+    for r in range(world):
+        s, i, (b, e), bs, bi, rr, held, n = out[r]
+        rows.append(rr)
+        assert n == N and held == rr[1] - rr[0] and (world == 1 or held < N)
+        assert np.array_equal(i, ref_i) and np.array_equal(s, ref_s)
+        assert np.array_equal(bi, ref_i[b:e]) and np.array_equal(bs, ref_s[b:e])
+    assert rows[0][0] == 0 and rows[-1][1] == N
 
 
 @pytest.mark.parametrize("world,signed", [(1, False), (2, False), (3, False), (2, True)])
 def test_candidate_sharded_index_hip(cuda, world, signed):
-    from oracle import oracle
-    from pkg.modelling import hip_ops
-
     rng = np.random.default_rng(40 + world)
     N, Q, E, k = 20011, 1500, 128, 100
     c = rng.standard_normal((N, E)).astype(np.float32)
@@ -55,21 +79,20 @@ def test_candidate_sharded_index_hip(cuda, world, signed):
         c, q = np.maximum(c, 0), np.maximum(q, 0)
     c[15000:15030] = c[20:50]  # exact ties across shards resolve by global index
     q[::50] = 0.0              # zero queries: every score ties at 0
-    tc = torch.as_tensor(c, device=cuda)
-    ref_s, ref_i = hip_ops.bruteforce_search(hip_ops.bruteforce_build(tc), tc, torch.as_tensor(q, device=cuda), k)
-    ref_s, ref_i = ref_s.cpu().numpy(), ref_i.cpu().numpy()
-    sel = np.arange(0, Q, 7)
-    os_, oi_, _ = oracle.bruteforce_topk(q[sel], c, k)
-    assert np.array_equal(ref_i[sel], oi_) and np.array_equal(ref_s[sel], os_)
-    out = mp.Manager().dict()
-    mp.spawn(_worker, args=(world, _free_port(), c, q, k, out), nprocs=world, join=True)
-    rows = []
-    for r in range(world):
-        s, i, (b, e), bs, bi, rr = out[r]
-        rows.append(rr)
-        assert np.array_equal(i, ref_i) and np.array_equal(s, ref_s)
-        assert np.array_equal(bi, ref_i[b:e]) and np.array_equal(bs, ref_s[b:e])
-    assert rows[0][0] == 0 and rows[-1][1] == N
+    _check_sharded(cuda, world, c, q, k)
+
+
+def test_candidate_sharded_index_c4_eight_shards(cuda):
+    """configs[3] at its stated 8-way candidate sharding: N = 105,542
+    candidates (relu(N(0,1)), the towers' final ReLU), 2048 queries with 1 %
+    all-zero rows, top-100; eight processes on cuda:0, ~13.2k rows each."""
+    rng = np.random.default_rng(8)
+    N, Q, E, k = 105542, 2048, 128, 100
+    c = np.maximum(rng.standard_normal((N, E)), 0).astype(np.float32)
+    q = np.maximum(rng.standard_normal((Q, E)), 0).astype(np.float32)
+    q[rng.choice(Q, Q // 100, replace=False)] = 0.0
+    c[13200:13240] = c[40:80]  # duplicate rows straddling the first shard boundary
+    _check_sharded(cuda, 8, c, q, k)
 
 
 def _small_model(dev, seed):
@@ -147,3 +170,50 @@ def test_global_negatives_sharded_step_matches_full_batch(cuda, world):
         for ti, t in enumerate(ref.towers):
             for name, e in t.input_layer.embedding_layers.items():
                 np.testing.assert_allclose(tables[(ti, name)], e.weight.cpu().numpy(), rtol=1e-4, atol=2e-6)
+
+
+def _integration_worker(rank, world, port, code, C, batches, qemb, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    model = _small_model(dev, 3)
+    b = len(batches["cust"]) // world
+    env = {"model": model, "C": torch.as_tensor(C), "N": C.shape[0],
+           "local_batch": {k: torch.as_tensor(v[rank * b:(rank + 1) * b], device=dev) for k, v in batches.items()},
+           "query_embeddings": torch.as_tensor(qemb, device=dev)}
+    exec(code, env)
+    torch.cuda.synchronize()
+    out[rank] = (env["scores"].cpu().numpy(), env["ids"].cpu().numpy(), float(env["out"]["loss"].item()),
+                 int(env["index"].shard.shape[0]))
+    dist.destroy_process_group()
+
+
+def test_integration_example(cuda):
+    """INTEGRATION.md §4's code block, run as written on 2 ranks (gloo, one
+    GPU): the index answers like the single-GPU search, and the sharded step's
+    loss is the single-GPU loss of the global batch."""
+    import re
+
+    from pkg.modelling import hip_ops
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    text = open(os.path.join(root, "INTEGRATION.md")).read()
+    sec = text[text.index("## 4. Multi-GPU"):]
+    code = re.search(r"```python\n(.*?)```", sec, re.S).group(1)
+    rng = np.random.default_rng(5)
+    C = np.maximum(rng.standard_normal((1000, 32)), 0).astype(np.float32)
+    qemb = np.maximum(rng.standard_normal((64, 32)), 0).astype(np.float32)
+    gb = _global_batches(1, 128)[0]
+    tc = torch.as_tensor(C, device=cuda)
+    ref_s, ref_i = hip_ops.bruteforce_search(hip_ops.bruteforce_build(tc), tc, torch.as_tensor(qemb, device=cuda), 100)
+    ref = _small_model(cuda, 3)
+    ref_loss = float(ref.train_step({k: torch.as_tensor(v, device=cuda) for k, v in gb.items()})["loss"].item())
+    out = mp.Manager().dict()
+    mp.spawn(_integration_worker, args=(2, _free_port(), code, C, gb, qemb, out), nprocs=2, join=True)
+    for r in range(2):
+        s, i, loss, held = out[r]
+        assert held == 500
+        assert np.array_equal(i, ref_i.cpu().numpy()) and np.array_equal(s, ref_s.cpu().numpy())
+        np.testing.assert_allclose(loss, ref_loss, rtol=2e-5)

@@ -392,7 +392,7 @@ def test_sharded_train_step_world1_matches_single_gpu(cuda):
                             device_id=torch.device(cuda))
     try:
         a, b = _small_model(cuda, seed=3), _small_model(cuda, seed=3)
-        step = ShardedTrainStep(a, shard_min_rows=300)
+        step = ShardedTrainStep(a, shard_min_rows=300, global_negatives=False)
         assert step.tables is not None and len(step.tables.names) == 2
         rng = np.random.default_rng(7)
         batches = [_batch(cuda, rng, 256) for _ in range(5)]

@@ -55,8 +55,17 @@ def test_native_vocab_value_kinds():
     # a value listed twice maps to its last row (the dict of Feature.lookup_table)
     d = NativeVocab(["a", "b", "a"])
     np.testing.assert_array_equal(d.encode(["a", "b", "c"]), [3, 2, 0])
-    with pytest.raises(ValueError):
-        v.encode(np.array(["x", None], dtype=object))
+    # None reads as str(None) and float32 as str(np.float32(x)), the text a
+    # str()-cast column holds (no widening of 0.1f to 0.10000000149011612)
+    wv = ["None", "0.1", "x", "2.5", "nan"]
+    w = NativeVocab(wv)
+    for vals in (np.array(["x", None], dtype=object), [None, "x", 0.1],
+                 np.array([0.1, 2.5, 0.3], np.float32), np.array([0.1, np.nan], np.float64),
+                 np.array([np.float32(0.1), None, "x"], dtype=object)):
+        np.testing.assert_array_equal(w.encode(vals), dict_lookup(wv, list(vals)))
+    import pyarrow as pa
+    with pytest.raises(ValueError):  # an Arrow array's nulls have no text
+        v.encode(pa.array(["x", None]))
 
 
 def test_native_vocab_host_validation():
