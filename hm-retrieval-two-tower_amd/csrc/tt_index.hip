@@ -237,10 +237,10 @@ struct ScreenArgs {
   int S;              // candidate splits
   int NS;             // sample tiles per split (0: keep every score)
   int jsel;           // tau = jsel-th largest of a query's 64 bins
-  int cap;            // entries per (query, split, lane half) list
+  int cap;            // entries per (query, split) list; the last slot is scratch
   unsigned index_offset;  // id of image row r = index_offset + r
-  uint2* buf;         // [nq_pad][S][2][cap] (score bits, id)
-  int* count;         // [nq_pad][S][2]; -1 = list overflowed
+  uint2* buf;         // [nq_pad][S][cap] (score bits, id)
+  int* count;         // [nq_pad][S]; -1 = list overflowed
   float* tau_split;   // sample pass output [nq_pad][S]
   const float* tau;   // scan pass input [nq_pad]: keep s~ > tau[q]
 };
@@ -286,17 +286,15 @@ __device__ float bins_select(const float (&ba)[16], const float (&bb)[16], int j
   return (t > -INFINITY) ? t : -INFINITY;  // NaN (no prefix found) -> keep everything
 }
 
-// SAMPLE = true: the estimate pass (phase 1) over the split's spread sample
-// tiles, writes tau[q][split].  SAMPLE = false: the scan (phase 2) of every
-// tile of the split against that tau.  Separate launches, so each keeps its
-// registers for its own loop.
-template <int D, bool SAMPLE>
-__global__ void __launch_bounds__(kSThreads) screen_kernel(const ScreenArgs a) {
+// The estimate pass (phase 1) over the split's spread sample tiles: writes
+// tau[q][split].  (scan_kernel below is phase 2.)
+template <int D>
+__global__ void __launch_bounds__(kSThreads) sample_kernel(const ScreenArgs a) {
+  constexpr bool SAMPLE = true;
   constexpr int KS = D / 16, CH = D / 8, RB = D * 2;
   constexpr int TILE_BYTES = kCTile * RB;                 // 16 KiB at D = 128
   constexpr int PIECES = TILE_BYTES / 1024;               // 1 KiB LDS-DMA pieces per tile
   constexpr int PPW = PIECES >= kSWaves ? PIECES / kSWaves : 1;
-  constexpr int RPS = 16 / KS;                            // filtered registers per k-step
   __shared__ __attribute__((aligned(1024))) char smem[kStages * TILE_BYTES];
   const int tid = threadIdx.x;
   const int wave = tid / kWave;
@@ -416,132 +414,292 @@ __global__ void __launch_bounds__(kSThreads) screen_kernel(const ScreenArgs a) {
       a.tau_split[q1 * a.S + split] = tq1;
     }
   }
-  if constexpr (!SAMPLE) {
-  // the estimate of the sample pass; queries past nq keep nothing
-  float tau0 = q0 < a.nq ? a.tau[q0] : INFINITY;
-  float tau1 = q1 < a.nq ? a.tau[q1] : INFINITY;
+}
 
-  // ---- phase 2: every tile of the split once, keep s~ > tau -----------------
-  const int64_t lst0 = ((q0 * a.S + split) * 2 + h) * static_cast<int64_t>(a.cap);
-  const int64_t lst1 = ((q1 * a.S + split) * 2 + h) * static_cast<int64_t>(a.cap);
-  uint2* const reg0 = a.buf + lst0;
-  uint2* const reg1 = a.buf + lst1;
-  uint2* w0 = reg0;  // next free entry
-  uint2* w1 = reg1;
-  uint2* const lim0 = reg0 + (a.cap - 48);  // a list grows by <= 48 between two checks
-  uint2* const lim1 = reg1 + (a.cap - 48);
-  bool ovf0 = false, ovf1 = false;
-#ifdef TT_INDEX_NOINSERT  // probe build (tools/index_probe.hip): screen cost without list stores
-  tau0 = tau1 = __uint_as_float(a.cap > 0 ? 0x7f800000u : 0u);  // +inf, opaque to the compiler
+// ---- scan: every tile of the split once, keep s~ > tau ----------------------
+// Staged hit rows per wave: a lane whose 16 scores of a block hold one above
+// its query's tau copies the whole row (16 scores + tag) into its wave's LDS
+// stage; once >= 64 rows are staged the wave filters them one row per lane
+// and appends the hits to the queries' lists.  The per-block filter is thus
+// a 16-way max per query set and one compare (branch-free, interleaved with
+// the next block's MFMAs); the per-score work runs on full waves of hit rows.
+constexpr int kStageRows = 128;  // a wave's ring of staged rows: < 64 pending before a set, + <= 64 per set
+constexpr int kRowF = 20;        // floats per staged row: 16 scores, candidate base, query, 2 pad (80 B: no
+                                 // bank conflicts when 8 lanes read 8 consecutive rows by ds_read_b128)
+
+template <int D>
+struct ScanGeo {
+  static constexpr int TILE_BYTES = kCTile * D * 2;
+  static constexpr int RING = kStages * TILE_BYTES;
+};
+
+__device__ __forceinline__ float max16(const f32x16& c) {
+  const float x0 = fmaxf(fmaxf(c[0], c[1]), c[2]);
+  float x1 = fmaxf(fmaxf(c[3], c[4]), c[5]);
+  float x2 = fmaxf(fmaxf(c[6], c[7]), c[8]);
+  float x3 = fmaxf(fmaxf(c[9], c[10]), c[11]);
+  float x4 = fmaxf(fmaxf(c[12], c[13]), c[14]);
+  return fmaxf(fmaxf(fmaxf(x0, x1), x2), fmaxf(fmaxf(x3, x4), c[15]));
+}
+
+template <int D>
+__global__ void __launch_bounds__(kSThreads) scan_kernel(const ScreenArgs a) {
+  using G = ScanGeo<D>;
+  constexpr int KS = D / 16, CH = D / 8, RB = D * 2;
+  constexpr int TILE_BYTES = G::TILE_BYTES;
+  constexpr int PIECES = TILE_BYTES / 1024;               // 1 KiB LDS-DMA pieces per tile
+  constexpr int PPW = PIECES >= kSWaves ? PIECES / kSWaves : 1;
+  // separate LDS objects: the compiler can tell the staging area from the
+  // LDS-DMA ring, so staging does not wait for the ring's loads (vmcnt)
+  __shared__ __attribute__((aligned(1024))) char smem[G::RING];
+  __shared__ __attribute__((aligned(16))) float s_rows[kSWaves * kStageRows * kRowF];
+  __shared__ float s_tau[kQPerWG];
+  __shared__ int s_cnt[kQPerWG];
+  const int tid = threadIdx.x;
+  const int wave = tid / kWave;
+  const int lane = lane_id();
+  const int h = lane >> 5, l32 = lane & 31;
+  const int split = static_cast<int>(blockIdx.x % a.S);
+  const int64_t qblk = static_cast<int64_t>(blockIdx.x / a.S) * kQPerWG;
+  const int ql0 = wave * kQPerWave + l32, ql1 = ql0 + 32;  // this lane's queries in the workgroup
+  const int64_t q0 = qblk + ql0, q1 = qblk + ql1;
+  const int t0 = static_cast<int>(a.row0 / kCTile);
+  const int ntiles = static_cast<int>((a.row1 + kCTile - 1) / kCTile) - t0;
+  const int per = (ntiles + a.S - 1) / a.S;
+  const int tb = t0 + split * per;
+  const int nv = max(min(ntiles - split * per, per), 0);
+  const __bf16* crow = index_rows(a.index);
+  const bool my_pieces = wave * PPW < PIECES;  // D = 32: waves 4..7 stage nothing
+  float* const srow = s_rows + wave * kStageRows * kRowF;
+  float* const tau_l = s_tau;
+  int* const cnt_l = s_cnt;
+
+  bf16x8 bq0[KS], bq1[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    bq0[s] = *reinterpret_cast<const bf16x8*>(a.qb + q0 * D + 16 * s + 8 * h);
+    bq1[s] = *reinterpret_cast<const bf16x8*>(a.qb + q1 * D + 16 * s + 8 * h);
+  }
+  // the sample pass's estimate; queries past nq keep nothing
+#ifndef TT_INDEX_NOINSERT
+  const float tau0 = q0 < a.nq ? a.tau[q0] : INFINITY;
+  const float tau1 = q1 < a.nq ? a.tau[q1] : INFINITY;
+#else  // probe build: scan cost without staging (tau +inf, opaque to the compiler)
+  const float tau0 = __uint_as_float(a.cap > 0 ? 0x7f800000u : 0u), tau1 = tau0;
 #endif
+  if (h == 0) {  // each wave owns its 64 queries' LDS words
+    tau_l[ql0] = tau0;
+    tau_l[ql1] = tau1;
+    cnt_l[ql0] = 0;
+    cnt_l[ql1] = 0;
+  }
+  wait_vmcnt<0>();  // ordinary loads retired before the LDS-DMA ring starts
 
-  // Each wave reads a block's A fragments one block ahead (af / af2), so the
-  // ring barrier sits in the middle of a tile: at mid-tile u every wave holds
-  // block (u, 1) in registers, tile u + 1 has landed, and tile u + 4 is issued
-  // into the stage tile u vacated.  List stores share the vector-memory
-  // counter with the LDS-DMA, so the wait for tile u + 1 counts the ops each
-  // wave issued after that tile's DMA: windows wa / wb / wc = ops from the DMA
-  // of tile u + 1 / u + 2 / u + 3 up to the next DMA (da / db / dc = pieces).
-  int wa, wb, wc, da, db, dc;
-  auto keep = [&](float v, float tau, unsigned c, uint2*& w) {
-    // uniform skip when no lane keeps v; marked unlikely so that the common
-    // case falls through (a taken branch per score costs more than the test)
-    if (__builtin_expect(__builtin_amdgcn_ballot_w64(v > tau) != 0, 0)) {
-      if (v > tau) {
-        *w = make_uint2(__float_as_uint(v), c);
-        ++w;
+  auto issue = [&](int tile, int stage) {
+    const int64_t base = static_cast<int64_t>(tile) * kCTile;
+#pragma unroll
+    for (int u = 0; u < PPW; ++u) {
+      const int p = wave * PPW + u;
+      if (p < PIECES) {
+        const int off = p * 1024 + lane * 16;
+        const int row = off / RB, chp = (off % RB) / 16;
+        const int ch = chp ^ ((row * CH / 16) % CH);
+        const __bf16* src = crow + (base + row) * D + ch * 8;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src),
+                                         (__attribute__((address_space(3))) void*)(smem + stage * TILE_BYTES + p * 1024),
+                                         16, 0, 0);
       }
-      ++wc;  // one store instruction issued
     }
   };
-  f32x16 p0, p1;  // the block waiting to be filtered
-#pragma unroll
-  for (int r = 0; r < 16; ++r) p0[r] = p1[r] = -INFINITY;
-  unsigned pc = 0;  // its lane candidate base (index_offset + first + 4h)
-  auto filter_regs = [&](int r0) {
-#pragma unroll
-    for (int i = 0; i < RPS; ++i) {
-      const int r = r0 + i;
-      const unsigned c = pc + static_cast<unsigned>((r & 3) + 8 * (r >> 2));
-      keep(p0[r], tau0, c, w0);
-      keep(p1[r], tau1, c, w1);
-    }
+  auto frag = [&](const char* B, int t, int s) {
+    const int row = 32 * t + l32, ch = 2 * s + h;
+    const int swz = (row * CH / 16) % CH;
+    return *reinterpret_cast<const bf16x8*>(B + row * RB + ((ch ^ swz) << 4));
   };
-  const int dpieces = my_pieces ? PPW : 0;
-  bf16x8 af[KS], af2[KS];
   auto load_frags = [&](bf16x8 (&f)[KS], const char* B, int t) {
 #pragma unroll
     for (int s = 0; s < KS; ++s) f[s] = frag(B, t, s);
   };
-  // MFMAs of block (t) of the tile at cbase from fragments f, the previous
-  // block's filter in their issue gaps; the results become the next p0 / p1.
-  // A block: its MFMAs, then its compares; the SIMD's other wave keeps the
-  // matrix pipe busy meanwhile.  (Measured alternatives, all slower or
-  // equal: the compares of block b-1 interleaved with the MFMAs of block b
-  // — 2 waves/SIMD spill, 1 wave/SIMD leaves the pipe idle — and staggering
-  // the two SIMD partners by half a block.)
-  auto block = [&](const bf16x8 (&f)[KS], int t, int64_t cbase) {
-    p0 = f32x16{};
-    p1 = f32x16{};
+  auto mask_pad = [&](f32x16& acc, int64_t cfirst) {  // rows outside [row0, row1) (edge tiles only)
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      p0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[s], bq0[s], p0, 0, 0, 0);
-      p1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[s], bq1[s], p1, 0, 0, 0);
+    for (int r = 0; r < 16; ++r) {
+      const int64_t c = cfirst + (r & 3) + 8 * (r >> 2);
+      if (c < a.row0 || c >= a.row1) acc[r] = -INFINITY;
     }
-    if (edge(cbase)) {
-      mask_pad(p0, cbase + 32 * t + 4 * h);
-      mask_pad(p1, cbase + 32 * t + 4 * h);
-    }
-    pc = a.index_offset + static_cast<unsigned>(cbase + 32 * t + 4 * h);
-#pragma unroll
-    for (int s = 0; s < KS; ++s) filter_regs(s * RPS);
   };
+  auto edge = [&](int64_t cbase) { return cbase < a.row0 || cbase + kCTile > a.row1; };
+
+  // ---- vector-memory accounting (as in the ring loop of the sample pass,
+  // plus the list stores of the flushes, which share vmcnt with the LDS-DMA):
+  // windows wa / wb / wc = ops issued from the DMA of tile u + 1 / u + 2 /
+  // u + 3 up to the next DMA; da / db / dc = that DMA's pieces.
+  const int dpieces = my_pieces ? PPW : 0;
+  int wa, wb, wc, da, db, dc;
+  int head = 0, tail = 0;  // staged rows [tail, head) of the wave's ring (wave-uniform counters)
+  // the workgroup's lists: (query ql, split) at entry (ql * S + split) * cap
+  const __amdgpu_buffer_rsrc_t lists = __builtin_amdgcn_make_buffer_rsrc(
+      a.buf + qblk * a.S * static_cast<int64_t>(a.cap), 0, 0x7fffffff, 0x00020000);
+
+  // Filters nrows staged rows from the tail (one per lane) and appends their
+  // hits to the lists: per register r, the lanes whose score r beats their
+  // row's tau store it at their list's next slot.  A store is issued only
+  // when some lane has a hit in r (and then counted into the vmcnt window).
+  auto flush = [&](int nrows) {
+    wsync();
+    const float* row = srow + ((tail + lane) & (kStageRows - 1)) * kRowF;
+    const bool valid = lane < nrows;
+    f32x4 x[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = reinterpret_cast<const f32x4*>(row)[i];
+    const f32x4 tg4 = reinterpret_cast<const f32x4*>(row)[4];
+    const unsigned pcr = __float_as_uint(tg4[0]);
+    const int ql = valid ? static_cast<int>(__float_as_uint(tg4[1])) : 0;
+    const float tr = valid ? tau_l[ql] : INFINITY;
+    int n = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) n += (x[r >> 2][r & 3] > tr) ? 1 : 0;
+    int pos = 0;
+    if (n) {  // reserve n list slots (an LDS atomic the compiler would order behind the ring's loads)
+      const unsigned addr = static_cast<unsigned>(
+          reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) int*)(cnt_l + ql)));
+      asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(pos) : "v"(addr), "v"(n) : "memory");
+    }
+    const unsigned lbase = static_cast<unsigned>((ql * a.S + split) * a.cap) * 8u;
+    const int last = a.cap - 1;  // scratch slot: entries past it are dropped with the list
+    int stores = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float v = x[r >> 2][r & 3];
+      const bool keepit = v > tr;
+      if (__ballot(keepit)) {
+        if (keepit) {
+          typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+          const u32x2 e = {__float_as_uint(v), pcr + static_cast<unsigned>((r & 3) + 8 * (r >> 2))};
+          __builtin_amdgcn_raw_buffer_store_b64(e, lists, lbase + static_cast<unsigned>(min(pos, last)) * 8u, 0, 0);
+          ++pos;
+        }
+        ++stores;
+      }
+    }
+    wc += stores;
+    tail += nrows;
+    wsync();
+  };
+  // Stages the rows of this block's lanes whose max beats their tau.
+  auto stage = [&](const f32x16& c, bool hit, int ql, unsigned pc) {
+    const uint64_t m = __ballot(hit);
+    if (m) {
+      if (hit) {
+        f32x4* d = reinterpret_cast<f32x4*>(srow + ((head + __popcll(m & lanemask_lt64())) & (kStageRows - 1)) * kRowF);
+        d[0] = f32x4{c[0], c[1], c[2], c[3]};
+        d[1] = f32x4{c[4], c[5], c[6], c[7]};
+        d[2] = f32x4{c[8], c[9], c[10], c[11]};
+        d[3] = f32x4{c[12], c[13], c[14], c[15]};
+        reinterpret_cast<uint2*>(d + 4)[0] = make_uint2(pc, static_cast<unsigned>(ql));
+      }
+      head += __popcll(m);
+      if (head - tail >= kWave) flush(kWave);
+    }
+  };
+
+#pragma unroll
+  for (int s = 0; s < kStages - 1; ++s)
+    if (s < nv) issue(tb + s, s);
+  if (!my_pieces || nv <= 1) wait_vmcnt<0>();
+  else if (nv == 2) wait_vmcnt<PPW>();
+  else wait_vmcnt<2 * PPW>();
+  __builtin_amdgcn_s_barrier();
+
   // entering: tile 0 landed (barrier passed), tiles up to 2 issued, the
   // stage of tile 3 free
   dc = 0;
   if (3 < nv) {
-    issue(phys(3), 3);
+    issue(tb + 3, 3);
     dc = dpieces;
   }
   da = wa = (1 < nv) ? dpieces : 0;
   db = wb = (2 < nv) ? dpieces : 0;
   wc = dc;
-  if (0 < nv) load_frags(af, smem, 0);
+  // Two accumulator pairs, A for the first half of a tile (block (u, 0)),
+  // B for the second (u, 1), and two fragment sets F0 / F1.  A half issues
+  // one pair's 16 MFMAs from fragments read during the previous half, then
+  // the next block's fragment reads, then filters the other pair (whose
+  // MFMAs finished during the previous half).  The ring barrier sits between
+  // the halves: every wave has read stage u by then (refill it; tile u + 1
+  // has landed).
+  bf16x8 f0[KS], f1[KS];
+  f32x16 a0 = {}, a1 = {}, b0 = {}, b1 = {};
+  auto mfmas = [&](const bf16x8 (&f)[KS], f32x16& x0, f32x16& x1) {
+    x0 = f32x16{};
+    x1 = f32x16{};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      x0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[s], bq0[s], x0, 0, 0, 0);
+      x1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[s], bq1[s], x1, 0, 0, 0);
+    }
+  };
+  // block (tile u, half t) held in (x0, x1): edge mask, candidate base, maxima
+  struct Pend {
+    unsigned pc;
+    float m0, m1;
+  };
+  auto prep = [&](f32x16& x0, f32x16& x1, int u, int t) {
+    const int64_t cb = static_cast<int64_t>(tb + u) * kCTile + 32 * t;
+    if (edge(cb - 32 * t)) {
+      mask_pad(x0, cb + 4 * h);
+      mask_pad(x1, cb + 4 * h);
+    }
+    return Pend{a.index_offset + static_cast<unsigned>(cb + 4 * h), max16(x0), max16(x1)};
+  };
+  auto stage_pair = [&](const f32x16& x0, const f32x16& x1, const Pend& p) {
+    stage(x0, p.m0 > tau0, ql0, p.pc);
+    stage(x1, p.m1 > tau1, ql1, p.pc);
+  };
+  if (nv > 0) load_frags(f0, smem, 0);
   for (int u = 0; u < nv; ++u) {
-    const char* B = smem + (u % kStages) * TILE_BYTES;
-    const int64_t cbase = static_cast<int64_t>(phys(u)) * kCTile;
-    if (w0 > lim0) {
-      ovf0 = true;
-      tau0 = INFINITY;
-    }
-    if (w1 > lim1) {
-      ovf1 = true;
-      tau1 = INFINITY;
-    }
-    load_frags(af2, B, 1);
-    block(af, 0, cbase);
-    if (u + 1 < nv) {  // mid-tile: tile u + 1 landed, every wave holds block (u, 1)
+    // half A: MFMAs (u, 0) into A (F0 read during the previous half), then
+    // read F1 <- (u, 1), then filter (u - 1, 1) from B
+    mfmas(f0, a0, a1);
+    load_frags(f1, smem + (u % kStages) * TILE_BYTES, 1);
+    if (u > 0) stage_pair(b0, b1, prep(b0, b1, u - 1, 1));
+    if (u + 1 < nv) {  // next tile: landed, every wave done with tile u, refill its stage
       wait_vmcnt_atmost((wa - da) + wb + wc);
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      // compiler-visible wait + barrier: it then knows the fragment reads
+      // before it are complete and puts no wait in front of the next MFMAs
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // vmcnt(63) expcnt(7) lgkmcnt(0)
+      __builtin_amdgcn_s_barrier();
       wa = wb;
       da = db;
       wb = wc;
       db = dc;
       dc = 0;
       if (u + 4 < nv) {
-        issue(phys(u + 4), (u + 4) % kStages);
+        issue(tb + u + 4, (u + 4) % kStages);
         dc = dpieces;
       }
       wc = dc;
-      load_frags(af, smem + ((u + 1) % kStages) * TILE_BYTES, 0);
     }
-    block(af2, 1, cbase);
+    // half B: MFMAs (u, 1) into B, then read F0 <- (u + 1, 0) (stale after the
+    // last tile: unused), then filter (u, 0) from A
+    mfmas(f1, b0, b1);
+    load_frags(f0, smem + ((u + 1) % kStages) * TILE_BYTES, 0);
+    stage_pair(a0, a1, prep(a0, a1, u, 0));
+#ifndef TT_SCAN_FLUSH_TILES
+#define TT_SCAN_FLUSH_TILES 4
+#endif
+    // every wave flushes at the same tiles (a wave flushing alone would hold
+    // the others at the next ring barrier)
+    if (TT_SCAN_FLUSH_TILES > 0 && u % TT_SCAN_FLUSH_TILES == TT_SCAN_FLUSH_TILES - 1)
+      while (head > tail) flush(min(head - tail, kWave));
   }
-  const int cnt0 = static_cast<int>(w0 - reg0), cnt1 = static_cast<int>(w1 - reg1);
-  a.count[(q0 * a.S + split) * 2 + h] = ovf0 ? -1 : cnt0;
-  a.count[(q1 * a.S + split) * 2 + h] = ovf1 ? -1 : cnt1;
-  TT_STAT(0, cnt0 + cnt1);
+  if (nv > 0) stage_pair(b0, b1, prep(b0, b1, nv - 1, 1));
+  while (head > tail) flush(min(head - tail, kWave));
+  if (h == 0) {
+    const int n0c = cnt_l[ql0], n1c = cnt_l[ql1];
+    a.count[q0 * a.S + split] = n0c > a.cap - 1 ? -1 : n0c;  // slot cap - 1 is scratch
+    a.count[q1 * a.S + split] = n1c > a.cap - 1 ? -1 : n1c;
   }
+  TT_STAT(0, (h == 0 ? cnt_l[ql0] + cnt_l[ql1] : 0));
 }
 
 // tau[q] = min over the splits' estimates (the lowest is the safest: more
@@ -1066,11 +1224,11 @@ SearchPlan plan_search(int64_t nq, int64_t n_rows, int k, int shards) {
   const int64_t nts = ceil_div(ntiles, p.S);  // tiles per split
   const double ns_cand = static_cast<double>(nts) * kCTile;
   const double R = (3.0 * k + 100.0) / (static_cast<double>(p.S) * (shards > 0 ? shards : 1));
-  double mu;  // expected entries per (query, split, lane half)
+  double mu;  // expected entries per (query, split)
   if (nts < 16 || R >= 0.25 * ns_cand) {
     p.NS = 0;  // keep every score of the split
     p.jsel = 1;
-    mu = ns_cand / 2.0;
+    mu = ns_cand;
   } else {
     // 64 bins of NS samples each; the smallest bin must sit well below
     // rank R: NS <= N ln64 / (1.5 R)
@@ -1082,11 +1240,11 @@ SearchPlan plan_search(int64_t nq, int64_t n_rows, int k, int shards) {
     const double pbin = 1.0 - std::exp(-1.0 * NS * R / ns_cand);
     int j = static_cast<int>(std::lround(64.0 * pbin));
     p.jsel = j < 1 ? 1 : (j > 64 ? 64 : j);
-    mu = R / 2.0;
+    mu = R;
   }
   // the lowest of S (x shards) estimates lands lower than each: room for it
   p.cap = next_pow2(static_cast<int>(3.0 * mu * (p.S > 1 ? 2.0 : 1.0)) + 64);
-  const size_t per_query = static_cast<size_t>(p.S) * 2 * p.cap * sizeof(uint2);
+  const size_t per_query = static_cast<size_t>(p.S) * p.cap * sizeof(uint2);
   int64_t chunk = static_cast<int64_t>(kListBudget / per_query) / kQPerWG * kQPerWG;
   if (chunk < kQPerWG) chunk = kQPerWG;
   const int64_t need = round_up(nq > 0 ? nq : 1, kQPerWG);
@@ -1115,8 +1273,8 @@ SearchWs carve_search(Carver& cv, int D, const SearchPlan& p, bool lists, bool f
   w.qflags = cv.take<int>(nq_pad);
   w.qmarg = cv.take<float>(nq_pad);
   if (lists) {
-    w.buf = cv.take<uint2>(nq_pad * p.S * 2 * static_cast<int64_t>(p.cap));
-    w.count = cv.take<int>(nq_pad * p.S * 2);
+    w.buf = cv.take<uint2>(nq_pad * p.S * static_cast<int64_t>(p.cap));
+    w.count = cv.take<int>(nq_pad * p.S);
     w.tau_split = cv.take<float>(nq_pad * p.S);
     w.tau = cv.take<float>(nq_pad);
   }
@@ -1133,10 +1291,10 @@ template <int D>
 void launch_pass(const ScreenArgs& sa, int64_t nq_pad, bool sample, hipStream_t st) {
   const dim3 grid((nq_pad / kQPerWG) * sa.S), block(kSThreads);
   if (sample) {
-    hipLaunchKernelGGL((screen_kernel<D, true>), grid, block, 0, st, sa);
+    hipLaunchKernelGGL((sample_kernel<D>), grid, block, 0, st, sa);
   } else {
     probe_begin(TT_PROBE_INDEX_SCREEN, st);
-    hipLaunchKernelGGL((screen_kernel<D, false>), grid, block, 0, st, sa);
+    hipLaunchKernelGGL((scan_kernel<D>), grid, block, 0, st, sa);
     probe_end(TT_PROBE_INDEX_SCREEN, st);
   }
 }
@@ -1269,7 +1427,7 @@ extern "C" int tt_bruteforce_search(const void* index, const float* cand, int64_
     if (int rc = run_prep(qc, ldq, nq, dim, D, index, w, true, st)) return rc;
     if (int rc = run_estimate(D, index, 0, n_cand, nq, p, w, w.tau, st)) return rc;
     if (int rc = run_scan(D, index, 0, n_cand, nq, p, w, w.tau, static_cast<unsigned>(index_offset), st)) return rc;
-    Lists ls{w.buf, w.count, w.tau, 2 * p.S, p.cap, nullptr, 2 * p.S, 1};
+    Lists ls{w.buf, w.count, w.tau, p.S, p.cap, nullptr, p.S, 1};
     FinalArgs fa{qc, ldq, cand, ldc, n_cand, index_offset, index_offset, dim, k, p.L, p.P, vec4,
                  nq, w.qflags, w.qmarg, ls, out_scores + q0 * k, out_idx + q0 * k, w.fail_count, w.fail_list};
     FallbackArgs fb{qc, ldq, cand, ldc, n_cand, index_offset, dim, k, p.L, p.P, p.parts, vec4,

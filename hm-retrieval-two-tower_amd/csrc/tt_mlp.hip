@@ -308,25 +308,28 @@ __global__ void __launch_bounds__(1024) mlp_colsum_kernel(const float* __restric
 //   layer's output gradient, optionally Gm = (gmask > 0) ? G * s : 0 — the
 //   ReluGrad of the layer's own relu folded into the load)
 // The output [Ka + 1, N] is exactly the flat parameter layout (kernel rows
-// then the bias row).  Grid = S batch splits x CG column groups of 64: each
-// workgroup reduces its split's rows for ALL Ka + 1 rows of the output and
-// one 64-column group, writes that slice of its split's partial [Ka + 1, N],
-// and mlp_sum_parts_kernel adds the partials in split order (deterministic).
-// The CG workgroups of one split sit on one XCD (blockIdx % 8 picks the XCD),
-// so the split's A rows they all stage come from that XCD's L2.
-// MFMA view: C[i][j] += A'[i][k] B[k][j] with A' = [A | 1]^T (i = activation
-// column, k = batch row), B = Gm.  Both operands need 8 consecutive BATCH
-// rows per lane, so the staged fp32 rows are split hi/lo and written
-// TRANSPOSED into LDS (column-major: 16 batch rows of one column = 32 B,
-// XOR-swizzled 16-B chunks), then read as conflict-free ds_read_b128
-// fragments.  8 waves: wave w owns column block (w & 1) of the group and the
-// 32-row blocks (w >> 1) + 4 t of Ka + 1 (<= 9 blocks: Ka <= 287).
-constexpr int kWgThreads = 512;
-constexpr int kWgBK = 16;      // batch rows per stage (one MFMA k-step)
-constexpr int kWgMaxIB = 9;    // 32-row blocks of Ka + 1 (Ka + 1 <= 288)
-constexpr int kWgCols = 64;    // output columns per workgroup
-constexpr int kWgIMax = 3;     // row blocks per wave
-constexpr int kWgDepth = 4;    // stages of loads in flight
+// then the bias row).  Split-K over the batch: grid = S splits x 64 x 64
+// output tiles; each workgroup reduces its split's rows for one tile into
+// its split's partial [Ka + 1, N], and mlp_sum_parts_kernel adds the
+// partials in split order (deterministic).  The tiles of one split sit on
+// one XCD (blockIdx % 8 picks the XCD), so the split's rows that its tiles
+// all stage come from that XCD's L2.
+// Both MFMA operands need 8 consecutive BATCH rows per lane; the staged
+// 32-row stages are written ROW-major (as loaded: each thread converts 8
+// consecutive columns of one row to bf16 hi / lo and stores 16 B per plane)
+// and the fragments are read with the hardware transposing read
+// ds_read_b64_tr_b16 (4 rows x 16 columns per 16-lane group, delivered
+// column-major).  Rows are 192 B apart (128 B of data): the 4 rows x 2 groups
+// of a 32-lane half then start at banks 48q + 8g mod 64, all distinct.
+// 4 waves; wave w owns the 32 x 32 block (w & 1, w >> 1) of the tile;
+// bf16x3 (a_lo b_hi + a_hi b_lo + a_hi b_hi), fp32 accumulation.
+constexpr int kWgThreads = 256;
+constexpr int kWgTile = 64;       // output tile: 64 rows of [A | 1]^T x 64 columns of Gm
+constexpr int kWgBK = 32;         // batch rows per stage (2 MFMA k-steps)
+constexpr int kWgRowB = 192;      // LDS bytes per staged row
+constexpr int kWgPlaneB = kWgBK * kWgRowB;       // 6 KiB
+constexpr int kWgStageB = 4 * kWgPlaneB;         // A hi, A lo, G hi, G lo: 24 KiB
+constexpr int kWgDepth = 3;       // stages of global loads in flight
 
 struct WgradArgs {
   const float* A;
@@ -337,202 +340,162 @@ struct WgradArgs {
   int64_t ldgm;
   const float* scale;
   int64_t M;
-  int Ka, N, IB;       // IB = ceil((Ka + 1) / 32)
-  int CG, S;           // column groups, splits
+  int Ka, N;
+  int TI, TJ, S;       // tiles along [A | 1] columns and Gm columns, splits
   int64_t rows_per_split;
   float* parts;        // [S][(Ka + 1) * N]
 };
 
-// transposed LDS tile: plane p, column c, 16-B chunk q (8 batch rows) of the
-// 16-row stage, 48 B per column (32 used): 12-word column stride, so the 16
-// lanes of one ds_read_b128 cycle (16 consecutive columns) hit 16 distinct
-// 4-bank groups, and the staging writes (8 row pairs x columns 4 apart per
-// instruction) spread over the banks (a 32-B stride put every 8th column on
-// the same 8 banks: 56 % of the LDS cycles were conflicts)
-constexpr int kWtColBytes = 48;
-__device__ __forceinline__ int wt_off(int ncols, int plane, int col, int chunk) {
-  return (plane * ncols + col) * kWtColBytes + (chunk << 4);
-}
+typedef __bf16 wg_bf16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) wg_bf16x4 lds_bf16x4_t;
 
 template <bool MASK>
 __global__ void __launch_bounds__(kWgThreads) mlp_wgrad_kernel(const WgradArgs a) {
-  constexpr int AC = kWgMaxIB * 32;   // A' columns staged (zero beyond Ka + 1)
-  constexpr int GC = kWgCols;         // G columns staged (this group's)
-  constexpr int STAGE_BYTES = 2 * (AC + GC) * kWtColBytes;
-  extern __shared__ __attribute__((aligned(16))) char wsm[];  // 2 stage buffers (dynamic: > 64 KiB)
-  char* const smem[2] = {wsm, wsm + STAGE_BYTES};
+  __shared__ __attribute__((aligned(16))) char wsm[2 * kWgStageB];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
   const int lane = lane_id();
-  const int l32 = lane & 31, h = lane >> 5;
-  // blockIdx -> (split, column group); XCD-grouped when S % 8 == 0
-  int split, cg;
+  // blockIdx -> (split, tile); the tiles of a split on one XCD when S % 8 == 0
+  const int tiles = a.TI * a.TJ;
+  int split, tile;
   {
     const int b = blockIdx.x;
     if (a.S % 8 == 0) {
       const int q = b >> 3;
-      cg = q % a.CG;
-      split = (q / a.CG) * 8 + (b & 7);
+      tile = q % tiles;
+      split = (q / tiles) * 8 + (b & 7);
     } else {
-      cg = b % a.CG;
-      split = b / a.CG;
+      tile = b % tiles;
+      split = b / tiles;
     }
   }
-  const int c0 = cg * GC;  // first output column of the group
+  const int i0 = (tile / a.TJ) * kWgTile;  // first [A | 1] column (= output row)
+  const int j0 = (tile % a.TJ) * kWgTile;  // first Gm column
   const int64_t r0 = static_cast<int64_t>(split) * a.rows_per_split;
   int64_t r1 = r0 + a.rows_per_split;
   if (r1 > a.M) r1 = a.M;
   const int nstage = r1 > r0 ? static_cast<int>((r1 - r0 + kWgBK - 1) / kWgBK) : 0;
   const float s = a.scale ? *a.scale : 1.0f;
 
-  // staging units: (row pair p of 16, column quad c).  A' has RP * AQ = 576
-  // units: every thread one, threads < 64 (wave 0) a second; G has RP * GQ
-  // = 128 units, on threads 256..383 (waves 4, 5).  Roles are per wave, so
-  // each load names ONE buffer descriptor (a per-lane choice between two made
-  // the compiler emit waterfall loops that drained every load).
-  constexpr int RP = kWgBK / 2;  // row pairs per stage
-  constexpr int AQ = AC / 4, GQ = GC / 4;
-  static_assert(RP * AQ == kWgThreads + 64 && RP * GQ == 128, "unit split below assumes Ka+1 <= 288, 64 G columns");
-  const bool a2 = tid < 64;                        // second A unit (wave 0)
-  const bool gu = tid >= 256 && tid < 256 + 128;   // G unit (waves 4, 5)
-  const int ua0 = tid, ua1 = kWgThreads + tid, ug = tid - 256;
-  // load-side units: every thread issues the same loads (threads without a
-  // second A unit / a G unit re-load lines their wave already fetches, L1
-  // hits), so the loop has no load branches and the compiler's vmcnt waits
-  // stay exact across the kWgDepth stages in flight
-  const int la1 = a2 ? ua1 : ua0, lg = tid & 127;
-  // kWgDepth stages of staged rows in registers: stage st + kWgDepth is
-  // loaded while stage st is computed (slot = st % kWgDepth, static under the
-  // unroll), raw (column limits applied by stash, so no load is waited on early)
-  f32x4 va0[kWgDepth][2], va1[kWgDepth][2], vg[kWgDepth][2];
-  f32x4 vm[kWgDepth][MASK ? 2 : 1];
-  // range-checked buffer loads: rows past the split and past M read as 0
+  // loader: thread t stages row t / 8 of a stage, columns 8 (t % 8) .. + 7 of
+  // both operand tiles; range-checked buffer loads (rows past the split read 0)
+  const int lrow = tid >> 3, lcol = (tid & 7) * 8;
   const __amdgpu_buffer_rsrc_t dA = mlp_desc(a.A + r0 * a.lda, static_cast<uint64_t>(r1 - r0) * a.lda * 4);
   const __amdgpu_buffer_rsrc_t dG = mlp_desc(a.G + r0 * a.ldg, static_cast<uint64_t>(r1 - r0) * a.ldg * 4);
   const __amdgpu_buffer_rsrc_t dM =
       mlp_desc(MASK ? a.gmask + r0 * a.ldgm : a.G, static_cast<uint64_t>(r1 - r0) * (MASK ? a.ldgm : a.ldg) * 4);
-  // per-lane byte offsets inside a stage (loop-invariant); the stage's row
-  // offset goes in the scalar soffset
   const unsigned lda4 = static_cast<unsigned>(a.lda) * 4, ldg4 = static_cast<unsigned>(a.ldg) * 4,
                  ldm4 = static_cast<unsigned>(MASK ? a.ldgm : a.ldg) * 4;
-  const unsigned oa0 = 2 * (ua0 % RP) * lda4 + (ua0 / RP) * 16;
-  const unsigned oa1 = 2 * (la1 % RP) * lda4 + (la1 / RP) * 16;
-  const unsigned og = 2 * (lg % RP) * ldg4 + (c0 + (lg / RP) * 4) * 4;
-  const unsigned om = 2 * (lg % RP) * ldm4 + (c0 + (lg / RP) * 4) * 4;
+  // columns past Ka (A) / N (Gm) are zeroed after the load (their loads read
+  // on into the row's padding or the next row, or 0 past the split)
+  const int ca = i0 + lcol, cg = j0 + lcol;
+  const unsigned oa = lrow * lda4 + static_cast<unsigned>(ca) * 4;
+  const unsigned og = lrow * ldg4 + static_cast<unsigned>(cg) * 4;
+  const unsigned om = lrow * ldm4 + static_cast<unsigned>(cg) * 4;
+  f32x4 va[kWgDepth][2], vg[kWgDepth][2], vm[kWgDepth][MASK ? 2 : 1];
   auto fetch = [&](int st, auto slot_c) {
     constexpr int SL = decltype(slot_c)::value;
     const unsigned sa = static_cast<unsigned>(st * kWgBK) * lda4, sg = static_cast<unsigned>(st * kWgBK) * ldg4,
                    sm = static_cast<unsigned>(st * kWgBK) * ldm4;
 #pragma unroll
-    for (int e2 = 0; e2 < 2; ++e2) {
-      va0[SL][e2] = mlp_load4s(dA, oa0 + e2 * lda4, sa);
-      va1[SL][e2] = mlp_load4s(dA, oa1 + e2 * lda4, sa);
-      vg[SL][e2] = mlp_load4s(dG, og + e2 * ldg4, sg);
-      if constexpr (MASK) vm[SL][e2] = mlp_load4s(dM, om + e2 * ldm4, sm);
+    for (int e = 0; e < 2; ++e) {
+      va[SL][e] = mlp_load4s(dA, oa + 16 * e, sa);
+      vg[SL][e] = mlp_load4s(dG, og + 16 * e, sg);
+      if constexpr (MASK) vm[SL][e] = mlp_load4s(dM, om + 16 * e, sm);
     }
   };
-  // one unit's 2 rows x 4 columns -> hi / lo bf16 planes of the transposed tile
-  auto put = [&](char* tb, int ncols, int pr, int c, int gc, int lim, bool isg, int st, const f32x4* v,
-                 const f32x4* m) {
-    const bool live0 = r0 + st * kWgBK + 2 * pr < r1, live1 = r0 + st * kWgBK + 2 * pr + 1 < r1;
+  // 8 values -> 16 B of hi and 16 B of lo at (plane pair, this thread's row, columns)
+  auto put8 = [&](char* base, const float (&x)[8]) {
+    unsigned hw[4], lw[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int col = gc + e;
-      const bool ones = !isg && col == a.Ka;  // the bias row of A' = [A | 1]^T
-      float x0 = col < lim ? v[0][e] : ((ones && live0) ? 1.0f : 0.0f);
-      float x1 = col < lim ? v[1][e] : ((ones && live1) ? 1.0f : 0.0f);
-      if (MASK && isg) {
-        x0 = m[0][e] > 0.0f ? x0 * s : 0.0f;
-        x1 = m[1][e] > 0.0f ? x1 * s : 0.0f;
-      }
-      const unsigned h0 = bf16_bits(x0), h1 = bf16_bits(x1);
-      const unsigned l0 = bf16_bits(x0 - bf16_val(h0)), l1 = bf16_bits(x1 - bf16_val(h1));
-      const int tcol = c + e, k = 2 * pr;  // tile column; rows k, k + 1 of the stage
-      *reinterpret_cast<unsigned*>(tb + wt_off(ncols, 0, tcol, k >> 3) + (k & 7) * 2) = h0 | (h1 << 16);
-      *reinterpret_cast<unsigned*>(tb + wt_off(ncols, 1, tcol, k >> 3) + (k & 7) * 2) = l0 | (l1 << 16);
+      const unsigned h0 = bf16_bits(x[2 * e]), h1 = bf16_bits(x[2 * e + 1]);
+      const unsigned l0 = bf16_bits(x[2 * e] - bf16_val(h0)), l1 = bf16_bits(x[2 * e + 1] - bf16_val(h1));
+      hw[e] = h0 | (h1 << 16);
+      lw[e] = l0 | (l1 << 16);
     }
+    char* p = base + lrow * kWgRowB + lcol * 2;
+    *reinterpret_cast<u32x4*>(p) = u32x4{hw[0], hw[1], hw[2], hw[3]};
+    *reinterpret_cast<u32x4*>(p + kWgPlaneB) = u32x4{lw[0], lw[1], lw[2], lw[3]};
   };
   auto stash = [&](int st, int buf, auto slot_c) {
     constexpr int SL = decltype(slot_c)::value;
-    char* base = smem[buf];
-    put(base, AC, ua0 % RP, (ua0 / RP) * 4, (ua0 / RP) * 4, a.Ka, false, st, va0[SL], nullptr);
-    if (a2) put(base, AC, ua1 % RP, (ua1 / RP) * 4, (ua1 / RP) * 4, a.Ka, false, st, va1[SL], nullptr);
-    if (gu) put(base + 2 * AC * kWtColBytes, GC, lg % RP, (lg / RP) * 4, c0 + (lg / RP) * 4, a.N, true, st, vg[SL],
-                MASK ? vm[SL] : nullptr);
-  };
-
-  const int jl = wave & 1;    // column block inside the group
-  const int ig = wave >> 1;   // row blocks ig, ig + 4, ig + 8
-  f32x16 acc[kWgIMax];
+    char* base = wsm + buf * kWgStageB;
+    const bool live = r0 + static_cast<int64_t>(st) * kWgBK + lrow < r1;
+    float x[8];
 #pragma unroll
-  for (int i = 0; i < kWgIMax; ++i) acc[i] = f32x16{};
-
-  if (nstage > 0) {
-    fetch(0, std::integral_constant<int, 0>());
-    fetch(1, std::integral_constant<int, 1>());
-    fetch(2, std::integral_constant<int, 2>());
-    fetch(3, std::integral_constant<int, 3>());
-    stash(0, 0, std::integral_constant<int, 0>());
-    lds_barrier();
-  }
-  // stage st: buffer st % 2, register slot st % kWgDepth
-  auto stage = [&](int st, auto slot_c) {
-    constexpr int SLOT = decltype(slot_c)::value;
-    constexpr int PAR = SLOT & 1;
-    constexpr int NEXT = (SLOT + 1) % kWgDepth;
-    fetch(st + kWgDepth, slot_c);  // the slot stage st came from (past the split: zeros, unused)
-    const char* base = smem[PAR];
-    const char* gb = base + 2 * AC * kWtColBytes;
-    {
-      const int chunk = h;
-      const int gcol = 32 * jl + l32;
-      const bf16x8 bh = *reinterpret_cast<const bf16x8*>(gb + wt_off(GC, 0, gcol, chunk));
-      const bf16x8 bl = *reinterpret_cast<const bf16x8*>(gb + wt_off(GC, 1, gcol, chunk));
-      // row blocks past Ka + 1 multiply zero fragments (the tile is zero
-      // there): no branches, and the three products of a block are issued
-      // one block apart (independent accumulators back to back)
-      bf16x8 ah[kWgIMax], al[kWgIMax];
-#pragma unroll
-      for (int i = 0; i < kWgIMax; ++i) {
-        const int col = min(32 * (ig + 4 * i), AC - 32) + l32;
-        ah[i] = *reinterpret_cast<const bf16x8*>(base + wt_off(AC, 0, col, chunk));
-        al[i] = *reinterpret_cast<const bf16x8*>(base + wt_off(AC, 1, col, chunk));
-      }
-#pragma unroll
-      for (int i = 0; i < kWgIMax; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh, acc[i], 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < kWgIMax; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl, acc[i], 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < kWgIMax; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh, acc[i], 0, 0, 0);
+    for (int e = 0; e < 8; ++e) {  // [A | 1]: the ones column is the bias row of the output
+      const int col = ca + e;
+      x[e] = col < a.Ka ? va[SL][e >> 2][e & 3] : ((col == a.Ka && live) ? 1.0f : 0.0f);
     }
-    lds_barrier();  // everyone is done reading the other buffer (read one stage ago)
-    stash(st + 1, 1 - PAR, std::integral_constant<int, NEXT>());
-    lds_barrier();
+    put8(base, x);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int col = cg + e;
+      float v = col < a.N ? vg[SL][e >> 2][e & 3] : 0.0f;
+      if constexpr (MASK) v = vm[SL][e >> 2][e & 3] > 0.0f ? v * s : 0.0f;
+      x[e] = v;
+    }
+    put8(base + 2 * kWgPlaneB, x);
   };
-  // branch-free body: every stage fetches, computes and stashes (stages past
-  // the split read zeros, which add nothing), so vmcnt waits stay exact; the
-  // stage count is rounded up to the 4x unroll
-  static_assert(kWgDepth == 4, "the stage loop below is unrolled 4x");
-  for (int st = 0; st < nstage; st += 4) {
-    stage(st, std::integral_constant<int, 0>());
-    stage(st + 1, std::integral_constant<int, 1>());
-    stage(st + 2, std::integral_constant<int, 2>());
-    stage(st + 3, std::integral_constant<int, 3>());
+
+  // fragments: 16-lane group g -> MFMA rows / columns 16 (g & 1) .. + 15 of
+  // the wave's 32-block, batch rows 8 (g >> 1) .. + 7 of the k-step; lane
+  // 4q + p of the group addresses row q, columns 4p .. 4p + 3
+  const int ib = wave & 1, jb = wave >> 1;
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int frow = 8 * (g >> 1) + q;
+  const int fa = frow * kWgRowB + (32 * ib + 16 * (g & 1) + 4 * p) * 2;
+  const int fg = 2 * kWgPlaneB + frow * kWgRowB + (32 * jb + 16 * (g & 1) + 4 * p) * 2;
+  auto frag = [&](const char* base, int off) {
+    const wg_bf16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(base + off));
+    const wg_bf16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(base + off + 4 * kWgRowB));
+    return __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  f32x16 acc = {};
+  auto compute = [&](int buf) {
+    const char* base = wsm + buf * kWgStageB;
+#pragma unroll
+    for (int ks = 0; ks < kWgBK / 16; ++ks) {
+      const int ko = ks * 16 * kWgRowB;
+      const bf16x8 ah = frag(base, fa + ko), al = frag(base + kWgPlaneB, fa + ko);
+      const bf16x8 gh = frag(base, fg + ko), gl = frag(base + kWgPlaneB, fg + ko);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, gh, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, gl, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, gh, acc, 0, 0, 0);
+    }
+  };
+
+  // pipeline: kWgDepth stages of loads in flight; stage st is stashed into
+  // buffer st % 2 right after its loads land, one barrier per stage (a wave
+  // passes it only after computing stage st - 1 from the other buffer)
+  static_assert(kWgDepth == 3, "the stage loop below is unrolled 3x");
+  fetch(0, std::integral_constant<int, 0>());
+  fetch(1, std::integral_constant<int, 1>());
+  fetch(2, std::integral_constant<int, 2>());
+  auto step = [&](int st, auto slot_c) {
+    stash(st, st & 1, slot_c);
+    fetch(st + kWgDepth, slot_c);  // past the split: zeros, unused
+    lds_barrier();
+    compute(st & 1);
+  };
+  // branch-free body (stages past the split stage zeros, which add nothing),
+  // so the compiler's vmcnt waits stay exact across the stages in flight
+  for (int st = 0; st < nstage; st += 3) {
+    step(st, std::integral_constant<int, 0>());
+    step(st + 1, std::integral_constant<int, 1>());
+    step(st + 2, std::integral_constant<int, 2>());
   }
 
-  // this group's slice of the split's partial [Ka + 1, N]: lane (l32, h),
-  // register r -> row 32 ib + (r & 3) + 8 (r >> 2) + 4 h, column c0 + 32 jl + l32
+  // this block of the split's partial: lane (l32, h), register r -> row
+  // 32 ib + (r & 3) + 8 (r >> 2) + 4 h, column 32 jb + l32
   const int rows_out = a.Ka + 1;
   float* P = a.parts + static_cast<int64_t>(split) * rows_out * a.N;
-  const int n = c0 + 32 * jl + l32;
+  const int n = j0 + 32 * jb + (lane & 31);
 #pragma unroll
-  for (int i = 0; i < kWgIMax; ++i) {
-    const int ib = ig + 4 * i;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = 32 * ib + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (ib < a.IB && n < a.N && row < rows_out) P[static_cast<int64_t>(row) * a.N + n] = acc[i][r];
-    }
+  for (int r = 0; r < 16; ++r) {
+    const int row = i0 + 32 * ib + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    if (n < a.N && row < rows_out) P[static_cast<int64_t>(row) * a.N + n] = acc[r];
   }
 }
 
@@ -768,30 +731,25 @@ extern "C" int tt_mlp_rows(const float* A, int64_t lda, const float* amask, int6
   return TT_OK;
 }
 
-// splits of the batch reduction: enough (split, column group) workgroups to
-// fill the chip, >= 64 rows each; a multiple of 8 when there are >= 8 (the
-// XCD grouping)
-static int wgrad_splits(int64_t M, int N) {
-  const int cg = (N + kWgCols - 1) / kWgCols;
-  // TT_WGRAD_WGS: workgroups to aim for.  Default 128 (half the CUs): in the
-  // train step the two towers' backward chains run side by side, and one
-  // workgroup per CU (256) starved the other tower (step 0.631 vs 0.617 ms)
-  // although it is the faster kernel alone (28 vs 44 us)
+// splits of the batch reduction: enough (split, tile) workgroups to fill
+// the chip about twice, >= 256 rows each; a multiple of 8 when there are >= 8
+// (the XCD grouping)
+static int wgrad_splits(int64_t M, int Ka, int N) {
+  const int tiles = static_cast<int>(ceil_div(Ka + 1, kWgTile) * ceil_div(N, kWgTile));
+  // TT_WGRAD_WGS: workgroups to aim for (default 1024: ~4 per CU, so the
+  // loads of co-resident workgroups hide each other's latency)
   static const int64_t target = [] {
     const char* e = std::getenv("TT_WGRAD_WGS");
-    return static_cast<int64_t>(e ? std::atoi(e) : 128);
+    return static_cast<int64_t>(e ? std::atoi(e) : 1024);
   }();
-  int64_t S = target / cg;
-  if (S > 128) S = 128;
-  const int64_t by_rows = M / 64;
-  if (S > by_rows) S = by_rows >= 8 ? by_rows / 8 * 8 : by_rows;
-  if (S < 1) S = 1;
+  int64_t S = 1;
+  while (S < 256 && tiles * S * 2 <= target && M / (2 * S) >= 128) S *= 2;
   return static_cast<int>(S);
 }
 
 extern "C" size_t tt_mlp_wgrad_workspace_size(int64_t M, int32_t Ka, int32_t N) {
   if (M < 0 || Ka < 0 || N < 1) return 0;
-  return static_cast<size_t>(wgrad_splits(M, N)) * (Ka + 1) * N * sizeof(float);
+  return static_cast<size_t>(wgrad_splits(M, Ka, N)) * (Ka + 1) * N * sizeof(float);
 }
 
 extern "C" int tt_mlp_wgrad(const float* A, int64_t lda, const float* G, int64_t ldg, const float* gmask,
@@ -799,14 +757,19 @@ extern "C" int tt_mlp_wgrad(const float* A, int64_t lda, const float* G, int64_t
                             void* workspace, size_t workspace_bytes, tt_stream_t stream) {
   clear_error();
   TT_REQUIRE(A && G && dwb, "tt_mlp_wgrad: NULL A/G/dwb");
-  TT_REQUIRE(M >= 0 && Ka >= 1 && Ka + 1 <= kWgMaxIB * 32, "tt_mlp_wgrad: Ka=%d outside [1, %d]", Ka,
-             kWgMaxIB * 32 - 1);
-  TT_REQUIRE(N >= 1 && N <= 256 && N % 4 == 0, "tt_mlp_wgrad: N=%d must be a multiple of 4 in [4, 256]", N);
+  TT_REQUIRE(M >= 0 && Ka >= 1 && Ka <= 4096, "tt_mlp_wgrad: Ka=%d outside [1, 4096]", Ka);
+  TT_REQUIRE(N >= 4 && N <= 4096 && N % 4 == 0, "tt_mlp_wgrad: N=%d must be a multiple of 4 in [4, 4096]", N);
   TT_REQUIRE(lda >= Ka && ldg >= N && (!gmask || ldgm >= N), "tt_mlp_wgrad: leading dimension too small");
-  TT_REQUIRE(ldg % 4 == 0 && reinterpret_cast<uintptr_t>(G) % 16 == 0 &&
+  // 16-B vector loads of 8-column groups
+  TT_REQUIRE(lda % 4 == 0, "tt_mlp_wgrad: lda must be a multiple of 4");
+  TT_REQUIRE(reinterpret_cast<uintptr_t>(A) % 16 == 0 && ldg % 4 == 0 && reinterpret_cast<uintptr_t>(G) % 16 == 0 &&
                  (!gmask || (ldgm % 4 == 0 && reinterpret_cast<uintptr_t>(gmask) % 16 == 0)),
-             "tt_mlp_wgrad: G / gmask rows must be 16-B aligned");
-  const int S = wgrad_splits(M, N);
+             "tt_mlp_wgrad: A / G / gmask rows must be 16-B aligned");
+  const int S = wgrad_splits(M, Ka, N);
+  const int64_t rps = round_up(ceil_div(M > 0 ? M : 1, S), kWgBK);
+  // per-split byte offsets are 32-bit (buffer loads)
+  TT_REQUIRE(rps * std::max<int64_t>(lda, std::max<int64_t>(ldg, gmask ? ldgm : 0)) * 4 < (int64_t(1) << 31),
+             "tt_mlp_wgrad: a split's rows exceed 2 GiB");
   TT_REQUIRE(workspace && workspace_bytes >= tt_mlp_wgrad_workspace_size(M, Ka, N),
              "tt_mlp_wgrad: workspace %zu < %zu", workspace_bytes, tt_mlp_wgrad_workspace_size(M, Ka, N));
   WgradArgs a{};
@@ -820,22 +783,15 @@ extern "C" int tt_mlp_wgrad(const float* A, int64_t lda, const float* G, int64_t
   a.M = M;
   a.Ka = Ka;
   a.N = N;
-  a.IB = (Ka + 1 + 31) / 32;
-  a.CG = (N + kWgCols - 1) / kWgCols;
+  a.TI = static_cast<int>(ceil_div(Ka + 1, kWgTile));
+  a.TJ = static_cast<int>(ceil_div(N, kWgTile));
   a.S = S;
-  a.rows_per_split = round_up(ceil_div(M > 0 ? M : 1, S), kWgBK);
+  a.rows_per_split = rps;
   a.parts = static_cast<float*>(workspace);
   hipStream_t st = to_stream(stream);
-  const dim3 grid(static_cast<unsigned>(S * a.CG));
-  constexpr int shm = 2 * 2 * (kWgMaxIB * 32 + kWgCols) * kWtColBytes;
-  static const hipError_t attr_t = hipFuncSetAttribute(reinterpret_cast<const void*>(mlp_wgrad_kernel<true>),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, shm);
-  static const hipError_t attr_f = hipFuncSetAttribute(reinterpret_cast<const void*>(mlp_wgrad_kernel<false>),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, shm);
-  TT_CHECK_HIP(attr_t);
-  TT_CHECK_HIP(attr_f);
-  if (gmask) hipLaunchKernelGGL((mlp_wgrad_kernel<true>), grid, dim3(kWgThreads), shm, st, a);
-  else hipLaunchKernelGGL((mlp_wgrad_kernel<false>), grid, dim3(kWgThreads), shm, st, a);
+  const dim3 grid(static_cast<unsigned>(S * a.TI * a.TJ));
+  if (gmask) hipLaunchKernelGGL((mlp_wgrad_kernel<true>), grid, dim3(kWgThreads), 0, st, a);
+  else hipLaunchKernelGGL((mlp_wgrad_kernel<false>), grid, dim3(kWgThreads), 0, st, a);
   TT_CHECK_LAUNCH();
   const int64_t len = static_cast<int64_t>(Ka + 1) * N;
   hipLaunchKernelGGL(mlp_sum_parts_kernel, dim3(ceil_div(len, 256)), dim3(1024), 0, st, a.parts, S, len, dwb);

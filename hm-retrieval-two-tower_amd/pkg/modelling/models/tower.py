@@ -228,7 +228,7 @@ class DenseStack:
         below: G_{l-1} = (G_l W_l^T) * relu'(h_{l-1}) with db_{l-1} = colsum
         G_{l-1} in its epilogue (the ReluGrad / BiasAddGrad pair fused), or the
         input gradient dx = G_1 W_1^T (16-B padded rows, returned as a view)."""
-        if WGRAD_KERNEL == "tt" and gout.is_cuda and self._wgrad_fits(gout):
+        if WGRAD_KERNEL == "tt" and gout.is_cuda and self._wgrad_fits(gout, acts):
             return self._backward_mlp_tt(acts, flat, gout, gscale, need_input_grad)
         gflat = torch.empty_like(flat)
         params = self.params(flat)
@@ -267,12 +267,13 @@ class DenseStack:
             joins.append(ws)
         return dx, gflat
 
-    def _wgrad_fits(self, gout: torch.Tensor) -> bool:
-        """tt_mlp_wgrad's shape contract: N % 4 == 0, N <= 256, Ka + 1 <= 288,
-        16-B aligned gradient rows."""
-        if gout.stride(1) != 1 or gout.stride(0) % 4 or gout.data_ptr() % 16:
-            return False
-        return all(fo % 4 == 0 and fo <= 256 and fi + 1 <= 288 for _, fi, fo, _ in self.layout)
+    def _wgrad_fits(self, gout: torch.Tensor, acts: List[torch.Tensor]) -> bool:
+        """tt_mlp_wgrad's contract: N % 4 == 0, 16-B aligned rows of the
+        activations and gradients (16-B vector loads)."""
+        for t in [gout] + list(acts):
+            if t.stride(1) != 1 or t.stride(0) % 4 or t.data_ptr() % 16:
+                return False
+        return all(fo % 4 == 0 and fo <= 4096 and fi <= 4096 for _, fi, fo, _ in self.layout)
 
     def _backward_mlp_tt(self, acts: List[torch.Tensor], flat: torch.Tensor, gout: torch.Tensor,
                          gscale: Optional[torch.Tensor], need_input_grad: bool):

@@ -14,7 +14,7 @@ agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in a.csv:
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if a.match not in k:
+        if not any(m in k for m in a.match.split("\\|")):
             continue
         agg[k[:90]][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in agg.items():
