@@ -470,12 +470,19 @@ __global__ void __launch_bounds__(kWgThreads) mlp_wgrad_kernel(const WgradArgs a
   // buffer st % 2 right after its loads land, one barrier per stage (a wave
   // passes it only after computing stage st - 1 from the other buffer)
   static_assert(kWgDepth == 3, "the stage loop below is unrolled 3x");
-  fetch(0, std::integral_constant<int, 0>());
+  fetch(0, std::integral_constant<int, 0>());  // issued in stage order (the waits count on it)
+  __builtin_amdgcn_sched_barrier(0);
   fetch(1, std::integral_constant<int, 1>());
+  __builtin_amdgcn_sched_barrier(0);
   fetch(2, std::integral_constant<int, 2>());
   auto step = [&](int st, auto slot_c) {
+    // nothing crosses a step boundary: the scheduler would otherwise hoist the
+    // later steps' conversions to the loop top and wait for every load there
+    __builtin_amdgcn_sched_barrier(0);
     stash(st, st & 1, slot_c);
+    __builtin_amdgcn_sched_barrier(0);
     fetch(st + kWgDepth, slot_c);  // past the split: zeros, unused
+    __builtin_amdgcn_sched_barrier(0);
     lds_barrier();
     compute(st & 1);
   };

@@ -67,12 +67,20 @@ def _mirror(m):
     return ref
 
 
-def _train_steps_vs_cpu(cuda, emb, joint, B, steps, loss_rtol, upd_rtol):
+def _train_steps_vs_cpu(cuda, emb, joint, B, steps, loss_rtol, upd_rtol0, upd_rtol):
     """`steps` full train steps of the main.py schema at (emb, joint, towers
     [256]) and batch B, each vs oracle.CpuTwoTower started from the model's
     state before that step: the loss within loss_rtol and the update of every
     table (touched rows) and MLP buffer within upd_rtol (relative 2-norm of
-    the update difference).  Returns the observed relative errors."""
+    the update difference): upd_rtol0 at the first step (random init: the
+    bf16 in-batch operands move each update by ~2^-9 relative), upd_rtol
+    after it.  Adagrad's first step moves every touched parameter by ~lr =
+    0.05, so from the second step the in-batch scores are O(100) and the
+    softmax rows nearly one-hot: dS = P - I is then a small difference of
+    large terms and the bf16 rounding of the scores (~2^-8 |s|, tens of
+    percent of a row's off-diagonal mass) is amplified in the summed updates
+    while the loss stays within loss_rtol.  Returns the observed relative
+    errors."""
     schema = bench.main_schema(emb_big=emb, joint=joint, hidden=(256,))
     data = bench.SyntheticHM(cuda, seed=7)
     schema.set_candidate_prob_lookup(data.prob_lookup())
@@ -103,7 +111,7 @@ def _train_steps_vs_cpu(cuda, emb, joint, B, steps, loss_rtol, upd_rtol):
         mlp_before = [t.dense.flat.detach().cpu().numpy().copy() for t in m.towers]
         rl = ref.step([b[f.name].cpu().numpy() for f in qf], [b[f.name].cpu().numpy() for f in cf], lq)
         gl = float(m.train_step(b)["loss"].item())
-        errs[f"loss{step}"] = abs(gl - rl) / abs(rl)
+        errs[("loss", step)] = abs(gl - rl) / abs(rl)
         assert abs(gl - rl) <= loss_rtol * abs(rl), (step, gl, rl)
         refs = {}
         for feats, tabs in ((qf, ref.q_tables), (cf, ref.c_tables)):
@@ -114,28 +122,29 @@ def _train_steps_vs_cpu(cuda, emb, joint, B, steps, loss_rtol, upd_rtol):
                 r = rows[n]
                 got = tab.weight[torch.as_tensor(r, device=cuda).long()].cpu().numpy()
                 d_gpu, d_ref = got - before[n], refs[n][r] - before[n]
-                errs[f"{n}{step}"] = np.linalg.norm(d_gpu - d_ref) / np.linalg.norm(d_ref)
+                errs[(n, step)] = np.linalg.norm(d_gpu - d_ref) / np.linalg.norm(d_ref)
         flat = lambda layers: np.concatenate([np.concatenate([w.reshape(-1), bb]) for w, bb in layers])
         for ti, (t, mb, rlay) in enumerate(zip(m.towers, mlp_before, (ref.q_layers, ref.c_layers))):
             d_gpu = t.dense.flat.detach().cpu().numpy() - mb
             d_ref = flat(rlay) - mb
-            errs[f"mlp{ti}_{step}"] = np.linalg.norm(d_gpu - d_ref) / np.linalg.norm(d_ref)
+            errs[(f"mlp{ti}", step)] = np.linalg.norm(d_gpu - d_ref) / np.linalg.norm(d_ref)
         del ref
-    print({k: f"{v:.2e}" for k, v in errs.items()})
-    bad = {k: v for k, v in errs.items() if not k.startswith("loss") and not v <= upd_rtol}
+    print({f"{k[0]}@{k[1]}": f"{v:.2e}" for k, v in errs.items()})
+    bad = {k: v for k, v in errs.items()
+           if not k[0].startswith("loss") and not v <= (upd_rtol0 if k[1] == 0 else upd_rtol)}
     assert not bad, bad
     m.optimizer.check_status(cuda)
     return errs
 
 
 def test_c2_train_steps_match_cpu_restatement(cuda):
-    _train_steps_vs_cpu(cuda, 64, 64, 4096, 3, 1e-3, 1e-2)
+    _train_steps_vs_cpu(cuda, 64, 64, 4096, 3, 1e-3, 5e-3, 5e-2)
 
 
 def test_c3_train_steps_match_cpu_restatement(cuda):
     """configs[2], the headline train config: the main.py schema at D = E =
     128, H&M vocabularies, towers [256] -> 128, logQ, Adagrad, B = 16384."""
-    _train_steps_vs_cpu(cuda, 128, 128, 16384, 3, 1e-3, 1e-2)
+    _train_steps_vs_cpu(cuda, 128, 128, 16384, 3, 1e-3, 5e-3, 5e-2)
 
 
 def _c4_data(cuda, Q, seed=2):
