@@ -924,7 +924,7 @@ struct FinalArgs {
   int64_t zero_base;    // id of row 0 in the output numbering (zero queries)
   int dim;
   int k;
-  int L;                // LDS list capacity
+  int L;                // LDS capacity: the whole screened list when it fits (staged), then the cut
   int P;                // bitonic sort size (pow2 >= k)
   int vec4;             // candidate rows are 16-byte aligned float4 rows
   int64_t nq;
@@ -935,6 +935,9 @@ struct FinalArgs {
   int32_t* out_i;
   int* fail_count;
   int* fail_list;
+  // candidate-sharded two-phase form (tt_bruteforce_shard_*):
+  float* kth_lb;        // select pass: per query lb(k-th screened score) (-inf: certificate failed), then stop
+  const float* floor;   // rescore pass: per query lower bound on the GLOBAL k-th exact score
 };
 
 __host__ __device__ inline size_t final_lds_bytes(int L, int P) {
@@ -959,6 +962,10 @@ __global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
   int32_t* out_i = a.out_i + q * K;
   const int fl = a.qflags[q];
   if (fl & kQZero) {  // every score is exactly +0: indices 0..k-1 by the tie rule
+    if (a.kth_lb) {
+      if (lane == 0) a.kth_lb[q] = 0.0f;
+      return;
+    }
     for (int t = lane; t < K; t += kWave) {
       out_s[t] = 0.0f;
       out_i[t] = static_cast<int32_t>(a.zero_base + t);
@@ -978,10 +985,34 @@ __global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
   tmax = Ls.tau[q];
   fail = fail || ntot < K;
   float X = -INFINITY;
+  // the whole list read once into LDS when it fits (the select's passes and
+  // the cut then read LDS, not the lists in memory)
+  const bool staged = !fail && ntot <= a.L;
+  if (staged) {
+    int n0 = 0;
+    for (int j = 0; j < Ls.nseg; ++j) {
+      const int c = seg_count(Ls, q, j);
+      const uint2* e = seg_ptr(Ls, q, j);
+      for (int i = lane; i < c; i += kWave) {
+        const uint2 en = e[i];
+        sc[n0 + i] = __uint_as_float(en.x);
+        id[n0 + i] = en.y;
+      }
+      n0 += c;
+    }
+    wsync();
+  }
   if (!fail) {
     // K-th largest screened score to a 24-bit key prefix (rounded down)
     const Kth r = radix_select(
         [&](unsigned prefix, unsigned hi_mask, int shift) {
+          if (staged) {
+            for (int i = lane; i < ntot; i += kWave) {
+              const unsigned key = float_order_key(sc[i]);
+              if ((key & hi_mask) == prefix) atomicAdd(&hist[(key >> shift) & 0xFFu], 1u);
+            }
+            return;
+          }
           for (int j = 0; j < Ls.nseg; ++j) {
             const int c = seg_count(Ls, q, j);
             const uint2* e = seg_ptr(Ls, q, j);
@@ -1002,8 +1033,28 @@ __global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
       if (fail) TT_STAT0(1, 1);
     }
   }
+  if (a.kth_lb) {  // select pass: at least K rows of these candidates score >= X exactly
+    if (lane == 0) a.kth_lb[q] = fail ? -INFINITY : X;
+    return;
+  }
+  // a member of the global top-K scores >= floor: only those can matter
+  if (a.floor) X = fmaxf(X, a.floor[q]);
   int n = 0;
-  if (!fail) {
+  if (!fail && staged) {
+    for (int e = lane; e < a.dim; e += kWave) qs[e] = a.q[q * a.ldq + e];
+    // in-place compaction of the kept ids (writes never pass the reads)
+    for (int i0 = 0; i0 < ntot; i0 += kWave) {
+      const int i = i0 + lane;
+      const float sv = i < ntot ? sc[i] : 0.0f;
+      const unsigned iv = i < ntot ? id[i] : 0u;
+      const bool keepit = i < ntot && ub_of(sv, m, rel) >= X;
+      const uint64_t bm = __ballot(keepit);
+      wsync();
+      if (keepit) id[n + __popcll(bm & lanemask_lt64())] = iv;
+      n += __popcll(bm);
+      wsync();
+    }
+  } else if (!fail) {
     for (int e = lane; e < a.dim; e += kWave) qs[e] = a.q[q * a.ldq + e];
     for (int j = 0; j < Ls.nseg && !fail; ++j) {
       const int c = seg_count(Ls, q, j);
@@ -1042,7 +1093,12 @@ __global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
   wsync();
   float kth;
   n = exact_select(sc, id, n, K, &kth, hist);
-  rank_and_write(sc, id, n, K, a.P, sk, out_s, out_i);
+  rank_and_write(sc, id, n, min(n, K), a.P, sk, out_s, out_i);
+  // with a floor fewer than K may remain: pad (sorts after every real entry)
+  for (int t = n + lane; t < K; t += kWave) {
+    out_s[t] = -INFINITY;
+    out_i[t] = 0x7FFFFFFF;
+  }
 }
 
 // Exact fallback for the queries the finalize could not certify.  A
@@ -1204,7 +1260,7 @@ __global__ void __launch_bounds__(kFbWaves * kWave) fallback_kernel(const Fallba
 
 // ---- host plan -------------------------------------------------------------
 struct SearchPlan {
-  int S, NS, jsel, cap, L, P, k, parts;
+  int S, NS, jsel, cap, L, LF, P, k, parts;
   int64_t chunk;
 };
 
@@ -1218,6 +1274,7 @@ SearchPlan plan_search(int64_t nq, int64_t n_rows, int k, int shards) {
   p.k = k;
   p.parts = 8192 / k < 1 ? 1 : (8192 / k > 64 ? 64 : 8192 / k);
   p.L = static_cast<int>(round_up(2 * static_cast<int64_t>(k) + 256, kWave));
+  p.LF = p.L > 1024 ? p.L : 1024;  // finalize: a query's whole list (~3k + 100 entries) fits
   const int64_t qblocks = ceil_div(nq > 0 ? nq : 1, kQPerWG);
   p.S = 1;  // enough workgroups for the 256 CUs: split the candidates of few query blocks
   while (p.S < kMaxSplits && qblocks * p.S < 256 && ntiles / (2 * p.S) >= 64) p.S *= 2;
@@ -1337,7 +1394,7 @@ int run_scan(int D, const void* index, int64_t row0, int64_t row1, int64_t nq, c
 }
 
 int run_finalize(const FinalArgs& fa, const FallbackArgs& fb, int64_t nq, const SearchPlan& p, hipStream_t st) {
-  const size_t shm = final_lds_bytes(p.L, p.P);
+  const size_t shm = final_lds_bytes(p.LF, p.P);
   if (shm > 65536)
     TT_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(finalize_kernel),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(shm)));
@@ -1428,12 +1485,112 @@ extern "C" int tt_bruteforce_search(const void* index, const float* cand, int64_
     if (int rc = run_estimate(D, index, 0, n_cand, nq, p, w, w.tau, st)) return rc;
     if (int rc = run_scan(D, index, 0, n_cand, nq, p, w, w.tau, static_cast<unsigned>(index_offset), st)) return rc;
     Lists ls{w.buf, w.count, w.tau, p.S, p.cap, nullptr, p.S, 1};
-    FinalArgs fa{qc, ldq, cand, ldc, n_cand, index_offset, index_offset, dim, k, p.L, p.P, vec4,
-                 nq, w.qflags, w.qmarg, ls, out_scores + q0 * k, out_idx + q0 * k, w.fail_count, w.fail_list};
+    FinalArgs fa{qc, ldq, cand, ldc, n_cand, index_offset, index_offset, dim, k, p.LF, p.P, vec4,
+                 nq, w.qflags, w.qmarg, ls, out_scores + q0 * k, out_idx + q0 * k, w.fail_count, w.fail_list,
+                 nullptr, nullptr};
     FallbackArgs fb{qc, ldq, cand, ldc, n_cand, index_offset, dim, k, p.L, p.P, p.parts, vec4,
                     w.fail_count, w.fail_list, w.fail_count + 1, w.fb_scratch, w.fb_scratch_n,
                     out_scores + q0 * k, out_idx + q0 * k};
     if (int rc = run_finalize(fa, fb, nq, p, st)) return rc;
   }
   return TT_OK;
+}
+
+// ---- candidate-sharded two-phase search (ShardedBruteForceIndex) ----------
+// A shard's exact top-k over its own rows, cut by a lower bound on the GLOBAL
+// k-th score so each shard rescores only its share of the global candidates:
+//   screen   (this shard) prep + estimate + scan + the finalize's select:
+//            kth_lb[q] = lb(k-th largest screened score) — at least k rows of
+//            the shard, hence of the whole matrix, score >= it exactly;
+//   (caller) floor = all_reduce(MAX) of kth_lb over the shards;
+//   finalize rescoring of the entries with ub(s~) >= max(own cut, floor):
+//            every member of the global top-k on this shard is among them
+//            (it is in the shard's top-k and scores >= the global k-th >=
+//            floor), so the merged lists hold the global top-k exactly; fewer
+//            than k are padded with (-inf, INT32_MAX).
+// Queries whose certificate fails are scanned exactly over the shard's rows.
+// One chunk of <= tt_bruteforce_shard_chunk(...) queries per call pair; the
+// pair shares the workspace (its lists live there between the two calls).
+extern "C" int64_t tt_bruteforce_shard_chunk(int64_t n_queries, int64_t n_cand, int32_t dim, int32_t k) {
+  if (n_queries < 1 || n_cand < 1 || k < 1 || pick_dpad(dim) == 0) return 0;
+  return plan_search(n_queries, n_cand, k, 1).chunk;
+}
+
+extern "C" size_t tt_bruteforce_shard_workspace_size(int64_t n_queries, int64_t n_cand, int32_t dim, int32_t k) {
+  return tt_bruteforce_workspace_size(n_queries, n_cand, dim, k);
+}
+
+namespace {
+int shard_check(const char* fn, const void* index, int64_t n_cand, int32_t dim, int64_t n_queries, int32_t k,
+                void* workspace, size_t workspace_bytes, const SearchPlan& p, SearchWs* w) {
+  TT_REQUIRE(index, "%s: NULL index", fn);
+  TT_REQUIRE(n_cand >= 1 && dim >= 1, "%s: bad shapes", fn);
+  if (pick_dpad(dim) == 0) return fail(TT_ERR_UNSUPPORTED, "%s: dim=%d > 128", fn, dim);
+  TT_REQUIRE(k >= 1 && k <= n_cand && k <= 4000, "%s: bad k=%d", fn, k);
+  TT_REQUIRE(n_queries >= 1 && n_queries <= p.chunk, "%s: n_queries=%lld outside [1, chunk %lld]", fn,
+             static_cast<long long>(n_queries), static_cast<long long>(p.chunk));
+  Carver cv(workspace, workspace_bytes);
+  *w = carve_search(cv, pick_dpad(dim), p, true, true);
+  if (!workspace || cv.used() > workspace_bytes)
+    return fail(TT_ERR_WORKSPACE, "%s: workspace %zu < required %zu", fn, workspace_bytes, cv.used());
+  return TT_OK;
+}
+}  // namespace
+
+extern "C" int tt_bruteforce_shard_screen(const void* index, int64_t n_cand, int32_t dim, const float* queries,
+                                          int64_t ldq, int64_t n_queries, int32_t k, int64_t index_offset,
+                                          float* kth_lb, void* workspace, size_t workspace_bytes,
+                                          tt_stream_t stream) {
+  clear_error();
+  const SearchPlan p = plan_search(n_queries, n_cand, k, 1);
+  SearchWs w;
+  if (int rc = shard_check("tt_bruteforce_shard_screen", index, n_cand, dim, n_queries, k, workspace,
+                           workspace_bytes, p, &w))
+    return rc;
+  TT_REQUIRE(queries && kth_lb && ldq >= dim, "tt_bruteforce_shard_screen: NULL queries/kth_lb or bad ldq");
+  TT_REQUIRE(index_offset >= 0 && index_offset + n_cand < (1ll << 31),
+             "tt_bruteforce_shard_screen: index_offset range");
+  const int D = pick_dpad(dim);
+  hipStream_t st = to_stream(stream);
+  if (int rc = run_prep(queries, ldq, n_queries, dim, D, index, w, true, st)) return rc;
+  if (int rc = run_estimate(D, index, 0, n_cand, n_queries, p, w, w.tau, st)) return rc;
+  // the lists carry the ids the finalize call outputs (index_offset + row)
+  if (int rc = run_scan(D, index, 0, n_cand, n_queries, p, w, w.tau, static_cast<unsigned>(index_offset), st))
+    return rc;
+  Lists ls{w.buf, w.count, w.tau, p.S, p.cap, nullptr, p.S, 1};
+  FinalArgs fa{queries, ldq, nullptr, 0, n_cand, index_offset, index_offset, dim, k, p.LF, p.P, 0,
+               n_queries, w.qflags, w.qmarg, ls, nullptr, nullptr, nullptr, nullptr, kth_lb, nullptr};
+  const size_t shm = final_lds_bytes(p.LF, p.P);
+  if (shm > 65536)
+    TT_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(finalize_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(shm)));
+  hipLaunchKernelGGL(finalize_kernel, dim3(n_queries), dim3(kWave), shm, st, fa);
+  TT_CHECK_LAUNCH();
+  return TT_OK;
+}
+
+extern "C" int tt_bruteforce_shard_finalize(const void* index, const float* cand, int64_t ldc, int64_t n_cand,
+                                            int32_t dim, const float* queries, int64_t ldq, int64_t n_queries,
+                                            int32_t k, int64_t index_offset, const float* floor, float* out_scores,
+                                            int32_t* out_idx, void* workspace, size_t workspace_bytes,
+                                            tt_stream_t stream) {
+  clear_error();
+  const SearchPlan p = plan_search(n_queries, n_cand, k, 1);
+  SearchWs w;
+  if (int rc = shard_check("tt_bruteforce_shard_finalize", index, n_cand, dim, n_queries, k, workspace,
+                           workspace_bytes, p, &w))
+    return rc;
+  TT_REQUIRE(cand && ldc >= dim && queries && ldq >= dim && floor && out_scores && out_idx,
+             "tt_bruteforce_shard_finalize: NULL argument or bad leading dimension");
+  TT_REQUIRE(index_offset >= 0 && index_offset + n_cand < (1ll << 31),
+             "tt_bruteforce_shard_finalize: index_offset range");
+  hipStream_t st = to_stream(stream);
+  const int vec4 = is_vec4(cand, ldc, dim) ? 1 : 0;
+  TT_CHECK_HIP(hipMemsetAsync(w.fail_count, 0, (2 + kFbSlots) * sizeof(int), st));
+  Lists ls{w.buf, w.count, w.tau, p.S, p.cap, nullptr, p.S, 1};
+  FinalArgs fa{queries, ldq, cand, ldc, n_cand, index_offset, index_offset, dim, k, p.LF, p.P, vec4,
+               n_queries, w.qflags, w.qmarg, ls, out_scores, out_idx, w.fail_count, w.fail_list, nullptr, floor};
+  FallbackArgs fb{queries, ldq, cand, ldc, n_cand, index_offset, dim, k, p.L, p.P, p.parts, vec4,
+                  w.fail_count, w.fail_list, w.fail_count + 1, w.fb_scratch, w.fb_scratch_n, out_scores, out_idx};
+  return run_finalize(fa, fb, n_queries, p, st);
 }

@@ -89,6 +89,7 @@ struct TableDesc {
   int32_t n_pad;       // region size, multiple of kBlock
   int32_t lanes;       // P: lanes per block slot (pow2 <= 64)
   int32_t wave_begin;  // first global wave of this table in the block kernels
+  int32_t chunk_begin; // first global chunk of this table in the chunked sort
   int64_t piece_off;   // first float of this table's pieces [blocks][2][dim]
 };
 
@@ -102,6 +103,8 @@ struct Job {
   const uint32_t* keys;  // sorted
   const uint32_t* vals;  // sorted
   float* pieces;
+  uint32_t* chunk_hist;  // chunked sort of small tables: digit counts [chunks][256]
+  int32_t num_chunks;
   float* dense_out;      // kWriteSum: per-sorted-index segment sums [total][dim_max]
   int32_t dense_dim;
   SparseHeader* hdr;     // workspace header
@@ -447,6 +450,272 @@ __global__ void __launch_bounds__(kLsThreads) region_sort_kernel(const Job j) {
   }
 }
 
+// Chunked region sort (default): the same stable sort of every region by
+// (row key, position), spread over many small workgroups so that it finishes
+// in a few microseconds wherever the graph places it and sits beside other
+// kernels on a CU (~13 KB of LDS instead of 150 KB).
+//   chunk_sort_kernel: one 256-thread workgroup per kChunk consecutive
+//   positions of a region sorts them in LDS (the LSD passes above, 8 tiles per
+//   wave) into the key/value staging buffers: chunk-sorted row keys and
+//   region positions; small tables (<= 8 key bits) also write the chunk's
+//   digit counts.
+//   chunk_merge_kernel: the final slot of a chunk's i-th element with row key
+//   k is i + #{keys <= k in earlier chunks} + #{keys < k in later chunks}
+//   (stable: equal keys keep chunk order, and chunks are in position order),
+//   found by binary search of each other chunk's sorted keys staged in LDS
+//   (regions <= kLdsSortMax: <= 8 chunks), or for small tables from the
+//   digit counts of all chunks (any region size).
+constexpr int kChunk = 2048;
+constexpr int kCsThreads = 256;
+constexpr int kCsWaves = kCsThreads / kWave;
+constexpr int kCsTiles = kChunk / kCsThreads;
+constexpr int kCsHistStride = kCsWaves + 1;
+constexpr int kChunkMaxSmall = 64 * kChunk;  // small tables: the merge reads every chunk's counts
+
+__device__ __forceinline__ int table_of_chunk(const Job& j, int c) {
+  int t = 0;
+#pragma unroll 1
+  for (int i = 1; i < j.num; ++i)
+    if (c >= j.t[i].chunk_begin) t = i;
+  return __builtin_amdgcn_readfirstlane(t);
+}
+
+__device__ __forceinline__ Region region_of(const Job& j, int t) {
+  const TableDesc& T = j.t[t];
+  Region R;
+  R.ids0 = T.ids[0];
+  R.ids1 = T.ids[1];
+  R.ids2 = T.ids[2];
+  R.ids3 = T.ids[3];
+  R.batch = j.batch;
+  R.keys = const_cast<uint32_t*>(j.keys) + T.base;
+  R.vals = const_cast<uint32_t*>(j.vals) + T.base;
+  R.n = T.n;
+  R.nr = static_cast<uint32_t>(T.num_rows);
+  R.khi = static_cast<uint32_t>(t) << j.id_bits;
+  R.invalid = (1u << j.id_bits) - 1u;
+  return R;
+}
+
+// hist[digit][wave] (row stride kCsHistStride) -> exclusive offsets in
+// (digit, wave) order; 4 entries per thread
+__device__ __forceinline__ void cs_scan_counts(uint32_t* hist, uint32_t* wsum) {
+  const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
+  __syncthreads();
+  uint32_t h[4], run = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int L = 4 * tid + u;
+    h[u] = hist[(L / kCsWaves) * kCsHistStride + L % kCsWaves];
+    run += h[u];
+  }
+  uint32_t inc = run;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, kWave);
+    if (lane >= o) inc += y;
+  }
+  if (lane == kWave - 1) wsum[w] = inc;
+  __syncthreads();
+  uint32_t ex = inc - run;
+  for (int v = 0; v < w; ++v) ex += wsum[v];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int L = 4 * tid + u;
+    hist[(L / kCsWaves) * kCsHistStride + L % kCsWaves] = ex;
+    ex += h[u];
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(kCsThreads) chunk_sort_kernel(const Job j) {
+  __shared__ uint32_t lkey[kChunk];
+  __shared__ uint16_t pbuf[2][kChunk];
+  __shared__ uint32_t hist[256 * kCsHistStride];
+  __shared__ uint32_t wsum[kCsWaves];
+  const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
+  const int t = table_of_chunk(j, blockIdx.x);
+  const Region R = region_of(j, t);
+  const int c0 = (static_cast<int>(blockIdx.x) - j.t[t].chunk_begin) * kChunk;
+  const int n = min(kChunk, j.t[t].n_pad - c0);
+  uint32_t* ck = j.keys_in + j.t[t].base + c0;  // chunk-sorted row keys
+  uint32_t* cp = j.vals_in + j.t[t].base + c0;  // their region positions
+  if (blockIdx.x == 0 && tid == 0) {  // stamp the workspace with this call's fingerprint
+    if (j.hdr->magic != kHdrMagic) {
+      j.hdr->error = 0u;
+      j.hdr->magic = kHdrMagic;
+    }
+    j.hdr->fp0 = j.fp0;
+    j.hdr->fp1 = j.fp1;
+  }
+  {  // row keys of the chunk: kCsTiles independent id loads in flight per thread
+    uint32_t k[kCsTiles];
+#pragma unroll
+    for (int u = 0; u < kCsTiles; ++u) k[u] = region_key(R, c0 + u * kCsThreads + tid);
+#pragma unroll
+    for (int u = 0; u < kCsTiles; ++u) {
+      const int i = u * kCsThreads + tid;
+      if (i < n) {
+        lkey[i] = k[u];
+        pbuf[0][i] = static_cast<uint16_t>(i);
+      }
+    }
+  }
+  for (int e = tid; e < 256 * kCsHistStride; e += kCsThreads) hist[e] = 0u;
+  const int bits = 32 - __builtin_clz(R.nr);  // row keys lie in [0, nr]
+  const int per = ((n + kCsWaves - 1) / kCsWaves + kWave - 1) / kWave * kWave;
+  const int wbeg = w * per, wend = min(n, wbeg + per);
+  const uint64_t lt = (uint64_t(1) << lane) - 1u;
+  const int passes = (bits + 7) / 8;
+  const int width = (bits + passes - 1) / passes;
+  const uint32_t dmask = (1u << width) - 1u;
+  int cur = 0;
+  for (int p = 0; p < passes; ++p) {
+    const int sh = p * width;
+    if (p > 0)
+      for (int e = tid; e < 256 * kCsHistStride; e += kCsThreads) hist[e] = 0u;
+    __syncthreads();
+    uint16_t pos[kCsTiles];
+    uint32_t dig[kCsTiles];
+    uint64_t peer[kCsTiles];
+#pragma unroll
+    for (int q = 0; q < kCsTiles; ++q) {
+      const int i = wbeg + q * kWave + lane;
+      pos[q] = 0;
+      dig[q] = 0;
+      if (i < wend) {
+        pos[q] = pbuf[cur][i];
+        dig[q] = (lkey[pos[q]] >> sh) & dmask;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kCsTiles; ++q) {
+      peer[q] = 0;
+      if (wbeg + q * kWave < wend) {  // wave-uniform
+        peer[q] = digit_peers(dig[q], wbeg + q * kWave + lane < wend, width);
+        if (peer[q] != 0 && __builtin_ctzll(peer[q]) == lane) hist[dig[q] * kCsHistStride + w] += __builtin_popcountll(peer[q]);
+      }
+    }
+    const bool last = p == passes - 1;
+    if (passes == 1) {  // small table: the chunk's digit counts (block-uniform)
+      __syncthreads();
+      uint32_t s = 0;
+#pragma unroll
+      for (int v = 0; v < kCsWaves; ++v) s += hist[tid * kCsHistStride + v];
+      j.chunk_hist[static_cast<int64_t>(blockIdx.x) * 256 + tid] = s;
+    }
+    cs_scan_counts(hist, wsum);
+#pragma unroll
+    for (int q = 0; q < kCsTiles; ++q) {
+      if (wbeg + q * kWave < wend) {  // wave-uniform
+        const uint64_t m = peer[q];
+        if (m != 0) {
+          uint32_t* slot = &hist[dig[q] * kCsHistStride + w];
+          const uint32_t off = *slot;
+          const uint32_t o = off + __builtin_popcountll(m & lt);
+          if (last) {
+            ck[o] = lkey[pos[q]];
+            cp[o] = static_cast<uint32_t>(c0) + pos[q];
+          } else {
+            pbuf[cur ^ 1][o] = pos[q];
+          }
+          if (__builtin_ctzll(m) == lane) *slot = off + __builtin_popcountll(m);
+        }
+      }
+    }
+    cur ^= 1;
+    __syncthreads();  // the scatter is complete before hist is cleared / the order read
+  }
+}
+
+__global__ void __launch_bounds__(kCsThreads) chunk_merge_kernel(const Job j) {
+  __shared__ uint32_t other[kChunk];
+  __shared__ uint32_t base[256], first[256], wsum[2][kCsWaves];
+  const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
+  const int t = table_of_chunk(j, blockIdx.x);
+  const Region R = region_of(j, t);
+  const TableDesc& T = j.t[t];
+  const int ci = static_cast<int>(blockIdx.x) - T.chunk_begin;
+  const int nch = (T.n_pad + kChunk - 1) / kChunk;
+  const int c0 = ci * kChunk;
+  const int n = min(kChunk, T.n_pad - c0);
+  const uint32_t* ck = j.keys_in + T.base;
+  const uint32_t* cp = j.vals_in + T.base;
+  uint32_t key[kCsTiles], pos[kCsTiles], out[kCsTiles];
+#pragma unroll
+  for (int u = 0; u < kCsTiles; ++u) {
+    const int i = u * kCsThreads + tid;
+    key[u] = i < n ? ck[c0 + i] : 0u;
+    pos[u] = i < n ? cp[c0 + i] : 0u;
+    out[u] = static_cast<uint32_t>(i);
+  }
+  const int bits = 32 - __builtin_clz(R.nr);
+  if (bits <= 8) {
+    // digit d: base = #{keys < d in the region} + #{keys == d in earlier
+    // chunks}; first = #{keys < d in this chunk}
+    uint32_t tot = 0, before = 0, mine = 0;
+    const uint32_t* h = j.chunk_hist + static_cast<int64_t>(T.chunk_begin) * 256 + tid;
+#pragma unroll 4
+    for (int c = 0; c < nch; ++c) {
+      const uint32_t x = h[static_cast<int64_t>(c) * 256];
+      tot += x;
+      before += c < ci ? x : 0u;
+      mine = c == ci ? x : mine;
+    }
+    uint32_t it = tot, im = mine;  // inclusive scans over the digits
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const uint32_t yt = __shfl_up(it, o, kWave), ym = __shfl_up(im, o, kWave);
+      if (lane >= o) {
+        it += yt;
+        im += ym;
+      }
+    }
+    if (lane == kWave - 1) {
+      wsum[0][w] = it;
+      wsum[1][w] = im;
+    }
+    __syncthreads();
+    uint32_t et = it - tot, em = im - mine;
+    for (int v = 0; v < w; ++v) {
+      et += wsum[0][v];
+      em += wsum[1][v];
+    }
+    base[tid] = et + before;
+    first[tid] = em;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kCsTiles; ++u) out[u] = base[key[u]] + (out[u] - first[key[u]]);
+  } else {
+    for (int c = 0; c < nch; ++c) {
+      if (c == ci) continue;  // block-uniform
+      const int m = min(kChunk, T.n_pad - c * kChunk);
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < kCsTiles; ++u) {
+        const int i = u * kCsThreads + tid;
+        other[i] = i < m ? ck[c * kChunk + i] : 0xFFFFFFFFu;
+      }
+      __syncthreads();
+      // earlier chunk: keys <= k come first; later chunk: keys < k (k + 0 vs
+      // k + 1 against the sorted keys; keys < 2^31, the padding compares high)
+      const uint32_t bump = c < ci ? 1u : 0u;
+#pragma unroll
+      for (int u = 0; u < kCsTiles; ++u) {
+        const uint32_t kk = key[u] + bump;
+        int b = 0;
+#pragma unroll
+        for (int s = kChunk / 2; s >= 1; s >>= 1) b += other[b + s - 1] < kk ? s : 0;
+        b += other[kChunk - 1] < kk ? 1 : 0;
+        out[u] += static_cast<uint32_t>(b);
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kCsTiles; ++u)
+    if (u * kCsThreads + tid < n) region_store(R, static_cast<int>(out[u]), pos[u], key[u]);
+}
+
 // The optimizer update of one distinct row, split into a load phase and a
 // compute/store phase so that a lane can have every row of its block in
 // flight at once (the applies are independent, the latency is not).
@@ -731,7 +1000,7 @@ int make_plan(const tt_sparse_table* tables, int cnt, int64_t batch, const float
   p->end_bit = j.id_bits + table_bits;
   if (p->end_bit > 32) return fail(TT_ERR_UNSUPPORTED, "sparse: %d tables x %lld rows exceed 32-bit keys", cnt,
                                    static_cast<long long>(max_rows));
-  int base = 0, waves = 0;
+  int base = 0, waves = 0, chunks = 0;
   int64_t poff = 0;
   for (int i = 0; i < cnt; ++i) {
     const tt_sparse_table& s = tables[i];
@@ -759,14 +1028,17 @@ int make_plan(const tt_sparse_table* tables, int cnt, int64_t batch, const float
     T.n_pad = static_cast<int32_t>(round_up(std::max<int64_t>(T.n, 1), kBlock));
     T.lanes = lanes_per_slot(s.dim);
     T.wave_begin = waves;
+    T.chunk_begin = chunks;
     T.piece_off = poff;
     base += T.n_pad;
+    chunks += static_cast<int>(ceil_div(T.n_pad, kChunk));
     const int nblk = T.n_pad / kBlock;
     waves += static_cast<int>(ceil_div(nblk, kWave / T.lanes));
     poff += static_cast<int64_t>(nblk) * 2 * s.dim;
   }
   p->total = base;
   p->waves = waves;
+  j.num_chunks = chunks;
   p->piece_floats = poff;
   // fingerprint of what the sort stage sorts (ids, tables, batch): two
   // independent 32-bit FNV-1a hashes
@@ -804,6 +1076,7 @@ struct PlanWs {
   SparseHeader* hdr;
   uint32_t *keys_in, *vals_in, *keys, *vals;
   float* pieces;
+  uint32_t* chunk_hist;
   float* dense_out;
   void* sort_tmp;
 };
@@ -815,6 +1088,7 @@ PlanWs carve_plan(Carver& cv, const Plan& p, int dense_dim) {
   w.keys = cv.take<uint32_t>(p.total);
   w.vals = cv.take<uint32_t>(p.total);
   w.pieces = cv.take<float>(std::max<int64_t>(p.piece_floats, 1));
+  w.chunk_hist = cv.take<uint32_t>(static_cast<int64_t>(p.job.num_chunks) * 256);
   w.dense_out = dense_dim > 0 ? cv.take<float>(static_cast<int64_t>(p.total) * dense_dim) : nullptr;
   w.sort_tmp = cv.take<char>(static_cast<int64_t>(p.sort_bytes) + 256);
   return w;
@@ -854,12 +1128,16 @@ size_t tables_ws_bytes(const tt_sparse_table* tables, int32_t num_tables, int64_
   return total;
 }
 
-// TT_SPARSE_SORT=device forces the key build + rocPRIM sort for every call
-// (the LDS region sort is used when every region fits, by default).
-bool use_lds_sort() {
-  static const bool v = [] {
+// TT_SPARSE_SORT: "chunk" (default: chunked LDS sort when every region fits),
+// "region" (one workgroup per region) or "device" (key build + rocPRIM sort
+// for every call).
+enum SortMode { kSortChunk = 0, kSortRegion = 1, kSortDevice = 2 };
+int sort_mode() {
+  static const int v = [] {
     const char* e = std::getenv("TT_SPARSE_SORT");
-    return !(e && std::strcmp(e, "device") == 0);
+    if (e && std::strcmp(e, "device") == 0) return int(kSortDevice);
+    if (e && std::strcmp(e, "region") == 0) return int(kSortRegion);
+    return int(kSortChunk);
   }();
   return v;
 }
@@ -892,13 +1170,24 @@ int run_sparse(const tt_sparse_table* tables, int32_t num_tables, int64_t batch,
     j.keys = w.keys;
     j.vals = w.vals;
     j.pieces = w.pieces;
+    j.chunk_hist = w.chunk_hist;
     j.dense_out = w.dense_out;
     j.dense_dim = dense_dim;
     j.hdr = w.hdr;
     if (stage != kStageApply) {
-      bool lds = use_lds_sort();
-      for (int i = 0; i < cnt && lds; ++i) lds = j.t[i].n_pad <= kLdsSortMax || bits_for(j.t[i].num_rows) <= 8;
-      if (lds) {
+      const int mode = sort_mode();
+      bool lds = mode != kSortDevice, chunked = mode == kSortChunk;
+      for (int i = 0; i < cnt; ++i) {
+        const bool small = bits_for(j.t[i].num_rows) <= 8;
+        lds = lds && (j.t[i].n_pad <= kLdsSortMax || small);
+        chunked = chunked && (j.t[i].n_pad <= kLdsSortMax || (small && j.t[i].n_pad <= kChunkMaxSmall));
+      }
+      if (lds && chunked) {
+        hipLaunchKernelGGL(chunk_sort_kernel, dim3(j.num_chunks), dim3(kCsThreads), 0, st, j);
+        TT_CHECK_LAUNCH();
+        hipLaunchKernelGGL(chunk_merge_kernel, dim3(j.num_chunks), dim3(kCsThreads), 0, st, j);
+        TT_CHECK_LAUNCH();
+      } else if (lds) {
         static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(region_sort_kernel),
                                                            hipFuncAttributeMaxDynamicSharedMemorySize, kLsLdsBytes);
         TT_CHECK_HIP(attr);

@@ -192,6 +192,18 @@ _PROTOS = {
         [c_void_p, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int64, c_int64, c_int32, c_int64, c_void_p,
          c_void_p, c_void_p, c_size_t, c_void_p],
     ),
+    "tt_bruteforce_shard_chunk": (c_int64, [c_int64, c_int64, c_int32, c_int32]),
+    "tt_bruteforce_shard_workspace_size": (c_size_t, [c_int64, c_int64, c_int32, c_int32]),
+    "tt_bruteforce_shard_screen": (
+        c_int32,
+        [c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int64, c_int32, c_int64, c_void_p, c_void_p, c_size_t,
+         c_void_p],
+    ),
+    "tt_bruteforce_shard_finalize": (
+        c_int32,
+        [c_void_p, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int64, c_int64, c_int32, c_int64, c_void_p,
+         c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
+    ),
     "tt_topk_merge": (c_int32, [c_void_p, c_void_p, c_int32, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
     "tt_recall_hits": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, POINTER(c_int32), c_int32, c_void_p, c_void_p]),
     "tt_vocab_create": (c_int32, [c_void_p, c_void_p, c_int64, POINTER(c_void_p)]),

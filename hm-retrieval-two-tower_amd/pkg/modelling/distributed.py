@@ -69,6 +69,9 @@ class IndexOps:
     build: Callable[[torch.Tensor], Any]
     search: Callable[..., Tuple[torch.Tensor, torch.Tensor]]
     merge: Callable[[torch.Tensor, torch.Tensor, int], Tuple[torch.Tensor, torch.Tensor]]
+    # (image, rows, queries, k, offset, reduce_max) -> this shard's exact top-k
+    # of the rows that can reach the global k-th score (padded); None: search
+    shard_search: Optional[Callable[..., Tuple[torch.Tensor, torch.Tensor]]] = None
 
     @staticmethod
     def hip() -> "IndexOps":
@@ -76,12 +79,21 @@ class IndexOps:
 
         return IndexOps(hip_ops.bruteforce_build,
                         lambda img, cand, q, k, off: hip_ops.bruteforce_search(img, cand, q, k, off),
-                        hip_ops.topk_merge)
+                        hip_ops.topk_merge, hip_ops.bruteforce_shard_search)
 
 
 def _staged(group) -> bool:
     """gloo moves host tensors only: device tensors go through the host."""
     return dist.get_backend(group) == "gloo"
+
+
+def _all_reduce_max(t: torch.Tensor, group) -> None:
+    if _staged(group) and t.is_cuda:
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.MAX, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
 
 
 def _all_gather_any(t: torch.Tensor, group) -> torch.Tensor:
@@ -120,13 +132,19 @@ class ShardedBruteForceIndex:
     rank order.
 
     Per search (queries replicated on every rank):
-      1. tt_bruteforce_search on the local rows with index_offset = b_g: the
-         exact top-k of the shard, indices global (ties -> lower index);
+      1. per chunk of queries, tt_bruteforce_shard_screen on the local rows:
+         a lower bound on each query's k-th exact score among them; one
+         all_reduce(MAX) makes it a bound on the GLOBAL k-th score (floor);
+         tt_bruteforce_shard_finalize rescores only the entries that can reach
+         the floor: the exact top-k of the shard among them, indices global
+         (index_offset = b_g, ties -> lower index), padded past the survivors
+         (so each shard rescores ~1/G of the rows the global top-k needs);
       2. all_to_all: the lists of query block r (shard_range(Q, G, r)) go to
          rank r — Q·k·8 B sent per rank, 1/G of it kept;
       3. tt_topk_merge of the G lists -> the owner's exact global top-k.
     Exact: a candidate of the global top-k outranks every other candidate of
-    its own shard that it beats globally, so it is in its shard's top-k; the
+    its own shard that it beats globally, so it is in its shard's top-k, and
+    it scores >= the global k-th score >= floor, so it survives the cut; the
     merge orders by the same (score desc, index asc) key top_k uses, and the
     scores are the same fp32 chains wherever a row lives.  search() then
     all-gathers the owners' blocks so every rank holds the whole answer.
@@ -183,6 +201,12 @@ class ShardedBruteForceIndex:
             raise ValueError(f"k={k} exceeds the number of candidates {self.num_candidates}")
         q = query_embeddings.contiguous()
         kl = min(k, int(self.shard.shape[0]))
+        # collective decision: every rank takes the same branch (its all_reduce)
+        if self.world > 1 and self.ops.shard_search is not None and min(self.sizes) >= k:
+            # two-phase: the shards' lower bounds on their k-th scores, max-reduced,
+            # cut each shard's exact rescoring to what can reach the global top-k
+            return self.ops.shard_search(self.image, self.shard, q, k, self.offset,
+                                         lambda t: _all_reduce_max(t, self.group))
         s, i = self.ops.search(self.image, self.shard, q, kl, self.offset)
         if kl < k:
             ps = torch.full((q.shape[0], k), float("-inf"), dtype=s.dtype, device=s.device)
@@ -427,19 +451,22 @@ class BatchComm:
     all_gather_into_tensor / reduce_scatter_tensor; over gloo (CPU tests, or
     several ranks sharing one GPU) through the host."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, always: bool = False):
+        """always: run the collectives at world 1 too (one-rank RCCL calls;
+        the tests use it to put real collectives into a captured step)."""
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        self.always = bool(always)
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
-        if self.world == 1:
+        if self.world == 1 and not self.always:
             return t
         out = _all_gather_any(t.contiguous(), self.group)
         return out.reshape((self.world * t.shape[0],) + tuple(t.shape[1:]))
 
     def reduce_scatter(self, t: torch.Tensor) -> torch.Tensor:
-        if self.world == 1:
+        if self.world == 1 and not self.always:
             return t
         n = t.shape[0] // self.world
         if _staged(self.group):  # gloo has no reduce_scatter: sum everywhere, keep this rank's block
@@ -664,8 +691,10 @@ class ShardedTrainStep:
     all of them against this rank's candidates (dC of its columns).  The
     loss and every gradient are those of the global batch (tests:
     test_distributed_gloo global loss, test_distributed_gpu step).  This is
-    the default.  With world > 1 that middle runs eagerly unless its RCCL
-    collectives are captured into the hipGraph (TT_GRAPH_COLLECTIVES=1).
+    the default.  Over RCCL the middle's all_gathers and reduce_scatters are
+    captured into its hipGraph with the kernels (test_model_gpu: a captured
+    world-1 step with forced one-rank RCCL collectives is bit-identical to
+    the eager one); over gloo it runs eagerly.
     global_negatives=False keeps per-replica negatives (a labelled variant:
     each rank's loss over its own batch).
 
@@ -673,7 +702,7 @@ class ShardedTrainStep:
     """
 
     def __init__(self, model, shard_min_rows: int = 100_000, group=None, ops: Optional[EmbeddingOps] = None,
-                 use_graph: bool = True, global_negatives: bool = True):
+                 use_graph: bool = True, global_negatives: bool = True, comm: Optional[BatchComm] = None):
         from pkg.modelling.optimizer_factory import Adagrad
 
         opt = model.optimizer
@@ -685,13 +714,14 @@ class ShardedTrainStep:
         self.world = dist.get_world_size(group)
         self.lr, self.eps, self.init = opt.learning_rate, opt.epsilon, opt.initial_accumulator_value
         self.global_negatives = bool(global_negatives)
-        self.comm = BatchComm(group) if self.global_negatives else None
-        # the global-negatives middle holds collectives: it runs eagerly unless
-        # TT_GRAPH_COLLECTIVES=1 asks to capture them with RCCL (never over
-        # gloo, whose host staging synchronises)
+        self.comm = (comm or BatchComm(group)) if self.global_negatives else None
+        # the global-negatives middle holds collectives: over RCCL they are
+        # captured into the step's hipGraph with the kernels (the default;
+        # TT_SHARDED_EAGER=1 runs the middle eagerly); over gloo, whose host
+        # staging synchronises, the middle runs eagerly
+        collectives = self.global_negatives and (self.world > 1 or self.comm.always)
         self.use_graph = use_graph and os.environ.get("TT_SHARDED_EAGER") != "1" and not (
-            self.global_negatives and self.world > 1 and (
-                _staged(group) or os.environ.get("TT_GRAPH_COLLECTIVES") != "1"))
+            collectives and _staged(group))
         big: Dict[str, torch.Tensor] = {}
         self.small: Dict[Any, Any] = {}
         for tower in model.towers:

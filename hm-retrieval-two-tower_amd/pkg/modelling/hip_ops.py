@@ -39,6 +39,7 @@ __all__ = [
     "route_owner",
     "bruteforce_build",
     "bruteforce_search",
+    "bruteforce_shard_search",
     "topk_merge",
     "recall_hits",
     "Workspace",
@@ -634,6 +635,43 @@ def bruteforce_search(index: torch.Tensor, cand: torch.Tensor, queries: torch.Te
     check(L.tt_bruteforce_search(index.data_ptr(), cand.data_ptr(), ldc, n, d, queries.data_ptr(), ldq, nq, k,
                                  index_offset, out_s.data_ptr(), out_i.data_ptr(), ws.data_ptr(), ws.numel(),
                                  _stream()))
+    return out_s, out_i
+
+
+def bruteforce_shard_search(index: torch.Tensor, cand: torch.Tensor, queries: torch.Tensor, k: int,
+                            index_offset: int, reduce_max) -> Tuple[torch.Tensor, torch.Tensor]:
+    """This shard's part of a candidate-sharded exact top-k (tt.h
+    tt_bruteforce_shard_*): per chunk of queries, the screen's lower bound on
+    the shard's k-th score, `reduce_max(t)` (in place: the max over the shards,
+    an all_reduce) as the floor, then the shard's exact top-k of the entries
+    that can reach it, padded with (-inf, INT32_MAX)."""
+    _req(index, "index", torch.uint8, 1)
+    _req(cand, "cand", torch.float32, 2)
+    _req(queries, "queries", torch.float32, 2)
+    ldc, ldq = _row_major(cand, "cand"), _row_major(queries, "queries")
+    n, d = cand.shape
+    nq = queries.shape[0]
+    if queries.shape[1] != d:
+        raise ValueError("queries and candidates must share the embedding size")
+    if k > n:
+        raise ValueError(f"k={k} exceeds the shard's {n} candidates")
+    L = lib()
+    out_s = torch.empty(nq, k, dtype=torch.float32, device=queries.device)
+    out_i = torch.empty(nq, k, dtype=torch.int32, device=queries.device)
+    if nq == 0:
+        return out_s, out_i
+    chunk = int(L.tt_bruteforce_shard_chunk(nq, n, d, k))
+    ws = Workspace.get(L.tt_bruteforce_shard_workspace_size(chunk, n, d, k), queries.device, "bruteforce_shard")
+    kth = torch.empty(chunk, dtype=torch.float32, device=queries.device)
+    for q0 in range(0, nq, chunk):
+        m = min(chunk, nq - q0)
+        qc = queries[q0:q0 + m]
+        check(L.tt_bruteforce_shard_screen(index.data_ptr(), n, d, qc.data_ptr(), ldq, m, k, index_offset,
+                                           kth.data_ptr(), ws.data_ptr(), ws.numel(), _stream()))
+        reduce_max(kth[:m])
+        check(L.tt_bruteforce_shard_finalize(index.data_ptr(), cand.data_ptr(), ldc, n, d, qc.data_ptr(), ldq, m, k,
+                                             index_offset, kth.data_ptr(), out_s[q0:q0 + m].data_ptr(),
+                                             out_i[q0:q0 + m].data_ptr(), ws.data_ptr(), ws.numel(), _stream()))
     return out_s, out_i
 
 

@@ -2,9 +2,11 @@
 
 train_step (two_tower_model.py:94-130) on MI355X:
   1. query / candidate InputLayer gathers        tt_gather_grouped (1 launch per tower)
-  2. tower MLPs                                   torch addmm + relu (hipBLASLt)
-  3. scores + logQ + eye-label CE-SUM + dQ/dC     tt_inbatch_xent_rows / _cols (fused, bf16 MFMA)
-  4. MLP backward                                 torch autograd (hipBLASLt)
+  2. tower MLPs                                   tt_mlp_rows (bf16x3 MFMA, bias + relu epilogue)
+  3. scores + logQ + eye-label CE-SUM + dQ/dC     tt_inbatch_xent_rows / _cols (fused, bf16x3 MFMA)
+  4. MLP backward                                 tt_mlp_rows input gradients (ReluGrad + bias
+                                                  column sums fused) + weight gradients
+                                                  (tower.WGRAD_KERNEL, on a side stream)
   5. optimizer                                    tt_dense_adagrad + tt_sparse_adagrad (dedup in-kernel)
 Every launch is stream-ordered with no host synchronisation, so the whole step
 can be captured once and replayed as a hipGraph (GraphedTrainStep).
@@ -380,7 +382,7 @@ class GraphedTrainStep:
 
     The batch lives in two static device buffers (int32 ids [K, B], float32
     values [F, B]); a replay is one D2D copy per buffer (or none, for
-    `replay()`), then the whole step — gathers, hipBLASLt GEMMs, the fused
+    `replay()`), then the whole step — gathers, MLP GEMMs, the fused
     loss kernels and the optimizer kernels — with no Python or launch
     overhead.  Warm-up steps (run eagerly on a side stream before capture)
     are real optimisation steps on the example batch.  Requires an optimizer

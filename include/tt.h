@@ -363,6 +363,41 @@ int tt_bruteforce_search(const void* index, const float* cand, int64_t ldc,
                          int32_t* out_idx, void* workspace,
                          size_t workspace_bytes, tt_stream_t stream);
 
+/* Candidate-sharded two-phase search (ShardedBruteForceIndex).
+ * Replaces the same BruteForceIndex.call (brute_force.py:76-83) with the
+ * candidate rows split over G ranks, each holding only its rows:
+ *  1. tt_bruteforce_shard_screen on the rank's rows: bf16 screen + the
+ *     finalize's select; kth_lb[q] = a lower bound on the k-th largest exact
+ *     score of these rows (-inf when the query's certificate failed);
+ *  2. the caller all-reduces kth_lb with MAX over the ranks: floor[q] bounds
+ *     the GLOBAL k-th exact score from below;
+ *  3. tt_bruteforce_shard_finalize: rescoring of the screened entries that
+ *     can still reach floor, the shard's exact top-k of them with global
+ *     indices (index_offset = the shard's first global row), padded with
+ *     (-inf, INT32_MAX) past the survivors; failed certificates are scanned
+ *     exactly over the shard.  Merging the G lists (tt_topk_merge) gives the
+ *     exact global top-k.
+ * Queries go in chunks of at most tt_bruteforce_shard_chunk(total, ...); a
+ * screen / finalize pair of one chunk shares the workspace. */
+int64_t tt_bruteforce_shard_chunk(int64_t n_queries, int64_t n_cand,
+                                  int32_t dim, int32_t k);
+size_t tt_bruteforce_shard_workspace_size(int64_t n_queries, int64_t n_cand,
+                                          int32_t dim, int32_t k);
+int tt_bruteforce_shard_screen(const void* index, int64_t n_cand, int32_t dim,
+                               const float* queries, int64_t ldq,
+                               int64_t n_queries, int32_t k,
+                               int64_t index_offset, float* kth_lb,
+                               void* workspace, size_t workspace_bytes,
+                               tt_stream_t stream);
+int tt_bruteforce_shard_finalize(const void* index, const float* cand,
+                                 int64_t ldc, int64_t n_cand, int32_t dim,
+                                 const float* queries, int64_t ldq,
+                                 int64_t n_queries, int32_t k,
+                                 int64_t index_offset, const float* floor,
+                                 float* out_scores, int32_t* out_idx,
+                                 void* workspace, size_t workspace_bytes,
+                                 tt_stream_t stream);
+
 /* Merge `num_lists` per-shard sorted top-k_in lists laid out
  * [num_lists][n_queries][k_in] into the global top-k_out with the same
  * order (score descending, index ascending on ties). */

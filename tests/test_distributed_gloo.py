@@ -25,7 +25,7 @@ def _init(rank, world, port):
     dist.init_process_group("gloo", rank=rank, world_size=world)
 
 
-def _oracle_ops():
+def _oracle_ops(two_phase=False):
     from oracle import oracle
     from pkg.modelling.distributed import IndexOps
 
@@ -37,7 +37,20 @@ def _oracle_ops():
         ms, mi = oracle.topk_merge(s.numpy(), i.numpy(), k)
         return torch.from_numpy(np.ascontiguousarray(ms)), torch.from_numpy(np.ascontiguousarray(mi))
 
-    return IndexOps(build=lambda c: None, search=search, merge=merge)
+    def shard_search(img, cand, q, k, off, reduce_max):
+        # the two-phase contract with the loosest legal screen: a lower bound on
+        # the shard's k-th score, max-reduced, then the exact top-k of the
+        # entries scoring >= the floor, padded with (-inf, INT32_MAX)
+        s, i, _ = oracle.bruteforce_topk(q.numpy(), cand.numpy(), k)
+        kth = torch.from_numpy(s[:, k - 1] - np.abs(s[:, k - 1]) * 0.25 - 0.5)
+        reduce_max(kth)
+        keep = s >= kth.numpy()[:, None]
+        s = np.where(keep, s, -np.inf).astype(np.float32)
+        i = np.where(keep, i + off, 0x7FFFFFFF).astype(np.int32)
+        return torch.from_numpy(s), torch.from_numpy(i)
+
+    return IndexOps(build=lambda c: None, search=search, merge=merge,
+                    shard_search=shard_search if two_phase else None)
 
 
 def _index_worker(rank, world, port, q, c, k, out):
@@ -63,6 +76,10 @@ def _index_worker(rank, world, port, q, c, k, out):
         blk, os_, oi = idx.search_owned(torch.from_numpy(q))
         out[(mode, rank)] = (s.numpy(), i.numpy(), idx.num_candidates, blk, os_.numpy(), oi.numpy(),
                              idx.rows, int(idx.shard.shape[0]))
+        # two-phase (screen floor all-reduced, cut rescoring): same answer
+        idx2 = ShardedBruteForceIndex(k, None, torch.from_numpy(c[b:e].copy()), ops=_oracle_ops(True))
+        s2, i2 = idx2.search(torch.from_numpy(q))
+        out[(mode + "2", rank)] = (s2.numpy(), i2.numpy())
     dist.destroy_process_group()
 
 
@@ -87,6 +104,8 @@ def test_sharded_index_equals_unsharded(world):
             assert n == 301 and held == r1 - r0 < 301  # no rank holds every row
             rows.append((r0, r1))
             assert np.array_equal(i, ri) and np.array_equal(s, rs), mode
+            s2, i2 = out[(mode + "2", r)]
+            assert np.array_equal(i2, ri) and np.array_equal(s2, rs), mode + " two-phase"
             # search_owned: this rank's query block only, same global lists
             assert np.array_equal(oi, ri[b:e]) and np.array_equal(os_, rs[b:e]), mode
             covered += list(range(b, e))

@@ -565,13 +565,18 @@ def test_route_requests_match_torch_restatement(cuda, world):
 
 
 @pytest.mark.parametrize("rows,sources,B", [(255, 2, 20000), (256, 1, 16384), (256, 2, 9000), (1, 1, 100),
-                                             (1371980, 1, 16384), (40, 3, 5000)])
+                                             (1371980, 1, 16384), (40, 3, 5000), (3000, 1, 2049),
+                                             (100000, 2, 8000), (1371980, 1, 2048), (200, 4, 30000),
+                                             (255, 4, 40000)])
 def test_sparse_adagrad_sort_paths_bitexact(cuda, rows, sources, B):
     """The embedding update's id sort takes one of three paths per call: the
-    single-pass LDS counting sort (tables of <= 255 rows, any region size),
-    the multi-pass LDS radix sort (regions <= 16384 lookups), or the key build
-    + device radix sort (anything else).  Each is bit-exact vs the restatement
-    (rows = 256 x 18000 lookups takes the device path)."""
+    chunked LDS sort (2048-lookup chunks sorted by their own workgroups, then
+    merged: by binary search of the other chunks for regions <= 16384
+    lookups, by the chunks' digit counts for tables of <= 255 rows up to 64
+    chunks), the one-workgroup LDS counting sort (tables of <= 255 rows with
+    larger regions: 255 x 160000 lookups), or the key build + device radix
+    sort (anything else: 256 x 18000 lookups).  Each is bit-exact vs the
+    restatement; chunk edges (2048, 2049) included."""
     rng = np.random.default_rng(rows + B)
     D = 8
     w = rng.uniform(-0.05, 0.05, (rows, D)).astype(np.float32)

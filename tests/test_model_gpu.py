@@ -410,3 +410,44 @@ def test_sharded_train_step_world1_matches_single_gpu(cuda):
                 assert torch.equal(full, t.weight), name
     finally:
         dist.destroy_process_group()
+
+
+def test_global_negatives_step_captures_rccl_collectives(cuda, monkeypatch):
+    """ShardedTrainStep's global-negatives middle with its collectives as real
+    RCCL calls (a one-rank process group with BatchComm(always=True), so the
+    all_gathers / reduce_scatters run even at world 1) captured into the
+    step's hipGraph — the default over RCCL — trains bit-identically to the
+    same step run eagerly (TT_SHARDED_EAGER=1), step for step."""
+    import socket
+
+    import torch.distributed as dist
+    from pkg.modelling.distributed import BatchComm, ShardedTrainStep
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device(cuda))
+    try:
+        a, b = _small_model(cuda, seed=5), _small_model(cuda, seed=5)
+        graphed = ShardedTrainStep(a, shard_min_rows=300, global_negatives=True, comm=BatchComm(always=True))
+        monkeypatch.setenv("TT_SHARDED_EAGER", "1")
+        eager = ShardedTrainStep(b, shard_min_rows=300, global_negatives=True, comm=BatchComm(always=True))
+        monkeypatch.delenv("TT_SHARDED_EAGER")
+        assert graphed.use_graph and not eager.use_graph
+        rng = np.random.default_rng(9)
+        batches = [_batch(cuda, rng, 256) for _ in range(5)]
+        for i, batch in enumerate(batches):  # call 1 eager, then graph replays
+            la, lb = graphed(batch)["loss"], eager(batch)["loss"]
+            assert torch.equal(la, lb), i
+        assert graphed._graph is not None
+        for ta, tb in zip(a.towers, b.towers):
+            assert torch.equal(ta.dense.flat, tb.dense.flat)
+            for name, t in tb.input_layer.embedding_layers.items():
+                mine = ta.input_layer.embedding_layers[name]
+                ga = graphed.tables.gather_full(mine._shard_key) if hasattr(mine, "_shard_key") else mine.weight
+                gb = eager.tables.gather_full(t._shard_key) if hasattr(t, "_shard_key") else t.weight
+                assert torch.equal(ga, gb), name
+    finally:
+        dist.destroy_process_group()
