@@ -34,10 +34,12 @@
 // The image's XOR swizzle keeps both kinds of read bank-conflict free.
 // The stationary extent is split into 128-row workgroups and the streamed
 // extent into S splits (flash-decoding) so that >= 256 workgroups fill the
-// 256 CUs; small combine kernels merge the splits.
+// 256 CUs; small combine kernels merge the splits.  (Merging them inside the
+// passes instead — write-through partials, the last of a block's S
+// workgroups merging them — measured 10-30 us per step slower: the merging
+// workgroups' dependent reads form a serial tail of the pass.)
 #include <cmath>
 #include <cstdlib>
-#include <cstring>
 #include <type_traits>
 
 #include "tt_common.h"
@@ -97,16 +99,12 @@ struct PrepJob {
   float* bias;
   float* bias2;
   int vec;  // src 16-B aligned, ld % 4 == 0, dim % 4 == 0: float4 loads
-  int* zero;  // (first job) pass arrival counters to clear, nzero of them
-  int nzero;
 };
 
 template <int D>
 __global__ void __launch_bounds__(256) prep_kernel(PrepJob j0, PrepJob j1, int dim) {
   const PrepJob& j = blockIdx.y ? j1 : j0;
   const int64_t r0 = blockIdx.x * 32ll;
-  if (blockIdx.x == 0 && blockIdx.y == 0)
-    for (int i = threadIdx.x; i < j0.nzero; i += 256) j0.zero[i] = 0;
   constexpr int TPR = D / 8;  // threads per row
   for (int i = threadIdx.x; i < 32 * TPR; i += 256) {
     const int64_t r = r0 + i / TPR;
@@ -149,23 +147,6 @@ struct PassArgs {
   float* part_m;          // [S, n_stat_pad]   (rows pass)
   float* part_l;          // [S, n_stat_pad]   (rows pass)
   float* part_o;          // [S, n_stat_pad, D]
-  // split combine fused into the pass (done != NULL): the last of a
-  // stationary block's S workgroups to finish merges the block's partials
-  int* done;              // [n_stat_pad / kRowsPerWG] arrival counters (0 at launch; reset by the last)
-  int nsplit;
-  const float* q;         // the combine's operands (combine_rows / combine_cols below)
-  int64_t ldq;
-  const float* c;
-  int64_t ldc;
-  const float* logq;
-  int64_t n;              // real stationary rows
-  int dim;
-  int64_t pos_offset;
-  float* lse;
-  float* loss;
-  float* dq;
-  float* neg_lse;
-  float* dc;
 };
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -207,127 +188,6 @@ template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
-}
-
-// Split combines: D/4 lanes per row (float4 partials).  Run by the pass's
-// last workgroup of each stationary block (fused), or as their own launches
-// (1024/D rows per block).
-// Rows: lse, row loss, dq = O / L - c_pos (and -lse as the cols-pass bias).
-template <int D>
-__device__ __forceinline__ void combine_row(
-    int64_t i, int sub, const float* __restrict__ part_m, const float* __restrict__ part_l,
-    const float* __restrict__ part_o, int nsplit, int64_t n_stat_pad, const float* __restrict__ q, int64_t ldq,
-    const float* __restrict__ c, int64_t ldc, const float* __restrict__ logq, int dim, int64_t pos_offset,
-    float* __restrict__ lse_out, float* __restrict__ loss_out, float* __restrict__ dq,
-    float* __restrict__ neg_lse_bias) {
-  constexpr int LPR = D / 4;  // lanes per row
-  // splits in groups of 4 whose loads are all issued before any is used
-  // (index clamped, weight 0 past nsplit); splits added in order as before
-  float M = -1.0e30f;
-  for (int s0 = 0; s0 < nsplit; s0 += 4) {
-    float m[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) m[u] = part_m[min(s0 + u, nsplit - 1) * n_stat_pad + i];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) M = fmaxf(M, m[u]);
-  }
-  float L = 0.0f;
-  f32x4 o = {0.0f, 0.0f, 0.0f, 0.0f};
-  for (int s0 = 0; s0 < nsplit; s0 += 4) {
-    float m[4], l[4];
-    f32x4 ps[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t sr = min(s0 + u, nsplit - 1) * n_stat_pad + i;
-      m[u] = part_m[sr];
-      l[u] = part_l[sr];
-      ps[u] = *reinterpret_cast<const f32x4*>(part_o + sr * D + 4 * sub);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (s0 + u < nsplit) {
-        const float w = expf(m[u] - M);
-        L += l[u] * w;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] += ps[u][e] * w;
-      }
-    }
-  }
-  const float lse = M + logf(L);
-  const float inv = 1.0f / L;
-  const int64_t pos = i + pos_offset;
-  float dot = 0.0f;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int e = 4 * sub + u;
-    if (e < dim) {
-      const float ce = c[pos * ldc + e];
-      if (dq) dq[i * dim + e] = o[u] * inv - ce;
-      dot = __builtin_fmaf(q[i * ldq + e], ce, dot);
-    }
-  }
-#pragma unroll
-  for (int m = LPR / 2; m >= 1; m >>= 1) dot += __shfl_xor(dot, m, LPR);
-  if (sub == 0) {
-    const float pos_logit = dot - (logq ? logq[pos] : 0.0f);
-    lse_out[i] = lse;
-    loss_out[i] = lse - pos_logit;
-    if (neg_lse_bias) neg_lse_bias[i] = -lse;
-  }
-}
-
-template <int D>
-__global__ void __launch_bounds__(256) combine_rows_kernel(
-    const float* __restrict__ part_m, const float* __restrict__ part_l, const float* __restrict__ part_o,
-    int nsplit, int64_t n_stat_pad, const float* __restrict__ q, int64_t ldq, const float* __restrict__ c,
-    int64_t ldc, const float* __restrict__ logq, int64_t n_rows, int dim, int64_t pos_offset,
-    float* __restrict__ lse_out, float* __restrict__ loss_out, float* __restrict__ dq,
-    float* __restrict__ neg_lse_bias) {
-  constexpr int LPR = D / 4;
-  const int64_t i = blockIdx.x * (256ll / LPR) + threadIdx.x / LPR;
-  if (i >= n_rows) return;
-  combine_row<D>(i, threadIdx.x % LPR, part_m, part_l, part_o, nsplit, n_stat_pad, q, ldq, c, ldc, logq, dim,
-                 pos_offset, lse_out, loss_out, dq, neg_lse_bias);
-}
-
-// Cols: dc_j = exp(-logq_j) * sum_s O_s[j] - q_pos(j).
-template <int D>
-__device__ __forceinline__ void combine_col(int64_t j, int sub, const float* __restrict__ part_o, int nsplit,
-                                            int64_t n_stat_pad, const float* __restrict__ q, int64_t ldq,
-                                            const float* __restrict__ logq, int dim, int64_t pos_offset,
-                                            float* __restrict__ dc) {
-  const float scale = logq ? expf(-logq[j]) : 1.0f;
-  const int64_t pos = j + pos_offset;
-  f32x4 o = {0.0f, 0.0f, 0.0f, 0.0f};
-  for (int s0 = 0; s0 < nsplit; s0 += 4) {  // 4 splits' loads in flight, added in order
-    f32x4 ps[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      ps[u] = *reinterpret_cast<const f32x4*>(part_o + (min(s0 + u, nsplit - 1) * n_stat_pad + j) * D + 4 * sub);
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (s0 + u < nsplit) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] += ps[u][e];
-      }
-  }
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int e = 4 * sub + u;
-    if (e < dim) dc[j * dim + e] = o[u] * scale - q[pos * ldq + e];
-  }
-}
-
-template <int D>
-__global__ void __launch_bounds__(256) combine_cols_kernel(const float* __restrict__ part_o, int nsplit,
-                                                           int64_t n_stat_pad, const float* __restrict__ q,
-                                                           int64_t ldq, const float* __restrict__ logq,
-                                                           int64_t n_cols, int dim, int64_t pos_offset,
-                                                           float* __restrict__ dc) {
-  constexpr int LPR = D / 4;
-  const int64_t j = blockIdx.x * (256ll / LPR) + threadIdx.x / LPR;
-  if (j >= n_cols) return;
-  combine_col<D>(j, threadIdx.x % LPR, part_o, nsplit, n_stat_pad, q, ldq, logq, dim, pos_offset, dc);
 }
 
 // ---------------------------------------------------------------------------
@@ -589,81 +449,123 @@ __global__ void __launch_bounds__(kThreads) inbatch_pass_kernel(const PassArgs a
   }
 
   const int64_t prow = static_cast<int64_t>(split) * a.n_stat_pad + stat_row;
-  float* po = a.part_o + prow * D;
-  if (a.done == nullptr) {
-    if constexpr (MODE == 0) {
-      const float l_tot = l_run + __shfl_xor(l_run, 32, kWave);
-      if (h == 0) {
-        a.part_m[prow] = m_run;
-        a.part_l[prow] = l_tot;
-      }
-    }
-#pragma unroll
-    for (int dt = 0; dt < G::DT; ++dt)
-#pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4) {
-        f32x4 v;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = o[dt][4 * r4 + u];
-        *reinterpret_cast<f32x4*>(po + 32 * dt + 8 * r4 + 4 * h) = v;
-      }
-    return;
-  }
-  // Fused combine (the in-launch split reduction): partials stored
-  // write-through (sc1) and drained, so no release fence; one relaxed
-  // agent-scope ticket per workgroup; the block's last arriver acquires
-  // (agent) and merges the S partials of its 128 rows.  The ticket is
-  // broadcast through the ring (no second __shared__ object: it would put
-  // vmcnt(0) waits into the tile loop).
-  {
-    const float* wbase = a.part_o + (static_cast<int64_t>(split) * a.n_stat_pad +
-                                     static_cast<int64_t>(blockIdx.x) * kRowsPerWG + wave * kRowsPerWave) * D;
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wbase), 0,
-                                                        kRowsPerWave * D * 4, 0x00020000);
-#pragma unroll
-    for (int dt = 0; dt < G::DT; ++dt)
-#pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4) {
-        f32x4 v;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = o[dt][4 * r4 + u];
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc,
-                                               (l32 * D + 32 * dt + 8 * r4 + 4 * h) * 4, 0, 16);
-      }
-  }
   if constexpr (MODE == 0) {
     const float l_tot = l_run + __shfl_xor(l_run, 32, kWave);
     if (h == 0) {
-      __hip_atomic_store(a.part_m + prow, m_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(a.part_l + prow, l_tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      a.part_m[prow] = m_run;
+      a.part_l[prow] = l_tot;
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-  __syncthreads();
-  int* flag = reinterpret_cast<int*>(ring);
-  if (threadIdx.x == 0) {
-    const int old = __hip_atomic_fetch_add(&a.done[blockIdx.x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == a.nsplit - 1;
-    if (last) {
-      __hip_atomic_store(&a.done[blockIdx.x], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float* po = a.part_o + prow * D;
+#pragma unroll
+  for (int dt = 0; dt < G::DT; ++dt)
+#pragma unroll
+    for (int r4 = 0; r4 < 4; ++r4) {
+      f32x4 v;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = o[dt][4 * r4 + u];
+      *reinterpret_cast<f32x4*>(po + 32 * dt + 8 * r4 + 4 * h) = v;
     }
-    *flag = last;
+}
+
+// Split combines: D/4 lanes per row (float4 partials), 1024/D rows per block.
+// Rows: lse, row loss, dq = O / L - c_pos (and -lse as the cols-pass bias).
+template <int D>
+__global__ void __launch_bounds__(256) combine_rows_kernel(
+    const float* __restrict__ part_m, const float* __restrict__ part_l, const float* __restrict__ part_o,
+    int nsplit, int64_t n_stat_pad, const float* __restrict__ q, int64_t ldq, const float* __restrict__ c,
+    int64_t ldc, const float* __restrict__ logq, int64_t n_rows, int dim, int64_t pos_offset,
+    float* __restrict__ lse_out, float* __restrict__ loss_out, float* __restrict__ dq,
+    float* __restrict__ neg_lse_bias) {
+  constexpr int LPR = D / 4;  // lanes per row
+  const int64_t i = blockIdx.x * (256ll / LPR) + threadIdx.x / LPR;
+  const int sub = threadIdx.x % LPR;
+  if (i >= n_rows) return;
+  // splits in groups of 4 whose loads are all issued before any is used
+  // (index clamped, weight 0 past nsplit); splits added in order as before
+  float M = -1.0e30f;
+  for (int s0 = 0; s0 < nsplit; s0 += 4) {
+    float m[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) m[u] = part_m[min(s0 + u, nsplit - 1) * n_stat_pad + i];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) M = fmaxf(M, m[u]);
   }
-  __syncthreads();
-  if (*flag == 0) return;
-  constexpr int LPR = D / 4, RPI = kThreads / LPR;
-  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kRowsPerWG;
-  for (int rr = static_cast<int>(threadIdx.x) / LPR; rr < kRowsPerWG; rr += RPI) {
-    const int64_t i = r0 + rr;
-    if (i >= a.n) break;
-    if constexpr (MODE == 0)
-      combine_row<D>(i, threadIdx.x % LPR, a.part_m, a.part_l, a.part_o, a.nsplit, a.n_stat_pad, a.q, a.ldq, a.c,
-                     a.ldc, a.logq, a.dim, a.pos_offset, a.lse, a.loss, a.dq, a.neg_lse);
-    else
-      combine_col<D>(i, threadIdx.x % LPR, a.part_o, a.nsplit, a.n_stat_pad, a.q, a.ldq, a.logq, a.dim,
-                     a.pos_offset, a.dc);
+  float L = 0.0f;
+  f32x4 o = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (int s0 = 0; s0 < nsplit; s0 += 4) {
+    float m[4], l[4];
+    f32x4 ps[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t sr = min(s0 + u, nsplit - 1) * n_stat_pad + i;
+      m[u] = part_m[sr];
+      l[u] = part_l[sr];
+      ps[u] = *reinterpret_cast<const f32x4*>(part_o + sr * D + 4 * sub);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (s0 + u < nsplit) {
+        const float w = expf(m[u] - M);
+        L += l[u] * w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] += ps[u][e] * w;
+      }
+    }
+  }
+  const float lse = M + logf(L);
+  const float inv = 1.0f / L;
+  const int64_t pos = i + pos_offset;
+  float dot = 0.0f;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = 4 * sub + u;
+    if (e < dim) {
+      const float ce = c[pos * ldc + e];
+      if (dq) dq[i * dim + e] = o[u] * inv - ce;
+      dot = __builtin_fmaf(q[i * ldq + e], ce, dot);
+    }
+  }
+#pragma unroll
+  for (int m = LPR / 2; m >= 1; m >>= 1) dot += __shfl_xor(dot, m, LPR);
+  if (sub == 0) {
+    const float pos_logit = dot - (logq ? logq[pos] : 0.0f);
+    lse_out[i] = lse;
+    loss_out[i] = lse - pos_logit;
+    if (neg_lse_bias) neg_lse_bias[i] = -lse;
+  }
+}
+
+// Cols: dc_j = exp(-logq_j) * sum_s O_s[j] - q_pos(j).
+template <int D>
+__global__ void __launch_bounds__(256) combine_cols_kernel(const float* __restrict__ part_o, int nsplit,
+                                                           int64_t n_stat_pad, const float* __restrict__ q,
+                                                           int64_t ldq, const float* __restrict__ logq,
+                                                           int64_t n_cols, int dim, int64_t pos_offset,
+                                                           float* __restrict__ dc) {
+  constexpr int LPR = D / 4;
+  const int64_t j = blockIdx.x * (256ll / LPR) + threadIdx.x / LPR;
+  const int sub = threadIdx.x % LPR;
+  if (j >= n_cols) return;
+  const float scale = logq ? expf(-logq[j]) : 1.0f;
+  const int64_t pos = j + pos_offset;
+  f32x4 o = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (int s0 = 0; s0 < nsplit; s0 += 4) {  // 4 splits' loads in flight, added in order
+    f32x4 ps[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      ps[u] = *reinterpret_cast<const f32x4*>(part_o + (min(s0 + u, nsplit - 1) * n_stat_pad + j) * D + 4 * sub);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (s0 + u < nsplit) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] += ps[u][e];
+      }
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = 4 * sub + u;
+    if (e < dim) dc[j * dim + e] = o[u] * scale - q[pos * ldq + e];
   }
 }
 
@@ -674,29 +576,28 @@ int pick_dpad(int dim) {
   return 0;
 }
 
-#ifndef TT_INBATCH_WG_TARGET
-#define TT_INBATCH_WG_TARGET 512
-#endif
-// Splits of the streamed extent so that the grid has >= TT_INBATCH_WG_TARGET
-// workgroups (several per CU: two waves per SIMD hide each other's softmax).
+// Splits of the streamed extent so that the grid has >= 256 workgroups, one
+// per CU (the pass holds 426 registers per lane: one workgroup per CU).  The
+// split partials cost an fp32 [S, n, D] write and read per pass, so the
+// fewest splits that fill the chip win: at the C3 batch (B = 16384, 128
+// stationary blocks) S = 2 beat S = 4 by 19 us per train step (interleaved
+// A/B, two pairs).  TT_INBATCH_WGS overrides the target.
+int wg_target() {
+  static const int v = [] {
+    const char* e = std::getenv("TT_INBATCH_WGS");
+    const int x = e ? std::atoi(e) : 0;
+    return x > 0 ? x : 256;
+  }();
+  return v;
+}
 int pick_split(int64_t n_stat_pad, int64_t n_strm_pad) {
   const int64_t wgs = n_stat_pad / kRowsPerWG;
-  int64_t s = ceil_div(TT_INBATCH_WG_TARGET, wgs);
+  int64_t s = ceil_div(wg_target(), wgs);
   const int64_t tiles = n_strm_pad / kTile;
   if (s > tiles) s = tiles;
   if (s > kMaxSplit) s = kMaxSplit;
   if (s < 1) s = 1;
   return static_cast<int>(s);
-}
-
-// TT_INBATCH_COMBINE=separate: the split combines as their own launches
-// (default: fused into the passes' last workgroups).
-bool fused_combine() {
-  static const bool v = [] {
-    const char* e = std::getenv("TT_INBATCH_COMBINE");
-    return !(e && std::strcmp(e, "separate") == 0);
-  }();
-  return v;
 }
 
 struct Plan {
@@ -723,7 +624,6 @@ struct PassWs {
   float* part_m;
   float* part_l;
   float* part_o;
-  int* done;
 };
 
 PassWs carve_pass(Carver& cv, const Plan& p) {
@@ -734,7 +634,6 @@ PassWs carve_pass(Carver& cv, const Plan& p) {
   w.part_m = cv.take<float>(int64_t(p.split) * p.stat_pad);
   w.part_l = cv.take<float>(int64_t(p.split) * p.stat_pad);
   w.part_o = cv.take<float>(int64_t(p.split) * p.stat_pad * p.D);
-  w.done = cv.take<int>(p.stat_pad / kRowsPerWG);
   return w;
 }
 
@@ -747,23 +646,7 @@ size_t pass_bytes(int64_t n_stat, int64_t n_strm, int dim) {
 PrepJob prep_job(const float* src, int64_t ld, int64_t n, int dim, __bf16* dst, const float* bv = nullptr,
                  float* bias = nullptr, float* bias2 = nullptr) {
   const int vec = (reinterpret_cast<uintptr_t>(src) % 16 == 0 && ld % 4 == 0 && dim % 4 == 0) ? 1 : 0;
-  return PrepJob{src, ld, n, dst, bv, -1.0f, bias, bias2, vec, nullptr, 0};
-}
-
-// the pass's fused-combine operands (a.done stays NULL for separate combines)
-void set_combine(PassArgs& a, int* done, int nsplit, const float* q, int64_t ldq, const float* c, int64_t ldc,
-                 const float* logq, int64_t n, int dim, int64_t pos_offset) {
-  if (!fused_combine()) return;
-  a.done = done;
-  a.nsplit = nsplit;
-  a.q = q;
-  a.ldq = ldq;
-  a.c = c;
-  a.ldc = ldc;
-  a.logq = logq;
-  a.n = n;
-  a.dim = dim;
-  a.pos_offset = pos_offset;
+  return PrepJob{src, ld, n, dst, bv, -1.0f, bias, bias2, vec};
 }
 
 // Preps one or two matrices padded to n_pad rows (j1.src == NULL: one).
@@ -888,18 +771,10 @@ extern "C" int tt_inbatch_xent_rows(const float* q, int64_t ldq, int64_t n_rows,
     return fail(TT_ERR_WORKSPACE, "tt_inbatch_xent_rows: workspace %zu < required %zu", workspace_bytes, cv.used());
   hipStream_t st = to_stream(stream);
   const PrepJob none{};
-  PrepJob jq = prep_job(q, ldq, n_rows, dim, w.stat);
-  jq.zero = w.done;
-  jq.nzero = static_cast<int>(p.stat_pad / kRowsPerWG);
-  if ((rc = prep(p.D, jq, none, dim, p.stat_pad, st))) return rc;
+  if ((rc = prep(p.D, prep_job(q, ldq, n_rows, dim, w.stat), none, dim, p.stat_pad, st))) return rc;
   if ((rc = prep(p.D, prep_job(c, ldc, n_cols, dim, w.strm, logq, w.bias), none, dim, p.strm_pad, st))) return rc;
   PassArgs a{w.stat, w.strm, w.bias, p.stat_pad, p.strm_pad, p.per_split, w.part_m, w.part_l, w.part_o};
-  set_combine(a, w.done, p.split, q, ldq, c, ldc, logq, n_rows, dim, pos_offset);
-  a.lse = lse;
-  a.loss = row_loss;
-  a.dq = dq;
   if ((rc = launch_pass<0>(p, a, st))) return rc;
-  if (a.done) return TT_OK;
   return combine_rows(p.D, st, w.part_m, w.part_l, w.part_o, p.split, p.stat_pad, q, ldq, c, ldc, logq, n_rows, dim,
                       pos_offset, lse, row_loss, dq, nullptr);
 }
@@ -921,31 +796,23 @@ extern "C" int tt_inbatch_xent_cols(const float* q, int64_t ldq, int64_t n_rows,
     return fail(TT_ERR_WORKSPACE, "tt_inbatch_xent_cols: workspace %zu < required %zu", workspace_bytes, cv.used());
   hipStream_t st = to_stream(stream);
   const PrepJob none{};
-  PrepJob jc = prep_job(c, ldc, n_cols, dim, w.stat);
-  jc.zero = w.done;
-  jc.nzero = static_cast<int>(p.stat_pad / kRowsPerWG);
-  if ((rc = prep(p.D, jc, none, dim, p.stat_pad, st))) return rc;
+  if ((rc = prep(p.D, prep_job(c, ldc, n_cols, dim, w.stat), none, dim, p.stat_pad, st))) return rc;
   if ((rc = prep(p.D, prep_job(q, ldq, n_rows, dim, w.strm, lse, w.bias), none, dim, p.strm_pad, st))) return rc;
   PassArgs a{w.stat, w.strm, w.bias, p.stat_pad, p.strm_pad, p.per_split, nullptr, nullptr, w.part_o};
-  set_combine(a, w.done, p.split, q, ldq, nullptr, 0, logq, n_cols, dim, pos_offset);
-  a.dc = dc;
   if ((rc = launch_pass<1>(p, a, st))) return rc;
-  if (a.done) return TT_OK;
   return combine_cols(p.D, st, w.part_o, p.split, p.stat_pad, q, ldq, logq, n_cols, dim, pos_offset, dc);
 }
 
 // ---------------------------------------------------------------------------
 // Single-device fused loss: rows and cols passes share one bf16 preparation of
 // q and c (one row-major image each), the cols pass's -lse bias is
-// written by the rows combine.  3 launches in total (prep + 2 passes, the
-// split combines fused into the passes), 5 with TT_INBATCH_COMBINE=separate.
+// written by the rows combine.  5 launches in total.
 namespace tt {
 namespace {
 struct FusedWs {
   __bf16 *qb, *cb;
   float *bias_logq, *bias_lse;
   float *part_m, *part_l, *part_o_rows, *part_o_cols;
-  int* done;  // arrival counters: rows pass [n_pad/128], then cols pass
 };
 struct FusedPlan {
   int D;
@@ -971,7 +838,6 @@ FusedWs carve_fused(Carver& cv, const FusedPlan& p) {
   w.part_l = cv.take<float>(int64_t(p.split) * p.n_pad);
   w.part_o_rows = cv.take<float>(int64_t(p.split) * p.n_pad * p.D);
   w.part_o_cols = cv.take<float>(int64_t(p.split) * p.n_pad * p.D);
-  w.done = cv.take<int>(2 * (p.n_pad / kRowsPerWG));
   return w;
 }
 }  // namespace
@@ -999,28 +865,16 @@ extern "C" int tt_inbatch_softmax_xent(const float* q, int64_t ldq, const float*
                 cv.used());
   hipStream_t st = to_stream(stream);
   // one prep launch for both matrices; c's job also writes both bias vectors
-  const int nblk = static_cast<int>(p.n_pad / kRowsPerWG);
-  PrepJob jq = prep_job(q, ldq, n, dim, w.qb);
-  jq.zero = w.done;
-  jq.nzero = 2 * nblk;
-  if ((rc = prep(p.D, jq, prep_job(c, ldc, n, dim, w.cb, logq, w.bias_logq, w.bias_lse), dim, p.n_pad, st)))
+  if ((rc = prep(p.D, prep_job(q, ldq, n, dim, w.qb), prep_job(c, ldc, n, dim, w.cb, logq, w.bias_logq, w.bias_lse),
+                 dim, p.n_pad, st)))
     return rc;
   const Plan pl{p.D, p.n_pad, p.n_pad, p.split, p.per_split};
   PassArgs ar{w.qb, w.cb, w.bias_logq, p.n_pad, p.n_pad, p.per_split, w.part_m, w.part_l, w.part_o_rows};
-  set_combine(ar, w.done, p.split, q, ldq, c, ldc, logq, n, dim, 0);
-  ar.lse = lse;
-  ar.loss = row_loss;
-  ar.dq = dq;
-  ar.neg_lse = w.bias_lse;
   if ((rc = launch_pass<0>(pl, ar, st))) return rc;
-  if (!ar.done &&
-      (rc = combine_rows(p.D, st, w.part_m, w.part_l, w.part_o_rows, p.split, p.n_pad, q, ldq, c, ldc, logq, n, dim,
+  if ((rc = combine_rows(p.D, st, w.part_m, w.part_l, w.part_o_rows, p.split, p.n_pad, q, ldq, c, ldc, logq, n, dim,
                          0, lse, row_loss, dq, w.bias_lse)))
     return rc;
   PassArgs ac{w.cb, w.qb, w.bias_lse, p.n_pad, p.n_pad, p.per_split, nullptr, nullptr, w.part_o_cols};
-  set_combine(ac, w.done + nblk, p.split, q, ldq, nullptr, 0, logq, n, dim, 0);
-  ac.dc = dc;
   if ((rc = launch_pass<1>(pl, ac, st))) return rc;
-  if (ac.done) return TT_OK;
   return combine_cols(p.D, st, w.part_o_cols, p.split, p.n_pad, q, ldq, logq, n, dim, 0, dc);
 }

@@ -462,11 +462,11 @@ __global__ void __launch_bounds__(kLsThreads) region_sort_kernel(const Job j) {
 //   chunk_merge_kernel: the final slot of a chunk's i-th element with row key
 //   k is i + #{keys <= k in earlier chunks} + #{keys < k in later chunks}
 //   (stable: equal keys keep chunk order, and chunks are in position order),
-//   found by binary search of each other chunk's sorted keys staged in LDS
-//   (regions <= kLdsSortMax: <= 8 chunks), or for small tables from the
-//   digit counts of all chunks (any region size).
+//   found by binary search of each other chunk's sorted keys, all staged in
+//   LDS by one round of loads (regions <= kLdsSortMax: <= 8 chunks), or for
+//   small tables from the digit counts of all chunks (<= 64 chunks).
 constexpr int kChunk = 2048;
-constexpr int kCsThreads = 256;
+constexpr int kCsThreads = 512;
 constexpr int kCsWaves = kCsThreads / kWave;
 constexpr int kCsTiles = kChunk / kCsThreads;
 constexpr int kCsHistStride = kCsWaves + 1;
@@ -599,10 +599,12 @@ __global__ void __launch_bounds__(kCsThreads) chunk_sort_kernel(const Job j) {
     const bool last = p == passes - 1;
     if (passes == 1) {  // small table: the chunk's digit counts (block-uniform)
       __syncthreads();
-      uint32_t s = 0;
+      if (tid < 256) {
+        uint32_t s = 0;
 #pragma unroll
-      for (int v = 0; v < kCsWaves; ++v) s += hist[tid * kCsHistStride + v];
-      j.chunk_hist[static_cast<int64_t>(blockIdx.x) * 256 + tid] = s;
+        for (int v = 0; v < kCsWaves; ++v) s += hist[tid * kCsHistStride + v];
+        j.chunk_hist[static_cast<int64_t>(blockIdx.x) * 256 + tid] = s;
+      }
     }
     cs_scan_counts(hist, wsum);
 #pragma unroll
@@ -628,8 +630,11 @@ __global__ void __launch_bounds__(kCsThreads) chunk_sort_kernel(const Job j) {
   }
 }
 
+constexpr int kMergeMaxChunks = kLdsSortMax / kChunk;  // binary-search merge: every chunk's keys in LDS
+constexpr int kMergeLdsBytes = kMergeMaxChunks * kChunk * 4;
+
 __global__ void __launch_bounds__(kCsThreads) chunk_merge_kernel(const Job j) {
-  __shared__ uint32_t other[kChunk];
+  extern __shared__ __attribute__((aligned(16))) uint32_t allk[];  // [chunks][kChunk] sorted keys (large tables)
   __shared__ uint32_t base[256], first[256], wsum[2][kCsWaves];
   const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
   const int t = table_of_chunk(j, blockIdx.x);
@@ -652,15 +657,17 @@ __global__ void __launch_bounds__(kCsThreads) chunk_merge_kernel(const Job j) {
   const int bits = 32 - __builtin_clz(R.nr);
   if (bits <= 8) {
     // digit d: base = #{keys < d in the region} + #{keys == d in earlier
-    // chunks}; first = #{keys < d in this chunk}
+    // chunks}; first = #{keys < d in this chunk} (threads 0..255: one digit each)
     uint32_t tot = 0, before = 0, mine = 0;
-    const uint32_t* h = j.chunk_hist + static_cast<int64_t>(T.chunk_begin) * 256 + tid;
+    if (tid < 256) {
+      const uint32_t* h = j.chunk_hist + static_cast<int64_t>(T.chunk_begin) * 256 + tid;
 #pragma unroll 4
-    for (int c = 0; c < nch; ++c) {
-      const uint32_t x = h[static_cast<int64_t>(c) * 256];
-      tot += x;
-      before += c < ci ? x : 0u;
-      mine = c == ci ? x : mine;
+      for (int c = 0; c < nch; ++c) {
+        const uint32_t x = h[static_cast<int64_t>(c) * 256];
+        tot += x;
+        before += c < ci ? x : 0u;
+        mine = c == ci ? x : mine;
+      }
     }
     uint32_t it = tot, im = mine;  // inclusive scans over the digits
 #pragma unroll
@@ -681,22 +688,21 @@ __global__ void __launch_bounds__(kCsThreads) chunk_merge_kernel(const Job j) {
       et += wsum[0][v];
       em += wsum[1][v];
     }
-    base[tid] = et + before;
-    first[tid] = em;
+    if (tid < 256) {
+      base[tid] = et + before;
+      first[tid] = em;
+    }
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < kCsTiles; ++u) out[u] = base[key[u]] + (out[u] - first[key[u]]);
   } else {
+    // every chunk's sorted keys into LDS at once (one round trip), padded
+    // with keys above every row key
+    for (int e = tid; e < nch * kChunk; e += kCsThreads) allk[e] = e < T.n_pad ? ck[e] : 0xFFFFFFFFu;
+    __syncthreads();
     for (int c = 0; c < nch; ++c) {
       if (c == ci) continue;  // block-uniform
-      const int m = min(kChunk, T.n_pad - c * kChunk);
-      __syncthreads();
-#pragma unroll
-      for (int u = 0; u < kCsTiles; ++u) {
-        const int i = u * kCsThreads + tid;
-        other[i] = i < m ? ck[c * kChunk + i] : 0xFFFFFFFFu;
-      }
-      __syncthreads();
+      const uint32_t* other = allk + c * kChunk;
       // earlier chunk: keys <= k come first; later chunk: keys < k (k + 0 vs
       // k + 1 against the sorted keys; keys < 2^31, the padding compares high)
       const uint32_t bump = c < ci ? 1u : 0u;
@@ -1185,7 +1191,14 @@ int run_sparse(const tt_sparse_table* tables, int32_t num_tables, int64_t batch,
       if (lds && chunked) {
         hipLaunchKernelGGL(chunk_sort_kernel, dim3(j.num_chunks), dim3(kCsThreads), 0, st, j);
         TT_CHECK_LAUNCH();
-        hipLaunchKernelGGL(chunk_merge_kernel, dim3(j.num_chunks), dim3(kCsThreads), 0, st, j);
+        bool large = false;
+        for (int i = 0; i < cnt; ++i) large = large || bits_for(j.t[i].num_rows) > 8;
+        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(chunk_merge_kernel),
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                           kMergeLdsBytes);
+        TT_CHECK_HIP(attr);
+        hipLaunchKernelGGL(chunk_merge_kernel, dim3(j.num_chunks), dim3(kCsThreads), large ? kMergeLdsBytes : 0, st,
+                           j);
         TT_CHECK_LAUNCH();
       } else if (lds) {
         static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(region_sort_kernel),
