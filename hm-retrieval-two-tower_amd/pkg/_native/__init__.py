@@ -149,18 +149,6 @@ _PROTOS = {
         [POINTER(RouteLookup), c_int32, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          c_size_t, c_void_p]),
     "tt_route_owner": (c_int32, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "tt_relu_bias_grad_workspace_size": (c_size_t, [c_int64, c_int32]),
-    "tt_relu_bias_grad": (
-        c_int32,
-        [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int64, c_void_p, c_void_p,
-         c_size_t, c_void_p]),
-    "tt_sum_slices": (c_int32, [c_void_p, c_int32, c_int64, c_void_p, c_void_p]),
-    "tt_gemm": (
-        c_int32,
-        [c_int32, c_int32, c_int64, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_int64,
-         c_void_p, c_int64, c_void_p, c_int32, c_void_p, c_int64, c_int32, c_int64, c_int32, c_void_p, c_size_t,
-         c_void_p]),
-    "tt_gemm_workspace_size": (c_size_t, [c_int64, c_int64]),
     "tt_sum": (c_int32, [c_void_p, c_int64, c_float, c_void_p, c_void_p]),
     "tt_dense_adagrad": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p]),
     "tt_dense_adam": (

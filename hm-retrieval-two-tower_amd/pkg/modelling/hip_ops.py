@@ -16,12 +16,7 @@ from pkg import _native
 from pkg._native import GatherSegment, SparseTable, check, lib
 
 __all__ = [
-    "relu_bias_grad",
-    "sum_slices",
-    "gemm",
     "loss_sum",
-    "GEMM_BF16",
-    "GEMM_BF16X3",
     "gather_grouped",
     "sparse_adagrad",
     "sparse_sort",
@@ -379,48 +374,6 @@ def dedup_sum(ids: torch.Tensor, grad: torch.Tensor, num_rows: int) -> Tuple[tor
     return uniq[:u], summed[:u]
 
 
-def relu_bias_grad(gin: torch.Tensor, act: torch.Tensor, gscale: Optional[torch.Tensor] = None,
-                   out: Optional[torch.Tensor] = None, db: Optional[torch.Tensor] = None):
-    """K4 backward glue of a Dense(relu) layer: (gout, db) with
-    gout = (act > 0) * s * gin, s = gscale (a 1-element device tensor or None),
-    db = column sums of gout.  `out` may be gin itself."""
-    _req(gin, "gin", torch.float32, 2)
-    _req(act, "act", torch.float32, 2)
-    if gin.shape != act.shape:
-        raise ValueError("gin and act must have the same shape")
-    rows, cols = gin.shape
-    if out is None:
-        out = torch.empty_like(gin)
-    if db is None:
-        db = torch.empty(cols, dtype=torch.float32, device=gin.device)
-    _req(out, "out", torch.float32, 2)
-    if not db.is_contiguous() or db.numel() != cols:
-        raise ValueError("db must be a contiguous [cols] tensor")
-    if gscale is not None:
-        _req(gscale, "gscale", torch.float32)
-        if gscale.numel() != 1:
-            raise ValueError("gscale must have one element")
-    L = lib()
-    ws = Workspace.get(L.tt_relu_bias_grad_workspace_size(rows, cols), gin.device, "relu_bias_grad")
-    check(L.tt_relu_bias_grad(gin.data_ptr(), _row_major(gin, "gin"), gscale.data_ptr() if gscale is not None else None,
-                              act.data_ptr(), _row_major(act, "act"), rows, cols, out.data_ptr(),
-                              _row_major(out, "out"), db.data_ptr(), ws.data_ptr(), ws.numel(), _stream()))
-    return out, db
-
-
-def sum_slices(parts: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
-    """out = parts.sum(0) for parts [S, ...] contiguous, slices added in order."""
-    _req(parts, "parts", torch.float32)
-    _req(out, "out", torch.float32)
-    if not parts.is_contiguous() or not out.is_contiguous() or parts[0].numel() != out.numel():
-        raise ValueError("parts must be contiguous [S, *out.shape] and out contiguous")
-    check(lib().tt_sum_slices(parts.data_ptr(), parts.shape[0], out.numel(), out.data_ptr(), _stream()))
-    return out
-
-
-GEMM_BF16, GEMM_BF16X3 = 0, 1
-
-
 def loss_sum(x: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
     """0-d tensor scale * x.sum() (tt_sum: one deterministic launch)."""
     _req(x, "x", torch.float32)
@@ -428,65 +381,6 @@ def loss_sum(x: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
         raise ValueError("x must be contiguous")
     out = torch.empty((), dtype=torch.float32, device=x.device)
     check(lib().tt_sum(x.data_ptr(), x.numel(), float(scale), out.data_ptr(), _stream()))
-    return out
-
-
-def _operand(t: torch.Tensor, name: str) -> Tuple[int, int]:
-    """(pointer, leading dimension) of a 2-D fp32 tensor with unit inner stride."""
-    _req(t, name, torch.float32, 2)
-    return t.data_ptr(), _row_major(t, name)
-
-
-def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, a_t: bool = False, b_t: bool = False,
-         mask: Optional[torch.Tensor] = None, mask_on: str = "", scale: Optional[torch.Tensor] = None,
-         ones_row: bool = False, bias: Optional[torch.Tensor] = None, relu: bool = False, splits: int = 1,
-         precision: int = GEMM_BF16X3) -> torch.Tensor:
-    """K4 tower GEMM on bf16 MFMA (tt_gemm): out = epi(op(a) @ op(b)).
-
-    op(a) = a (a_t False, [M, K]) or a^T (a_t True, a is [K, M]); op(b) = b
-    ([K, N]) or b^T (b is [N, K]).  mask / mask_on ("a" or "b"): that
-    operand's entries become (mask > 0) * s * v, s = scale[0] (mask has the
-    operand's stored shape).  ones_row: out has one extra last row holding
-    the column sums of op(b) (op(a) gets a row of ones).  bias [N] and relu:
-    epilogue.  splits > 1: out is [splits, M, N] partials over equal k ranges
-    (sum them in order with sum_slices).  precision: GEMM_BF16X3 (hi/lo split
-    operands, fp32-faithful) or GEMM_BF16."""
-    pa, lda = _operand(a, "a")
-    pb, ldb = _operand(b, "b")
-    M = (a.shape[1] if a_t else a.shape[0]) + (1 if ones_row else 0)
-    K = a.shape[0] if a_t else a.shape[1]
-    kb = b.shape[1] if b_t else b.shape[0]
-    N = b.shape[0] if b_t else b.shape[1]
-    if kb != K:
-        raise ValueError(f"gemm: inner dimensions differ ({K} vs {kb})")
-    if splits > 1:
-        _req(out, "out", torch.float32, 3)
-        if not out.is_contiguous() or tuple(out.shape) != (splits, M, N):
-            raise ValueError(f"gemm: split output must be contiguous [{splits}, {M}, {N}]")
-        pc, ldc, slice_ = out.data_ptr(), N, M * N
-    else:
-        pc, ldc = _operand(out, "out")
-        slice_ = 0
-        if tuple(out.shape) != (M, N):
-            raise ValueError(f"gemm: out must be [{M}, {N}], got {tuple(out.shape)}")
-    mo = {"": 0, "a": 1, "b": 2}[mask_on]
-    pm, ldm = (0, 0)
-    if mo:
-        if mask is None or mask.shape != (a if mo == 1 else b).shape:
-            raise ValueError("gemm: mask must have the masked operand's shape")
-        pm, ldm = _operand(mask, "mask")
-    if scale is not None:
-        _req(scale, "scale", torch.float32)
-    if bias is not None:
-        _req(bias, "bias", torch.float32, 1)
-        if bias.numel() != N or not bias.is_contiguous():
-            raise ValueError("gemm: bias must be contiguous [N]")
-    L = lib()
-    ws = Workspace.get(L.tt_gemm_workspace_size(N, K), a.device, "gemm_weight_image")
-    check(L.tt_gemm(int(a_t), int(b_t), M, N, K, pa, lda, pb, ldb, mo, pm or None, ldm,
-                    scale.data_ptr() if scale is not None else None, M - 1 if ones_row else -1,
-                    bias.data_ptr() if bias is not None else None, int(relu), pc, ldc, int(splits), slice_,
-                    int(precision), ws.data_ptr(), ws.numel(), _stream()))
     return out
 
 

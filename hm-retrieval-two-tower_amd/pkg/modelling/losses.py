@@ -11,7 +11,6 @@ gradient.  The [B, B] score matrix never exists.
 """
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
@@ -43,12 +42,6 @@ _SIDE: dict = {}
 # train step sorts and applies that tower's embedding update in this scope).
 TOWER_C_SCOPE = "tower_c"
 
-# TT_WGRAD_STREAM=1: the towers' weight gradients on side streams beside the
-# input-gradient chains.  Off by default: the concurrent hipBLASLt GEMMs slow
-# the chains they run beside (C3 step 0.625-0.629 vs 0.601 ms in line).
-WGRAD_STREAM = os.environ.get("TT_WGRAD_STREAM", "0") == "1"
-
-
 def _tower_stream(device: torch.device) -> torch.cuda.Stream:
     """The stream the candidate tower's MLP runs on, beside the query tower's."""
     key = device.index if device.index is not None else torch.cuda.current_device()
@@ -63,9 +56,8 @@ class _TowersInBatchXent(torch.autograd.Function):
     tower's forward and backward run on a second stream concurrently with
     the query tower's (fork / join with stream waits: captured as parallel
     branches of the step's hipGraph).  The backward hands the loss's incoming
-    gradient to the top layers' fused relu/bias kernels as a device scalar (no
-    separate scaling pass over dQ, dC) and overwrites dQ / dC in place (they
-    are not needed afterwards)."""
+    gradient to the top layers' weight-gradient and input-gradient kernels as
+    a device scalar (no separate scaling pass over dQ, dC)."""
 
     @staticmethod
     def forward(ctx, qi, ci, flat_q, flat_c, logq, stack_q, stack_c, scale, on_tower=None):
@@ -93,19 +85,14 @@ class _TowersInBatchXent(torch.autograd.Function):
         main = torch.cuda.current_stream()
         side = _tower_stream(dq.device)
         side.wait_stream(main)
-        # weight-gradient side streams, joined here from the origin stream (the
-        # fused per-tower apply needs d flat on the tower's stream: in line there)
-        joins = [] if (ctx.on_tower is None and WGRAD_STREAM) else None
         with torch.cuda.stream(side), hip_ops.Workspace.scope(TOWER_C_SCOPE):
-            gci, gflat_c = stack_c.backward_acts(ca, flat_c, dc, s, ctx.needs_input_grad[1], joins=joins)
+            gci, gflat_c = stack_c.backward_acts(ca, flat_c, dc, s, ctx.needs_input_grad[1])
             if ctx.on_tower is not None:  # this tower's updates, beside the other tower's backward
                 ctx.on_tower(1, gci, gflat_c)
-        gqi, gflat_q = stack_q.backward_acts(qa, flat_q, dq, s, ctx.needs_input_grad[0], joins=joins)
+        gqi, gflat_q = stack_q.backward_acts(qa, flat_q, dq, s, ctx.needs_input_grad[0])
         if ctx.on_tower is not None:
             ctx.on_tower(0, gqi, gflat_q)
         main.wait_stream(side)
-        for ws in joins or ():
-            main.wait_stream(ws)
         return gqi, gci, gflat_q, gflat_c, None, None, None, None, None
 
 

@@ -4,9 +4,8 @@ train_step (two_tower_model.py:94-130) on MI355X:
   1. query / candidate InputLayer gathers        tt_gather_grouped (1 launch per tower)
   2. tower MLPs                                   tt_mlp_rows (bf16x3 MFMA, bias + relu epilogue)
   3. scores + logQ + eye-label CE-SUM + dQ/dC     tt_inbatch_xent_rows / _cols (fused, bf16x3 MFMA)
-  4. MLP backward                                 tt_mlp_rows input gradients (ReluGrad + bias
-                                                  column sums fused) + weight gradients
-                                                  (tower.WGRAD_KERNEL, on a side stream)
+  4. MLP backward                                 tt_mlp_wgrad weight + bias gradients and
+                                                  tt_mlp_rows input gradients (ReluGrad fused)
   5. optimizer                                    tt_dense_adagrad + tt_sparse_adagrad (dedup in-kernel)
 Every launch is stream-ordered with no host synchronisation, so the whole step
 can be captured once and replayed as a hipGraph (GraphedTrainStep).

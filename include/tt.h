@@ -237,53 +237,6 @@ int tt_dedup_sum(const int32_t* ids, int64_t n, int64_t num_rows,
                  int32_t* unique_ids, float* summed, int32_t* num_unique,
                  void* workspace, size_t workspace_bytes, tt_stream_t stream);
 
-/* K4 backward glue of the tower MLPs (Dense + ReLU, tower.py:45,48; TF's
- * ReluGrad + BiasAddGrad beside the MatMul gradients):
- *   gout = (act > 0) * s * gin with s = *gscale (device scalar, NULL -> 1),
- *   db   = column sums of gout (64-row blocks in row order; the block
- *          partials in 16 consecutive chunks, each in order; then the chunk
- *          sums in order: deterministic).  gout may alias gin.
- * act is the layer's relu output (the mask), all matrices row-major. */
-size_t tt_relu_bias_grad_workspace_size(int64_t rows, int32_t cols);
-int tt_relu_bias_grad(const float* gin, int64_t ldg, const float* gscale,
-                      const float* act, int64_t lda, int64_t rows, int32_t cols,
-                      float* gout, int64_t ldo, float* db, void* workspace,
-                      size_t workspace_bytes, tt_stream_t stream);
-/* out[i] = sum over s < nslices of parts[s*n + i] (slices in order): the
- * split-K reduction of a weight gradient computed as batched partial GEMMs. */
-int tt_sum_slices(const float* parts, int32_t nslices, int64_t n, float* out,
-                  tt_stream_t stream);
-
-/* K4  Tower MLP GEMMs (Dense, tower.py:41-49: MatMul + BiasAdd + Relu and
- * their gradients MatMul / BiasAddGrad / ReluGrad):
- *   C[i][j] = epi( sum_{r<K} opA(i,r) * opB(r,j) ),  i < M, j < N
- * opA(i,r) = A[i*lda + r] (a_col_major = 0) or A[r*lda + i] (1);
- * opB(r,j) = B[r*ldb + j] (b_col_major = 0) or B[j*ldb + r] (1).
- * mask_operand 1 (A) / 2 (B): that operand's values v become
- *   (mask > 0) ? s * v : 0, s = *scale (NULL -> 1), mask in the operand's
- *   layout with leading dimension ldm (the relu output of the layer).
- * ones_row = M - 1: row M-1 of opA is all ones (C's last row = column sums
- *   of opB: the bias gradient, stored after dW in the flat layout); -1: none.
- * epi: + bias[j] (bias != NULL), relu (relu != 0); only with splits == 1.
- * splits > 1: the reduction is split into `splits` equal k ranges, range z
- *   written to C + z*slice (reduce with tt_sum_slices, slice order).
- * precision: TT_GEMM_BF16 (bf16 operands) or TT_GEMM_BF16X3 (hi/lo split
- *   operands, three bf16 MFMAs per product: fp32-faithful to ~2^-17).
- * Layouts built: (0,0, no mask) y = x W;  (0,1, mask A) dx = G W^T;
- * (1,0, mask B) dW = x^T G;  (0,1) and (1,0) without a mask.
- * workspace (>= tt_gemm_workspace_size(N, K) bytes, may be NULL): lets the
- * bf16 y = x W / dx = G W^T forms (N <= 288, splits 1) pack the weight once
- * into a bf16 MFMA image that every workgroup keeps whole in LDS. */
-enum { TT_GEMM_BF16 = 0, TT_GEMM_BF16X3 = 1 };
-size_t tt_gemm_workspace_size(int64_t N, int64_t K);
-int tt_gemm(int32_t a_col_major, int32_t b_col_major, int64_t M, int64_t N,
-            int64_t K, const float* A, int64_t lda, const float* B, int64_t ldb,
-            int32_t mask_operand, const float* mask, int64_t ldm,
-            const float* scale, int64_t ones_row, const float* bias,
-            int32_t relu, float* C, int64_t ldc, int32_t splits, int64_t slice,
-            int32_t precision, void* workspace, size_t workspace_bytes,
-            tt_stream_t stream);
-
 /* K10  Dense optimizer steps on a flat parameter buffer (tower MLP weights).
  * ResourceApplyAdagradV2 / ResourceApplyAdam (optimizer_factory.py:15-18). */
 int tt_dense_adagrad(float* param, float* accum, const float* grad, int64_t n,

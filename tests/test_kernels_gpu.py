@@ -2,8 +2,8 @@
 
 Tolerances:
   gather, dedup, Adagrad, top-k indices + scores, merge, recall: bit-exact.
-  tower GEMMs vs fp64: norm-relative 2e-5 (bf16x3; fp32 accumulation of K
-    products alone is ~sqrt(K) 2^-24), 8e-3 (bf16).
+  tower GEMMs (tt_mlp_rows, tt_mlp_wgrad) vs fp64: norm-relative 2e-5
+    (bf16x3; fp32 accumulation of K products alone is ~sqrt(K) 2^-24).
   in-batch softmax CE (bf16 MFMA operands, fp32 accumulate) vs fp64 oracle:
     loss rel 1e-3 (north star) wherever B >= 32, and at every size within the
     certified bf16 error bound oracle.inbatch_error_bound (lse per row and the
@@ -150,128 +150,6 @@ def test_sparse_adagrad_per_table_grads_one_call(cuda):
     oracle.sparse_adagrad(tc, ac, np.concatenate([ic1, ic2]), np.concatenate([gc[:, 0:32], gc[:, 36:68]]), 0.05, 1e-7)
     for got, ref in zip(d, (tq, aq, tc, ac)):
         assert np.array_equal(got.cpu().numpy(), ref)
-
-
-@pytest.mark.parametrize("rows,cols", [(16384, 256), (1000, 128), (7, 3), (130, 300)])
-def test_relu_bias_grad_matches_reference(cuda, rows, cols):
-    """tt_relu_bias_grad: gout bit-exact to mask * s * gin; db equals the
-    column sums in the kernel's order (64-row blocks, 16 chunks of block
-    partials, chunk sums) exactly."""
-    rng = np.random.default_rng(rows + cols)
-    g = rng.standard_normal((rows, cols)).astype(np.float32)
-    act = np.maximum(rng.standard_normal((rows, cols)), 0).astype(np.float32)
-    s = np.float32(0.37)
-    gout, db = hip_ops.relu_bias_grad(_t(g, cuda), _t(act, cuda), _t(np.array([s], np.float32), cuda))
-    ref = np.where(act > 0, g * s, np.float32(0)).astype(np.float32)
-    assert np.array_equal(gout.cpu().numpy(), ref)
-    blocks = [ref[i:i + 64] for i in range(0, rows, 64)]
-    part = []
-    for b in blocks:
-        acc = np.zeros(cols, np.float32)
-        for r in b:
-            acc = (acc + r).astype(np.float32)
-        part.append(acc)
-    chunk = (len(part) + 15) // 16
-    exp = np.zeros(cols, np.float32)
-    for k in range(16):
-        acc = np.zeros(cols, np.float32)
-        for p_ in part[k * chunk:(k + 1) * chunk]:
-            acc = (acc + p_).astype(np.float32)
-        exp = (exp + acc).astype(np.float32)
-    assert np.array_equal(db.cpu().numpy(), exp)
-    # in place, no scale
-    tg = _t(g, cuda)
-    hip_ops.relu_bias_grad(tg, _t(act, cuda), None, out=tg)
-    assert np.array_equal(tg.cpu().numpy(), np.where(act > 0, g, np.float32(0)))
-
-
-def test_sum_slices_in_order(cuda):
-    rng = np.random.default_rng(5)
-    parts = rng.standard_normal((16, 258, 256)).astype(np.float32)
-    out = torch.empty(258, 256, device=cuda)
-    hip_ops.sum_slices(_t(parts, cuda), out)
-    exp = np.zeros((258, 256), np.float32)
-    for p_ in parts:
-        exp = (exp + p_).astype(np.float32)
-    assert np.array_equal(out.cpu().numpy(), exp)
-
-
-# --------------------------------------------------------------------------- tower GEMMs
-def _padded(x, dev, pad=4):
-    """x on the GPU as a column slice of a wider buffer (row stride > width)."""
-    buf = torch.full((x.shape[0], x.shape[1] + pad), float("nan"), device=dev)
-    buf[:, :x.shape[1]] = _t(x, dev)
-    return buf[:, :x.shape[1]]
-
-
-def _rel(got, ref):
-    return float(np.linalg.norm(got.astype(np.float64) - ref) / max(np.linalg.norm(ref), 1e-300))
-
-
-GEMM_TOL = {hip_ops.GEMM_BF16X3: 2e-5, hip_ops.GEMM_BF16: 8e-3}
-
-
-@pytest.mark.parametrize("precision", [hip_ops.GEMM_BF16X3, hip_ops.GEMM_BF16])
-@pytest.mark.parametrize("M,K,N", [(16384, 258, 256), (16384, 256, 128), (37, 200, 256), (130, 3, 7), (1, 1, 1)])
-def test_gemm_forward_bias_relu(cuda, precision, M, K, N):
-    """y = relu(x W + b) (tower.py:45,48) against fp64; x with a padded row stride."""
-    rng = np.random.default_rng(M + K + N)
-    x = rng.uniform(-0.05, 0.05, (M, K)).astype(np.float32)
-    w = rng.uniform(-0.1, 0.1, (K, N)).astype(np.float32)
-    b = rng.uniform(-0.01, 0.01, N).astype(np.float32)
-    out = torch.empty(M, N, device=cuda)
-    hip_ops.gemm(_padded(x, cuda), _t(w, cuda), out, bias=_t(b, cuda), relu=True, precision=precision)
-    ref = np.maximum(x.astype(np.float64) @ w + b, 0.0)
-    assert _rel(out.cpu().numpy(), ref) <= GEMM_TOL[precision]
-
-
-@pytest.mark.parametrize("precision", [hip_ops.GEMM_BF16X3, hip_ops.GEMM_BF16])
-@pytest.mark.parametrize("M,fi,fo", [(16384, 258, 256), (16384, 256, 128), (300, 200, 256), (9, 5, 3)])
-def test_gemm_input_grad_masked(cuda, precision, M, fi, fo):
-    """dx = (relu'(h) * s * g) W^T: the relu mask and scale fused into the A loads."""
-    rng = np.random.default_rng(M + fi)
-    g = rng.standard_normal((M, fo)).astype(np.float32)
-    act = np.maximum(rng.standard_normal((M, fo)), 0).astype(np.float32)
-    w = rng.uniform(-0.1, 0.1, (fi, fo)).astype(np.float32)
-    s = np.float32(0.73)
-    out = torch.empty(M, fi, device=cuda)
-    hip_ops.gemm(_t(g, cuda), _t(w, cuda), out, b_t=True, mask=_t(act, cuda), mask_on="a",
-                 scale=_t(np.array([s]), cuda, torch.float32), precision=precision)
-    gm = np.where(act > 0, g.astype(np.float64) * s, 0.0)
-    assert _rel(out.cpu().numpy(), gm @ w.T.astype(np.float64)) <= GEMM_TOL[precision]
-
-
-@pytest.mark.parametrize("precision", [hip_ops.GEMM_BF16X3, hip_ops.GEMM_BF16])
-@pytest.mark.parametrize("M,fi,fo,splits", [(16384, 258, 256, 64), (16384, 256, 128, 32), (1000, 200, 256, 1),
-                                            (77, 6, 5, 2), (4096, 2, 130, 8)])
-def test_gemm_weight_grad_with_bias_row(cuda, precision, M, fi, fo, splits):
-    """[dW; db] = [x, 1]^T (relu'(h) * g): split-K partials summed in slice
-    order; the last row is the bias gradient."""
-    rng = np.random.default_rng(M + fo)
-    x = rng.uniform(-0.05, 0.05, (M, fi)).astype(np.float32)
-    g = rng.standard_normal((M, fo)).astype(np.float32)
-    act = np.maximum(rng.standard_normal((M, fo)), 0).astype(np.float32)
-    gm = np.where(act > 0, g.astype(np.float64), 0.0)
-    out = torch.empty(fi + 1, fo, device=cuda)
-    if splits > 1:
-        part = torch.empty(splits, fi + 1, fo, device=cuda)
-        hip_ops.gemm(_padded(x, cuda), _t(g, cuda), part, a_t=True, mask=_t(act, cuda), mask_on="b", ones_row=True,
-                     splits=splits, precision=precision)
-        hip_ops.sum_slices(part, out)
-    else:
-        hip_ops.gemm(_padded(x, cuda), _t(g, cuda), out, a_t=True, mask=_t(act, cuda), mask_on="b", ones_row=True,
-                     precision=precision)
-    got = out.cpu().numpy()
-    assert _rel(got[:fi], x.T.astype(np.float64) @ gm) <= GEMM_TOL[precision]
-    assert _rel(got[fi], gm.sum(0)) <= GEMM_TOL[precision]
-
-
-def test_gemm_rejects_bad_shapes(cuda):
-    a = torch.empty(8, 4, device=cuda)
-    with pytest.raises(ValueError):
-        hip_ops.gemm(a, torch.empty(5, 3, device=cuda), torch.empty(8, 3, device=cuda))
-    with pytest.raises(ValueError):
-        hip_ops.gemm(a, torch.empty(4, 3, device=cuda), torch.empty(8, 4, device=cuda))
 
 
 @pytest.mark.parametrize("n", [0, 1, 1023, 16384, 100003])

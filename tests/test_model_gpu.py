@@ -112,29 +112,21 @@ def _cpu_mirror(m):
     return ref
 
 
-@pytest.mark.parametrize("zipf,backend,precision", [(True, "hipblaslt", None), (False, "hipblaslt", None),
-                                                    (True, "tt", "x3"), (False, "tt", "x3"), (True, "tt", "bf16"),
-                                                    (True, "mlp", None), (False, "mlp", None),
-                                                    (True, "mlp", "wgrad_tt"), (False, "mlp", "wgrad_tt")])
-def test_train_steps_match_cpu_restatement(cuda, zipf, backend, precision, monkeypatch):
-    """First step: every parameter update within 1e-2 rel of the fp32 CPU
-    restatement (bf16 MFMA operands in the fused loss give ~1e-3 per-example
-    gradient error, amplified where a batch-summed gradient cancels).  Then the
-    loss trajectory over 3 steps within 1e-3 rel (parameters themselves drift
-    apart: lr 0.05 on a 0.1 accumulator moves embeddings by about their own
-    scale every step, so any rounding difference is amplified).  Both tower
-    GEMM backends: hipBLASLt fp32, libtt tt_gemm (bf16x3 and plain bf16) and
-    libtt tt_mlp_rows (bf16x3) for the forward / input-gradient GEMMs."""
-    from pkg.modelling.models import tower as tower_mod
-
+@pytest.mark.parametrize("zipf", [True, False])
+def test_train_steps_match_cpu_restatement(cuda, zipf):
+    """First step: every parameter update within a norm-relative bound of the
+    fp32 CPU restatement — 3e-3 for the embedding tables, 1e-2 for the tower
+    MLP buffers.  The only non-fp32-faithful arithmetic is the fused loss's
+    bf16 MFMA operands (~1e-3 per-example gradient error); the MLP weight
+    gradients sum that error over the whole batch, where the exact sum
+    largely cancels (P - I), so their relative error is the larger one.
+    Observed (round 3, both id distributions): tables <= 2.7e-3, MLP
+    buffers <= 6.2e-3.  Then the loss trajectory over 3
+    steps within 1e-3 rel (parameters themselves drift apart: lr 0.05 on a
+    0.1 accumulator moves embeddings by about their own scale every step, so
+    any rounding difference is amplified).  Every tower GEMM is libtt's
+    (tt_mlp_rows forward / input gradients, tt_mlp_wgrad weight gradients)."""
     m = _small_model(cuda)
-    if precision == "wgrad_tt":  # "mlp" backend with tt_mlp_wgrad: no vendor GEMM in the step
-        monkeypatch.setattr(tower_mod, "WGRAD_KERNEL", "tt")
-        precision = None
-    for t in (m.query_tower, m.candidate_tower):
-        t.dense.backend = backend
-        if precision:
-            t.dense.precision = hip_ops.GEMM_BF16X3 if precision == "x3" else hip_ops.GEMM_BF16
     ref = _cpu_mirror(m)
     rng = np.random.default_rng(5)
 
@@ -163,11 +155,9 @@ def test_train_steps_match_cpu_restatement(cuda, zipf, backend, precision, monke
             after, r = snapshot(), ref_snapshot()
             for k in after:  # includes the shared ptn table (one combined update of both lookups)
                 d_gpu, d_ref = after[k] - before[k], r[k] - before[k]
-                # plain-bf16 tower GEMMs round activations and weights too (another
-                # ~2^-9 per operand before the same cancellation; measured ~5e-2 on
-                # the query tables): 8e-2, which is why the product keeps fp32-faithful GEMMs
-                tol = 8e-2 if precision == "bf16" else 1e-2
-                assert np.linalg.norm(d_gpu - d_ref) <= tol * np.linalg.norm(d_ref), k
+                err = np.linalg.norm(d_gpu - d_ref) / np.linalg.norm(d_ref)
+                print(f"first-step update {k}: rel err {err:.2e}")
+                assert err <= (1e-2 if k.endswith("mlp") else 3e-3), (k, err)
 
 
 @pytest.mark.parametrize("B", [1, 2, 37, 1000])

@@ -91,12 +91,8 @@ for K1 in (258, 200):
     print(f"K1={K1} wgrad1 rel {rel(dwb1, r1):.2e} wgrad2 rel {rel(dwb2, r2):.2e}")
     tw1 = gtime(lambda: hip_ops.mlp_wgrad(Xv, G1, dwb1))
     tw2 = gtime(lambda: hip_ops.mlp_wgrad(H1, G2, dwb2, gmask=E, scale=s))
-    part1 = torch.empty(16, K1, 256, device=dev)
-    part2 = torch.empty(16, 256, 128, device=dev)
-    tb1 = gtime(lambda: hip_ops.sum_slices(torch.bmm(Xv.reshape(16, M // 16, K1).transpose(1, 2),
-                                                     G1.view(16, M // 16, 256), out=part1), dwb1[:K1]))
-    tb2 = gtime(lambda: hip_ops.sum_slices(torch.bmm(H1.view(16, M // 16, 256).transpose(1, 2),
-                                                     G2.view(16, M // 16, 128), out=part2), dwb2[:256]))
-    print(f"K1={K1} us wgrad tt: dW1 {tw1:.1f} dW2(+mask) {tw2:.1f} | torch bmm+sum_slices: {tb1:.1f} {tb2:.1f}")
+    tb1 = gtime(lambda: torch.mm(Xv.t(), G1, out=dwb1[:K1]))
+    tb2 = gtime(lambda: torch.mm(H1.t(), G2, out=dwb2[:256]))
+    print(f"K1={K1} us wgrad tt: dW1 {tw1:.1f} dW2(+mask) {tw2:.1f} | torch mm (hipBLASLt): {tb1:.1f} {tb2:.1f}")
     print(f"K1={K1} us tt: fwd1 {t[0]:.1f} fwd2 {t[1]:.1f} dx2 {t[2]:.1f} dx1 {t[3]:.1f} | "
           f"torch: {tp[0]:.1f} {tp[1]:.1f} {tp[2]:.1f} {tp[3]:.1f} | pack x2 {tpk:.1f}")
