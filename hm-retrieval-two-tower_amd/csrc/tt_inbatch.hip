@@ -576,17 +576,18 @@ int pick_dpad(int dim) {
   return 0;
 }
 
-// Splits of the streamed extent so that the grid has >= 256 workgroups, one
-// per CU (the pass holds 426 registers per lane: one workgroup per CU).  The
-// split partials cost an fp32 [S, n, D] write and read per pass, so the
-// fewest splits that fill the chip win: at the C3 batch (B = 16384, 128
-// stationary blocks) S = 2 beat S = 4 by 19 us per train step (interleaved
-// A/B, two pairs).  TT_INBATCH_WGS overrides the target.
+// Splits of the streamed extent so that the grid has >= 512 workgroups: two
+// rounds over the 256 CUs (the pass holds 426 registers per lane, so one
+// workgroup per CU).  At the C3 batch (B = 16384, 128 stationary blocks)
+// S = 4 beat S = 2 — one round, fewer split partials — by 19-24 us per train
+// step (same box, 3 interleaved pairs; rows pass 116 vs 129 us, cols 104 vs
+// 118 us: the second round evens out the workgroups' finishing times).
+// TT_INBATCH_WGS overrides the target.
 int wg_target() {
   static const int v = [] {
     const char* e = std::getenv("TT_INBATCH_WGS");
     const int x = e ? std::atoi(e) : 0;
-    return x > 0 ? x : 256;
+    return x > 0 ? x : 512;
   }();
   return v;
 }
