@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_model_gpu.py tests/test_configs_gpu.py -x -q --timeout 200 --timeout-method thread -k "sparse or sort or dedup or adagrad or adam or train_step or c3 or c2 or scatter" > gpurun_out/t_r03y.log 2>&1; rc=$?
+grep -E "FAIL|Error" gpurun_out/t_r03y.log | tail -12; tail -1 gpurun_out/t_r03y.log; [ $rc -eq 0 ] || { tail -30 gpurun_out/t_r03y.log; exit $rc; }
+bash tools/gpu_trace_step.sh r03y > /dev/null; grep -E "block_sum|join|chunk|gather" gpurun_out/trace_r03y/timeline.txt; grep -o '"ms_per_step[^,]*' gpurun_out/trace_r03y/line.json
+for v in origin_join nested_join nested_twice; do timeout -k 10 60 python3 tools/graph_fork_probe.py $v || { echo "$v: exit $?"; exit 0; }; done
