@@ -99,10 +99,10 @@ class Adagrad(_Optimizer):
             side = self._side_streams[cur.device] = torch.cuda.Stream(device=cur.device)
         side.wait_stream(cur)
         for tower, scope in zip(towers, scopes):
-            specs, batch = self._sparse_specs([tower], with_grad=False)
-            if not specs or len(specs) > 16 or not batch:
-                continue
             with torch.cuda.stream(side), hip_ops.Workspace.scope(scope):
+                specs, batch = self._sparse_specs([tower], with_grad=False)  # new accumulators filled on `side`
+                if not specs or len(specs) > 16 or not batch:
+                    continue
                 hip_ops.sparse_sort(specs, batch)
                 key = hip_ops.Workspace._scope  # the apply must find its sorted keys in this scope's buffer
             done = torch.cuda.Event()
@@ -148,9 +148,6 @@ class Adagrad(_Optimizer):
         self._prepared = None
         if not torch.cuda.is_available():
             return
-        specs, batch = self._sparse_specs(towers, with_grad=False)
-        if not specs or len(specs) > 16 or not batch:
-            return
         cur = torch.cuda.current_stream()
         side = self._side_streams.get(cur.device)
         if side is None:
@@ -160,6 +157,11 @@ class Adagrad(_Optimizer):
         else:
             side.wait_stream(cur)
         with torch.cuda.stream(side):
+            # accumulators created here are filled on this stream, ahead of
+            # anything ordered after the sort
+            specs, batch = self._sparse_specs(towers, with_grad=False)
+            if not specs or len(specs) > 16 or not batch:
+                return
             hip_ops.sparse_sort(specs, batch)
         done = torch.cuda.Event()
         done.record(side)
