@@ -463,8 +463,8 @@ __global__ void __launch_bounds__(kLsThreads) region_sort_kernel(const Job j) {
 //   k is i + #{keys <= k in earlier chunks} + #{keys < k in later chunks}
 //   (stable: equal keys keep chunk order, and chunks are in position order),
 //   found by binary search of each other chunk's sorted keys, all staged in
-//   LDS by one round of loads (regions <= kLdsSortMax: <= 8 chunks), or for
-//   small tables from the digit counts of all chunks (<= 64 chunks).
+//   LDS by one round of loads (regions <= 32768 lookups: <= 16 chunks), or
+//   for small tables from the digit counts of all chunks (<= 64 chunks).
 constexpr int kChunk = 2048;
 constexpr int kCsThreads = 512;
 constexpr int kCsWaves = kCsThreads / kWave;
@@ -630,8 +630,12 @@ __global__ void __launch_bounds__(kCsThreads) chunk_sort_kernel(const Job j) {
   }
 }
 
-constexpr int kMergeMaxChunks = kLdsSortMax / kChunk;  // binary-search merge: every chunk's keys in LDS
-constexpr int kMergeLdsBytes = kMergeMaxChunks * kChunk * 4;
+// binary-search merge: every chunk's sorted keys staged in LDS (up to 16
+// chunks = 128 KB: regions of <= 32768 lookups, e.g. an owner's requests in
+// the row-sharded step)
+constexpr int kMergeMaxChunks = 16;
+constexpr int kChunkMaxLarge = kMergeMaxChunks * kChunk;
+constexpr int kMergeLdsMax = kMergeMaxChunks * kChunk * 4;
 
 __global__ void __launch_bounds__(kCsThreads) chunk_merge_kernel(const Job j) {
   extern __shared__ __attribute__((aligned(16))) uint32_t allk[];  // [chunks][kChunk] sorted keys (large tables)
@@ -1183,21 +1187,20 @@ int run_sparse(const tt_sparse_table* tables, int32_t num_tables, int64_t batch,
     if (stage != kStageApply) {
       const int mode = sort_mode();
       bool lds = mode != kSortDevice, chunked = mode == kSortChunk;
+      int merge_chunks = 0;  // most chunks of a large-key region: the merge's LDS
       for (int i = 0; i < cnt; ++i) {
         const bool small = bits_for(j.t[i].num_rows) <= 8;
         lds = lds && (j.t[i].n_pad <= kLdsSortMax || small);
-        chunked = chunked && (j.t[i].n_pad <= kLdsSortMax || (small && j.t[i].n_pad <= kChunkMaxSmall));
+        chunked = chunked && (small ? j.t[i].n_pad <= kChunkMaxSmall : j.t[i].n_pad <= kChunkMaxLarge);
+        if (!small) merge_chunks = std::max(merge_chunks, static_cast<int>(ceil_div(j.t[i].n_pad, kChunk)));
       }
-      if (lds && chunked) {
+      if (chunked) {
         hipLaunchKernelGGL(chunk_sort_kernel, dim3(j.num_chunks), dim3(kCsThreads), 0, st, j);
         TT_CHECK_LAUNCH();
-        bool large = false;
-        for (int i = 0; i < cnt; ++i) large = large || bits_for(j.t[i].num_rows) > 8;
         static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(chunk_merge_kernel),
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                           kMergeLdsBytes);
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, kMergeLdsMax);
         TT_CHECK_HIP(attr);
-        hipLaunchKernelGGL(chunk_merge_kernel, dim3(j.num_chunks), dim3(kCsThreads), large ? kMergeLdsBytes : 0, st,
+        hipLaunchKernelGGL(chunk_merge_kernel, dim3(j.num_chunks), dim3(kCsThreads), merge_chunks * kChunk * 4, st,
                            j);
         TT_CHECK_LAUNCH();
       } else if (lds) {

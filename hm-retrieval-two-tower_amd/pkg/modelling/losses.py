@@ -50,6 +50,38 @@ def _tower_stream(device: torch.device) -> torch.cuda.Stream:
     return _SIDE[key]
 
 
+class _TowerFork:
+    """Work in this block runs on the candidate tower's stream (forked from the
+    current one) and workspace scope; plain on CPU tensors."""
+
+    def __init__(self, like: torch.Tensor):
+        self.cuda = like.is_cuda
+        self.dev = like.device
+
+    def __enter__(self):
+        self.scope = hip_ops.Workspace.scope(TOWER_C_SCOPE)
+        self.scope.__enter__()
+        if self.cuda:
+            side = _tower_stream(self.dev)
+            side.wait_stream(torch.cuda.current_stream())
+            self.ctx = torch.cuda.stream(side)
+            self.ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.cuda:
+            self.ctx.__exit__(*exc)
+        self.scope.__exit__(*exc)
+        return False
+
+
+def _tower_join(like: torch.Tensor) -> None:
+    """The current stream waits for the candidate tower's stream (joined from
+    the fork's origin: a captured branch must not join a sub-branch itself)."""
+    if like.is_cuda:
+        torch.cuda.current_stream().wait_stream(_tower_stream(like.device))
+
+
 class _TowersInBatchXent(torch.autograd.Function):
     """Both tower MLPs and the in-batch loss as ONE autograd node.  The two
     towers' MLPs are independent chains of small GEMMs, so the candidate
@@ -128,8 +160,11 @@ class _GlobalTowersInBatchXent(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, qi, ci, flat_q, flat_c, logq, stack_q, stack_c, scale, comm):
+        # the two towers' MLPs on two streams, as in _TowersInBatchXent
+        with _TowerFork(qi):
+            ca = stack_c.forward_acts(ci, flat_c)
         qa = stack_q.forward_acts(qi, flat_q)
-        ca = stack_c.forward_acts(ci, flat_c)
+        _tower_join(qi)
         row_loss, dq, dc = global_inbatch_grads(qa[-1], ca[-1], logq, comm)
         ctx.stacks = (stack_q, stack_c)
         ctx.nq = len(qa)
@@ -143,8 +178,10 @@ class _GlobalTowersInBatchXent(torch.autograd.Function):
         qa, ca = acts[:ctx.nq], acts[ctx.nq:]
         s = (g * ctx.scale if ctx.scale != 1.0 else g).reshape(1).float().contiguous()
         stack_q, stack_c = ctx.stacks
-        gci, gflat_c = stack_c.backward_acts(ca, flat_c, dc, s, ctx.needs_input_grad[1])
+        with _TowerFork(dq):
+            gci, gflat_c = stack_c.backward_acts(ca, flat_c, dc, s, ctx.needs_input_grad[1])
         gqi, gflat_q = stack_q.backward_acts(qa, flat_q, dq, s, ctx.needs_input_grad[0])
+        _tower_join(dq)
         return gqi, gci, gflat_q, gflat_c, None, None, None, None, None
 
 

@@ -445,16 +445,16 @@ def test_route_requests_match_torch_restatement(cuda, world):
 @pytest.mark.parametrize("rows,sources,B", [(255, 2, 20000), (256, 1, 16384), (256, 2, 9000), (1, 1, 100),
                                              (1371980, 1, 16384), (40, 3, 5000), (3000, 1, 2049),
                                              (100000, 2, 8000), (1371980, 1, 2048), (200, 4, 30000),
-                                             (255, 4, 40000)])
+                                             (255, 4, 40000), (1371980, 2, 12000), (352900, 2, 16500)])
 def test_sparse_adagrad_sort_paths_bitexact(cuda, rows, sources, B):
     """The embedding update's id sort takes one of three paths per call: the
     chunked LDS sort (2048-lookup chunks sorted by their own workgroups, then
-    merged: by binary search of the other chunks for regions <= 16384
+    merged: by binary search of the other chunks for regions <= 32768
     lookups, by the chunks' digit counts for tables of <= 255 rows up to 64
     chunks), the one-workgroup LDS counting sort (tables of <= 255 rows with
     larger regions: 255 x 160000 lookups), or the key build + device radix
-    sort (anything else: 256 x 18000 lookups).  Each is bit-exact vs the
-    restatement; chunk edges (2048, 2049) included."""
+    sort (anything else: 352900 x 33000 lookups).  Each is bit-exact vs the
+    restatement; chunk edges (2048, 2049) and 16-chunk regions included."""
     rng = np.random.default_rng(rows + B)
     D = 8
     w = rng.uniform(-0.05, 0.05, (rows, D)).astype(np.float32)
@@ -472,13 +472,14 @@ def test_sparse_adagrad_sort_paths_bitexact(cuda, rows, sources, B):
     assert np.array_equal(ta.cpu().numpy(), ref_acc)
 
 
-@pytest.mark.parametrize("n", [16384, 16385, 20000])
+@pytest.mark.parametrize("n", [16384, 16385, 20000, 40000])
 def test_sparse_adagrad_mostly_invalid_ids_bitexact(cuda, n):
     """Lookups whose ids are mostly outside the table (the owner-side update
     of a sharded step marks other tables' requests -1, or ids past the last
     row) leave only the valid rows updated, bit-exact against the restatement.
-    n = 16384 is the largest region the LDS region sort takes; 16385 and 20000
-    go through the key build + device radix sort."""
+    n = 16384 fills 8 chunks of the chunked sort, 16385 and 20000 take 9 and
+    10 chunks (every chunk's keys staged in the merge's LDS), 40000 the key
+    build + device radix sort."""
     rng = np.random.default_rng(11)
     V, D = 3000, 128
     ids = np.where(rng.random(n) < 0.7, -1, zipf_ids(rng, n, V)).astype(np.int32)
