@@ -1259,6 +1259,12 @@ __global__ void __launch_bounds__(kFbWaves * kWave) fallback_kernel(const Fallba
 }
 
 // ---- host plan -------------------------------------------------------------
+#ifndef TT_INDEX_R_MUL  // target screened entries per query: TT_INDEX_R_MUL * k + TT_INDEX_R_ADD
+#define TT_INDEX_R_MUL 3.0
+#endif
+#ifndef TT_INDEX_R_ADD
+#define TT_INDEX_R_ADD 100.0
+#endif
 struct SearchPlan {
   int S, NS, jsel, cap, L, LF, P, k, parts;
   int64_t chunk;
@@ -1280,7 +1286,7 @@ SearchPlan plan_search(int64_t nq, int64_t n_rows, int k, int shards) {
   while (p.S < kMaxSplits && qblocks * p.S < 256 && ntiles / (2 * p.S) >= 64) p.S *= 2;
   const int64_t nts = ceil_div(ntiles, p.S);  // tiles per split
   const double ns_cand = static_cast<double>(nts) * kCTile;
-  const double R = (3.0 * k + 100.0) / (static_cast<double>(p.S) * (shards > 0 ? shards : 1));
+  const double R = (TT_INDEX_R_MUL * k + TT_INDEX_R_ADD) / (static_cast<double>(p.S) * (shards > 0 ? shards : 1));
   double mu;  // expected entries per (query, split)
   if (nts < 16 || R >= 0.25 * ns_cand) {
     p.NS = 0;  // keep every score of the split
