@@ -471,6 +471,33 @@ __global__ void __launch_bounds__(kThreads) inbatch_pass_kernel(const PassArgs a
 // Split combines: D/4 lanes per row (float4 partials), 1024/D rows per block.
 // Rows: lse, row loss, dq = O / L - c_pos (and -lse as the cols-pass bias).
 template <int D>
+__device__ __forceinline__ void combine_row_finish(int64_t i, int sub, float M, float L, const f32x4& o,
+                                                   const float (&ce)[4], const float (&qe)[4], float lq, int dim,
+                                                   float* __restrict__ lse_out, float* __restrict__ loss_out,
+                                                   float* __restrict__ dq, float* __restrict__ neg_lse_bias) {
+  constexpr int LPR = D / 4;
+  const float lse = M + logf(L);
+  const float inv = 1.0f / L;
+  float dot = 0.0f;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = 4 * sub + u;
+    if (e < dim) {
+      if (dq) dq[i * dim + e] = o[u] * inv - ce[u];
+      dot = __builtin_fmaf(qe[u], ce[u], dot);
+    }
+  }
+#pragma unroll
+  for (int m = LPR / 2; m >= 1; m >>= 1) dot += __shfl_xor(dot, m, LPR);
+  if (sub == 0) {
+    const float pos_logit = dot - lq;
+    lse_out[i] = lse;
+    loss_out[i] = lse - pos_logit;
+    if (neg_lse_bias) neg_lse_bias[i] = -lse;
+  }
+}
+
+template <int D>
 __global__ void __launch_bounds__(256) combine_rows_kernel(
     const float* __restrict__ part_m, const float* __restrict__ part_l, const float* __restrict__ part_o,
     int nsplit, int64_t n_stat_pad, const float* __restrict__ q, int64_t ldq, const float* __restrict__ c,
@@ -481,9 +508,46 @@ __global__ void __launch_bounds__(256) combine_rows_kernel(
   const int64_t i = blockIdx.x * (256ll / LPR) + threadIdx.x / LPR;
   const int sub = threadIdx.x % LPR;
   if (i >= n_rows) return;
+  const int64_t pos = i + pos_offset;
+  // the positive's operands, loaded with the partials (one round of loads
+  // when nsplit <= 4; columns past dim read a clamped one and are dropped)
+  float ce[4], qe[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = min(4 * sub + u, dim - 1);
+    ce[u] = c[pos * ldc + e];
+    qe[u] = q[i * ldq + e];
+  }
+  const float lq = logq ? logq[pos] : 0.0f;
   // splits in groups of 4 whose loads are all issued before any is used
   // (index clamped, weight 0 past nsplit); splits added in order as before
   float M = -1.0e30f;
+  if (nsplit <= 4) {  // one pass: M from the same loads
+    float m[4], l[4];
+    f32x4 ps[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t sr = min(u, nsplit - 1) * n_stat_pad + i;
+      m[u] = part_m[sr];
+      l[u] = part_l[sr];
+      ps[u] = *reinterpret_cast<const f32x4*>(part_o + sr * D + 4 * sub);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) M = fmaxf(M, m[u]);
+    float L = 0.0f;
+    f32x4 o = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (u < nsplit) {
+        const float w = expf(m[u] - M);
+        L += l[u] * w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] += ps[u][e] * w;
+      }
+    }
+    combine_row_finish<D>(i, sub, M, L, o, ce, qe, lq, dim, lse_out, loss_out, dq, neg_lse_bias);
+    return;
+  }
   for (int s0 = 0; s0 < nsplit; s0 += 4) {
     float m[4];
 #pragma unroll
@@ -513,27 +577,7 @@ __global__ void __launch_bounds__(256) combine_rows_kernel(
       }
     }
   }
-  const float lse = M + logf(L);
-  const float inv = 1.0f / L;
-  const int64_t pos = i + pos_offset;
-  float dot = 0.0f;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int e = 4 * sub + u;
-    if (e < dim) {
-      const float ce = c[pos * ldc + e];
-      if (dq) dq[i * dim + e] = o[u] * inv - ce;
-      dot = __builtin_fmaf(q[i * ldq + e], ce, dot);
-    }
-  }
-#pragma unroll
-  for (int m = LPR / 2; m >= 1; m >>= 1) dot += __shfl_xor(dot, m, LPR);
-  if (sub == 0) {
-    const float pos_logit = dot - (logq ? logq[pos] : 0.0f);
-    lse_out[i] = lse;
-    loss_out[i] = lse - pos_logit;
-    if (neg_lse_bias) neg_lse_bias[i] = -lse;
-  }
+  combine_row_finish<D>(i, sub, M, L, o, ce, qe, lq, dim, lse_out, loss_out, dq, neg_lse_bias);
 }
 
 // Cols: dc_j = exp(-logq_j) * sum_s O_s[j] - q_pos(j).
@@ -549,6 +593,9 @@ __global__ void __launch_bounds__(256) combine_cols_kernel(const float* __restri
   if (j >= n_cols) return;
   const float scale = logq ? expf(-logq[j]) : 1.0f;
   const int64_t pos = j + pos_offset;
+  float qe[4];  // q_pos, loaded with the first partials (clamped past dim, dropped)
+#pragma unroll
+  for (int u = 0; u < 4; ++u) qe[u] = q[pos * ldq + min(4 * sub + u, dim - 1)];
   f32x4 o = {0.0f, 0.0f, 0.0f, 0.0f};
   for (int s0 = 0; s0 < nsplit; s0 += 4) {  // 4 splits' loads in flight, added in order
     f32x4 ps[4];
@@ -565,7 +612,7 @@ __global__ void __launch_bounds__(256) combine_cols_kernel(const float* __restri
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int e = 4 * sub + u;
-    if (e < dim) dc[j * dim + e] = o[u] * scale - q[pos * ldq + e];
+    if (e < dim) dc[j * dim + e] = o[u] * scale - qe[u];
   }
 }
 

@@ -784,7 +784,6 @@ __global__ void __launch_bounds__(kThreads) block_sum_kernel(const Job j, const 
   const int lane = lane_id();
   const int blk = (gw - T.wave_begin) * (kWave / P) + lane / P;
   const int nblk = T.n_pad / kBlock;
-  if (!keys_are_mine(j)) return;
   if (blk >= nblk) return;
   const int b0 = T.base + blk * kBlock;   // first sorted index of the block
   const int tend = T.base + T.n_pad;      // end of the table's region
@@ -797,6 +796,8 @@ __global__ void __launch_bounds__(kThreads) block_sum_kernel(const Job j, const 
   }
   const uint32_t kprev = blk > 0 ? j.keys[b0 - 1] : ~0u;
   const uint32_t knext = b0 + kBlock < tend ? j.keys[b0 + kBlock] : ~0u;
+  // the fingerprint check in the same round of loads as the keys
+  if (!keys_are_mine(j)) return;
   // grad offsets (validated to fit 32 bits) and the segment structure; both are
   // the same for every column this lane visits.  The table's source offsets
   // are read ONCE into registers (indexing T.goff[] by a per-lane source made
@@ -867,6 +868,10 @@ __global__ void __launch_bounds__(kThreads) block_sum_kernel(const Job j, const 
 #pragma unroll
       for (int r = 0; r < kBlock; ++r)
         if (apply >> r & 1u) st[r] = load_row<OP>(T, static_cast<int64_t>(key[r] & id_mask) * T.dim + col);
+      // one wait for every row's state: the loads sit under branches, so the
+      // compiler cannot count them and would otherwise drain the queue (the
+      // stores included) before each row's stores
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
 #pragma unroll
       for (int r = 0; r < kBlock; ++r)
         if (apply >> r & 1u)
@@ -886,16 +891,19 @@ __global__ void __launch_bounds__(kThreads) join_kernel(const Job j, const Apply
   const int lane = lane_id();
   const int blk = (gw - T.wave_begin) * (kWave / P) + lane / P;
   const int nblk = T.n_pad / kBlock;
-  if (!keys_are_mine(j)) return;
   if (blk >= nblk) return;
   const int b0 = T.base + blk * kBlock;
   const int tend = T.base + T.n_pad;
+  // most blocks end no segment that continues: that test first, with the
+  // fingerprint check in the same round of loads
+  const uint32_t klast = j.keys[b0 + kBlock - 1];
+  const uint32_t knext = b0 + kBlock < tend ? j.keys[b0 + kBlock] : ~0u;
+  const bool mine = keys_are_mine(j);
+  if (!mine || knext != klast) return;
   uint32_t key[kBlock];
 #pragma unroll
   for (int r = 0; r < kBlock; ++r) key[r] = j.keys[b0 + r];
-  const uint32_t klast = key[kBlock - 1];
-  const bool tail_cont = (b0 + kBlock < tend) && j.keys[b0 + kBlock] == klast;
-  if (!tail_cont) return;
+  const uint32_t kprev = blk > 0 ? j.keys[b0 - 1] : ~0u;
   // the invalid-id run (sorted last in the region) is never applied: skip its join
   if ((klast & ((1u << j.id_bits) - 1u)) >= static_cast<uint32_t>(T.num_rows)) return;
   // the continuing segment must START in this block
@@ -903,7 +911,7 @@ __global__ void __launch_bounds__(kThreads) join_kernel(const Job j, const Apply
 #pragma unroll
   for (int r = kBlock - 2; r >= 0; --r)
     if (key[r] == klast && seg_start == r + 1) seg_start = r;
-  if (seg_start == 0 && blk > 0 && j.keys[b0 - 1] == klast) return;  // began in an earlier block
+  if (seg_start == 0 && kprev == klast) return;  // began in an earlier block
   // end of the segment: first sorted index in (b0+kBlock, tend) with a larger key
   int lo = b0 + kBlock, hi = tend;  // keys[lo] == klast, answer in (lo, hi]
   while (hi - lo > 1) {
