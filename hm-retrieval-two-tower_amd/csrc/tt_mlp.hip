@@ -548,20 +548,25 @@ __global__ void __launch_bounds__(1024) mlp_sum_parts_kernel(const float* __rest
 // One thread per (k-step, column block, lane): 8 hi + 8 lo bf16 of
 // B[k = 16 ks + 8 (lane >> 5) + j][n = 32 cb + (lane & 31)], j < 8, zero padded.
 // trans: B = W^T with W [N, K] row-major (B[k][n] = W[n * ldw + k]).
-__global__ void __launch_bounds__(256) mlp_pack_kernel(const float* __restrict__ w, int64_t ldw, int K, int N,
-                                                       int trans, int KS, int NB, __bf16* __restrict__ img) {
-  const int64_t t = blockIdx.x * 256ll + threadIdx.x;
-  if (t >= static_cast<int64_t>(KS) * NB * 64) return;
-  const int lane = static_cast<int>(t & 63);
-  const int cb = static_cast<int>((t >> 6) % NB);
-  const int ks = static_cast<int>((t >> 6) / NB);
+// One lane's 8 consecutive k of column n, as bf16 hi and lo, into the image
+// (fragment (ks, cb) of the B image, planes hi / lo).  All 8 loads are issued
+// before any is used (branch-free: out-of-range elements read w[0], become 0).
+__device__ __forceinline__ void pack_fragment(const float* __restrict__ w, int64_t ldw, int K, int N, int trans,
+                                              int ks, int cb, int NB, int lane, __bf16* __restrict__ img) {
   const int n = 32 * cb + (lane & 31);
+  float x[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 16 * ks + 8 * (lane >> 5) + j;
+    const bool ok = k < K && n < N;
+    const int64_t at = trans ? static_cast<int64_t>(n) * ldw + k : static_cast<int64_t>(k) * ldw + n;
+    x[j] = w[ok ? at : 0];
+  }
   unsigned hb[8], lb[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int k = 16 * ks + 8 * (lane >> 5) + j;
-    const float v = (k < K && n < N) ? (trans ? w[static_cast<int64_t>(n) * ldw + k] : w[static_cast<int64_t>(k) * ldw + n])
-                                     : 0.0f;
+    const float v = (k < K && n < N) ? x[j] : 0.0f;
     hb[j] = bf16_bits(v);
     lb[j] = bf16_bits(v - bf16_val(hb[j]));
   }
@@ -571,6 +576,14 @@ __global__ void __launch_bounds__(256) mlp_pack_kernel(const float* __restrict__
   const int64_t base = ((static_cast<int64_t>(ks) * NB + cb) * 2) * 64 + lane;
   reinterpret_cast<u32x4*>(img)[base] = hv;        // plane 0: hi
   reinterpret_cast<u32x4*>(img)[base + 64] = lv;   // plane 1: lo
+}
+
+__global__ void __launch_bounds__(256) mlp_pack_kernel(const float* __restrict__ w, int64_t ldw, int K, int N,
+                                                       int trans, int KS, int NB, __bf16* __restrict__ img) {
+  const int64_t t = blockIdx.x * 256ll + threadIdx.x;
+  if (t >= static_cast<int64_t>(KS) * NB * 64) return;
+  const int lane = static_cast<int>(t & 63);
+  pack_fragment(w, ldw, K, N, trans, static_cast<int>((t >> 6) / NB), static_cast<int>((t >> 6) % NB), NB, lane, img);
 }
 
 // image k-steps padded to whole 64-deep stages, column blocks to 4 per wave row
@@ -590,30 +603,16 @@ struct PackJobs {
 __global__ void __launch_bounds__(256) mlp_pack_many_kernel(const PackJobs jobs, int64_t total) {
   const int64_t t = blockIdx.x * 256ll + threadIdx.x;
   if (t >= total) return;
+  // jobs start on multiples of 64 threads: the job is wave-uniform (scalar search)
+  const int64_t tw = (static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(t >> 6)))) << 6;
   int q = 0;
-  while (q + 1 < jobs.n && t >= jobs.j[q + 1].first) ++q;
+  while (q + 1 < jobs.n && tw >= jobs.j[q + 1].first) ++q;
   const PackJob& J = jobs.j[q];
   const int64_t u = t - J.first;
   const int lane = static_cast<int>(u & 63);
   const int cb = static_cast<int>((u >> 6) % J.NB);
   const int ks = static_cast<int>((u >> 6) / J.NB);
-  const int n = 32 * cb + (lane & 31);
-  unsigned hb[8], lb[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int k = 16 * ks + 8 * (lane >> 5) + j;
-    const float v = (k < J.K && n < J.N) ? (J.trans ? J.w[static_cast<int64_t>(n) * J.ldw + k]
-                                                    : J.w[static_cast<int64_t>(k) * J.ldw + n])
-                                         : 0.0f;
-    hb[j] = bf16_bits(v);
-    lb[j] = bf16_bits(v - bf16_val(hb[j]));
-  }
-  u32x4 hv, lv;
-  hv.x = hb[0] | (hb[1] << 16); hv.y = hb[2] | (hb[3] << 16); hv.z = hb[4] | (hb[5] << 16); hv.w = hb[6] | (hb[7] << 16);
-  lv.x = lb[0] | (lb[1] << 16); lv.y = lb[2] | (lb[3] << 16); lv.z = lb[4] | (lb[5] << 16); lv.w = lb[6] | (lb[7] << 16);
-  const int64_t base = ((static_cast<int64_t>(ks) * J.NB + cb) * 2) * 64 + lane;
-  reinterpret_cast<u32x4*>(J.img)[base] = hv;
-  reinterpret_cast<u32x4*>(J.img)[base + 64] = lv;
+  pack_fragment(J.w, J.ldw, J.K, J.N, J.trans, ks, cb, J.NB, lane, J.img);
 }
 
 inline int mlp_ks(int K) { return (K + 63) / 64 * 4; }
