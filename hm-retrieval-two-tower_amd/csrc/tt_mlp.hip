@@ -85,19 +85,25 @@ __device__ __forceinline__ int a_lds_off(int plane, int row, int chunk) {
   return ((plane * kMlpBM + row) << 7) + ((chunk ^ ((row >> 1) & 7)) << 4);
 }
 
+// A stages (2 x 2 planes x 64 rows x 128 B = 32 KiB), then the output tile
+// [64][NCB * 128 + 4] fp32 of the epilogue (<= 97 KiB)
+template <int NCB>
+struct MlpSmem {
+  static constexpr int OUT_LD = NCB * 128 + 4;
+  static constexpr int BYTES = kMlpBM * OUT_LD * 4 > 2 * 2 * kMlpBM * 128 ? kMlpBM * OUT_LD * 4 : 2 * 2 * kMlpBM * 128;
+};
+
+// One workgroup's rows [bid * kMlpBM, +kMlpBM) of one problem; smem_raw holds
+// MlpSmem<NCB>::BYTES.
 template <int NCB, bool HAS_MASK>
-__global__ void __launch_bounds__(kMlpThreads) mlp_rows_kernel(const MlpArgs a) {
-  // A stages (2 x 2 planes x 64 rows x 128 B = 32 KiB), then the output tile
-  // [64][NCB * 128 + 4] fp32 of the epilogue (<= 97 KiB)
-  constexpr int OUT_LD = NCB * 128 + 4;
-  constexpr int SMEM = kMlpBM * OUT_LD * 4 > 2 * 2 * kMlpBM * 128 ? kMlpBM * OUT_LD * 4 : 2 * 2 * kMlpBM * 128;
-  __shared__ __attribute__((aligned(16))) char smem_raw[SMEM];
+__device__ __forceinline__ void mlp_rows_block(const MlpArgs& a, const int64_t bid, char* smem_raw) {
+  constexpr int OUT_LD = MlpSmem<NCB>::OUT_LD;
   char (*smem)[2 * kMlpBM * 128] = reinterpret_cast<char (*)[2 * kMlpBM * 128]>(smem_raw);
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
   const int lane = lane_id();
   const int l32 = lane & 31, h = lane >> 5;
-  const int64_t m0 = static_cast<int64_t>(blockIdx.x) * kMlpBM;
+  const int64_t m0 = bid * kMlpBM;
   const float s = a.scale ? *a.scale : 1.0f;
 
   // ---- A stages: thread -> rows qrow + 16 u (u < 4), depths qk .. qk + 3 ------
@@ -266,8 +272,26 @@ __global__ void __launch_bounds__(kMlpThreads) mlp_rows_kernel(const MlpArgs a) 
   for (int c = tid; c < a.N; c += kMlpThreads) {
     float sum = 0.0f;
     for (int row = 0; row < rows; ++row) sum += tile[row * OUT_LD + c];  // already masked
-    a.parts[static_cast<int64_t>(blockIdx.x) * a.N + c] = sum;
+    a.parts[bid * a.N + c] = sum;
   }
+}
+
+template <int NCB, bool HAS_MASK>
+__global__ void __launch_bounds__(kMlpThreads) mlp_rows_kernel(const MlpArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem_raw[MlpSmem<NCB>::BYTES];
+  mlp_rows_block<NCB, HAS_MASK>(a, blockIdx.x, smem_raw);
+}
+
+// Two independent problems in one launch (the two towers' layers): blocks
+// [0, split) are a0's, the rest a1's.
+template <int NCB0, int NCB1, bool HAS_MASK>
+__global__ void __launch_bounds__(kMlpThreads) mlp_rows_pair_kernel(const MlpArgs a0, const MlpArgs a1,
+                                                                    const int split) {
+  constexpr int B0 = MlpSmem<NCB0>::BYTES, B1 = MlpSmem<NCB1>::BYTES;
+  __shared__ __attribute__((aligned(16))) char smem_raw[B0 > B1 ? B0 : B1];
+  const int b = blockIdx.x;
+  if (b < split) mlp_rows_block<NCB0, HAS_MASK>(a0, b, smem_raw);
+  else mlp_rows_block<NCB1, HAS_MASK>(a1, b - split, smem_raw);
 }
 
 // out[c] = sum over b of parts[b][c] in b order; 64 columns x 16 row groups
@@ -349,17 +373,16 @@ struct WgradArgs {
 typedef __bf16 wg_bf16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) wg_bf16x4 lds_bf16x4_t;
 
+// Workgroup b of one problem; wsm holds 2 * kWgStageB bytes.
 template <bool MASK>
-__global__ void __launch_bounds__(kWgThreads) mlp_wgrad_kernel(const WgradArgs a) {
-  __shared__ __attribute__((aligned(16))) char wsm[2 * kWgStageB];
+__device__ __forceinline__ void mlp_wgrad_block(const WgradArgs& a, const int b, char* wsm) {
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
   const int lane = lane_id();
-  // blockIdx -> (split, tile); the tiles of a split on one XCD when S % 8 == 0
+  // b -> (split, tile); the tiles of a split on one XCD when S % 8 == 0
   const int tiles = a.TI * a.TJ;
   int split, tile;
   {
-    const int b = blockIdx.x;
     if (a.S % 8 == 0) {
       const int q = b >> 3;
       tile = q % tiles;
@@ -506,15 +529,31 @@ __global__ void __launch_bounds__(kWgThreads) mlp_wgrad_kernel(const WgradArgs a
   }
 }
 
+template <bool MASK>
+__global__ void __launch_bounds__(kWgThreads) mlp_wgrad_kernel(const WgradArgs a) {
+  __shared__ __attribute__((aligned(16))) char wsm[2 * kWgStageB];
+  mlp_wgrad_block<MASK>(a, blockIdx.x, wsm);
+}
+
+// Two problems in one launch: blocks [0, split) are a0's (split % 8 == 0
+// keeps the second problem's split -> XCD mapping).
+template <bool MASK>
+__global__ void __launch_bounds__(kWgThreads) mlp_wgrad_pair_kernel(const WgradArgs a0, const WgradArgs a1,
+                                                                    const int split) {
+  __shared__ __attribute__((aligned(16))) char wsm[2 * kWgStageB];
+  const int b = blockIdx.x;
+  if (b < split) mlp_wgrad_block<MASK>(a0, b, wsm);
+  else mlp_wgrad_block<MASK>(a1, b - split, wsm);
+}
+
 // out[e] = sum over splits of parts[sp][e] (deterministic): a block covers 64
 // float4 of the output; group g of 16 adds splits [g S/16, (g+1) S/16) in
 // order (their loads all in flight), then the 16 group sums are added in
 // group order.  len % 4 == 0.
-__global__ void __launch_bounds__(1024) mlp_sum_parts_kernel(const float* __restrict__ parts, int S, int64_t len,
-                                                             float* __restrict__ out) {
-  __shared__ f32x4 red[16][64];
+__device__ __forceinline__ void mlp_sum_parts_block(const float* __restrict__ parts, int S, int64_t len,
+                                                    float* __restrict__ out, const int64_t bid, f32x4 (*red)[64]) {
   const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int64_t e4 = (blockIdx.x * 64ll + lane) * 4;
+  const int64_t e4 = (bid * 64 + lane) * 4;
   const int per = (S + 15) / 16;
   const int s0 = grp * per, s1 = min(S, s0 + per);
   f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -543,6 +582,23 @@ __global__ void __launch_bounds__(1024) mlp_sum_parts_kernel(const float* __rest
     }
     *reinterpret_cast<f32x4*>(out + e4) = t;
   }
+}
+
+__global__ void __launch_bounds__(1024) mlp_sum_parts_kernel(const float* __restrict__ parts, int S, int64_t len,
+                                                             float* __restrict__ out) {
+  __shared__ f32x4 red[16][64];
+  mlp_sum_parts_block(parts, S, len, out, blockIdx.x, red);
+}
+
+// Both problems' partial sums in one launch: blocks [0, split) are the first's.
+__global__ void __launch_bounds__(1024) mlp_sum_parts_pair_kernel(const float* __restrict__ p0, int S0, int64_t len0,
+                                                                  float* __restrict__ o0, const float* __restrict__ p1,
+                                                                  int S1, int64_t len1, float* __restrict__ o1,
+                                                                  const int split) {
+  __shared__ f32x4 red[16][64];
+  const int b = blockIdx.x;
+  if (b < split) mlp_sum_parts_block(p0, S0, len0, o0, b, red);
+  else mlp_sum_parts_block(p1, S1, len1, o1, b - split, red);
 }
 
 // One thread per (k-step, column block, lane): 8 hi + 8 lo bf16 of
@@ -676,21 +732,23 @@ extern "C" size_t tt_mlp_rows_workspace_size(int64_t M, int32_t N) {
   return static_cast<size_t>(ceil_div(M, kMlpBM)) * N * sizeof(float);
 }
 
-extern "C" int tt_mlp_rows(const float* A, int64_t lda, const float* amask, int64_t ldam, const float* scale,
-                           int64_t M, int32_t K, const void* img, int32_t N, const float* bias, int32_t relu,
-                           const float* cmask, int64_t ldcm, float* C, int64_t ldc, float* colsum, void* workspace,
-                           size_t workspace_bytes, tt_stream_t stream) {
-  clear_error();
-  TT_REQUIRE(A && img && C, "tt_mlp_rows: NULL A/img/C");
-  TT_REQUIRE(M >= 0 && K >= 1 && N >= 1, "tt_mlp_rows: bad M/K/N");
+// Validates one tt_mlp_rows problem (no colsum) into its kernel arguments;
+// *ncb = column blocks per wave.  TT_OK or the error code (message set).
+static int rows_setup(const char* fn, const float* A, int64_t lda, const float* amask, int64_t ldam,
+                      const float* scale, int64_t M, int32_t K, const void* img, int32_t N, const float* bias,
+                      int32_t relu, const float* cmask, int64_t ldcm, float* C, int64_t ldc, MlpArgs& a, int& ncb) {
+  TT_REQUIRE(A && img && C, "%s: NULL A/img/C", fn);
+  TT_REQUIRE(M >= 0 && K >= 1 && N >= 1, "%s: bad M/K/N", fn);
   const int NB = mlp_nb(N);
-  TT_REQUIRE(NB <= 4 * kMlpMaxCB, "tt_mlp_rows: N=%d > %d unsupported", N, 32 * 4 * kMlpMaxCB);
+  TT_REQUIRE(NB <= 4 * kMlpMaxCB, "%s: N=%d > %d unsupported", fn, N, 32 * 4 * kMlpMaxCB);
   TT_REQUIRE(M * lda < (int64_t(1) << 30) && (!amask || M * ldam < (int64_t(1) << 30)),
-             "tt_mlp_rows: operand too large for 32-bit buffer offsets");
+             "%s: operand too large for 32-bit buffer offsets", fn);
   TT_REQUIRE(lda >= K && ldc >= N && (!amask || ldam >= K) && (!cmask || ldcm >= N),
-             "tt_mlp_rows: leading dimension too small");
-  if (M == 0) return TT_OK;
-  MlpArgs a{};
+             "%s: leading dimension too small", fn);
+  TT_REQUIRE(reinterpret_cast<uintptr_t>(A) % 16 == 0 && lda % 4 == 0 &&
+                 (!amask || (reinterpret_cast<uintptr_t>(amask) % 16 == 0 && ldam % 4 == 0)),
+             "%s: A / amask rows must be 16-B aligned (ld %% 4 == 0)", fn);
+  a = MlpArgs{};
   a.A = A;
   a.lda = lda;
   a.amask = amask;
@@ -708,38 +766,91 @@ extern "C" int tt_mlp_rows(const float* A, int64_t lda, const float* amask, int6
   a.ldcm = ldcm;
   a.C = C;
   a.ldc = ldc;
+  ncb = NB / 4;
+  return TT_OK;
+}
+
+template <bool HM>
+static void launch_rows(const MlpArgs& a, int ncb, hipStream_t st) {
+  const dim3 grid(static_cast<unsigned>(ceil_div(a.M, kMlpBM)));
+  if (ncb == 1) hipLaunchKernelGGL((mlp_rows_kernel<1, HM>), grid, dim3(kMlpThreads), 0, st, a);
+  else if (ncb == 2) hipLaunchKernelGGL((mlp_rows_kernel<2, HM>), grid, dim3(kMlpThreads), 0, st, a);
+  else hipLaunchKernelGGL((mlp_rows_kernel<3, HM>), grid, dim3(kMlpThreads), 0, st, a);
+}
+
+template <int NCB0, bool HM>
+static void launch_rows_pair1(const MlpArgs& a0, const MlpArgs& a1, int ncb1, int split, dim3 grid,
+                              hipStream_t st) {
+  if (ncb1 == 1) hipLaunchKernelGGL((mlp_rows_pair_kernel<NCB0, 1, HM>), grid, dim3(kMlpThreads), 0, st, a0, a1, split);
+  else if (ncb1 == 2) hipLaunchKernelGGL((mlp_rows_pair_kernel<NCB0, 2, HM>), grid, dim3(kMlpThreads), 0, st, a0, a1, split);
+  else hipLaunchKernelGGL((mlp_rows_pair_kernel<NCB0, 3, HM>), grid, dim3(kMlpThreads), 0, st, a0, a1, split);
+}
+
+template <bool HM>
+static void launch_rows_pair(const MlpArgs& a0, int ncb0, const MlpArgs& a1, int ncb1, hipStream_t st) {
+  const int split = static_cast<int>(ceil_div(a0.M, kMlpBM));
+  const dim3 grid(static_cast<unsigned>(split + ceil_div(a1.M, kMlpBM)));
+  if (ncb0 == 1) launch_rows_pair1<1, HM>(a0, a1, ncb1, split, grid, st);
+  else if (ncb0 == 2) launch_rows_pair1<2, HM>(a0, a1, ncb1, split, grid, st);
+  else launch_rows_pair1<3, HM>(a0, a1, ncb1, split, grid, st);
+}
+
+extern "C" int tt_mlp_rows(const float* A, int64_t lda, const float* amask, int64_t ldam, const float* scale,
+                           int64_t M, int32_t K, const void* img, int32_t N, const float* bias, int32_t relu,
+                           const float* cmask, int64_t ldcm, float* C, int64_t ldc, float* colsum, void* workspace,
+                           size_t workspace_bytes, tt_stream_t stream) {
+  clear_error();
+  MlpArgs a;
+  int ncb = 0;
+  const int rc = rows_setup("tt_mlp_rows", A, lda, amask, ldam, scale, M, K, img, N, bias, relu, cmask, ldcm, C, ldc,
+                            a, ncb);
+  if (rc != TT_OK) return rc;
+  if (M == 0) return TT_OK;
   if (colsum) {
     TT_REQUIRE(workspace && workspace_bytes >= tt_mlp_rows_workspace_size(M, N),
                "tt_mlp_rows: colsum needs a workspace of tt_mlp_rows_workspace_size bytes");
     a.parts = static_cast<float*>(workspace);
   }
-  TT_REQUIRE(reinterpret_cast<uintptr_t>(A) % 16 == 0 && lda % 4 == 0 &&
-                 (!amask || (reinterpret_cast<uintptr_t>(amask) % 16 == 0 && ldam % 4 == 0)),
-             "tt_mlp_rows: A / amask rows must be 16-B aligned (ld %% 4 == 0)");
-  const dim3 grid(static_cast<unsigned>(ceil_div(M, kMlpBM)));
   hipStream_t st = to_stream(stream);
-  const int ncb = NB / 4;
-  if (amask) {
-    if (ncb == 1) hipLaunchKernelGGL((mlp_rows_kernel<1, true>), grid, dim3(kMlpThreads), 0, st, a);
-    else if (ncb == 2) hipLaunchKernelGGL((mlp_rows_kernel<2, true>), grid, dim3(kMlpThreads), 0, st, a);
-    else hipLaunchKernelGGL((mlp_rows_kernel<3, true>), grid, dim3(kMlpThreads), 0, st, a);
-  } else {
-    if (ncb == 1) hipLaunchKernelGGL((mlp_rows_kernel<1, false>), grid, dim3(kMlpThreads), 0, st, a);
-    else if (ncb == 2) hipLaunchKernelGGL((mlp_rows_kernel<2, false>), grid, dim3(kMlpThreads), 0, st, a);
-    else hipLaunchKernelGGL((mlp_rows_kernel<3, false>), grid, dim3(kMlpThreads), 0, st, a);
-  }
+  if (amask) launch_rows<true>(a, ncb, st);
+  else launch_rows<false>(a, ncb, st);
   TT_CHECK_LAUNCH();
   if (colsum) {
     hipLaunchKernelGGL(mlp_colsum_kernel, dim3(ceil_div(N, 64)), dim3(1024), 0, st, a.parts,
-                       static_cast<int>(grid.x), N, colsum);
+                       static_cast<int>(ceil_div(M, kMlpBM)), N, colsum);
   }
   TT_CHECK_LAUNCH();
   return TT_OK;
 }
 
-// splits of the batch reduction: enough (split, tile) workgroups to fill
-// the chip about twice, >= 256 rows each; a multiple of 8 when there are >= 8
-// (the XCD grouping)
+extern "C" int tt_mlp_rows_pair(const tt_mlp_rows_problem* p, tt_stream_t stream) {
+  clear_error();
+  TT_REQUIRE(p, "tt_mlp_rows_pair: NULL problems");
+  MlpArgs a[2];
+  int ncb[2];
+  for (int i = 0; i < 2; ++i) {
+    const tt_mlp_rows_problem& q = p[i];
+    const int rc = rows_setup("tt_mlp_rows_pair", q.A, q.lda, q.amask, q.ldam, q.scale, q.M, q.K, q.img, q.N,
+                              q.bias, q.relu, q.cmask, q.ldcm, q.C, q.ldc, a[i], ncb[i]);
+    if (rc != TT_OK) return rc;
+  }
+  hipStream_t st = to_stream(stream);
+  const bool hm0 = a[0].amask != nullptr, hm1 = a[1].amask != nullptr;
+  if (a[0].M == 0 || a[1].M == 0 || hm0 != hm1) {  // one problem, or masks differ: one launch each
+    for (int i = 0; i < 2; ++i) {
+      if (a[i].M == 0) continue;
+      if (a[i].amask) launch_rows<true>(a[i], ncb[i], st);
+      else launch_rows<false>(a[i], ncb[i], st);
+    }
+  } else if (hm0) {
+    launch_rows_pair<true>(a[0], ncb[0], a[1], ncb[1], st);
+  } else {
+    launch_rows_pair<false>(a[0], ncb[0], a[1], ncb[1], st);
+  }
+  TT_CHECK_LAUNCH();
+  return TT_OK;
+}
+
 static int wgrad_splits(int64_t M, int Ka, int N) {
   const int tiles = static_cast<int>(ceil_div(Ka + 1, kWgTile) * ceil_div(N, kWgTile));
   // TT_WGRAD_WGS: workgroups to aim for (default 1024: ~4 per CU, so the
@@ -758,27 +869,25 @@ extern "C" size_t tt_mlp_wgrad_workspace_size(int64_t M, int32_t Ka, int32_t N) 
   return static_cast<size_t>(wgrad_splits(M, Ka, N)) * (Ka + 1) * N * sizeof(float);
 }
 
-extern "C" int tt_mlp_wgrad(const float* A, int64_t lda, const float* G, int64_t ldg, const float* gmask,
-                            int64_t ldgm, const float* scale, int64_t M, int32_t Ka, int32_t N, float* dwb,
-                            void* workspace, size_t workspace_bytes, tt_stream_t stream) {
-  clear_error();
-  TT_REQUIRE(A && G && dwb, "tt_mlp_wgrad: NULL A/G/dwb");
-  TT_REQUIRE(M >= 0 && Ka >= 1 && Ka <= 4096, "tt_mlp_wgrad: Ka=%d outside [1, 4096]", Ka);
-  TT_REQUIRE(N >= 4 && N <= 4096 && N % 4 == 0, "tt_mlp_wgrad: N=%d must be a multiple of 4 in [4, 4096]", N);
-  TT_REQUIRE(lda >= Ka && ldg >= N && (!gmask || ldgm >= N), "tt_mlp_wgrad: leading dimension too small");
+// Validates one tt_mlp_wgrad problem into its kernel arguments (parts unset).
+static int wgrad_setup(const char* fn, const float* A, int64_t lda, const float* G, int64_t ldg, const float* gmask,
+                       int64_t ldgm, const float* scale, int64_t M, int32_t Ka, int32_t N, float* dwb,
+                       WgradArgs& a) {
+  TT_REQUIRE(A && G && dwb, "%s: NULL A/G/dwb", fn);
+  TT_REQUIRE(M >= 0 && Ka >= 1 && Ka <= 4096, "%s: Ka=%d outside [1, 4096]", fn, Ka);
+  TT_REQUIRE(N >= 4 && N <= 4096 && N % 4 == 0, "%s: N=%d must be a multiple of 4 in [4, 4096]", fn, N);
+  TT_REQUIRE(lda >= Ka && ldg >= N && (!gmask || ldgm >= N), "%s: leading dimension too small", fn);
   // 16-B vector loads of 8-column groups
-  TT_REQUIRE(lda % 4 == 0, "tt_mlp_wgrad: lda must be a multiple of 4");
+  TT_REQUIRE(lda % 4 == 0, "%s: lda must be a multiple of 4", fn);
   TT_REQUIRE(reinterpret_cast<uintptr_t>(A) % 16 == 0 && ldg % 4 == 0 && reinterpret_cast<uintptr_t>(G) % 16 == 0 &&
                  (!gmask || (ldgm % 4 == 0 && reinterpret_cast<uintptr_t>(gmask) % 16 == 0)),
-             "tt_mlp_wgrad: A / G / gmask rows must be 16-B aligned");
+             "%s: A / G / gmask rows must be 16-B aligned", fn);
   const int S = wgrad_splits(M, Ka, N);
   const int64_t rps = round_up(ceil_div(M > 0 ? M : 1, S), kWgBK);
   // per-split byte offsets are 32-bit (buffer loads)
   TT_REQUIRE(rps * std::max<int64_t>(lda, std::max<int64_t>(ldg, gmask ? ldgm : 0)) * 4 < (int64_t(1) << 31),
-             "tt_mlp_wgrad: a split's rows exceed 2 GiB");
-  TT_REQUIRE(workspace && workspace_bytes >= tt_mlp_wgrad_workspace_size(M, Ka, N),
-             "tt_mlp_wgrad: workspace %zu < %zu", workspace_bytes, tt_mlp_wgrad_workspace_size(M, Ka, N));
-  WgradArgs a{};
+             "%s: a split's rows exceed 2 GiB", fn);
+  a = WgradArgs{};
   a.A = A;
   a.lda = lda;
   a.G = G;
@@ -793,14 +902,74 @@ extern "C" int tt_mlp_wgrad(const float* A, int64_t lda, const float* G, int64_t
   a.TJ = static_cast<int>(ceil_div(N, kWgTile));
   a.S = S;
   a.rows_per_split = rps;
+  return TT_OK;
+}
+
+static void launch_wgrad(const WgradArgs& a, hipStream_t st) {
+  const dim3 grid(static_cast<unsigned>(a.S * a.TI * a.TJ));
+  if (a.gmask) hipLaunchKernelGGL((mlp_wgrad_kernel<true>), grid, dim3(kWgThreads), 0, st, a);
+  else hipLaunchKernelGGL((mlp_wgrad_kernel<false>), grid, dim3(kWgThreads), 0, st, a);
+}
+
+extern "C" int tt_mlp_wgrad(const float* A, int64_t lda, const float* G, int64_t ldg, const float* gmask,
+                            int64_t ldgm, const float* scale, int64_t M, int32_t Ka, int32_t N, float* dwb,
+                            void* workspace, size_t workspace_bytes, tt_stream_t stream) {
+  clear_error();
+  WgradArgs a;
+  const int rc = wgrad_setup("tt_mlp_wgrad", A, lda, G, ldg, gmask, ldgm, scale, M, Ka, N, dwb, a);
+  if (rc != TT_OK) return rc;
+  TT_REQUIRE(workspace && workspace_bytes >= tt_mlp_wgrad_workspace_size(M, Ka, N),
+             "tt_mlp_wgrad: workspace %zu < %zu", workspace_bytes, tt_mlp_wgrad_workspace_size(M, Ka, N));
   a.parts = static_cast<float*>(workspace);
   hipStream_t st = to_stream(stream);
-  const dim3 grid(static_cast<unsigned>(S * a.TI * a.TJ));
-  if (gmask) hipLaunchKernelGGL((mlp_wgrad_kernel<true>), grid, dim3(kWgThreads), 0, st, a);
-  else hipLaunchKernelGGL((mlp_wgrad_kernel<false>), grid, dim3(kWgThreads), 0, st, a);
+  launch_wgrad(a, st);
   TT_CHECK_LAUNCH();
   const int64_t len = static_cast<int64_t>(Ka + 1) * N;
-  hipLaunchKernelGGL(mlp_sum_parts_kernel, dim3(ceil_div(len, 256)), dim3(1024), 0, st, a.parts, S, len, dwb);
+  hipLaunchKernelGGL(mlp_sum_parts_kernel, dim3(ceil_div(len, 256)), dim3(1024), 0, st, a.parts, a.S, len, dwb);
+  TT_CHECK_LAUNCH();
+  return TT_OK;
+}
+
+// the second problem's partials start 256-B aligned after the first's
+static size_t wgrad_pair_offset(const tt_mlp_wgrad_problem* p) {
+  return static_cast<size_t>(round_up(static_cast<int64_t>(tt_mlp_wgrad_workspace_size(p[0].M, p[0].Ka, p[0].N)), 256));
+}
+
+extern "C" size_t tt_mlp_wgrad_pair_workspace_size(const tt_mlp_wgrad_problem* p) {
+  if (!p) return 0;
+  return wgrad_pair_offset(p) + tt_mlp_wgrad_workspace_size(p[1].M, p[1].Ka, p[1].N);
+}
+
+extern "C" int tt_mlp_wgrad_pair(const tt_mlp_wgrad_problem* p, void* workspace, size_t workspace_bytes,
+                                 tt_stream_t stream) {
+  clear_error();
+  TT_REQUIRE(p, "tt_mlp_wgrad_pair: NULL problems");
+  WgradArgs a[2];
+  for (int i = 0; i < 2; ++i) {
+    const tt_mlp_wgrad_problem& q = p[i];
+    const int rc = wgrad_setup("tt_mlp_wgrad_pair", q.A, q.lda, q.G, q.ldg, q.gmask, q.ldgm, q.scale, q.M, q.Ka, q.N,
+                               q.dwb, a[i]);
+    if (rc != TT_OK) return rc;
+  }
+  const size_t need = tt_mlp_wgrad_pair_workspace_size(p);
+  TT_REQUIRE(workspace && workspace_bytes >= need, "tt_mlp_wgrad_pair: workspace %zu < %zu", workspace_bytes, need);
+  a[0].parts = static_cast<float*>(workspace);
+  a[1].parts = reinterpret_cast<float*>(static_cast<char*>(workspace) + wgrad_pair_offset(p));
+  hipStream_t st = to_stream(stream);
+  const int nb0 = a[0].S * a[0].TI * a[0].TJ, nb1 = a[1].S * a[1].TI * a[1].TJ;
+  if ((a[0].gmask != nullptr) != (a[1].gmask != nullptr) || nb0 % 8 != 0) {
+    launch_wgrad(a[0], st);
+    launch_wgrad(a[1], st);
+  } else {
+    const dim3 grid(static_cast<unsigned>(nb0 + nb1));
+    if (a[0].gmask) hipLaunchKernelGGL((mlp_wgrad_pair_kernel<true>), grid, dim3(kWgThreads), 0, st, a[0], a[1], nb0);
+    else hipLaunchKernelGGL((mlp_wgrad_pair_kernel<false>), grid, dim3(kWgThreads), 0, st, a[0], a[1], nb0);
+  }
+  TT_CHECK_LAUNCH();
+  const int64_t len0 = static_cast<int64_t>(a[0].Ka + 1) * a[0].N, len1 = static_cast<int64_t>(a[1].Ka + 1) * a[1].N;
+  const int sb0 = static_cast<int>(ceil_div(len0, 256));
+  hipLaunchKernelGGL(mlp_sum_parts_pair_kernel, dim3(static_cast<unsigned>(sb0 + ceil_div(len1, 256))), dim3(1024), 0,
+                     st, a[0].parts, a[0].S, len0, p[0].dwb, a[1].parts, a[1].S, len1, p[1].dwb, sb0);
   TT_CHECK_LAUNCH();
   return TT_OK;
 }

@@ -21,6 +21,8 @@ __all__ = [
     "SparseTable",
     "RouteLookup",
     "MlpPackJob",
+    "MlpRowsProblem",
+    "MlpWgradProblem",
     "MAX_SEGMENTS",
     "MAX_SOURCES",
     "lib",
@@ -92,6 +94,42 @@ class MlpPackJob(ctypes.Structure):
         ("trans", c_int32),
         ("img", c_void_p),
         ("img_bytes", c_size_t),
+    ]
+
+
+class MlpRowsProblem(ctypes.Structure):
+    _fields_ = [
+        ("A", c_void_p),
+        ("lda", c_int64),
+        ("amask", c_void_p),
+        ("ldam", c_int64),
+        ("scale", c_void_p),
+        ("M", c_int64),
+        ("K", c_int32),
+        ("img", c_void_p),
+        ("N", c_int32),
+        ("bias", c_void_p),
+        ("relu", c_int32),
+        ("cmask", c_void_p),
+        ("ldcm", c_int64),
+        ("C", c_void_p),
+        ("ldc", c_int64),
+    ]
+
+
+class MlpWgradProblem(ctypes.Structure):
+    _fields_ = [
+        ("A", c_void_p),
+        ("lda", c_int64),
+        ("G", c_void_p),
+        ("ldg", c_int64),
+        ("gmask", c_void_p),
+        ("ldgm", c_int64),
+        ("scale", c_void_p),
+        ("M", c_int64),
+        ("Ka", c_int32),
+        ("N", c_int32),
+        ("dwb", c_void_p),
     ]
 
 
@@ -211,6 +249,9 @@ _PROTOS = {
         c_int32,
         [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int32, c_int32, c_void_p,
          c_void_p, c_size_t, c_void_p]),
+    "tt_mlp_rows_pair": (c_int32, [c_void_p, c_void_p]),
+    "tt_mlp_wgrad_pair_workspace_size": (c_size_t, [c_void_p]),
+    "tt_mlp_wgrad_pair": (c_int32, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "tt_batch_take": (
         c_int32,
         [c_void_p, c_int64, c_int32, c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_int64, c_void_p,

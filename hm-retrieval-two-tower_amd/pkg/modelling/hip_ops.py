@@ -645,12 +645,8 @@ def mlp_pack_many(jobs: Sequence[Tuple[torch.Tensor, bool, torch.Tensor]]) -> No
     check(lib().tt_mlp_pack_many(arr, len(jobs), _stream()))
 
 
-def mlp_rows(a: torch.Tensor, img: torch.Tensor, k: int, n: int, out: torch.Tensor, *,
-             amask: Optional[torch.Tensor] = None, scale: Optional[torch.Tensor] = None,
-             bias: Optional[torch.Tensor] = None, relu: bool = False,
-             cmask: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """out[M, n] = epi(maskA(a[:, :k]) . B) with B packed by mlp_pack (tt_mlp_rows);
-    colsum (a contiguous [n] tensor): also the column sums of out."""
+def _check_rows(a, k, n, out, amask, cmask, bias) -> int:
+    """mlp_rows' operand checks; returns M."""
     _req(a, "a", torch.float32, 2)
     _req(out, "out", torch.float32, 2)
     M = a.shape[0]
@@ -667,28 +663,57 @@ def mlp_rows(a: torch.Tensor, img: torch.Tensor, k: int, n: int, out: torch.Tens
         raise ValueError("cmask narrower than n")
     if bias is not None and (bias.dtype != torch.float32 or bias.numel() < n or not bias.is_contiguous()):
         raise ValueError("bias must be a contiguous fp32 vector of >= n entries")
+    return M
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return t.data_ptr() if t is not None else None
+
+
+def mlp_rows(a: torch.Tensor, img: torch.Tensor, k: int, n: int, out: torch.Tensor, *,
+             amask: Optional[torch.Tensor] = None, scale: Optional[torch.Tensor] = None,
+             bias: Optional[torch.Tensor] = None, relu: bool = False,
+             cmask: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out[M, n] = epi(maskA(a[:, :k]) . B) with B packed by mlp_pack (tt_mlp_rows);
+    colsum (a contiguous [n] tensor): also the column sums of out."""
+    M = _check_rows(a, k, n, out, amask, cmask, bias)
     ws = None
     if colsum is not None:
         if colsum.dtype != torch.float32 or colsum.numel() != n or not colsum.is_contiguous():
             raise ValueError("colsum must be a contiguous fp32 [n] tensor")
         ws = Workspace.get(lib().tt_mlp_rows_workspace_size(M, n), a.device, "mlp_colsum")
-    check(lib().tt_mlp_rows(a.data_ptr(), _row_major(a, "a"),
-                            amask.data_ptr() if amask is not None else None,
+    check(lib().tt_mlp_rows(a.data_ptr(), _row_major(a, "a"), _ptr(amask),
                             _row_major(amask, "amask") if amask is not None else 0,
-                            scale.data_ptr() if scale is not None else None, M, k, img.data_ptr(), n,
-                            bias.data_ptr() if bias is not None else None, int(bool(relu)),
-                            cmask.data_ptr() if cmask is not None else None,
+                            _ptr(scale), M, k, img.data_ptr(), n, _ptr(bias), int(bool(relu)), _ptr(cmask),
                             _row_major(cmask, "cmask") if cmask is not None else 0, out.data_ptr(),
-                            _row_major(out, "out"), colsum.data_ptr() if colsum is not None else None,
-                            ws.data_ptr() if ws is not None else None, ws.numel() if ws is not None else 0,
+                            _row_major(out, "out"), _ptr(colsum), _ptr(ws), ws.numel() if ws is not None else 0,
                             _stream()))
     return out
 
 
-def mlp_wgrad(a: torch.Tensor, g: torch.Tensor, dwb: torch.Tensor, *, gmask: Optional[torch.Tensor] = None,
-              scale: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """dwb [Ka + 1, N] = [a | 1]^T . Gm (weight gradient rows then the bias
-    gradient row), Gm = g or (gmask > 0) ? g * scale : 0 (tt_mlp_wgrad)."""
+def mlp_rows_pair(problems: Sequence[dict]) -> None:
+    """Two independent mlp_rows problems (the two towers' layers) in ONE
+    launch (tt_mlp_rows_pair); each problem is a dict of mlp_rows' arguments
+    a, img, k, n, out and optionally amask, scale, bias, relu, cmask (no
+    colsum).  Results equal two mlp_rows calls bit for bit."""
+    if len(problems) != 2:
+        raise ValueError("mlp_rows_pair takes exactly 2 problems")
+    arr = (_native.MlpRowsProblem * 2)()
+    for i, p in enumerate(problems):
+        a, img, k, n, out = p["a"], p["img"], p["k"], p["n"], p["out"]
+        amask, cmask, bias = p.get("amask"), p.get("cmask"), p.get("bias")
+        M = _check_rows(a, k, n, out, amask, cmask, bias)
+        q = arr[i]
+        q.A, q.lda, q.amask = a.data_ptr(), _row_major(a, "a"), _ptr(amask)
+        q.ldam = _row_major(amask, "amask") if amask is not None else 0
+        q.scale, q.M, q.K, q.img, q.N = _ptr(p.get("scale")), M, k, img.data_ptr(), n
+        q.bias, q.relu, q.cmask = _ptr(bias), int(bool(p.get("relu", False))), _ptr(cmask)
+        q.ldcm = _row_major(cmask, "cmask") if cmask is not None else 0
+        q.C, q.ldc = out.data_ptr(), _row_major(out, "out")
+    check(lib().tt_mlp_rows_pair(arr, _stream()))
+
+
+def _check_wgrad(a, g, dwb, gmask) -> Tuple[int, int, int]:
     _req(a, "a", torch.float32, 2)
     _req(g, "g", torch.float32, 2)
     _req(dwb, "dwb", torch.float32, 2)
@@ -700,10 +725,33 @@ def mlp_wgrad(a: torch.Tensor, g: torch.Tensor, dwb: torch.Tensor, *, gmask: Opt
         _req(gmask, "gmask", torch.float32, 2)
         if tuple(gmask.shape) != (M, N):
             raise ValueError("gmask must match g")
+    return M, Ka, N
+
+
+def mlp_wgrad(a: torch.Tensor, g: torch.Tensor, dwb: torch.Tensor, *, gmask: Optional[torch.Tensor] = None,
+              scale: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dwb [Ka + 1, N] = [a | 1]^T . Gm (weight gradient rows then the bias
+    gradient row), Gm = g or (gmask > 0) ? g * scale : 0 (tt_mlp_wgrad)."""
+    M, Ka, N = _check_wgrad(a, g, dwb, gmask)
     ws = Workspace.get(lib().tt_mlp_wgrad_workspace_size(M, Ka, N), a.device, "mlp_wgrad")
-    check(lib().tt_mlp_wgrad(a.data_ptr(), _row_major(a, "a"), g.data_ptr(), _row_major(g, "g"),
-                             gmask.data_ptr() if gmask is not None else None,
+    check(lib().tt_mlp_wgrad(a.data_ptr(), _row_major(a, "a"), g.data_ptr(), _row_major(g, "g"), _ptr(gmask),
                              _row_major(gmask, "gmask") if gmask is not None else 0,
-                             scale.data_ptr() if scale is not None else None, M, Ka, N, dwb.data_ptr(), ws.data_ptr(),
-                             ws.numel(), _stream()))
+                             _ptr(scale), M, Ka, N, dwb.data_ptr(), ws.data_ptr(), ws.numel(), _stream()))
     return dwb
+
+
+def mlp_wgrad_pair(problems: Sequence[dict]) -> None:
+    """Two mlp_wgrad problems (dicts of a, g, dwb and optionally gmask,
+    scale) in one launch plus one partial-sum launch (tt_mlp_wgrad_pair)."""
+    if len(problems) != 2:
+        raise ValueError("mlp_wgrad_pair takes exactly 2 problems")
+    arr = (_native.MlpWgradProblem * 2)()
+    for i, p in enumerate(problems):
+        a, g, dwb, gmask = p["a"], p["g"], p["dwb"], p.get("gmask")
+        M, Ka, N = _check_wgrad(a, g, dwb, gmask)
+        q = arr[i]
+        q.A, q.lda, q.G, q.ldg = a.data_ptr(), _row_major(a, "a"), g.data_ptr(), _row_major(g, "g")
+        q.gmask, q.ldgm = _ptr(gmask), _row_major(gmask, "gmask") if gmask is not None else 0
+        q.scale, q.M, q.Ka, q.N, q.dwb = _ptr(p.get("scale")), M, Ka, N, dwb.data_ptr()
+    ws = Workspace.get(lib().tt_mlp_wgrad_pair_workspace_size(arr), problems[0]["a"].device, "mlp_wgrad")
+    check(lib().tt_mlp_wgrad_pair(arr, ws.data_ptr(), ws.numel(), _stream()))

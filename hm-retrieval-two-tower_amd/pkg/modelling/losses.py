@@ -57,6 +57,35 @@ def _tower_stream(device: torch.device) -> torch.cuda.Stream:
 # World-1 sharded step, interleaved pairs: 16384 rows 0.896-0.903 vs
 # 0.942-0.945 ms; 2048 rows (an 8-way split) 0.579-0.605 vs 0.562-0.599.
 GLOBAL_TOWER_STREAMS = int(os.environ.get("TT_GLOBAL_TOWER_STREAMS", "4096"))
+# The single-GPU step's towers on two streams (TT_TOWER_STREAMS=0: one).
+TOWER_STREAMS = int(os.environ.get("TT_TOWER_STREAMS", "1"))
+# Both towers' layers as paired launches on one stream (tower.forward_acts_pair).
+TOWER_PAIR = int(os.environ.get("TT_TOWER_PAIR", "0"))
+
+
+def _paired(x: torch.Tensor, stack_q, stack_c) -> bool:
+    from pkg.modelling.models.tower import pair_compatible
+    return bool(TOWER_PAIR) and x.is_cuda and pair_compatible(stack_q, stack_c)
+
+
+def _pair_forward(qi, ci, flat_q, flat_c, stack_q, stack_c):
+    from pkg.modelling.models.tower import forward_acts_pair
+    return forward_acts_pair((stack_q, stack_c), (qi, ci), (flat_q, flat_c))
+
+
+def _pair_backward(ctx, qa, ca, flat_q, flat_c, dq, dc, s, on_tower=None):
+    """Both towers' backward as paired launches; on_tower(1, ...) runs in the
+    candidate tower's workspace scope (where its update was prepared)."""
+    from pkg.modelling.models.tower import backward_acts_pair
+    stack_q, stack_c = ctx.stacks
+    (gqi, gflat_q), (gci, gflat_c) = backward_acts_pair(
+        (stack_q, stack_c), (qa, ca), (flat_q, flat_c), (dq, dc), s,
+        (ctx.needs_input_grad[0], ctx.needs_input_grad[1]))
+    if on_tower is not None:
+        with hip_ops.Workspace.scope(TOWER_C_SCOPE):
+            on_tower(1, gci, gflat_c)
+        on_tower(0, gqi, gflat_q)
+    return gqi, gci, gflat_q, gflat_c
 
 
 class _TowerFork:
@@ -106,13 +135,21 @@ class _TowersInBatchXent(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, qi, ci, flat_q, flat_c, logq, stack_q, stack_c, scale, on_tower=None):
+        ctx.pair = _paired(qi, stack_q, stack_c)
+        if ctx.pair:
+            qa, ca = _pair_forward(qi, ci, flat_q, flat_c, stack_q, stack_c)
+            return _TowersInBatchXent._finish(ctx, qa, ca, flat_q, flat_c, logq, stack_q, stack_c, scale, on_tower)
         main = torch.cuda.current_stream()
-        side = _tower_stream(qi.device)
+        side = _tower_stream(qi.device) if TOWER_STREAMS else main
         side.wait_stream(main)
         with torch.cuda.stream(side), hip_ops.Workspace.scope(TOWER_C_SCOPE):
             ca = stack_c.forward_acts(ci, flat_c)
         qa = stack_q.forward_acts(qi, flat_q)
         main.wait_stream(side)
+        return _TowersInBatchXent._finish(ctx, qa, ca, flat_q, flat_c, logq, stack_q, stack_c, scale, on_tower)
+
+    @staticmethod
+    def _finish(ctx, qa, ca, flat_q, flat_c, logq, stack_q, stack_c, scale, on_tower):
         _, row_loss, dq, dc = hip_ops.inbatch_fused(qa[-1], ca[-1], logq)
         ctx.stacks = (stack_q, stack_c)
         ctx.nq = len(qa)
@@ -127,8 +164,11 @@ class _TowersInBatchXent(torch.autograd.Function):
         qa, ca = acts[:ctx.nq], acts[ctx.nq:]
         s = (g * ctx.scale if ctx.scale != 1.0 else g).reshape(1).float().contiguous()
         stack_q, stack_c = ctx.stacks
+        if ctx.pair:
+            return (*_pair_backward(ctx, qa, ca, flat_q, flat_c, dq, dc, s, ctx.on_tower),
+                    None, None, None, None, None)
         main = torch.cuda.current_stream()
-        side = _tower_stream(dq.device)
+        side = _tower_stream(dq.device) if TOWER_STREAMS else main
         side.wait_stream(main)
         with torch.cuda.stream(side), hip_ops.Workspace.scope(TOWER_C_SCOPE):
             gci, gflat_c = stack_c.backward_acts(ca, flat_c, dc, s, ctx.needs_input_grad[1])
@@ -173,11 +213,15 @@ class _GlobalTowersInBatchXent(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, qi, ci, flat_q, flat_c, logq, stack_q, stack_c, scale, comm):
-        # the two towers' MLPs on two streams, as in _TowersInBatchXent
-        with _TowerFork(qi):
-            ca = stack_c.forward_acts(ci, flat_c)
-        qa = stack_q.forward_acts(qi, flat_q)
-        _tower_join(qi)
+        ctx.pair = _paired(qi, stack_q, stack_c)
+        if ctx.pair:
+            qa, ca = _pair_forward(qi, ci, flat_q, flat_c, stack_q, stack_c)
+        else:
+            # the two towers' MLPs on two streams, as in _TowersInBatchXent
+            with _TowerFork(qi):
+                ca = stack_c.forward_acts(ci, flat_c)
+            qa = stack_q.forward_acts(qi, flat_q)
+            _tower_join(qi)
         row_loss, dq, dc = global_inbatch_grads(qa[-1], ca[-1], logq, comm)
         ctx.stacks = (stack_q, stack_c)
         ctx.nq = len(qa)
@@ -191,6 +235,8 @@ class _GlobalTowersInBatchXent(torch.autograd.Function):
         qa, ca = acts[:ctx.nq], acts[ctx.nq:]
         s = (g * ctx.scale if ctx.scale != 1.0 else g).reshape(1).float().contiguous()
         stack_q, stack_c = ctx.stacks
+        if ctx.pair:
+            return (*_pair_backward(ctx, qa, ca, flat_q, flat_c, dq, dc, s), None, None, None, None, None)
         with _TowerFork(dq):
             gci, gflat_c = stack_c.backward_acts(ca, flat_c, dc, s, ctx.needs_input_grad[1])
         gqi, gflat_q = stack_q.backward_acts(qa, flat_q, dq, s, ctx.needs_input_grad[0])

@@ -14,7 +14,11 @@ step is a single tt_dense_* launch.  Every GEMM is libtt's, on bf16x3 MFMA
     straight into the flat gradient (the top layer's ReluGrad and loss scale
     applied inside its loads), then ONE tt_mlp_rows for the layer below with
     the ReluGrad mask fused (G_{l-1} = (G_l W_l^T) * relu'(h_{l-1})), or the
-    input gradient of the first layer.
+    input gradient of the first layer;
+  * forward_acts_pair / backward_acts_pair: the same per-layer work of the
+    query and the candidate tower as ONE launch per layer and kind
+    (tt_mlp_rows_pair, tt_mlp_wgrad_pair) on one stream, bit-identical to the
+    single calls.
 """
 from __future__ import annotations
 
@@ -28,7 +32,18 @@ from pkg.modelling.device import default_device, make_generator
 from pkg.modelling.layers.input_layer import InputLayer
 from pkg.modelling.models.abstract_keras_model import AbstractKerasModel, TensorSpec
 
-__all__ = ["Tower", "DenseStack"]
+__all__ = ["Tower", "DenseStack", "pair_compatible", "forward_acts_pair", "backward_acts_pair"]
+
+
+def _rows(p: dict) -> torch.Tensor:
+    """hip_ops.mlp_rows on a problem dict (as mlp_rows_pair takes them)."""
+    q = dict(p)
+    return hip_ops.mlp_rows(q.pop("a"), q.pop("img"), q.pop("k"), q.pop("n"), q.pop("out"), **q)
+
+
+def _wgrad(p: dict) -> torch.Tensor:
+    q = dict(p)
+    return hip_ops.mlp_wgrad(q.pop("a"), q.pop("g"), q.pop("dwb"), **q)
 
 
 class _DenseStackFn(torch.autograd.Function):
@@ -73,12 +88,9 @@ class DenseStack:
         f = self.flat if flat is None else flat
         return [(f[w:w + fi * fo].view(fi, fo), f[b:b + fo]) for w, fi, fo, b in self.layout]
 
-    def _pack_images(self, flat: torch.Tensor) -> Dict[Tuple[str, int], torch.Tensor]:
-        """Every layer's packed bf16 hi/lo weight images, forward ("f": B = W)
-        and transposed ("t": B = W^T, the input-gradient GEMMs), in ONE
-        tt_mlp_pack_many launch into buffers owned by the stack (fixed
-        addresses: graph-capturable).  Packed at the start of each forward,
-        so they always match `flat`."""
+    def _pack_jobs(self, flat: torch.Tensor) -> Tuple[Dict[Tuple[str, int], torch.Tensor], list]:
+        """Image buffers (owned by the stack: fixed addresses, graph-capturable)
+        and the tt_mlp_pack_many jobs that fill them from `flat`."""
         imgs = self.__dict__.setdefault("_images", {})
         jobs = []
         for li, (w, _) in enumerate(self.params(flat)):
@@ -89,19 +101,30 @@ class DenseStack:
                 if buf is None or buf.numel() < nbytes or buf.device != w.device:
                     buf = imgs[(kind, li)] = torch.empty(nbytes, dtype=torch.uint8, device=w.device)
                 jobs.append((w, trans, buf))
+        return imgs, jobs
+
+    def _pack_images(self, flat: torch.Tensor) -> Dict[Tuple[str, int], torch.Tensor]:
+        """Every layer's packed bf16 hi/lo weight images, forward ("f": B = W)
+        and transposed ("t": B = W^T, the input-gradient GEMMs), in ONE
+        tt_mlp_pack_many launch.  Packed at the start of each forward, so they
+        always match `flat`."""
+        imgs, jobs = self._pack_jobs(flat)
         for i in range(0, len(jobs), 8):
             hip_ops.mlp_pack_many(jobs[i:i + 8])
         return imgs
+
+    def _fwd_problem(self, li: int, h: torch.Tensor, flat: torch.Tensor, imgs) -> dict:
+        w, b = self.params(flat)[li]
+        out = torch.empty(h.shape[0], w.shape[1], dtype=torch.float32, device=h.device)
+        return dict(a=h, img=imgs[("f", li)], k=w.shape[0], n=w.shape[1], out=out, bias=b, relu=True)
 
     def forward_acts(self, x: torch.Tensor, flat: torch.Tensor) -> List[torch.Tensor]:
         """[x, h_1, ..., h_L] with h_l = relu(h_{l-1} W_l + b_l) (tt_mlp_rows)."""
         imgs = self._pack_images(flat)
         acts = [x]
-        h = x
-        for li, (w, b) in enumerate(self.params(flat)):
-            out = torch.empty(h.shape[0], w.shape[1], dtype=torch.float32, device=h.device)
-            h = hip_ops.mlp_rows(h, imgs[("f", li)], w.shape[0], w.shape[1], out, bias=b, relu=True)
-            acts.append(h)
+        for li in range(len(self.layout)):
+            p = self._fwd_problem(li, acts[-1], flat, imgs)
+            acts.append(_rows(p))
         return acts
 
     def _wgrad_fits(self, li: int, g: torch.Tensor, acts: List[torch.Tensor]) -> bool:
@@ -112,6 +135,34 @@ class DenseStack:
             if t.stride(1) != 1 or t.stride(0) % 4 or t.data_ptr() % 16:
                 return False
         return fo % 4 == 0 and fo <= 4096 and fi <= 4096
+
+    def _wgrad_problem(self, li: int, acts, gflat, gout, g, gscale) -> dict:
+        """Layer li's [dW; db] as an mlp_wgrad problem (the top layer's
+        ReluGrad and scale applied to gout inside its loads)."""
+        w_off, fi, fo, _ = self.layout[li]
+        dwb = gflat[w_off:w_off + (fi + 1) * fo].view(fi + 1, fo)
+        if li == len(self.layout) - 1:
+            return dict(a=acts[li], g=gout, dwb=dwb, gmask=acts[-1], scale=gscale)
+        return dict(a=acts[li], g=g, dwb=dwb)
+
+    def _wgrad_torch(self, li: int, acts, gflat, g, gscale) -> None:
+        """The weight gradient outside tt_mlp_wgrad's contract (torch)."""
+        w_off, fi, fo, _ = self.layout[li]
+        dwb = gflat[w_off:w_off + (fi + 1) * fo].view(fi + 1, fo)
+        gm = g * (acts[-1] > 0) * (gscale if gscale is not None else 1.0) if li == len(self.layout) - 1 else g
+        torch.mm(acts[li].t(), gm, out=dwb[:fi])
+        torch.sum(gm, 0, out=dwb[fi])
+
+    def _igrad_problem(self, li: int, acts, g, gscale) -> dict:
+        """G_{l-1} = (G_l W_l^T) * relu'(h_{l-1}) (the top layer's relu mask and
+        scale on its A loads), or dx = G_1 W_1^T, as an mlp_rows problem."""
+        _, fi, fo, _ = self.layout[li]
+        top = li == len(self.layout) - 1
+        ld = (fi + 3) // 4 * 4  # 16-B rows for the kernel's vector stores
+        out = torch.empty(g.shape[0], ld, dtype=torch.float32, device=g.device)[:, :fi]
+        return dict(a=g, img=self.__dict__["_images"][("t", li)], k=fo, n=fi, out=out,
+                    amask=acts[-1] if top else None, scale=gscale if top else None,
+                    cmask=acts[li] if li > 0 else None)
 
     def backward_acts(self, acts: List[torch.Tensor], flat: torch.Tensor, gout: torch.Tensor,
                       gscale: Optional[torch.Tensor], need_input_grad: bool):
@@ -124,37 +175,81 @@ class DenseStack:
         gout is not modified.  A layer outside tt_mlp_wgrad's contract (output
         width not a multiple of 4, or wider than 4096) takes its weight
         gradient from torch (the only vendor GEMM left, never at the
-        reference's configurations)."""
+        reference's configurations).  Images: packed by this step's forward
+        (same flat)."""
         gflat = torch.empty_like(flat)
-        imgs = self.__dict__["_images"]  # packed by this step's forward (same flat)
-        L = len(self.layout)
         g = gout
-        for li in range(L - 1, -1, -1):
-            w_off, fi, fo, _ = self.layout[li]
-            dwb = gflat[w_off:w_off + (fi + 1) * fo].view(fi + 1, fo)
-            top = li == L - 1
+        for li in range(len(self.layout) - 1, -1, -1):
             if self._wgrad_fits(li, g, acts):
-                if top:
-                    hip_ops.mlp_wgrad(acts[li], gout, dwb, gmask=acts[L], scale=gscale)
-                else:
-                    hip_ops.mlp_wgrad(acts[li], g, dwb)
+                p = self._wgrad_problem(li, acts, gflat, gout, g, gscale)
+                _wgrad(p)
             else:
-                gm = g * (acts[L] > 0) * (gscale if gscale is not None else 1.0) if top else g
-                torch.mm(acts[li].t(), gm, out=dwb[:fi])
-                torch.sum(gm, 0, out=dwb[fi])
+                self._wgrad_torch(li, acts, gflat, g, gscale)
             if li == 0 and not need_input_grad:
                 return None, gflat
-            ld = (fi + 3) // 4 * 4  # 16-B rows for the kernel's vector stores
-            out = torch.empty(g.shape[0], ld, dtype=torch.float32, device=g.device)[:, :fi]
-            g = hip_ops.mlp_rows(g, imgs[("t", li)], fo, fi, out,
-                                 amask=acts[L] if top else None, scale=gscale if top else None,
-                                 cmask=acts[li] if li > 0 else None)
+            p = self._igrad_problem(li, acts, g, gscale)
+            g = _rows(p)
         return g, gflat
 
     def __call__(self, x: torch.Tensor) -> torch.Tensor:
         if torch.is_grad_enabled() and (x.requires_grad or self.flat.requires_grad):
             return _DenseStackFn.apply(x, self.flat, self)
         return self.forward_acts(x, self.flat.detach())[-1]
+
+
+def pair_compatible(a: "DenseStack", b: "DenseStack") -> bool:
+    """Both towers' layers can run as paired launches (same depth)."""
+    return len(a.layout) == len(b.layout) and len(a.layout) > 0
+
+
+def forward_acts_pair(stacks, xs, flats) -> List[List[torch.Tensor]]:
+    """DenseStack.forward_acts of the two towers on ONE stream with every
+    launch shared: one tt_mlp_pack_many for both towers' images (8 jobs at
+    one hidden layer), then one tt_mlp_rows_pair per layer."""
+    packed = [st._pack_jobs(f) for st, f in zip(stacks, flats)]
+    jobs = packed[0][1] + packed[1][1]
+    for i in range(0, len(jobs), 8):
+        hip_ops.mlp_pack_many(jobs[i:i + 8])
+    acts = [[xs[0]], [xs[1]]]
+    for li in range(len(stacks[0].layout)):
+        probs = [st._fwd_problem(li, a[-1], f, pk[0]) for st, a, f, pk in zip(stacks, acts, flats, packed)]
+        hip_ops.mlp_rows_pair(probs)
+        for a, p in zip(acts, probs):
+            a.append(p["out"])
+    return acts
+
+
+def backward_acts_pair(stacks, acts, flats, gouts, gscale, need_input_grad):
+    """DenseStack.backward_acts of the two towers with each layer's two weight
+    gradients in one tt_mlp_wgrad_pair and its two input-gradient GEMMs in one
+    tt_mlp_rows_pair (bit-identical to the single calls).  Returns
+    [(dx, dflat)] per tower."""
+    gflats = [torch.empty_like(f) for f in flats]
+    gs = list(gouts)
+    L = len(stacks[0].layout)
+    for li in range(L - 1, -1, -1):
+        fits = [st._wgrad_fits(li, g, a) for st, g, a in zip(stacks, gs, acts)]
+        if all(fits):
+            hip_ops.mlp_wgrad_pair([st._wgrad_problem(li, a, gf, go, g, gscale)
+                                    for st, a, gf, go, g in zip(stacks, acts, gflats, gouts, gs)])
+        else:
+            for t, st in enumerate(stacks):
+                if fits[t]:
+                    p = st._wgrad_problem(li, acts[t], gflats[t], gouts[t], gs[t], gscale)
+                    _wgrad(p)
+                else:
+                    st._wgrad_torch(li, acts[t], gflats[t], gs[t], gscale)
+        want = [li > 0 or need_input_grad[t] for t in range(2)]
+        probs = [st._igrad_problem(li, a, g, gscale) if w else None
+                 for st, a, g, w in zip(stacks, acts, gs, want)]
+        if all(want):
+            hip_ops.mlp_rows_pair(probs)
+        else:
+            for p in probs:
+                if p is not None:
+                    _rows(p)
+        gs = [p["out"] if p is not None else None for p in probs]
+    return [(gs[t], gflats[t]) for t in range(2)]
 
 
 class Tower(AbstractKerasModel):

@@ -447,6 +447,45 @@ int tt_mlp_wgrad(const float* A, int64_t lda, const float* G, int64_t ldg, const
                  const float* scale, int64_t M, int32_t Ka, int32_t N, float* dwb, void* workspace,
                  size_t workspace_bytes, tt_stream_t stream);
 
+/* The two towers' layers as ONE launch each (the query and the candidate
+ * tower are independent chains of the same shape of work: one stream, no
+ * fork/join).  p points at 2 problems with tt_mlp_rows' / tt_mlp_wgrad's
+ * arguments and contracts (rows: no colsum); the results equal two single
+ * calls bit for bit.  Replaces the two towers' Dense layers of
+ * two_tower_model.py:90-91 (query_tower(x), candidate_tower(x)). */
+typedef struct {
+  const float* A;
+  int64_t lda;
+  const float* amask;
+  int64_t ldam;
+  const float* scale;
+  int64_t M;
+  int32_t K;
+  const void* img;
+  int32_t N;
+  const float* bias;
+  int32_t relu;
+  const float* cmask;
+  int64_t ldcm;
+  float* C;
+  int64_t ldc;
+} tt_mlp_rows_problem;
+int tt_mlp_rows_pair(const tt_mlp_rows_problem* p, tt_stream_t stream);
+typedef struct {
+  const float* A;
+  int64_t lda;
+  const float* G;
+  int64_t ldg;
+  const float* gmask;
+  int64_t ldgm;
+  const float* scale;
+  int64_t M;
+  int32_t Ka, N;
+  float* dwb;
+} tt_mlp_wgrad_problem;
+size_t tt_mlp_wgrad_pair_workspace_size(const tt_mlp_wgrad_problem* p);
+int tt_mlp_wgrad_pair(const tt_mlp_wgrad_problem* p, void* workspace, size_t workspace_bytes, tt_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

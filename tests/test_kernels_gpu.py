@@ -558,3 +558,66 @@ def test_mlp_wgrad_vs_torch_fp64(cuda, M, Ka, N, masked):
     again = torch.empty_like(out)
     hip_ops.mlp_wgrad(A, G, again, gmask=Gm, scale=s if masked else None)
     assert torch.equal(out, again)
+
+
+def _rows_case(cuda, g, M, K, N, masked):
+    lda = (K + 3) // 4 * 4
+    A = torch.randn(M, lda, generator=g, device=cuda)[:, :K]
+    W = torch.randn(N, K, generator=g, device=cuda) * K ** -0.5 if masked else \
+        torch.randn(K, N, generator=g, device=cuda) * K ** -0.5
+    img = torch.empty(hip_ops.lib().tt_mlp_pack_bytes(K, N), dtype=torch.uint8, device=cuda)
+    hip_ops.mlp_pack_many([(W, masked, img)])
+    ldc = (N + 3) // 4 * 4
+    p = dict(a=A, img=img, k=K, n=N, out=torch.full((M, ldc), float("nan"), device=cuda)[:, :N])
+    if masked:
+        p.update(amask=torch.randn(M, lda, generator=g, device=cuda)[:, :K], scale=torch.full((1,), 0.5, device=cuda),
+                 cmask=torch.randn(M, ldc, generator=g, device=cuda)[:, :N] if N % 4 == 0 else None)
+    else:
+        p.update(bias=torch.randn(N, generator=g, device=cuda), relu=True)
+    return p
+
+
+@pytest.mark.parametrize("shapes,masked", [(((16384, 384, 256), (16384, 256, 256)), False),
+                                           (((16384, 256, 384), (16384, 256, 256)), True),
+                                           (((16384, 256, 128), (16384, 256, 128)), False),
+                                           (((1000, 37, 64), (130, 300, 384)), True),
+                                           (((0, 16, 32), (77, 16, 32)), False)])
+def test_mlp_rows_pair_equals_single(cuda, shapes, masked):
+    """tt_mlp_rows_pair (the two towers' layers in one launch, every NCB
+    combination of the pair kernel) is bit-identical to two tt_mlp_rows calls."""
+    g = torch.Generator(device=cuda)
+    g.manual_seed(sum(sum(s) for s in shapes))
+    probs = [_rows_case(cuda, g, *s, masked) for s in shapes]
+    hip_ops.mlp_rows_pair(probs)
+    for p in probs:
+        q = dict(p)
+        single = torch.full_like(q["out"], float("nan"))
+        q["out"] = single
+        hip_ops.mlp_rows(q.pop("a"), q.pop("img"), q.pop("k"), q.pop("n"), q.pop("out"), **q)
+        assert torch.equal(p["out"], single)
+
+
+@pytest.mark.parametrize("shapes,masked", [(((16384, 384, 256), (16384, 256, 256)), False),
+                                           (((16384, 256, 128), (16384, 256, 128)), True),
+                                           (((1000, 37, 64), (4099, 64, 100)), True),
+                                           (((1, 5, 4), (130, 287, 256)), False)])
+def test_mlp_wgrad_pair_equals_single(cuda, shapes, masked):
+    """tt_mlp_wgrad_pair (both towers' weight gradients in one launch, their
+    split partials summed by one launch) is bit-identical to two tt_mlp_wgrad."""
+    g = torch.Generator(device=cuda)
+    g.manual_seed(7 + sum(sum(s) for s in shapes))
+    probs = []
+    for M, Ka, N in shapes:
+        ldg = (N + 3) // 4 * 4
+        p = dict(a=torch.randn(M, (Ka + 3) // 4 * 4, generator=g, device=cuda)[:, :Ka],
+                 g=torch.randn(M, ldg, generator=g, device=cuda)[:, :N],
+                 dwb=torch.full((Ka + 1, N), float("nan"), device=cuda))
+        if masked:
+            p.update(gmask=torch.randn(M, ldg, generator=g, device=cuda)[:, :N],
+                     scale=torch.full((1,), 1.5, device=cuda))
+        probs.append(p)
+    hip_ops.mlp_wgrad_pair(probs)
+    for p in probs:
+        single = torch.full_like(p["dwb"], float("nan"))
+        hip_ops.mlp_wgrad(p["a"], p["g"], single, gmask=p.get("gmask"), scale=p.get("scale"))
+        assert torch.equal(p["dwb"], single)

@@ -250,6 +250,30 @@ def test_dense_early_bit_identical_to_dense_after_join(cuda, monkeypatch):
     b.optimizer.check_status(cuda)
 
 
+@pytest.mark.parametrize("fused", [False, True])
+def test_paired_tower_launches_bit_identical(cuda, monkeypatch, fused):
+    """TT_TOWER_PAIR (both towers' MLP layers as paired launches on one
+    stream: tt_mlp_rows_pair / tt_mlp_wgrad_pair) gives bit-identical losses,
+    tables, accumulators and MLP buffers to the two-stream step, unfused and
+    with the fused optimizer apply, at ragged batch sizes."""
+    from pkg.modelling import losses
+
+    a, b = _small_model(cuda, seed=21, fused=fused), _small_model(cuda, seed=21, fused=fused)
+    rng = np.random.default_rng(6)
+    for i, B in enumerate((512, 37, 256, 1)):
+        x = _batch(cuda, rng, B, True)
+        monkeypatch.setattr(losses, "TOWER_PAIR", 0)
+        la = a.train_step(x)["loss"]
+        monkeypatch.setattr(losses, "TOWER_PAIR", 1)
+        lb = b.train_step(x)["loss"]
+        assert torch.equal(la, lb), (i, B)
+        sa, sb = _state(a), _state(b)
+        for k in sa:
+            assert torch.equal(sa[k], sb[k]), (i, B, k)
+    a.optimizer.check_status(cuda)
+    b.optimizer.check_status(cuda)
+
+
 def test_stale_presorted_workspace_is_reported_not_applied(cuda):
     """A presorted sparse apply whose workspace holds another call's sorted
     keys applies nothing and is reported by tt_sparse_status (TTError), the
