@@ -629,14 +629,22 @@ __global__ void __launch_bounds__(kSThreads) scan_kernel(const ScreenArgs a) {
   // has landed).
   bf16x8 f0[KS], f1[KS];
   f32x16 a0 = {}, a1 = {}, b0 = {}, b1 = {};
+#ifndef TT_SCAN_PRIO
+#define TT_SCAN_PRIO 0
+#endif
+  // 1: the younger half of the workgroup (waves 4-7) at priority 1 for the
+  // whole loop; 2: priority 1 around each MFMA cluster
+  if (TT_SCAN_PRIO == 1 && __builtin_amdgcn_readfirstlane(tid) >= kSThreads / 2) __builtin_amdgcn_s_setprio(1);
   auto mfmas = [&](const bf16x8 (&f)[KS], f32x16& x0, f32x16& x1) {
     x0 = f32x16{};
     x1 = f32x16{};
+    if (TT_SCAN_PRIO == 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       x0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[s], bq0[s], x0, 0, 0, 0);
       x1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[s], bq1[s], x1, 0, 0, 0);
     }
+    if (TT_SCAN_PRIO == 2) __builtin_amdgcn_s_setprio(0);
   };
   // block (tile u, half t) held in (x0, x1): edge mask, candidate base, maxima
   struct Pend {
@@ -651,9 +659,21 @@ __global__ void __launch_bounds__(kSThreads) scan_kernel(const ScreenArgs a) {
     }
     return Pend{a.index_offset + static_cast<unsigned>(cb + 4 * h), max16(x0), max16(x1)};
   };
+#ifndef TT_SCAN_PROBE
+#define TT_SCAN_PROBE 0
+#endif
+  // probe builds (timing only, results unused): 1 = maxima without the
+  // ballot / staging branches, 2 = no filter work at all
+  float probe_acc = 0.f;
   auto stage_pair = [&](const f32x16& x0, const f32x16& x1, const Pend& p) {
-    stage(x0, p.m0 > tau0, ql0, p.pc);
-    stage(x1, p.m1 > tau1, ql1, p.pc);
+    if (TT_SCAN_PROBE == 1) {
+      probe_acc = fmaxf(probe_acc, fmaxf(p.m0, p.m1));
+    } else if (TT_SCAN_PROBE == 2) {
+      probe_acc += x0[0] + x1[5];
+    } else {
+      stage(x0, p.m0 > tau0, ql0, p.pc);
+      stage(x1, p.m1 > tau1, ql1, p.pc);
+    }
   };
   if (nv > 0) load_frags(f0, smem, 0);
   for (int u = 0; u < nv; ++u) {
@@ -693,6 +713,7 @@ __global__ void __launch_bounds__(kSThreads) scan_kernel(const ScreenArgs a) {
       while (head > tail) flush(min(head - tail, kWave));
   }
   if (nv > 0) stage_pair(b0, b1, prep(b0, b1, nv - 1, 1));
+  if (TT_SCAN_PROBE && probe_acc == 12345.f) a.count[0] = -2;  // keeps the probe's work alive
   while (head > tail) flush(min(head - tail, kWave));
   if (h == 0) {
     const int n0c = cnt_l[ql0], n1c = cnt_l[ql1];
@@ -1088,7 +1109,11 @@ __global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
   TT_STAT0(2, n);
   for (int j = lane; j < n; j += kWave) {
     const int64_t row = static_cast<int64_t>(id[j]) - a.cand_offset;
+#ifdef TT_FINAL_NORESCORE  // timing probe only: no candidate rows read (results wrong)
+    sc[j] = static_cast<float>(row & 1023);
+#else
     sc[j] = exact_score(qs, a.cand + row * a.ldc, a.dim, a.vec4 != 0) + 0.0f;
+#endif
   }
   wsync();
   float kth;

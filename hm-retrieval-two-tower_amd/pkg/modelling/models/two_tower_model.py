@@ -1,9 +1,10 @@
 """TwoTowerModel (mirror of /root/reference/pkg/modelling/models/two_tower_model.py:12-205).
 
 train_step (two_tower_model.py:94-130) on MI355X:
-  1. query / candidate InputLayer gathers        tt_gather_grouped (1 launch per tower)
+  1. query / candidate InputLayer gathers        tt_gather_multi (both towers + logq, 1 launch)
   2. tower MLPs                                   tt_mlp_rows (bf16x3 MFMA, bias + relu epilogue)
-  3. scores + logQ + eye-label CE-SUM + dQ/dC     tt_inbatch_xent_rows / _cols (fused, bf16x3 MFMA)
+  3. scores + logQ + eye-label CE-SUM + dQ/dC     tt_inbatch_softmax_xent (rows + cols passes,
+                                                  bf16 MFMA, fp32 accumulation)
   4. MLP backward                                 tt_mlp_wgrad weight + bias gradients and
                                                   tt_mlp_rows input gradients (ReluGrad fused)
   5. optimizer                                    tt_dense_adagrad + tt_sparse_adagrad (dedup in-kernel)
