@@ -737,7 +737,8 @@ extern "C" size_t tt_mlp_rows_workspace_size(int64_t M, int32_t N) {
 static int rows_setup(const char* fn, const float* A, int64_t lda, const float* amask, int64_t ldam,
                       const float* scale, int64_t M, int32_t K, const void* img, int32_t N, const float* bias,
                       int32_t relu, const float* cmask, int64_t ldcm, float* C, int64_t ldc, MlpArgs& a, int& ncb) {
-  TT_REQUIRE(A && img && C, "%s: NULL A/img/C", fn);
+  // a problem of no rows may come with NULL A / C (empty tensors have no storage)
+  TT_REQUIRE(img && (M == 0 || (A && C)), "%s: NULL A/img/C", fn);
   TT_REQUIRE(M >= 0 && K >= 1 && N >= 1, "%s: bad M/K/N", fn);
   const int NB = mlp_nb(N);
   TT_REQUIRE(NB <= 4 * kMlpMaxCB, "%s: N=%d > %d unsupported", fn, N, 32 * 4 * kMlpMaxCB);
@@ -873,7 +874,7 @@ extern "C" size_t tt_mlp_wgrad_workspace_size(int64_t M, int32_t Ka, int32_t N) 
 static int wgrad_setup(const char* fn, const float* A, int64_t lda, const float* G, int64_t ldg, const float* gmask,
                        int64_t ldgm, const float* scale, int64_t M, int32_t Ka, int32_t N, float* dwb,
                        WgradArgs& a) {
-  TT_REQUIRE(A && G && dwb, "%s: NULL A/G/dwb", fn);
+  TT_REQUIRE(dwb && (M == 0 || (A && G)), "%s: NULL A/G/dwb", fn);
   TT_REQUIRE(M >= 0 && Ka >= 1 && Ka <= 4096, "%s: Ka=%d outside [1, 4096]", fn, Ka);
   TT_REQUIRE(N >= 4 && N <= 4096 && N % 4 == 0, "%s: N=%d must be a multiple of 4 in [4, 4096]", fn, N);
   TT_REQUIRE(lda >= Ka && ldg >= N && (!gmask || ldgm >= N), "%s: leading dimension too small", fn);

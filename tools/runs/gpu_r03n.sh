@@ -1,4 +1,3 @@
-# Combined: scan probes, GPU suite, smoke, TT_TOWER_PAIR A/B.
-set -e
-bash tools/runs/gpu_r03m.sh
-bash tools/runs/gpu_r03k.sh
+set -o pipefail
+for n in noins base f2 f8; do echo "== $n"; timeout -k 10 60 ./tools/pbin/iprobe8_$n 131072 | tail -2 | head -1 || exit 1; done
+bash tools/gpu_idx_prof.sh iprobe8_base r03n
