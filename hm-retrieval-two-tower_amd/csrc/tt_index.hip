@@ -766,38 +766,6 @@ __device__ __forceinline__ float exact_score(const float* __restrict__ qs, const
   return acc;
 }
 
-// Two exact scores at once (vec4 rows): the chains interleave and both rows'
-// first CH chunks are in flight together.
-#ifndef TT_FINAL_R2
-#define TT_FINAL_R2 0
-#endif
-constexpr int kFinalR2 = TT_FINAL_R2 > 0 ? TT_FINAL_R2 : 1;
-template <int CH>
-__device__ __forceinline__ void exact_score2(const float* __restrict__ qs, const float* __restrict__ c0,
-                                             const float* __restrict__ c1, int dim, float& r0, float& r1) {
-  float a0 = 0.0f, a1 = 0.0f;
-  for (int e0 = 0; e0 < dim; e0 += 4 * CH) {
-    f32x4 v0[CH], v1[CH];
-#pragma unroll
-    for (int i = 0; i < CH; ++i)
-      if (e0 + 4 * i < dim) {
-        v0[i] = *reinterpret_cast<const f32x4*>(c0 + e0 + 4 * i);
-        v1[i] = *reinterpret_cast<const f32x4*>(c1 + e0 + 4 * i);
-      }
-#pragma unroll
-    for (int i = 0; i < CH; ++i)
-      if (e0 + 4 * i < dim) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          a0 = __builtin_fmaf(qs[e0 + 4 * i + u], v0[i][u], a0);
-          a1 = __builtin_fmaf(qs[e0 + 4 * i + u], v1[i][u], a1);
-        }
-      }
-  }
-  r0 = a0;
-  r1 = a1;
-}
-
 // Lists of one query: `nseg` segments; segment j of query q holds
 // count[q * cq + j * cj] entries (-1: overflowed) starting at
 // buf + (q * nseg + j) * cap (region form) or at off[q * cq + j * cj] (CSR
@@ -1139,20 +1107,6 @@ __global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
     return;
   }
   TT_STAT0(2, n);
-  if (TT_FINAL_R2 > 0 && a.vec4 != 0) {
-    for (int j = lane; j < n; j += 2 * kWave) {
-      const int j1 = j + kWave;
-      const float* c0 = a.cand + (static_cast<int64_t>(id[j]) - a.cand_offset) * a.ldc;
-      if (j1 < n) {
-        float r0, r1;
-        exact_score2<kFinalR2>(qs, c0, a.cand + (static_cast<int64_t>(id[j1]) - a.cand_offset) * a.ldc, a.dim, r0, r1);
-        sc[j] = r0 + 0.0f;
-        sc[j1] = r1 + 0.0f;
-      } else {
-        sc[j] = exact_score(qs, c0, a.dim, true) + 0.0f;
-      }
-    }
-  } else
   for (int j = lane; j < n; j += kWave) {
     const int64_t row = static_cast<int64_t>(id[j]) - a.cand_offset;
 #ifdef TT_FINAL_NORESCORE  // timing probe only: no candidate rows read (results wrong)
