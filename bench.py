@@ -478,6 +478,40 @@ def time_index(device, n_queries: int, n_cand: int, k: int, E: int = 128, check:
                                              f"oracle/tt_oracle.c (fp32 fmaf chain), {t_cpu:.1f}s"}
         except Exception as e:  # the check is informative only
             res["check_error"] = repr(e)
+    res["runner_point"] = time_index_runner_point(image, C, Q)
+    return res
+
+
+def time_index_runner_point(image, C: torch.Tensor, Q: torch.Tensor, batch: int = 2048, k: int = 1000,
+                            batches: int = 32, check: int = 4):
+    """The reference runner's own index operating point: IndexRecall over the
+    test set in batches of test_batch_size = 2048 (/root/reference/main.py:99)
+    at k = max(ks) = 1000 (main.py:107; brute_force.py:54-83 per batch).
+    `batches` consecutive search calls of 2048 queries each, back to back on
+    the stream (one call per test batch, as the runner issues them)."""
+    from pkg.modelling import hip_ops
+
+    nq = min(batch * batches, Q.shape[0])
+    chunks = [Q[b:b + batch] for b in range(0, nq, batch)]
+    hip_ops.bruteforce_search(image, C, chunks[0], k)  # warm: code + workspace
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    outs = [hip_ops.bruteforce_search(image, C, q, k) for q in chunks]
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    res = {"queries": nq, "batch": batch, "k": k, "calls": len(chunks), "seconds": dt, "qps": nq / dt,
+           "ms_per_batch": dt / len(chunks) * 1e3,
+           "tflops_scoring": 2.0 * nq * C.shape[0] * C.shape[1] / dt / 1e12}
+    if check:
+        try:
+            from oracle import oracle
+
+            qs = chunks[0][:check].cpu().numpy()
+            _, ri, _ = oracle.bruteforce_topk(qs, C.cpu().numpy(), k)
+            res["exact_match_rows"] = int((outs[0][1][:check].cpu().numpy() == ri).all(axis=1).sum())
+            res["checked_rows"] = int(check)
+        except Exception as e:  # informative only
+            res["check_error"] = repr(e)
     return res
 
 
