@@ -74,7 +74,13 @@ constexpr int kQPerWG = kSWaves * kQPerWave;     // 512
 constexpr int kCTile = 64;                       // candidates per LDS tile
 constexpr int kStages = 4;                       // LDS ring depth
 constexpr int kMaxSample = 128;                  // sample tiles per split
-constexpr int kMaxSplits = 16;
+#ifndef TT_INDEX_MAX_SPLITS
+#define TT_INDEX_MAX_SPLITS 32
+#endif
+#ifndef TT_INDEX_SPLIT_TILES
+#define TT_INDEX_SPLIT_TILES 32  // a split is halved only while each half keeps >= this many tiles
+#endif
+constexpr int kMaxSplits = TT_INDEX_MAX_SPLITS;
 constexpr float kEps = 0.0087890625f;            // 2^-7 + 2^-10
 constexpr float kTiny = 1e-30f;
 #ifndef TT_LIST_BUDGET
@@ -935,54 +941,6 @@ __device__ void rank_and_write(const float* sc, const unsigned* id, int n, int k
   }
 }
 
-// Survivors of a small cut (n <= 256, 2n <= L): one bitonic sort of all of
-// them by (score desc, index asc) in the LDS of sc, then the first min(n, k)
-// written.  Same result as exact_select + rank_and_write (the keys are
-// unique), without the select's radix passes.
-#ifndef TT_FINAL_SMALL_SORT
-#define TT_FINAL_SMALL_SORT 1
-#endif
-__device__ void sort_write_small(float* sc, const unsigned* id, int n, int k, float* out_s, int32_t* out_i) {
-  const int lane = lane_id();
-  int P2 = 2;
-  while (P2 < n) P2 <<= 1;
-  unsigned long long key[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int j = lane + kWave * u;
-    key[u] = j < n ? make_key(sc[j], id[j]) : 0ull;
-  }
-  wsync();
-  unsigned long long* sk = reinterpret_cast<unsigned long long*>(sc);
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int j = lane + kWave * u;
-    if (j < P2) sk[j] = key[u];
-  }
-  for (int size = 2; size <= P2; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      wsync();
-      for (int i = lane; i < P2 / 2; i += kWave) {
-        const int lo = 2 * i - (i & (stride - 1));
-        const int hi = lo + stride;
-        const bool desc = (lo & size) == 0;
-        const unsigned long long x = sk[lo], y = sk[hi];
-        if ((x < y) == desc) {
-          sk[lo] = y;
-          sk[hi] = x;
-        }
-      }
-    }
-  }
-  wsync();
-  const int m = n < k ? n : k;
-  for (int t = lane; t < m; t += kWave) {
-    const unsigned long long kk = sk[t];
-    out_s[t] = order_key_float(static_cast<unsigned>(kk >> 32));
-    out_i[t] = static_cast<int32_t>(0xFFFFFFFFu - static_cast<unsigned>(kk));
-  }
-}
-
 struct FinalArgs {
   const float* q;       // fp32 queries of this chunk
   int64_t ldq;
@@ -1164,14 +1122,9 @@ __global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
 #endif
   }
   wsync();
-  if (TT_FINAL_SMALL_SORT && n <= 256 && 2 * n <= a.L) {
-    sort_write_small(sc, id, n, K, out_s, out_i);
-    n = min(n, K);
-  } else {
-    float kth;
-    n = exact_select(sc, id, n, K, &kth, hist);
-    rank_and_write(sc, id, n, min(n, K), a.P, sk, out_s, out_i);
-  }
+  float kth;
+  n = exact_select(sc, id, n, K, &kth, hist);
+  rank_and_write(sc, id, n, min(n, K), a.P, sk, out_s, out_i);
   // with a floor fewer than K may remain: pad (sorts after every real entry)
   for (int t = n + lane; t < K; t += kWave) {
     out_s[t] = -INFINITY;
@@ -1364,7 +1317,7 @@ SearchPlan plan_search(int64_t nq, int64_t n_rows, int k, int shards) {
   p.LF = p.L > TT_INDEX_LF ? p.L : TT_INDEX_LF;  // finalize: a query's whole list (~3k + 100 entries) fits
   const int64_t qblocks = ceil_div(nq > 0 ? nq : 1, kQPerWG);
   p.S = 1;  // enough workgroups for the 256 CUs: split the candidates of few query blocks
-  while (p.S < kMaxSplits && qblocks * p.S < 256 && ntiles / (2 * p.S) >= 64) p.S *= 2;
+  while (p.S < kMaxSplits && qblocks * p.S < 256 && ntiles / (2 * p.S) >= TT_INDEX_SPLIT_TILES) p.S *= 2;
   const int64_t nts = ceil_div(ntiles, p.S);  // tiles per split
   const double ns_cand = static_cast<double>(nts) * kCTile;
   const double R = (TT_INDEX_R_MUL * k + TT_INDEX_R_ADD) / (static_cast<double>(p.S) * (shards > 0 ? shards : 1));
