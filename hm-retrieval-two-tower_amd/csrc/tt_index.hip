@@ -914,10 +914,29 @@ __device__ int exact_select(float* sc, unsigned* id, int n, int K, float* thr, u
 }
 
 // Ranks the n <= P entries (score desc, index asc) and writes the first k.
+// Sort sizes up to kAliasP build their keys in registers, so the key array
+// may alias the (score, index) arrays it is built from (the finalize's LDS).
+constexpr int kAliasP = 1024;
 __device__ void rank_and_write(const float* sc, const unsigned* id, int n, int k, int P, unsigned long long* sk,
                                float* out_s, int32_t* out_i) {
   const int lane = lane_id();
-  for (int j = lane; j < P; j += kWave) sk[j] = j < n ? make_key(sc[j], id[j]) : 0ull;
+  if (P <= kAliasP) {
+    // keys built in registers first: sk may alias sc / id
+    unsigned long long kv[kAliasP / kWave];
+#pragma unroll
+    for (int u = 0; u < kAliasP / kWave; ++u) {
+      const int j = lane + kWave * u;
+      kv[u] = j < n ? make_key(sc[j], id[j]) : 0ull;
+    }
+    wsync();
+#pragma unroll
+    for (int u = 0; u < kAliasP / kWave; ++u) {
+      const int j = lane + kWave * u;
+      if (j < P) sk[j] = kv[u];
+    }
+  } else {
+    for (int j = lane; j < P; j += kWave) sk[j] = j < n ? make_key(sc[j], id[j]) : 0ull;
+  }
   for (int size = 2; size <= P; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       wsync();
@@ -968,7 +987,8 @@ struct FinalArgs {
 };
 
 __host__ __device__ inline size_t final_lds_bytes(int L, int P) {
-  return 128 * sizeof(float) + static_cast<size_t>(L) * 8 + static_cast<size_t>(P) * 8 + 256 * sizeof(unsigned);
+  return 128 * sizeof(float) + static_cast<size_t>(L) * 8 + (P <= kAliasP ? 0 : static_cast<size_t>(P) * 8) +
+         256 * sizeof(unsigned);
 }
 
 __global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
@@ -976,8 +996,11 @@ __global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
   float* qs = reinterpret_cast<float*>(fsm);  // query row (dim <= 128)
   float* sc = qs + 128;
   unsigned* id = reinterpret_cast<unsigned*>(sc + a.L);
-  unsigned long long* sk = reinterpret_cast<unsigned long long*>(id + a.L);
-  unsigned* hist = reinterpret_cast<unsigned*>(sk + a.P);  // 256 radix bins
+  // for P <= kAliasP the ranking's keys reuse the LDS of sc / id (P <= L)
+  const bool alias = a.P <= kAliasP;
+  unsigned long long* sk = alias ? reinterpret_cast<unsigned long long*>(sc)
+                                 : reinterpret_cast<unsigned long long*>(id + a.L);
+  unsigned* hist = alias ? id + a.L : reinterpret_cast<unsigned*>(sk + a.P);  // 256 radix bins
   const int64_t q = blockIdx.x;
   const int lane = lane_id();
   const int K = a.k;
