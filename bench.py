@@ -206,6 +206,11 @@ def time_train(args, model, data, device, ws):
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
     loss = float(out["loss"].item())
+    # after the timed region: no sparse apply recorded refused keys
+    if hasattr(step, "check_status"):
+        step.check_status()  # the shards' owner applies and per-request sums
+    else:
+        model.optimizer.check_status(device)
     if getattr(step, "host_times", None):
         print("host ms/step by phase:", {k: round(v / args.steps * 1e3, 3)
                                          for k, v in step.host_times.items()}, file=sys.stderr)  # timed steps only
@@ -587,6 +592,99 @@ def time_index_sharded(device, n_queries: int, n_cand: int, k: int, ws: int, ran
     return res
 
 
+def time_c5_sharded(device, ws: int, rank: int, steps: int = 10, rows: int = 100_000_000, batch: int = 65536,
+                    D: int = 128):
+    """BASELINE configs[4]: a 100M x 128 fp32 table row-sharded over the ranks
+    (ShardedTables; global row r on rank r % G, each rank holding only its
+    rows and their Adagrad accumulator), each rank a batch of 65,536 uniform
+    ids per step (weak scaling): routing (dedup + owner buckets + count and
+    request all_to_alls), fetch (tt_gather_tagged on the owners + all_to_all
+    of rows), apply (tt_sparse_scatter_sum per request + all_to_all of the
+    sums + tt_sparse_adagrad on the owners).  Algorithmic HBM bytes per rank
+    and step: lookups x (4 B id + 2 x 4D row read/write + 4D gradient read)
+    + owner rows x 16D (param and accumulator read + write).  The
+    all_to_all share is the three data all_to_alls of the same sizes timed
+    alone."""
+    import torch.distributed as tdist
+
+    from pkg.modelling.distributed import ShardedTables, _a2a
+
+    own = not tdist.is_initialized()
+    if own:  # N = 1: a one-rank RCCL group, so the all_to_alls are real calls
+        import socket
+
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+        sk.close()
+        tdist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                 device_id=device)
+    try:
+        g = torch.Generator(device=device)
+        g.manual_seed(17 + rank)
+        n_local = len(range(rank, rows, ws))
+        shard = torch.empty(n_local, D, device=device)
+        for s0 in range(0, n_local, 1 << 24):
+            shard[s0:s0 + (1 << 24)].uniform_(-0.05, 0.05, generator=g)
+        st = ShardedTables({"big": shard, "__rows__": {"big": rows}}, full_tables=False)
+        del shard
+        ids = [torch.randint(0, rows, (batch,), generator=g, device=device, dtype=torch.int32) for _ in range(2)]
+        grad = torch.randn(batch, D, generator=g, device=device)
+
+        def step(i):
+            _, (idx,) = st.fetch([("big", ids[i % 2])])
+            st.apply([(grad, [(idx, 0)])], 0.05, 1e-7)
+
+        def timed(fn, n):
+            for i in range(2):
+                fn(i)
+            torch.cuda.synchronize()
+            tdist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(n):
+                fn(i)
+            torch.cuda.synchronize()
+            tdist.barrier()
+            torch.cuda.synchronize()
+            t = torch.tensor([time.perf_counter() - t0], device=device, dtype=torch.float64)
+            tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+            return float(t.item()) / n
+
+        sec = timed(step, steps)
+        rt = st.route([("big", ids[0])])
+        req = torch.zeros(rt.R, 2, dtype=torch.int32, device=device)
+        req_in = torch.empty(rt.n_recv, 2, dtype=torch.int32, device=device)
+        rows_out = torch.empty(rt.n_recv, D, device=device)
+        rows_in = torch.empty(rt.R, D, device=device)
+        grads_in = torch.empty(rt.n_recv, D, device=device)
+        group = st.group
+
+        def a2a(_):
+            _a2a(req_in, req, rt.r_split, rt.s_split, group)
+            _a2a(rows_in, rows_out, rt.s_split, rt.r_split, group)
+            _a2a(grads_in, rows_in, rt.r_split, rt.s_split, group)
+
+        a2a_sec = timed(a2a, steps)
+        nbytes = batch * (4 + 12 * D) + rt.n_recv * 16 * D
+        gbs = ws * nbytes / sec / 1e9
+        res = {"rows": rows, "dim": D, "ranks": ws, "batch_per_rank": batch, "rows_per_rank": n_local,
+               "requests_per_rank": rt.R, "owner_rows_per_rank": rt.n_recv, "ms_per_step": sec * 1e3,
+               "lookups_per_s": ws * batch / sec, "scaling": "weak (a batch of 65,536 ids per rank)",
+               "roofline": {"bound": "hbm", "achieved": gbs, "peak": MI355X_HBM_PEAK_GBS * ws, "unit": "GB/s",
+                            "frac": gbs / (MI355X_HBM_PEAK_GBS * ws),
+                            "algorithmic_bytes_per_rank_step": nbytes},
+               "all_to_all_ms": a2a_sec * 1e3, "all_to_all_share": a2a_sec / sec,
+               "note": "fetch + apply per step, eager (the route's one host sync per step included); "
+                       "uniform ids over the whole table"}
+        del st
+        torch.cuda.empty_cache()
+        return res
+    finally:
+        if own:
+            tdist.destroy_process_group()
+
+
 def time_pipeline(model, data, device, rows: int, B: int, encode_n: int = 2_000_000):
     """modelling_runner's training input path at scale: `rows` synthetic
     H&M-shaped examples encoded into an HBM-resident DeviceDataset, one epoch
@@ -708,6 +806,7 @@ def main():
     ap.add_argument("--pipeline-rows", type=int, default=10_000_000,
                     help="rows of the device-resident input-pipeline leg (0 skips it; N=1 only)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--no-c5", action="store_true", help="skip the row-sharded 100M-row table leg (configs[4])")
     ap.add_argument("--train-mode", choices=("auto", "sharded"), default="auto",
                     help="sharded: run the N>1 row-sharded step (ShardedTrainStep) even on one rank")
     ap.add_argument("--negatives", choices=("global", "replica"), default="global",
@@ -758,7 +857,8 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "strong" if global_neg else "weak",
+        # the default (--negatives global) fixes the global batch at every N
+        "scaling": "weak" if args.negatives == "replica" else "strong",
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic (H&M-shaped ids, Zipf; random-init weights)",
@@ -804,6 +904,8 @@ def main():
         result["index"] = time_index(device, args.index_queries, HM_VOCAB["article_id"], 100)
     elif not args.no_index:
         result["index"] = time_index_sharded(device, args.index_queries, HM_VOCAB["article_id"], 100, ws, rank)
+    if not args.no_c5:
+        result["c5_sharded_table"] = time_c5_sharded(device, ws, rank)
     if ws == 1 and args.pipeline_rows > 0:
         result["pipeline"] = time_pipeline(model, data, device, args.pipeline_rows, B)
         result["pipeline"]["vs_train_step_rate"] = result["pipeline"]["rows_per_s"] / value

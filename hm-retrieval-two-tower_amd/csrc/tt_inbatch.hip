@@ -55,7 +55,8 @@ constexpr int kTile = 64;                                // streamed rows per LD
 constexpr int kMaxSplit = 16;
 constexpr int kRingStages = 4;                           // LDS tile ring depth
 constexpr float kLog2e = 1.4426950408889634f;
-constexpr float kLazyRescale = 8.0f / kLog2e;  // 8 in log2 units (natural-log units here)
+constexpr float kLn2 = 0.6931471805599453f;
+constexpr float kLazyRescale = 8.0f;  // log2 units
 
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
@@ -144,7 +145,8 @@ struct PassArgs {
   int64_t n_stat_pad;
   int64_t n_strm_pad;
   int64_t per_split;      // streamed rows per split (multiple of kTile)
-  float* part_m;          // [S, n_stat_pad]   (rows pass)
+  int64_t diag_off;       // stationary row r's positive is streamed row r + diag_off (excluded from the sums)
+  float* part_m;          // [S, n_stat_pad]   (rows pass; log2 units, integer valued)
   float* part_l;          // [S, n_stat_pad]   (rows pass)
   float* part_o;          // [S, n_stat_pad, D]
 };
@@ -270,7 +272,7 @@ __global__ void __launch_bounds__(kThreads) inbatch_pass_kernel(const PassArgs a
   for (int dt = 0; dt < G::DT; ++dt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[dt][r] = 0.0f;
-  float m_run = -1.0e30f;  // natural-log units
+  float m_run = -1.0e30f;  // log2 units, integer valued
   float l_run = 0.0f;
 
   // Fragment reads.  Score step i: k-step i >> 1, sub-tile i & 1.
@@ -330,6 +332,22 @@ __global__ void __launch_bounds__(kThreads) inbatch_pass_kernel(const PassArgs a
     return __builtin_elementwise_maximum(m, __shfl_xor(m, 32, kWave));
   };
 
+  // The positive pair is left out of the MFMA sums (the combines add it in
+  // fp32, exactly): in a tile holding some of this wave's positives (at most
+  // two tiles per wave and split; a wave-uniform test) its score becomes -inf,
+  // so p = 0.  Score k of a lane is streamed row 32(k>>4) + 8((k&15)>>2) + 4h + (k&3).
+  const int64_t wave_row0 = static_cast<int64_t>(blockIdx.x) * kRowsPerWG + wave * kRowsPerWave;
+  auto mask_diag = [&](f32x16* sacc, int tile) {
+    const int64_t lo = wave_row0 + a.diag_off - (s_begin + static_cast<int64_t>(tile) * kTile);
+    if (lo + kRowsPerWave <= 0 || lo >= kTile) return;
+    const int64_t d = lo + l32;  // this lane's positive, as a row of the tile
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const int r = 32 * (k >> 4) + 8 * ((k & 15) >> 2) + 4 * h + (k & 3);
+      if (d == r) sacc[k >> 4][k & 15] = -INFINITY;
+    }
+  };
+
   const int pre = ntiles < kRingStages ? ntiles : kRingStages;
   for (int t = 0; t < pre; ++t) issue(t);
   f32x16 sa[2], sb[2];
@@ -338,6 +356,7 @@ __global__ void __launch_bounds__(kThreads) inbatch_pass_kernel(const PassArgs a
     wait_tiles(pre - 1);  // tile 0 landed
     __builtin_amdgcn_s_barrier();
     scores_plain(sa);
+    mask_diag(sa, 0);
     if constexpr (MODE == 0) mx = half_max(sa);
   }
 
@@ -357,9 +376,12 @@ __global__ void __launch_bounds__(kThreads) inbatch_pass_kernel(const PassArgs a
     constexpr int STG = decltype(stg)::value;
     constexpr int NXT = (STG + 1) % kRingStages;
     if constexpr (MODE == 0) {
-      if (__any(mx > m_run + kLazyRescale)) {
-        const float m_new = __builtin_elementwise_maximum(m_run, mx);
-        const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * kLog2e);
+      // m_run: an integer in log2 units, so every rescale factor is an exact
+      // power of two and bf16(p) does not depend on when m moved
+      const float mx2 = mx * kLog2e;
+      if (__any(mx2 > m_run + kLazyRescale)) {
+        const float m_new = __builtin_ceilf(__builtin_elementwise_maximum(m_run, mx2));
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
         l_run *= alpha;
 #pragma unroll
         for (int dt = 0; dt < G::DT; ++dt)
@@ -382,7 +404,7 @@ __global__ void __launch_bounds__(kThreads) inbatch_pass_kernel(const PassArgs a
     rd_bias(NXT, sn);
 #pragma unroll
     for (int i = 0; i < AHEAD; ++i) prefetch(i);
-    const float mb = (MODE == 0) ? m_run * kLog2e : 0.0f;
+    const float mb = (MODE == 0) ? m_run : 0.0f;
     bf16x8 pf[4];
     __builtin_amdgcn_sched_barrier(0);
 
@@ -406,6 +428,8 @@ __global__ void __launch_bounds__(kThreads) inbatch_pass_kernel(const PassArgs a
       }
       __builtin_amdgcn_sched_barrier(0);
     }
+
+    if (tile + 1 < ntiles) mask_diag(sn, tile + 1);
 
     // Region B: O^T += X^T . P^T of this tile || row sums, next tile's max.
     float mxa = -INFINITY;
@@ -469,30 +493,51 @@ __global__ void __launch_bounds__(kThreads) inbatch_pass_kernel(const PassArgs a
 }
 
 // Split combines: D/4 lanes per row (float4 partials), 1024/D rows per block.
-// Rows: lse, row loss, dq = O / L - c_pos (and -lse as the cols-pass bias).
+//
+// The passes leave the positive pair out of their sums; the combines add it
+// in fp32 from the fp32 operands.  Rows: with the off-diagonal partials
+// merged to (M, L, O) (M in log2 units), a = M ln2 + log L = lse over the
+// negatives and pos = q_i . c_pos - logq_pos:
+//   row loss  = softplus(a - pos)            (= lse - pos, without cancellation)
+//   lse       = pos + row loss
+//   dq        = sigmoid(a - pos) (O / L - c_pos)
+// (1 - P_pos = sigmoid(a - pos) and P_ij = sigmoid(a - pos) p_ij / L, so
+// dq = sum_j P_ij c_j - (1 - P_pos) c_pos: a mean of the negatives' rows minus
+// the positive's, weighted by the exact 1 - P_pos, with no P - I cancellation.)
+__device__ __forceinline__ float softplus_f(float x) {
+  return x > 0.0f ? x + log1pf(expf(-x)) : log1pf(expf(x));
+}
+
 template <int D>
 __device__ __forceinline__ void combine_row_finish(int64_t i, int sub, float M, float L, const f32x4& o,
                                                    const float (&ce)[4], const float (&qe)[4], float lq, int dim,
                                                    float* __restrict__ lse_out, float* __restrict__ loss_out,
                                                    float* __restrict__ dq, float* __restrict__ neg_lse_bias) {
   constexpr int LPR = D / 4;
-  const float lse = M + logf(L);
-  const float inv = 1.0f / L;
   float dot = 0.0f;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int e = 4 * sub + u;
-    if (e < dim) {
-      if (dq) dq[i * dim + e] = o[u] * inv - ce[u];
-      dot = __builtin_fmaf(qe[u], ce[u], dot);
-    }
-  }
+  for (int u = 0; u < 4; ++u)
+    if (4 * sub + u < dim) dot = __builtin_fmaf(qe[u], ce[u], dot);
 #pragma unroll
   for (int m = LPR / 2; m >= 1; m >>= 1) dot += __shfl_xor(dot, m, LPR);
+  const float pos = dot - lq;
+  // no negative with p > 0 (a single column, or every other score -inf): P_pos = 1
+  const bool none = !(L > 0.0f);
+  const float a = none ? -INFINITY : M * kLn2 + logf(L);
+  const float loss = none ? 0.0f : softplus_f(a - pos);
+  const float g = none ? 0.0f : 1.0f / (1.0f + expf(pos - a));  // sigmoid(a - pos) = 1 - P_pos
+  const float inv = none ? 0.0f : 1.0f / L;
+  if (dq) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = 4 * sub + u;
+      if (e < dim) dq[i * dim + e] = g * (o[u] * inv - ce[u]);
+    }
+  }
   if (sub == 0) {
-    const float pos_logit = dot - lq;
+    const float lse = pos + loss;
     lse_out[i] = lse;
-    loss_out[i] = lse - pos_logit;
+    loss_out[i] = loss;
     if (neg_lse_bias) neg_lse_bias[i] = -lse;
   }
 }
@@ -520,7 +565,8 @@ __global__ void __launch_bounds__(256) combine_rows_kernel(
   }
   const float lq = logq ? logq[pos] : 0.0f;
   // splits in groups of 4 whose loads are all issued before any is used
-  // (index clamped, weight 0 past nsplit); splits added in order as before
+  // (index clamped, weight 0 past nsplit); splits added in order.  The split
+  // maxima are integers in log2 units: every weight is an exact power of two.
   float M = -1.0e30f;
   if (nsplit <= 4) {  // one pass: M from the same loads
     float m[4], l[4];
@@ -539,7 +585,7 @@ __global__ void __launch_bounds__(256) combine_rows_kernel(
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (u < nsplit) {
-        const float w = expf(m[u] - M);
+        const float w = exp2f(m[u] - M);
         L += l[u] * w;
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] += ps[u][e] * w;
@@ -570,7 +616,7 @@ __global__ void __launch_bounds__(256) combine_rows_kernel(
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (s0 + u < nsplit) {
-        const float w = expf(m[u] - M);
+        const float w = exp2f(m[u] - M);
         L += l[u] * w;
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] += ps[u][e] * w;
@@ -580,22 +626,40 @@ __global__ void __launch_bounds__(256) combine_rows_kernel(
   combine_row_finish<D>(i, sub, M, L, o, ce, qe, lq, dim, lse_out, loss_out, dq, neg_lse_bias);
 }
 
-// Cols: dc_j = exp(-logq_j) * sum_s O_s[j] - q_pos(j).
+// Cols: dc_j = exp(-logq_j) * sum_s O_s[j] - (1 - P_pos) q_pos, the pass's
+// sums holding every row but the positive i = j + pos_offset, and
+// 1 - P_pos = -expm1(-row_loss_i) (exact; from lse_i when row_loss is NULL:
+// -expm1(pos - lse_i), pos = q_i . c_j - logq_j).
 template <int D>
 __global__ void __launch_bounds__(256) combine_cols_kernel(const float* __restrict__ part_o, int nsplit,
                                                            int64_t n_stat_pad, const float* __restrict__ q,
-                                                           int64_t ldq, const float* __restrict__ logq,
-                                                           int64_t n_cols, int dim, int64_t pos_offset,
-                                                           float* __restrict__ dc) {
+                                                           int64_t ldq, const float* __restrict__ c, int64_t ldc,
+                                                           const float* __restrict__ lse,
+                                                           const float* __restrict__ row_loss,
+                                                           const float* __restrict__ logq, int64_t n_cols, int dim,
+                                                           int64_t pos_offset, float* __restrict__ dc) {
   constexpr int LPR = D / 4;
   const int64_t j = blockIdx.x * (256ll / LPR) + threadIdx.x / LPR;
   const int sub = threadIdx.x % LPR;
   if (j >= n_cols) return;
-  const float scale = logq ? expf(-logq[j]) : 1.0f;
+  const float lq = logq ? logq[j] : 0.0f;
+  const float scale = logq ? expf(-lq) : 1.0f;
   const int64_t pos = j + pos_offset;
   float qe[4];  // q_pos, loaded with the first partials (clamped past dim, dropped)
 #pragma unroll
   for (int u = 0; u < 4; ++u) qe[u] = q[pos * ldq + min(4 * sub + u, dim - 1)];
+  float omp;  // 1 - P_pos
+  if (row_loss) {
+    omp = -expm1f(-row_loss[pos]);
+  } else {
+    float dot = 0.0f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (4 * sub + u < dim) dot = __builtin_fmaf(qe[u], c[j * ldc + 4 * sub + u], dot);
+#pragma unroll
+    for (int m = LPR / 2; m >= 1; m >>= 1) dot += __shfl_xor(dot, m, LPR);
+    omp = -expm1f(fminf(dot - lq - lse[pos], 0.0f));
+  }
   f32x4 o = {0.0f, 0.0f, 0.0f, 0.0f};
   for (int s0 = 0; s0 < nsplit; s0 += 4) {  // 4 splits' loads in flight, added in order
     f32x4 ps[4];
@@ -612,7 +676,7 @@ __global__ void __launch_bounds__(256) combine_cols_kernel(const float* __restri
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int e = 4 * sub + u;
-    if (e < dim) dc[j * dim + e] = o[u] * scale - qe[u];
+    if (e < dim) dc[j * dim + e] = o[u] * scale - omp * qe[u];
   }
 }
 
@@ -735,15 +799,16 @@ int combine_rows(int D, hipStream_t st, const float* pm, const float* pl, const 
 }
 
 int combine_cols(int D, hipStream_t st, const float* po, int nsplit, int64_t n_stat_pad, const float* q,
-                 int64_t ldq, const float* logq, int64_t n, int dim, int64_t pos_offset, float* dc) {
+                 int64_t ldq, const float* c, int64_t ldc, const float* lse, const float* row_loss,
+                 const float* logq, int64_t n, int dim, int64_t pos_offset, float* dc) {
   const dim3 grid(static_cast<unsigned>(ceil_div(n, 1024 / D)));
   switch (D) {
-    case 32: hipLaunchKernelGGL(combine_cols_kernel<32>, grid, dim3(256), 0, st, po, nsplit, n_stat_pad, q, ldq,
-                                logq, n, dim, pos_offset, dc); break;
-    case 64: hipLaunchKernelGGL(combine_cols_kernel<64>, grid, dim3(256), 0, st, po, nsplit, n_stat_pad, q, ldq,
-                                logq, n, dim, pos_offset, dc); break;
-    default: hipLaunchKernelGGL(combine_cols_kernel<128>, grid, dim3(256), 0, st, po, nsplit, n_stat_pad, q, ldq,
-                                logq, n, dim, pos_offset, dc); break;
+    case 32: hipLaunchKernelGGL(combine_cols_kernel<32>, grid, dim3(256), 0, st, po, nsplit, n_stat_pad, q, ldq, c,
+                                ldc, lse, row_loss, logq, n, dim, pos_offset, dc); break;
+    case 64: hipLaunchKernelGGL(combine_cols_kernel<64>, grid, dim3(256), 0, st, po, nsplit, n_stat_pad, q, ldq, c,
+                                ldc, lse, row_loss, logq, n, dim, pos_offset, dc); break;
+    default: hipLaunchKernelGGL(combine_cols_kernel<128>, grid, dim3(256), 0, st, po, nsplit, n_stat_pad, q, ldq, c,
+                                ldc, lse, row_loss, logq, n, dim, pos_offset, dc); break;
   }
   TT_CHECK_LAUNCH();
   return TT_OK;
@@ -821,16 +886,16 @@ extern "C" int tt_inbatch_xent_rows(const float* q, int64_t ldq, int64_t n_rows,
   const PrepJob none{};
   if ((rc = prep(p.D, prep_job(q, ldq, n_rows, dim, w.stat), none, dim, p.stat_pad, st))) return rc;
   if ((rc = prep(p.D, prep_job(c, ldc, n_cols, dim, w.strm, logq, w.bias), none, dim, p.strm_pad, st))) return rc;
-  PassArgs a{w.stat, w.strm, w.bias, p.stat_pad, p.strm_pad, p.per_split, w.part_m, w.part_l, w.part_o};
+  PassArgs a{w.stat, w.strm, w.bias, p.stat_pad, p.strm_pad, p.per_split, pos_offset, w.part_m, w.part_l, w.part_o};
   if ((rc = launch_pass<0>(p, a, st))) return rc;
   return combine_rows(p.D, st, w.part_m, w.part_l, w.part_o, p.split, p.stat_pad, q, ldq, c, ldc, logq, n_rows, dim,
                       pos_offset, lse, row_loss, dq, nullptr);
 }
 
-extern "C" int tt_inbatch_xent_cols(const float* q, int64_t ldq, int64_t n_rows, const float* lse, const float* c,
-                                    int64_t ldc, int64_t n_cols, int32_t dim, const float* logq,
-                                    int64_t pos_offset, float* dc, void* workspace, size_t workspace_bytes,
-                                    tt_stream_t stream) {
+extern "C" int tt_inbatch_xent_cols(const float* q, int64_t ldq, int64_t n_rows, const float* lse,
+                                    const float* row_loss, const float* c, int64_t ldc, int64_t n_cols, int32_t dim,
+                                    const float* logq, int64_t pos_offset, float* dc, void* workspace,
+                                    size_t workspace_bytes, tt_stream_t stream) {
   clear_error();
   int rc = check_common(q, ldq, n_rows, c, ldc, n_cols, dim);
   if (rc) return rc;
@@ -846,9 +911,10 @@ extern "C" int tt_inbatch_xent_cols(const float* q, int64_t ldq, int64_t n_rows,
   const PrepJob none{};
   if ((rc = prep(p.D, prep_job(c, ldc, n_cols, dim, w.stat), none, dim, p.stat_pad, st))) return rc;
   if ((rc = prep(p.D, prep_job(q, ldq, n_rows, dim, w.strm, lse, w.bias), none, dim, p.strm_pad, st))) return rc;
-  PassArgs a{w.stat, w.strm, w.bias, p.stat_pad, p.strm_pad, p.per_split, nullptr, nullptr, w.part_o};
+  PassArgs a{w.stat, w.strm, w.bias, p.stat_pad, p.strm_pad, p.per_split, pos_offset, nullptr, nullptr, w.part_o};
   if ((rc = launch_pass<1>(p, a, st))) return rc;
-  return combine_cols(p.D, st, w.part_o, p.split, p.stat_pad, q, ldq, logq, n_cols, dim, pos_offset, dc);
+  return combine_cols(p.D, st, w.part_o, p.split, p.stat_pad, q, ldq, c, ldc, lse, row_loss, logq, n_cols, dim,
+                      pos_offset, dc);
 }
 
 // ---------------------------------------------------------------------------
@@ -917,12 +983,12 @@ extern "C" int tt_inbatch_softmax_xent(const float* q, int64_t ldq, const float*
                  dim, p.n_pad, st)))
     return rc;
   const Plan pl{p.D, p.n_pad, p.n_pad, p.split, p.per_split};
-  PassArgs ar{w.qb, w.cb, w.bias_logq, p.n_pad, p.n_pad, p.per_split, w.part_m, w.part_l, w.part_o_rows};
+  PassArgs ar{w.qb, w.cb, w.bias_logq, p.n_pad, p.n_pad, p.per_split, 0, w.part_m, w.part_l, w.part_o_rows};
   if ((rc = launch_pass<0>(pl, ar, st))) return rc;
   if ((rc = combine_rows(p.D, st, w.part_m, w.part_l, w.part_o_rows, p.split, p.n_pad, q, ldq, c, ldc, logq, n, dim,
                          0, lse, row_loss, dq, w.bias_lse)))
     return rc;
-  PassArgs ac{w.cb, w.qb, w.bias_lse, p.n_pad, p.n_pad, p.per_split, nullptr, nullptr, w.part_o_cols};
+  PassArgs ac{w.cb, w.qb, w.bias_lse, p.n_pad, p.n_pad, p.per_split, 0, nullptr, nullptr, w.part_o_cols};
   if ((rc = launch_pass<1>(pl, ac, st))) return rc;
-  return combine_cols(p.D, st, w.part_o_cols, p.split, p.n_pad, q, ldq, logq, n, dim, 0, dc);
+  return combine_cols(p.D, st, w.part_o_cols, p.split, p.n_pad, q, ldq, c, ldc, lse, row_loss, logq, n, dim, 0, dc);
 }

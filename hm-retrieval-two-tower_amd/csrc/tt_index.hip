@@ -1572,26 +1572,44 @@ extern "C" int tt_bruteforce_search(const void* index, const float* cand, int64_
 //            floor), so the merged lists hold the global top-k exactly; fewer
 //            than k are padded with (-inf, INT32_MAX).
 // Queries whose certificate fails are scanned exactly over the shard's rows.
-// One chunk of <= tt_bruteforce_shard_chunk(...) queries per call pair; the
-// pair shares the workspace (its lists live there between the two calls).
+// Queries go in chunks: every call pair of one search plans with the same
+// `plan_queries` (the chunk the workspace was sized for, which every rank of
+// the search must use alike: tt_bruteforce_shard_chunk is a per-shard
+// recommendation, the caller takes the minimum over the shards) and carries
+// n_queries <= plan_queries of them; the pair shares the workspace (its lists
+// live there between the two calls).
 extern "C" int64_t tt_bruteforce_shard_chunk(int64_t n_queries, int64_t n_cand, int32_t dim, int32_t k) {
   if (n_queries < 1 || n_cand < 1 || k < 1 || pick_dpad(dim) == 0) return 0;
   return plan_search(n_queries, n_cand, k, 1).chunk;
 }
 
-extern "C" size_t tt_bruteforce_shard_workspace_size(int64_t n_queries, int64_t n_cand, int32_t dim, int32_t k) {
-  return tt_bruteforce_workspace_size(n_queries, n_cand, dim, k);
+namespace {
+// the plan of every chunk of a shard search: sized for plan_queries queries
+SearchPlan shard_plan(int64_t plan_queries, int64_t n_cand, int k) {
+  SearchPlan p = plan_search(plan_queries, n_cand, k, 1);
+  p.chunk = round_up(plan_queries, kQPerWG);
+  return p;
+}
+}  // namespace
+
+extern "C" size_t tt_bruteforce_shard_workspace_size(int64_t plan_queries, int64_t n_cand, int32_t dim, int32_t k) {
+  if (plan_queries < 1 || n_cand < 1 || k < 1 || pick_dpad(dim) == 0) return 0;
+  const SearchPlan p = shard_plan(plan_queries, n_cand, k);
+  Carver cv(nullptr, 0);
+  carve_search(cv, pick_dpad(dim), p, true, true);
+  return cv.used();
 }
 
 namespace {
-int shard_check(const char* fn, const void* index, int64_t n_cand, int32_t dim, int64_t n_queries, int32_t k,
-                void* workspace, size_t workspace_bytes, const SearchPlan& p, SearchWs* w) {
+int shard_check(const char* fn, const void* index, int64_t n_cand, int32_t dim, int64_t n_queries,
+                int64_t plan_queries, int32_t k, void* workspace, size_t workspace_bytes, const SearchPlan& p,
+                SearchWs* w) {
   TT_REQUIRE(index, "%s: NULL index", fn);
   TT_REQUIRE(n_cand >= 1 && dim >= 1, "%s: bad shapes", fn);
   if (pick_dpad(dim) == 0) return fail(TT_ERR_UNSUPPORTED, "%s: dim=%d > 128", fn, dim);
   TT_REQUIRE(k >= 1 && k <= n_cand && k <= 4000, "%s: bad k=%d", fn, k);
-  TT_REQUIRE(n_queries >= 1 && n_queries <= p.chunk, "%s: n_queries=%lld outside [1, chunk %lld]", fn,
-             static_cast<long long>(n_queries), static_cast<long long>(p.chunk));
+  TT_REQUIRE(n_queries >= 1 && n_queries <= plan_queries, "%s: n_queries=%lld outside [1, plan_queries %lld]", fn,
+             static_cast<long long>(n_queries), static_cast<long long>(plan_queries));
   Carver cv(workspace, workspace_bytes);
   *w = carve_search(cv, pick_dpad(dim), p, true, true);
   if (!workspace || cv.used() > workspace_bytes)
@@ -1601,13 +1619,14 @@ int shard_check(const char* fn, const void* index, int64_t n_cand, int32_t dim, 
 }  // namespace
 
 extern "C" int tt_bruteforce_shard_screen(const void* index, int64_t n_cand, int32_t dim, const float* queries,
-                                          int64_t ldq, int64_t n_queries, int32_t k, int64_t index_offset,
-                                          float* kth_lb, void* workspace, size_t workspace_bytes,
-                                          tt_stream_t stream) {
+                                          int64_t ldq, int64_t n_queries, int64_t plan_queries, int32_t k,
+                                          int64_t index_offset, float* kth_lb, void* workspace,
+                                          size_t workspace_bytes, tt_stream_t stream) {
   clear_error();
-  const SearchPlan p = plan_search(n_queries, n_cand, k, 1);
+  TT_REQUIRE(plan_queries >= 1, "tt_bruteforce_shard_screen: plan_queries must be >= 1");
+  const SearchPlan p = shard_plan(plan_queries, n_cand, k);
   SearchWs w;
-  if (int rc = shard_check("tt_bruteforce_shard_screen", index, n_cand, dim, n_queries, k, workspace,
+  if (int rc = shard_check("tt_bruteforce_shard_screen", index, n_cand, dim, n_queries, plan_queries, k, workspace,
                            workspace_bytes, p, &w))
     return rc;
   TT_REQUIRE(queries && kth_lb && ldq >= dim, "tt_bruteforce_shard_screen: NULL queries/kth_lb or bad ldq");
@@ -1634,14 +1653,15 @@ extern "C" int tt_bruteforce_shard_screen(const void* index, int64_t n_cand, int
 
 extern "C" int tt_bruteforce_shard_finalize(const void* index, const float* cand, int64_t ldc, int64_t n_cand,
                                             int32_t dim, const float* queries, int64_t ldq, int64_t n_queries,
-                                            int32_t k, int64_t index_offset, const float* floor, float* out_scores,
-                                            int32_t* out_idx, void* workspace, size_t workspace_bytes,
-                                            tt_stream_t stream) {
+                                            int64_t plan_queries, int32_t k, int64_t index_offset,
+                                            const float* floor, float* out_scores, int32_t* out_idx,
+                                            void* workspace, size_t workspace_bytes, tt_stream_t stream) {
   clear_error();
-  const SearchPlan p = plan_search(n_queries, n_cand, k, 1);
+  TT_REQUIRE(plan_queries >= 1, "tt_bruteforce_shard_finalize: plan_queries must be >= 1");
+  const SearchPlan p = shard_plan(plan_queries, n_cand, k);
   SearchWs w;
-  if (int rc = shard_check("tt_bruteforce_shard_finalize", index, n_cand, dim, n_queries, k, workspace,
-                           workspace_bytes, p, &w))
+  if (int rc = shard_check("tt_bruteforce_shard_finalize", index, n_cand, dim, n_queries, plan_queries, k,
+                           workspace, workspace_bytes, p, &w))
     return rc;
   TT_REQUIRE(cand && ldc >= dim && queries && ldq >= dim && floor && out_scores && out_idx,
              "tt_bruteforce_shard_finalize: NULL argument or bad leading dimension");

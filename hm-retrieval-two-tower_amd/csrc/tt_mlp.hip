@@ -397,6 +397,10 @@ __device__ __forceinline__ void mlp_wgrad_block(const WgradArgs& a, const int b,
   const int64_t r0 = static_cast<int64_t>(split) * a.rows_per_split;
   int64_t r1 = r0 + a.rows_per_split;
   if (r1 > a.M) r1 = a.M;
+  // a split starting past M (rows_per_split is rounded up to whole stages)
+  // has no rows: its descriptors get 0 bytes, so the prologue's loads return
+  // zeros instead of reading past the operands
+  if (r1 < r0) r1 = r0;
   const int nstage = r1 > r0 ? static_cast<int>((r1 - r0 + kWgBK - 1) / kWgBK) : 0;
   const float s = a.scale ? *a.scale : 1.0f;
 

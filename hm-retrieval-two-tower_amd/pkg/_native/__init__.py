@@ -201,8 +201,8 @@ _PROTOS = {
     ),
     "tt_inbatch_xent_cols": (
         c_int32,
-        [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int64, c_void_p,
-         c_void_p, c_size_t, c_void_p],
+        [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int64,
+         c_void_p, c_void_p, c_size_t, c_void_p],
     ),
     "tt_inbatch_fused_workspace_size": (c_size_t, [c_int64, c_int32]),
     "tt_inbatch_softmax_xent": (
@@ -222,13 +222,13 @@ _PROTOS = {
     "tt_bruteforce_shard_workspace_size": (c_size_t, [c_int64, c_int64, c_int32, c_int32]),
     "tt_bruteforce_shard_screen": (
         c_int32,
-        [c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int64, c_int32, c_int64, c_void_p, c_void_p, c_size_t,
-         c_void_p],
+        [c_void_p, c_int64, c_int32, c_void_p, c_int64, c_int64, c_int64, c_int32, c_int64, c_void_p, c_void_p,
+         c_size_t, c_void_p],
     ),
     "tt_bruteforce_shard_finalize": (
         c_int32,
-        [c_void_p, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int64, c_int64, c_int32, c_int64, c_void_p,
-         c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
+        [c_void_p, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int64, c_int64, c_int64, c_int32, c_int64,
+         c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
     ),
     "tt_topk_merge": (c_int32, [c_void_p, c_void_p, c_int32, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
     "tt_recall_hits": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, POINTER(c_int32), c_int32, c_void_p, c_void_p]),

@@ -1,6 +1,6 @@
 """Multi-GPU paths: one process per GPU, torch.distributed over RCCL/xGMI.
 
-SURVEY §8e.  Two pieces the reference's call sites shard naturally:
+SURVEY §8e.  Three pieces the reference's call sites shard naturally:
 
 * ShardedBruteForceIndex — BruteForceIndex with the candidate matrix
   row-sharded over the ranks: each rank holds only its block of rows and
@@ -10,13 +10,18 @@ SURVEY §8e.  Two pieces the reference's call sites shard naturally:
   global index asc), which equals tf.math.top_k over the unsharded scores
   (brute_force.py:76-81).
 
-* DataParallelTrainStep — the reference's train_step
-  (two_tower_model.py:94-130) replicated per GPU the way a data-parallel
-  Keras run executes it: each replica computes its in-batch loss over its
-  own batch (per-replica negatives), dense gradients are summed with one
-  all_reduce bucket, and the sparse embedding gradients (the IndexedSlices
-  rows + ids) are all-gathered in rank order so every replica applies the
-  same global dedup + Adagrad update — replicas stay identical.
+* ShardedTables / ShardedTrainStep — the reference's train_step
+  (two_tower_model.py:94-130) over G ranks: each large embedding table
+  (Embedding, input_layer.py:37-40) row-sharded (global row r at rank r mod G),
+  lookups routed to their owners with all_to_all (tt_route_requests,
+  tt_gather_tagged), the gradient rows returned the same way and applied by
+  the owner (tt_sparse_scatter_sum, tt_sparse_adagrad); the batch split over
+  the ranks with global in-batch negatives (C and logq all-gathered for the
+  rows pass, Q and lse for the cols pass, gradients reduce_scattered), small
+  tables and the tower MLPs replicated and all_reduced in one bucket.
+
+* QueryShardedBruteForceIndex — replicated candidates, each rank answers its
+  block of the queries (no exchange); bench.py's query-parallel leg.
 
 Collective and kernel entry points are injectable (`ops=`), so the
 orchestration is exercised on CPU with the gloo backend by the tests; the
@@ -36,7 +41,7 @@ import torch.distributed as dist
 
 logger = logging.getLogger(__name__)
 
-__all__ = ["IndexOps", "BatchComm", "ShardedBruteForceIndex", "QueryShardedBruteForceIndex", "DataParallelTrainStep", "shard_range", "all_gather_cat",
+__all__ = ["IndexOps", "BatchComm", "ShardedBruteForceIndex", "QueryShardedBruteForceIndex", "shard_range", "all_gather_cat",
            "EmbeddingOps", "ShardedTables", "ShardedTrainStep"]
 
 
@@ -69,9 +74,12 @@ class IndexOps:
     build: Callable[[torch.Tensor], Any]
     search: Callable[..., Tuple[torch.Tensor, torch.Tensor]]
     merge: Callable[[torch.Tensor, torch.Tensor, int], Tuple[torch.Tensor, torch.Tensor]]
-    # (image, rows, queries, k, offset, reduce_max) -> this shard's exact top-k
-    # of the rows that can reach the global k-th score (padded); None: search
+    # (image, rows, queries, k, offset, reduce_max, chunk) -> this shard's exact
+    # top-k of the rows that can reach the global k-th score (padded), one
+    # reduce_max per chunk of queries; None: search
     shard_search: Optional[Callable[..., Tuple[torch.Tensor, torch.Tensor]]] = None
+    # (n_queries, shard sizes of ALL ranks, dim, k) -> the common query chunk
+    shard_chunk: Optional[Callable[[int, Sequence[int], int, int], int]] = None
 
     @staticmethod
     def hip() -> "IndexOps":
@@ -79,7 +87,7 @@ class IndexOps:
 
         return IndexOps(hip_ops.bruteforce_build,
                         lambda img, cand, q, k, off: hip_ops.bruteforce_search(img, cand, q, k, off),
-                        hip_ops.topk_merge, hip_ops.bruteforce_shard_search)
+                        hip_ops.topk_merge, hip_ops.bruteforce_shard_search, hip_ops.bruteforce_shard_chunk)
 
 
 def _staged(group) -> bool:
@@ -204,9 +212,12 @@ class ShardedBruteForceIndex:
         # collective decision: every rank takes the same branch (its all_reduce)
         if self.world > 1 and self.ops.shard_search is not None and min(self.sizes) >= k:
             # two-phase: the shards' lower bounds on their k-th scores, max-reduced,
-            # cut each shard's exact rescoring to what can reach the global top-k
+            # cut each shard's exact rescoring to what can reach the global top-k.
+            # The query chunk is computed from ALL shard sizes, so every rank makes
+            # the same all_reduce calls (same count, same lengths).
+            chunk = self.ops.shard_chunk(int(q.shape[0]), self.sizes, int(q.shape[1]), k)
             return self.ops.shard_search(self.image, self.shard, q, k, self.offset,
-                                         lambda t: _all_reduce_max(t, self.group))
+                                         lambda t: _all_reduce_max(t, self.group), chunk)
         s, i = self.ops.search(self.image, self.shard, q, kl, self.offset)
         if kl < k:
             ps = torch.full((q.shape[0], k), float("-inf"), dtype=s.dtype, device=s.device)
@@ -296,59 +307,6 @@ class QueryShardedBruteForceIndex:
         with torch.no_grad():
             emb = self.query_model(queries)
         return self.search(emb)[1]
-
-
-class DataParallelTrainStep:
-    """One train step per call on every rank (see module docstring).
-
-    `model` is a compiled TwoTowerModel created with the same seed on every
-    rank.  The batch passed on each rank is that replica's share of the
-    global batch; all replicas must use the same per-replica batch size.
-    """
-
-    def __init__(self, model, example_batch: Optional[Dict[str, Any]] = None, group=None):
-        self.model = model
-        self.group = group
-        self.world = dist.get_world_size(group)
-
-    # -- collectives ---------------------------------------------------------
-    def allreduce_dense(self) -> None:
-        towers = self.model.towers
-        grads = [t.dense.flat.grad for t in towers]
-        bucket = torch.cat([g.reshape(-1) for g in grads])
-        dist.all_reduce(bucket, group=self.group)
-        off = 0
-        for g in grads:
-            g.copy_(bucket[off:off + g.numel()].view_as(g))
-            off += g.numel()
-
-    def gather_sparse(self, layer) -> None:
-        """Replace the layer's sparse batch (ids per lookup, output grad) by the
-        rank-ordered concatenation over all replicas."""
-        calls = layer._last_calls
-        if not calls or layer.last_grad is None:
-            return
-        B = layer.last_grad.shape[0]
-        ids = torch.stack([c[1] for c in calls], 1).contiguous()  # [B, n_lookups]
-        all_ids = all_gather_cat(ids, self.group).reshape(self.world * B, ids.shape[1])
-        g = layer.last_grad.contiguous()
-        all_g = all_gather_cat(g, self.group).reshape(self.world * B, g.shape[1])
-        layer._last_calls = [(name, all_ids[:, j].contiguous(), off) for j, (name, _, off) in enumerate(calls)]
-        layer.last_grad = all_g
-
-    def __call__(self, batch: Dict[str, Any]) -> Dict[str, torch.Tensor]:
-        m = self.model
-        loss = m.compute_loss(batch, training=True)
-        for t in m.towers:
-            t.dense.flat.grad = None
-        loss.backward()
-        self.allreduce_dense()
-        for t in m.towers:
-            self.gather_sparse(t.input_layer)
-        m.optimizer.apply_gradients(m.towers)
-        total = loss.detach().clone()
-        dist.all_reduce(total, group=self.group)
-        return {"loss": total}
 
 
 # --------------------------------------------------------------------------- row-sharded tables
@@ -991,14 +949,19 @@ class ShardedTrainStep:
         self._tick("prefetch", tm)
         return {"loss": loss}
 
+    # workspaces the sharded step's sparse kernels write (EmbeddingOps.hip)
+    STATUS_TAGS = ("sparse_owner", "sparse_mid")
+
     def check_status(self) -> None:
-        """Raise if a shard's sparse apply since the last check refused keys
-        that were not its call's (tt_sparse_status); one stream sync.  Call it
-        once per epoch, like TwoTowerModel.fit does."""
+        """Raise if a shard's owner apply or per-request scatter sum since the
+        last check refused keys that were not its call's (tt_sparse_status on
+        the "sparse_owner" / "sparse_mid" workspaces, every scope); one stream
+        sync.  Call it once per epoch, like TwoTowerModel.fit does (the
+        reference's legacy apply raises, optimizer_factory.py:15-18)."""
         if self.model.device.type == "cuda":
             from pkg.modelling import hip_ops
 
-            hip_ops.sparse_status(self.model.device, "sparse", "")
+            hip_ops.sparse_status_all(self.model.device, self.STATUS_TAGS)
 
     def _finish_routes(self, which) -> None:
         keep = []

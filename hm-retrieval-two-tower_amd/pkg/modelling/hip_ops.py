@@ -93,6 +93,12 @@ class Workspace:
         return cls._bufs.get((idx, pre + tag))
 
     @classmethod
+    def all_with_tag(cls, device: torch.device, tag: str) -> List[torch.Tensor]:
+        """Every buffer of (device, any scope, tag) allocated so far."""
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        return [b for (d, k), b in cls._bufs.items() if d == idx and (k == tag or k.endswith("/" + tag))]
+
+    @classmethod
     def clear(cls) -> None:
         cls._bufs.clear()
 
@@ -255,13 +261,27 @@ def sparse_status(device: torch.device, ws_tag: str = "sparse", scope: Optional[
     check(lib().tt_sparse_status(ws.data_ptr(), ws.numel(), _stream()))
 
 
-def sparse_sort(tables: Sequence[dict], batch: int) -> None:
+def sparse_status_all(device: torch.device, ws_tags: Sequence[str]) -> None:
+    """sparse_status over every scope's workspace of each tag (all are read
+    and cleared; the first recorded error is raised)."""
+    err = None
+    for tag in ws_tags:
+        for ws in Workspace.all_with_tag(device, tag):
+            try:
+                check(lib().tt_sparse_status(ws.data_ptr(), ws.numel(), _stream()))
+            except Exception as e:  # noqa: BLE001 - re-raised below after every workspace is cleared
+                err = err or e
+    if err is not None:
+        raise err
+
+
+def sparse_sort(tables: Sequence[dict], batch: int, ws_tag: str = "sparse") -> None:
     """First stage of sparse_adagrad(..., presorted=True): build and sort the lookup keys
     (reads only the ids; no gradient needed), on the current stream."""
     arr = _sparse_tables(tables, batch, adam=False)
     L = lib()
     need = L.tt_sparse_workspace_size(arr, len(tables), batch)
-    ws = Workspace.get(need, tables[0]["table"].device, "sparse")
+    ws = Workspace.get(need, tables[0]["table"].device, ws_tag)
     check(L.tt_sparse_sort(arr, len(tables), batch, ws.data_ptr(), ws.numel(), _stream()))
 
 
@@ -458,8 +478,9 @@ def inbatch_rows(q: torch.Tensor, c: torch.Tensor, logq: Optional[torch.Tensor],
 
 
 def inbatch_cols(q: torch.Tensor, lse: torch.Tensor, c: torch.Tensor, logq: Optional[torch.Tensor],
-                 pos_offset: int = 0) -> torch.Tensor:
-    """Column pass: dc [C,E]."""
+                 pos_offset: int = 0, row_loss: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Column pass: dc [C,E] from every row's q [R,E], lse [R] and (optional,
+    for the exact 1 - P_pos of confident rows) row_loss [R]."""
     _req(q, "q", torch.float32, 2)
     _req(c, "c", torch.float32, 2)
     ldq, ldc = _row_major(q, "q"), _row_major(c, "c")
@@ -468,7 +489,8 @@ def inbatch_cols(q: torch.Tensor, lse: torch.Tensor, c: torch.Tensor, logq: Opti
     L = lib()
     ws = Workspace.get(L.tt_inbatch_workspace_size(R, C, E), q.device, "inbatch")
     dc = torch.empty(C, E, dtype=torch.float32, device=q.device)
-    check(L.tt_inbatch_xent_cols(q.data_ptr(), ldq, R, _opt_ptr(lse, "lse", R), c.data_ptr(), ldc, C, E,
+    check(L.tt_inbatch_xent_cols(q.data_ptr(), ldq, R, _opt_ptr(lse, "lse", R), _opt_ptr(row_loss, "row_loss", R),
+                                 c.data_ptr(), ldc, C, E,
                                  _opt_ptr(logq, "logq", C), pos_offset, dc.data_ptr(), ws.data_ptr(), ws.numel(),
                                  _stream()))
     return dc
@@ -532,13 +554,24 @@ def bruteforce_search(index: torch.Tensor, cand: torch.Tensor, queries: torch.Te
     return out_s, out_i
 
 
+def bruteforce_shard_chunk(n_queries: int, shard_sizes: Sequence[int], dim: int, k: int) -> int:
+    """The query chunk every rank of a candidate-sharded search uses: the
+    smallest of the shards' recommendations (tt_bruteforce_shard_chunk), so
+    all ranks make the same number of all_reduce calls with the same lengths."""
+    L = lib()
+    return max(1, min(int(L.tt_bruteforce_shard_chunk(max(int(n_queries), 1), int(n), dim, k)) for n in shard_sizes))
+
+
 def bruteforce_shard_search(index: torch.Tensor, cand: torch.Tensor, queries: torch.Tensor, k: int,
-                            index_offset: int, reduce_max) -> Tuple[torch.Tensor, torch.Tensor]:
+                            index_offset: int, reduce_max, chunk: Optional[int] = None
+                            ) -> Tuple[torch.Tensor, torch.Tensor]:
     """This shard's part of a candidate-sharded exact top-k (tt.h
     tt_bruteforce_shard_*): per chunk of queries, the screen's lower bound on
     the shard's k-th score, `reduce_max(t)` (in place: the max over the shards,
     an all_reduce) as the floor, then the shard's exact top-k of the entries
-    that can reach it, padded with (-inf, INT32_MAX)."""
+    that can reach it, padded with (-inf, INT32_MAX).  `chunk` must be the
+    same on every rank (bruteforce_shard_chunk over all shard sizes); the
+    default, this shard's own recommendation, is only safe for one rank."""
     _req(index, "index", torch.uint8, 1)
     _req(cand, "cand", torch.float32, 2)
     _req(queries, "queries", torch.float32, 2)
@@ -554,17 +587,19 @@ def bruteforce_shard_search(index: torch.Tensor, cand: torch.Tensor, queries: to
     out_i = torch.empty(nq, k, dtype=torch.int32, device=queries.device)
     if nq == 0:
         return out_s, out_i
-    chunk = int(L.tt_bruteforce_shard_chunk(nq, n, d, k))
+    chunk = int(chunk) if chunk else int(L.tt_bruteforce_shard_chunk(nq, n, d, k))
+    if chunk < 1:
+        raise ValueError(f"chunk must be >= 1, got {chunk}")
     ws = Workspace.get(L.tt_bruteforce_shard_workspace_size(chunk, n, d, k), queries.device, "bruteforce_shard")
     kth = torch.empty(chunk, dtype=torch.float32, device=queries.device)
     for q0 in range(0, nq, chunk):
         m = min(chunk, nq - q0)
         qc = queries[q0:q0 + m]
-        check(L.tt_bruteforce_shard_screen(index.data_ptr(), n, d, qc.data_ptr(), ldq, m, k, index_offset,
+        check(L.tt_bruteforce_shard_screen(index.data_ptr(), n, d, qc.data_ptr(), ldq, m, chunk, k, index_offset,
                                            kth.data_ptr(), ws.data_ptr(), ws.numel(), _stream()))
         reduce_max(kth[:m])
-        check(L.tt_bruteforce_shard_finalize(index.data_ptr(), cand.data_ptr(), ldc, n, d, qc.data_ptr(), ldq, m, k,
-                                             index_offset, kth.data_ptr(), out_s[q0:q0 + m].data_ptr(),
+        check(L.tt_bruteforce_shard_finalize(index.data_ptr(), cand.data_ptr(), ldc, n, d, qc.data_ptr(), ldq, m,
+                                             chunk, k, index_offset, kth.data_ptr(), out_s[q0:q0 + m].data_ptr(),
                                              out_i[q0:q0 + m].data_ptr(), ws.data_ptr(), ws.numel(), _stream()))
     return out_s, out_i
 

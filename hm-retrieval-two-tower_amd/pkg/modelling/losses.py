@@ -201,8 +201,9 @@ def global_inbatch_grads(q: torch.Tensor, c: torch.Tensor, logq: Optional[torch.
     L = comm.all_gather(logq) if logq is not None else None   # [G b]
     lse, row_loss, dq = rows(q, C, L, pos_offset=off)
     Qa = comm.all_gather(q)                                    # [G b, E]
-    lse_a = comm.all_gather(lse)                               # [G b]
-    dc = cols(Qa, lse_a, c, logq, pos_offset=off)              # local columns, every row
+    st = comm.all_gather(torch.stack([lse, row_loss], 1))      # [G b, 2]: every row's lse and loss
+    lse_a, loss_a = st[:, 0].contiguous(), st[:, 1].contiguous()
+    dc = cols(Qa, lse_a, c, logq, pos_offset=off, row_loss=loss_a)  # local columns, every row
     return row_loss, dq, dc
 
 

@@ -258,7 +258,13 @@ int tt_dense_adam(float* param, float* m, float* v, const float* grad,
  *   dq_i     = sum_j softmax_j(S'[i]) c_j - c_pos(i)
  *   dc_j     = sum_i softmax(S'[i])_j q_i - q_pos^-1(j)
  *
- * bf16 MFMA operands, fp32 accumulation, fp32 outputs; the [rows, cols]
+ * Arithmetic contract: the NEGATIVE pairs are scored with bf16 (RNE)
+ * operands and fp32 accumulation, and their exp weights enter the P.C /
+ * P^T.Q products rounded to bf16 (relative to a power-of-two scale, so the
+ * rounding is reproducible: oracle.inbatch_softmax_xent_bf16); the positive
+ * pair is scored in fp32 and enters through the exact 1 - P_pos
+ * (row_loss = softplus(lse_neg - pos), dq = (1 - P_pos)(mean_neg c - c_pos)),
+ * so there is no P - I cancellation.  fp32 outputs; the [rows, cols]
  * score matrix is never materialised.  Rows and columns are given
  * separately so a rank can score its local rows against all-gathered
  * columns (global in-batch negatives): the positive column of local row i
@@ -275,12 +281,16 @@ int tt_inbatch_xent_rows(const float* q, int64_t ldq, int64_t n_rows,
                          void* workspace, size_t workspace_bytes,
                          tt_stream_t stream);
 
-/* Column pass: dc [n_cols, dim] (ld = dim) from all rows' q and lse. */
+/* Column pass: dc [n_cols, dim] (ld = dim) from all rows' q, lse and
+ * row_loss (the rows pass's outputs; 1 - P_pos = -expm1(-row_loss).
+ * row_loss may be NULL: then 1 - P_pos comes from lse and the fp32 positive
+ * score, which cancels when the positive dominates). */
 int tt_inbatch_xent_cols(const float* q, int64_t ldq, int64_t n_rows,
-                         const float* lse, const float* c, int64_t ldc,
-                         int64_t n_cols, int32_t dim, const float* logq,
-                         int64_t pos_offset, float* dc, void* workspace,
-                         size_t workspace_bytes, tt_stream_t stream);
+                         const float* lse, const float* row_loss,
+                         const float* c, int64_t ldc, int64_t n_cols,
+                         int32_t dim, const float* logq, int64_t pos_offset,
+                         float* dc, void* workspace, size_t workspace_bytes,
+                         tt_stream_t stream);
 
 /* Single-device form of the two passes above (rows = cols = the batch,
  * positive of row i is column i): one shared bf16 preparation of q and c,
@@ -330,23 +340,28 @@ int tt_bruteforce_search(const void* index, const float* cand, int64_t ldc,
  *     (-inf, INT32_MAX) past the survivors; failed certificates are scanned
  *     exactly over the shard.  Merging the G lists (tt_topk_merge) gives the
  *     exact global top-k.
- * Queries go in chunks of at most tt_bruteforce_shard_chunk(total, ...); a
- * screen / finalize pair of one chunk shares the workspace. */
+ * Queries go in chunks of n_queries <= plan_queries; every call pair of one
+ * search passes the same plan_queries, which must be equal on every rank
+ * (tt_bruteforce_shard_chunk(total, n_g, ...) is rank g's recommendation: take
+ * the minimum over the ranks) and the workspace is sized for it
+ * (tt_bruteforce_shard_workspace_size(plan_queries, n_g, ...)).  A screen /
+ * finalize pair of one chunk shares the workspace. */
 int64_t tt_bruteforce_shard_chunk(int64_t n_queries, int64_t n_cand,
                                   int32_t dim, int32_t k);
-size_t tt_bruteforce_shard_workspace_size(int64_t n_queries, int64_t n_cand,
+size_t tt_bruteforce_shard_workspace_size(int64_t plan_queries, int64_t n_cand,
                                           int32_t dim, int32_t k);
 int tt_bruteforce_shard_screen(const void* index, int64_t n_cand, int32_t dim,
                                const float* queries, int64_t ldq,
-                               int64_t n_queries, int32_t k,
+                               int64_t n_queries, int64_t plan_queries, int32_t k,
                                int64_t index_offset, float* kth_lb,
                                void* workspace, size_t workspace_bytes,
                                tt_stream_t stream);
 int tt_bruteforce_shard_finalize(const void* index, const float* cand,
                                  int64_t ldc, int64_t n_cand, int32_t dim,
                                  const float* queries, int64_t ldq,
-                                 int64_t n_queries, int32_t k,
-                                 int64_t index_offset, const float* floor,
+                                 int64_t n_queries, int64_t plan_queries,
+                                 int32_t k, int64_t index_offset,
+                                 const float* floor,
                                  float* out_scores, int32_t* out_idx,
                                  void* workspace, size_t workspace_bytes,
                                  tt_stream_t stream);

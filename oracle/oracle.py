@@ -163,6 +163,118 @@ def inbatch_softmax_xent(q: np.ndarray, c: np.ndarray, logq: Optional[np.ndarray
     }
 
 
+def bf16_round(x: np.ndarray) -> np.ndarray:
+    """fp32 -> bf16 -> fp32, round to nearest even (v_cvt_pk_bf16_f32; the
+    in-batch prep and P packing of csrc/tt_inbatch.hip)."""
+    u = np.ascontiguousarray(x, np.float32).view(np.uint32).astype(np.uint64)
+    u = (u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000
+    return u.astype(np.uint32).view(np.float32)
+
+
+# log2(e) as the kernels hold it (an fp32 constant)
+LOG2E_F32 = float(np.float32(1.4426950408889634))
+
+
+def _exp2_arg(s32: np.ndarray, m: np.ndarray) -> np.ndarray:
+    """fp32 fmaf(s, LOG2E_F32, -m) for fp32 s and integer-valued m: the fp64
+    product of two fp32 values is exact and so is subtracting the integer,
+    so one rounding to fp32 gives exactly the fused result."""
+    return (np.asarray(s32, np.float32).astype(np.float64) * LOG2E_F32 - m).astype(np.float32)
+
+
+def _softplus(x: np.ndarray) -> np.ndarray:
+    return np.where(x > 0, x + np.log1p(np.exp(-np.abs(x))), np.log1p(np.exp(np.minimum(x, 0.0))))
+
+
+def inbatch_softmax_xent_bf16(q: np.ndarray, c: np.ndarray, logq: Optional[np.ndarray] = None, pos_offset: int = 0,
+                              rows_q: Optional[np.ndarray] = None, block: int = 2048) -> Dict[str, np.ndarray]:
+    """The arithmetic contract of tt_inbatch_* (include/tt.h), restated: the
+    same loss and gradients as inbatch_softmax_xent (two_tower_model.py:92,
+    113-124; logq_correction.py:66-71), computed the way the kernels compute
+    them, so the GPU can be held to it tightly:
+      * negative pairs: S = bf16(q) . bf16(c) (RNE, exact products, rounded to
+        fp32) - logq; p = fp32(2^(S log2e - M)) with M an integer (the kernel's
+        running max is an integer in log2 units, so any integer gives the same
+        bf16(p) up to rare last-bit ties of the fp32 exponent argument); the
+        P.C product uses bf16(p) and bf16(c); the row sum L uses the fp32 p;
+      * the positive pair is scored in fp32: a = lse over the negatives,
+        row_loss = softplus(a - pos), dq = sigmoid(a - pos) (O / L - c_pos);
+      * columns (every row i of q against c, with the rows' lse and loss):
+        p = bf16(fp32(exp(bf16(q_i).bf16(c_j) - lse_i))) for the negatives,
+        dc_j = exp(-logq_j) sum_i p bf16(q_i) - (-expm1(-row_loss_pos)) q_pos.
+    Rows q [R,E] against columns c [C,E]; the positive of row i is column
+    i + pos_offset.  `rows_q` ([C + ...] rows for the column pass; default q
+    with R == C) is every row of the batch when q holds one rank's block.
+    Returns dict(loss, row_loss, lse, dq) and, when the rows cover every
+    column's positive (rows_q None and R == C, pos_offset 0), dc."""
+    q32, c32 = np.asarray(q, np.float32), np.asarray(c, np.float32)
+    R, E = q32.shape
+    C = c32.shape[0]
+    qb = bf16_round(q32).astype(np.float64)
+    cb = bf16_round(c32).astype(np.float64)
+    lq = np.zeros(C) if logq is None else np.asarray(logq, np.float32).astype(np.float64)
+    pos = np.arange(R) + pos_offset
+    # fp32 positive logits (q_i . c_pos in fp64, rounded; the GPU's fp32 fma
+    # chain agrees to a few ulp)
+    pos_logit = (np.einsum("ij,ij->i", q32.astype(np.float64), c32[pos].astype(np.float64)) - lq[pos])
+    pos_logit = pos_logit.astype(np.float32).astype(np.float64)
+    row_loss = np.empty(R)
+    lse = np.empty(R)
+    dq = np.empty((R, E))
+    for r0 in range(0, R, block):
+        r1 = min(R, r0 + block)
+        S = ((qb[r0:r1] @ cb.T) - lq[None, :]).astype(np.float32).astype(np.float64)
+        rr = np.arange(r1 - r0)
+        S[rr, pos[r0:r1]] = -np.inf
+        mx = (S.max(axis=1) * LOG2E_F32)
+        M = np.where(np.isfinite(mx), np.ceil(mx), 0.0)
+        p = np.exp2(_exp2_arg(S, M[:, None]).astype(np.float64)).astype(np.float32)
+        L = p.astype(np.float64).sum(axis=1)
+        O = bf16_round(p).astype(np.float64) @ cb
+        none = ~(L > 0)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            a = np.where(none, -np.inf, M * np.log(2.0) + np.log(np.where(none, 1.0, L)))
+            d = a - pos_logit[r0:r1]
+            loss = np.where(none, 0.0, _softplus(np.where(none, 0.0, d)))
+            g = np.where(none, 0.0, 1.0 / (1.0 + np.exp(-np.where(none, 0.0, d))))
+            mean = np.where(none[:, None], 0.0, O / np.where(none, 1.0, L)[:, None])
+        dq[r0:r1] = g[:, None] * (mean - c32[pos[r0:r1]].astype(np.float64))
+        row_loss[r0:r1] = loss
+        lse[r0:r1] = pos_logit[r0:r1] + loss
+    row_loss32 = row_loss.astype(np.float32)
+    lse32 = (pos_logit.astype(np.float32) + row_loss32).astype(np.float32)
+    out = {"loss": float(row_loss32.astype(np.float64).sum()), "row_loss": row_loss32, "lse": lse32,
+           "dq": dq.astype(np.float32)}
+    if rows_q is None and R == C and pos_offset == 0:
+        out["dc"] = inbatch_cols_bf16(q32, lse32, row_loss32, c32, logq, 0, block)
+    return out
+
+
+def inbatch_cols_bf16(q_all: np.ndarray, lse: np.ndarray, row_loss: np.ndarray, c: np.ndarray,
+                      logq: Optional[np.ndarray] = None, pos_offset: int = 0, block: int = 2048) -> np.ndarray:
+    """Column pass of the contract (inbatch_softmax_xent_bf16): dc [C,E] of the
+    columns c against every row q_all [R,E] with its lse and row_loss; the
+    positive of column j is row j + pos_offset."""
+    q32, c32 = np.asarray(q_all, np.float32), np.asarray(c, np.float32)
+    R, E = q32.shape
+    C = c32.shape[0]
+    qb = bf16_round(q32).astype(np.float64)
+    cb = bf16_round(c32).astype(np.float64)
+    lse64 = np.asarray(lse, np.float32).astype(np.float64)
+    O = np.zeros((C, E))
+    cols = np.arange(C)
+    for r0 in range(0, R, block):
+        r1 = min(R, r0 + block)
+        s = ((qb[r0:r1] @ cb.T) - lse64[r0:r1, None]).astype(np.float32).astype(np.float64)
+        hit = (cols + pos_offset >= r0) & (cols + pos_offset < r1)
+        s[cols[hit] + pos_offset - r0, cols[hit]] = -np.inf
+        p = np.exp2(_exp2_arg(s, 0.0).astype(np.float64)).astype(np.float32)
+        O += bf16_round(p).astype(np.float64).T @ qb[r0:r1]
+    scale = np.ones(C) if logq is None else np.exp(-np.asarray(logq, np.float32).astype(np.float64))
+    omp = -np.expm1(-np.asarray(row_loss, np.float32).astype(np.float64)[cols + pos_offset])
+    return (O * scale[:, None] - omp[:, None] * q32[cols + pos_offset].astype(np.float64)).astype(np.float32)
+
+
 # bf16 operands (8 significant bits, round to nearest): unit roundoff 2^-8 per
 # operand, so a product of two rounded operands is within 2^-7 + 2^-16 of the
 # exact one; fp32 accumulation of <= 128 exact bf16 products adds < 2^-17.
@@ -319,7 +431,17 @@ class CpuTwoTower:
     """fp32 numpy train step: gather -> towers -> scores/logQ/CE-SUM -> grads ->
     dense Adagrad (MLP) + dedup + sparse Adagrad (tables)."""
 
-    def __init__(self, q_tables: List[np.ndarray], c_tables: List[np.ndarray], q_layers, c_layers, lr: float):
+    def __init__(self, q_tables: List[np.ndarray], c_tables: List[np.ndarray], q_layers, c_layers, lr: float,
+                 inbatch: str = "fp32"):
+        """inbatch: "fp32" — the in-batch scores, softmax and gradients in
+        fp32 (the reference's arithmetic); "bf16" — the gradients dQ, dC by
+        the kernels' arithmetic contract (inbatch_softmax_xent_bf16), the
+        returned loss still the fp32 one (self.last_contract_loss holds the
+        contract's)."""
+        if inbatch not in ("fp32", "bf16"):
+            raise ValueError(f"inbatch must be 'fp32' or 'bf16', got {inbatch!r}")
+        self.inbatch = inbatch
+        self.last_contract_loss = None
         self.q_tables, self.c_tables = q_tables, c_tables
         self.q_layers = [[w.copy(), b.copy()] for w, b in q_layers]
         self.c_layers = [[w.copy(), b.copy()] for w, b in c_layers]
@@ -347,12 +469,16 @@ class CpuTwoTower:
             g = g @ w.T
         return grads[::-1], g
 
-    def step(self, q_ids: List[np.ndarray], c_ids: List[np.ndarray], logq: Optional[np.ndarray]) -> float:
+    def forward(self, q_ids: List[np.ndarray], c_ids: List[np.ndarray]):
+        """Both towers' activations [x, h_1, ..., h_L] (fp32)."""
         xq = gather_concat([], self.q_tables, q_ids)
         xc = gather_concat([], self.c_tables, c_ids)
-        qa = self._tower(xq, self.q_layers)
-        ca = self._tower(xc, self.c_layers)
-        Q, C = qa[-1], ca[-1]
+        return self._tower(xq, self.q_layers), self._tower(xc, self.c_layers)
+
+    @staticmethod
+    def _scores_loss(Q, C, logq):
+        """fp32 scores - logQ, softmax terms and the CE-SUM loss
+        (two_tower_model.py:92,113-122, logq_correction.py:66-71)."""
         S = Q @ C.T
         if logq is not None:
             S -= logq[None, :]
@@ -361,10 +487,38 @@ class CpuTwoTower:
         z = e.sum(1, keepdims=True)
         B = S.shape[0]
         loss = float(np.sum(np.log(z[:, 0]) + m[:, 0] - S[np.arange(B), np.arange(B)]))
-        P = e / z
-        P[np.arange(B), np.arange(B)] -= 1.0
-        dQ = P @ C
-        dC = P.T @ Q
+        return S, m, e, z, loss
+
+    def loss_only(self, q_ids: List[np.ndarray], c_ids: List[np.ndarray], logq: Optional[np.ndarray]) -> float:
+        """The fp32 loss of a batch from this restatement's own forward (no update)."""
+        qa, ca = self.forward(q_ids, c_ids)
+        return self._scores_loss(qa[-1], ca[-1], logq)[-1]
+
+    def step(self, q_ids: List[np.ndarray], c_ids: List[np.ndarray], logq: Optional[np.ndarray],
+             acts=None) -> float:
+        """One train step.  acts: optional (query, candidate) activation lists
+        to use instead of this restatement's own forward (a caller holding
+        another implementation's forward — equal to this one within fp32
+        rounding — checks the rest of the step against the same ReLU masks: a
+        unit whose pre-activation rounds to the other side of 0 would otherwise
+        switch a whole row's gradient path)."""
+        if acts is None:
+            qa, ca = self.forward(q_ids, c_ids)
+        else:
+            qa, ca = [np.asarray(a, np.float32) for a in acts[0]], [np.asarray(a, np.float32) for a in acts[1]]
+        Q, C = qa[-1], ca[-1]
+        S, m, e, z, loss = self._scores_loss(Q, C, logq)
+        B = S.shape[0]
+        if self.inbatch == "bf16":
+            del S, e
+            r = inbatch_softmax_xent_bf16(Q, C, logq)
+            self.last_contract_loss = r["loss"]
+            dQ, dC = r["dq"], r["dc"]
+        else:
+            P = e / z
+            P[np.arange(B), np.arange(B)] -= 1.0
+            dQ = P @ C
+            dC = P.T @ Q
         gq, dxq = self._tower_bwd(qa, self.q_layers, dQ)
         gc, dxc = self._tower_bwd(ca, self.c_layers, dC)
         for layers, accs, grads in ((self.q_layers, self.ql_acc, gq), (self.c_layers, self.cl_acc, gc)):

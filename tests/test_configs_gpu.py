@@ -5,8 +5,9 @@ restatement (oracle/).
   headline: emb 128, towers [256] -> 128, batch 16384): three full train
   steps (gather, towers, fused in-batch CE, MLP backward, dense + sparse
   Adagrad), each vs oracle.CpuTwoTower started from the model's state
-  before the step: loss within 1e-3 rel, update of every table and MLP
-  buffer within 1e-2 rel;
+  before the step: loss within 1e-3 rel of the fp32 restatement, update of
+  every table and MLP buffer within 2e-3 rel of the restatement of the
+  kernels' arithmetic contract (bf16 in-batch negatives);
 - C4: 105,542 x 128 candidates, top-100 (and the reference runner's k = 1000
   at test_batch_size 2048, /root/reference/main.py:99,107): indices and
   scores bit-exact vs the fp32 fmaf-chain oracle;
@@ -28,10 +29,12 @@ from pkg.modelling.optimizer_factory import OptimizerFactory
 pytestmark = pytest.mark.gpu
 
 
-def _mirror(m):
+def _mirror(m, inbatch="bf16"):
     """oracle.CpuTwoTower holding the model's CURRENT weights and Adagrad
     accumulators; one table object per distinct feature name (main.py
-    declares product_type_name twice)."""
+    declares product_type_name twice).  inbatch="bf16": the in-batch
+    gradients by the kernels' arithmetic contract (include/tt.h K5-K7,
+    oracle.inbatch_softmax_xent_bf16); the loss it returns stays fp32."""
     opt = m.optimizer
     init = opt.initial_accumulator_value
 
@@ -52,7 +55,7 @@ def _mirror(m):
 
     qt, ct = tables(m.query_tower.input_layer), tables(m.candidate_tower.input_layer)
     ref = oracle.CpuTwoTower([t for t, _ in qt], [t for t, _ in ct], dense(m.query_tower), dense(m.candidate_tower),
-                             0.05)
+                             0.05, inbatch=inbatch)
     for pairs, accs in ((qt, ref.q_acc), (ct, ref.c_acc)):
         for i, (_, a) in enumerate(pairs):  # a shared table shares its accumulator
             accs[i] = a
@@ -67,20 +70,20 @@ def _mirror(m):
     return ref
 
 
-def _train_steps_vs_cpu(cuda, emb, joint, B, steps, loss_rtol, upd_rtol0, upd_rtol):
+def _train_steps_vs_cpu(cuda, emb, joint, B, steps, loss_rtol, upd_rtol):
     """`steps` full train steps of the main.py schema at (emb, joint, towers
     [256]) and batch B, each vs oracle.CpuTwoTower started from the model's
-    state before that step: the loss within loss_rtol and the update of every
-    table (touched rows) and MLP buffer within upd_rtol (relative 2-norm of
-    the update difference): upd_rtol0 at the first step (random init: the
-    bf16 in-batch operands move each update by ~2^-9 relative), upd_rtol
-    after it.  Adagrad's first step moves every touched parameter by ~lr =
-    0.05, so from the second step the in-batch scores are O(100) and the
-    softmax rows nearly one-hot: dS = P - I is then a small difference of
-    large terms and the bf16 rounding of the scores (~2^-8 |s|, tens of
-    percent of a row's off-diagonal mass) is amplified in the summed updates
-    while the loss stays within loss_rtol.  Returns the observed relative
-    errors."""
+    state before that step: the loss within loss_rtol of the fp32 (exact
+    arithmetic) restatement, and the update of every table (touched rows) and
+    MLP buffer within upd_rtol (relative 2-norm of the update difference) of
+    the restatement with the in-batch gradients computed by the kernels'
+    arithmetic contract (bf16 negative scores and weights, exact positive
+    pair: include/tt.h K5-K7, oracle.inbatch_softmax_xent_bf16).  Holding the
+    updates to the contract separates the precision choice from a bug: the
+    fp32 restatement differs from it by the bf16 rounding of the scores
+    themselves (from the second step Adagrad has made the scores O(100), and
+    2^-8 of that is a large change of the softmax).  Returns the observed
+    relative errors."""
     schema = bench.main_schema(emb_big=emb, joint=joint, hidden=(256,))
     data = bench.SyntheticHM(cuda, seed=7)
     schema.set_candidate_prob_lookup(data.prob_lookup())
@@ -109,10 +112,27 @@ def _train_steps_vs_cpu(cuda, emb, joint, B, steps, loss_rtol, upd_rtol0, upd_rt
                   for layer in (m.query_tower.input_layer, m.candidate_tower.input_layer)
                   for n in layer.embedding_layers}
         mlp_before = [t.dense.flat.detach().cpu().numpy().copy() for t in m.towers]
-        rl = ref.step([b[f.name].cpu().numpy() for f in qf], [b[f.name].cpu().numpy() for f in cf], lq)
+        ids = ([b[f.name].cpu().numpy() for f in qf], [b[f.name].cpu().numpy() for f in cf])
+        # the GPU's own tower activations (the kernels are deterministic: the
+        # step computes the same ones): the forward is checked against the
+        # restatement here, and the rest of the step then runs on the GPU's
+        # ReLU masks (a unit at ~0 may round to either side of it)
+        with torch.no_grad():
+            acts = [[a.cpu().numpy() for a in t.dense.forward_acts(
+                t.input_layer({f.name: b[f.name] for f in t.input_layer.categorical_features}), t.dense.flat)]
+                for t in m.towers]
+        own = ref.forward(*ids)
+        for ga, oa in zip(acts, own):
+            for li, (x, y) in enumerate(zip(ga, oa)):
+                e = np.linalg.norm(x - y) / max(np.linalg.norm(y), 1e-30)
+                errs[("fwd", li)] = max(errs.get(("fwd", li), 0.0), e)
+                assert e <= 1e-5, (step, li, e)  # bf16x3 tower GEMMs: fp32-faithful
+        del own
+        rl_own = ref.loss_only(*ids, lq)
+        rl = ref.step(*ids, lq, acts=acts)
         gl = float(m.train_step(b)["loss"].item())
-        errs[("loss", step)] = abs(gl - rl) / abs(rl)
-        assert abs(gl - rl) <= loss_rtol * abs(rl), (step, gl, rl)
+        errs[("loss", step)] = abs(gl - rl_own) / abs(rl_own)
+        assert abs(gl - rl_own) <= loss_rtol * abs(rl_own), (step, gl, rl_own)
         refs = {}
         for feats, tabs in ((qf, ref.q_tables), (cf, ref.c_tables)):
             for f, t in zip(feats, tabs):
@@ -130,21 +150,20 @@ def _train_steps_vs_cpu(cuda, emb, joint, B, steps, loss_rtol, upd_rtol0, upd_rt
             errs[(f"mlp{ti}", step)] = np.linalg.norm(d_gpu - d_ref) / np.linalg.norm(d_ref)
         del ref
     print({f"{k[0]}@{k[1]}": f"{v:.2e}" for k, v in errs.items()})
-    bad = {k: v for k, v in errs.items()
-           if not k[0].startswith("loss") and not v <= (upd_rtol0 if k[1] == 0 else upd_rtol)}
+    bad = {k: v for k, v in errs.items() if k[0] not in ("loss", "fwd") and not v <= upd_rtol}
     assert not bad, bad
     m.optimizer.check_status(cuda)
     return errs
 
 
 def test_c2_train_steps_match_cpu_restatement(cuda):
-    _train_steps_vs_cpu(cuda, 64, 64, 4096, 3, 1e-3, 5e-3, 5e-2)
+    _train_steps_vs_cpu(cuda, 64, 64, 4096, 3, 1e-3, 2e-3)
 
 
 def test_c3_train_steps_match_cpu_restatement(cuda):
     """configs[2], the headline train config: the main.py schema at D = E =
     128, H&M vocabularies, towers [256] -> 128, logQ, Adagrad, B = 16384."""
-    _train_steps_vs_cpu(cuda, 128, 128, 16384, 3, 1e-3, 5e-3, 5e-2)
+    _train_steps_vs_cpu(cuda, 128, 128, 16384, 3, 1e-3, 2e-3)
 
 
 def _c4_data(cuda, Q, seed=2):

@@ -37,20 +37,28 @@ def _oracle_ops(two_phase=False):
         ms, mi = oracle.topk_merge(s.numpy(), i.numpy(), k)
         return torch.from_numpy(np.ascontiguousarray(ms)), torch.from_numpy(np.ascontiguousarray(mi))
 
-    def shard_search(img, cand, q, k, off, reduce_max):
-        # the two-phase contract with the loosest legal screen: a lower bound on
+    def shard_search(img, cand, q, k, off, reduce_max, chunk):
+        # the two-phase contract with the loosest legal screen, per chunk of
+        # queries like tt_bruteforce_shard_screen/_finalize: a lower bound on
         # the shard's k-th score, max-reduced, then the exact top-k of the
         # entries scoring >= the floor, padded with (-inf, INT32_MAX)
         s, i, _ = oracle.bruteforce_topk(q.numpy(), cand.numpy(), k)
         kth = torch.from_numpy(s[:, k - 1] - np.abs(s[:, k - 1]) * 0.25 - 0.5)
-        reduce_max(kth)
+        for q0 in range(0, q.shape[0], chunk):
+            reduce_max(kth[q0:q0 + chunk])  # a view: reduced in place
         keep = s >= kth.numpy()[:, None]
         s = np.where(keep, s, -np.inf).astype(np.float32)
         i = np.where(keep, i + off, 0x7FFFFFFF).astype(np.int32)
         return torch.from_numpy(s), torch.from_numpy(i)
 
+    def shard_chunk(nq, sizes, dim, k):
+        # a recommendation that differs per shard size (like plan_search's),
+        # reduced over every shard: ranks that used their own would issue
+        # different numbers of all_reduce calls and gloo would fail
+        return min(3 + n % 5 for n in sizes)
+
     return IndexOps(build=lambda c: None, search=search, merge=merge,
-                    shard_search=shard_search if two_phase else None)
+                    shard_search=shard_search if two_phase else None, shard_chunk=shard_chunk)
 
 
 def _index_worker(rank, world, port, q, c, k, out):
@@ -65,12 +73,17 @@ def _index_worker(rank, world, port, q, c, k, out):
     # whose first shard has fewer rows than k (its list is padded)
     N = c.shape[0]
     ragged = [3] + [(N - 3) // (world - 1) + (1 if r < (N - 3) % (world - 1) else 0) for r in range(world - 1)]
-    for mode in ("even", "ragged"):
+    # ragged with every shard >= k (two-phase path) and shard sizes whose chunk
+    # recommendations differ: more than one query chunk, same on every rank
+    ragged_big = [k + 1] + [(N - k - 1) // (world - 1) + (1 if r < (N - k - 1) % (world - 1) else 0)
+                            for r in range(world - 1)]
+    for mode in ("even", "ragged", "ragged_big"):
         if mode == "even":
             b, e = shard_range(N, world, rank)
         else:
-            b = sum(ragged[:rank])
-            e = b + ragged[rank]
+            sz = ragged if mode == "ragged" else ragged_big
+            b = sum(sz[:rank])
+            e = b + sz[rank]
         idx = ShardedBruteForceIndex(k, None, torch.from_numpy(c[b:e].copy()), ops=_oracle_ops())
         s, i = idx.search(torch.from_numpy(q))
         blk, os_, oi = idx.search_owned(torch.from_numpy(q))
@@ -97,7 +110,7 @@ def test_sharded_index_equals_unsharded(world):
     out = mp.Manager().dict()
     mp.spawn(_index_worker, args=(world, _free_port(), q, c, k, out), nprocs=world, join=True)
     rs, ri, _ = oracle.bruteforce_topk(q, c, k)
-    for mode in ("even", "ragged"):
+    for mode in ("even", "ragged", "ragged_big"):
         covered, rows = [], []
         for r in range(world):
             s, i, n, (b, e), os_, oi, (r0, r1), held = out[(mode, r)]
@@ -114,67 +127,6 @@ def test_sharded_index_equals_unsharded(world):
     for r in range(world):
         qs_s, qs_i = out[("q", r)]  # query-sharded: every rank holds the full answer
         assert np.array_equal(qs_i, ri) and np.array_equal(qs_s, rs)
-
-
-class _Dense:
-    def __init__(self, g):
-        self.flat = torch.zeros(g.numel(), requires_grad=True)
-        self.flat.grad = g.clone()
-
-
-class _Layer:
-    def __init__(self, calls, grad):
-        self._last_calls = calls
-        self.last_grad = grad
-
-
-class _Tower:
-    def __init__(self, g, calls, grad):
-        self.dense = _Dense(g)
-        self.input_layer = _Layer(calls, grad)
-
-
-class _Model:
-    def __init__(self, towers):
-        self.towers = towers
-
-
-def _dp_worker(rank, world, port, out):
-    _init(rank, world, port)
-    from pkg.modelling.distributed import DataParallelTrainStep
-
-    B = 4
-    towers = []
-    for t in range(2):
-        g = torch.arange(5, dtype=torch.float32) * (rank + 1) + t
-        ids = [("a", torch.arange(B, dtype=torch.int32) + 10 * rank, 0),
-               ("p", torch.full((B,), 7 + rank, dtype=torch.int32), 3),
-               ("p", torch.full((B,), 100 + rank, dtype=torch.int32), 5)]
-        grad = torch.full((B, 6), float(rank + 10 * t))
-        towers.append(_Tower(g, ids, grad))
-    step = DataParallelTrainStep(_Model(towers))
-    step.allreduce_dense()
-    for tw in towers:
-        step.gather_sparse(tw.input_layer)
-    out[rank] = [(tw.dense.flat.grad.numpy().copy(), [(n, i.numpy().copy(), o) for n, i, o in tw.input_layer._last_calls],
-                  tw.input_layer.last_grad.numpy().copy()) for tw in towers]
-    dist.destroy_process_group()
-
-
-def test_dp_collectives_sum_dense_and_concat_sparse_rank_major():
-    world = 2
-    out = mp.Manager().dict()
-    mp.spawn(_dp_worker, args=(world, _free_port(), out), nprocs=world, join=True)
-    for r in range(world):
-        for t, (g, calls, grad) in enumerate(out[r]):
-            assert np.array_equal(g, np.arange(5) * 3 + 2 * t)  # (1 + 2) * arange + t + t
-            names = [c[0] for c in calls]
-            assert names == ["a", "p", "p"]
-            assert calls[0][1].tolist() == [0, 1, 2, 3, 10, 11, 12, 13]
-            assert calls[1][1].tolist() == [7] * 4 + [8] * 4
-            assert calls[2][1].tolist() == [100] * 4 + [101] * 4
-            assert [c[2] for c in calls] == [0, 3, 5]
-            assert grad.shape == (8, 6) and grad[0, 0] == 10 * t and grad[4, 0] == 1 + 10 * t
 
 
 # --------------------------------------------------------------------------- row-sharded tables (C5)
@@ -298,7 +250,7 @@ def _global_loss_worker(rank, world, port, q, c, logq, out):
         r = oracle.inbatch_softmax_xent(qq.numpy(), C.numpy(), None if L is None else L.numpy(), pos_offset)
         return torch.from_numpy(r["lse"]), torch.from_numpy(r["row_loss"]), torch.from_numpy(r["dq"])
 
-    def cols(Qa, lse, cl, L, pos_offset):  # all rows (with their lse) against the local columns
+    def cols(Qa, lse, cl, L, pos_offset, row_loss=None):  # all rows (with their lse) against the local columns
         S = Qa.numpy() @ cl.numpy().T - (0.0 if L is None else L.numpy()[None, :])
         P = np.exp(S - lse.numpy()[:, None])
         P[pos_offset + np.arange(cl.shape[0]), np.arange(cl.shape[0])] -= 1.0

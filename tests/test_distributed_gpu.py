@@ -166,7 +166,7 @@ def test_global_negatives_sharded_step_matches_full_batch(cuda, world):
         losses, flats, tables = out[r]
         np.testing.assert_allclose(losses, ref_losses, rtol=2e-5)
         for fl, t in zip(flats, ref.towers):
-            np.testing.assert_allclose(fl, t.dense.flat.detach().cpu().numpy(), rtol=1e-4, atol=2e-6)
+            np.testing.assert_allclose(fl, t.dense.flat.detach().cpu().numpy(), rtol=1e-4, atol=1e-5)
         for ti, t in enumerate(ref.towers):
             for name, e in t.input_layer.embedding_layers.items():
                 np.testing.assert_allclose(tables[(ti, name)], e.weight.cpu().numpy(), rtol=1e-4, atol=2e-6)
@@ -217,3 +217,109 @@ def test_integration_example(cuda):
         assert held == 500
         assert np.array_equal(i, ref_i.cpu().numpy()) and np.array_equal(s, ref_s.cpu().numpy())
         np.testing.assert_allclose(loss, ref_loss, rtol=2e-5)
+
+
+# --------------------------------------------------------------------------- C5 at its 8-way layout
+C5_ROWS, C5_DIM, C5_BATCH, C5_WORLD = 100_000_000, 128, 65536, 8
+_C5_SCALE = np.float32(0.05 / 32768)
+
+
+def _c5_values_np(rows: np.ndarray) -> np.ndarray:
+    """Initial value of global rows `rows` (int64): a hash of (row, column),
+    restated by _c5_fill on the GPU with the same fp32 operations."""
+    h = (rows.astype(np.int64)[:, None] * 2654435761 + np.arange(C5_DIM, dtype=np.int64)[None, :] * 97) % 65536
+    return (h - 32768).astype(np.float32) * _C5_SCALE
+
+
+def _c5_fill(shard: torch.Tensor, rank: int, world: int, chunk: int = 1 << 20) -> None:
+    k = torch.arange(C5_DIM, dtype=torch.int64, device=shard.device)[None, :] * 97
+    scale = torch.tensor(_C5_SCALE, device=shard.device)
+    for s in range(0, shard.shape[0], chunk):
+        n = min(chunk, shard.shape[0] - s)
+        g = (torch.arange(s, s + n, dtype=torch.int64, device=shard.device) * world + rank)[:, None]
+        shard[s:s + n] = ((g * 2654435761 + k) % 65536 - 32768).to(torch.float32) * scale
+
+
+def _c5_ids() -> np.ndarray:
+    rng = np.random.default_rng(3)
+    ids = (((rng.zipf(1.8, C5_BATCH) - 1) % C5_ROWS) * 7919 % C5_ROWS).astype(np.int32)  # Zipf-like, spread
+    ids[::7] = rng.integers(0, C5_ROWS, len(ids[::7]))  # plus uniform ids
+    return ids
+
+
+def _c5_grad(rank: int, b: int) -> np.ndarray:
+    return np.random.default_rng(100 + rank).standard_normal((b, C5_DIM)).astype(np.float32)
+
+
+def _c5_worker(rank, world, port, ids, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "hm-retrieval-two-tower_amd")]
+    from pkg.modelling.distributed import ShardedTables
+
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    n_local = len(range(rank, C5_ROWS, world))
+    shard = torch.empty(n_local, C5_DIM, device=dev)  # ONLY this rank's rows: 12.5M x 128 (6.4 GB)
+    _c5_fill(shard, rank, world)
+    st = ShardedTables({"big": shard, "__rows__": {"big": C5_ROWS}}, full_tables=False)
+    b = C5_BATCH // world
+    mine = ids[rank * b:(rank + 1) * b]
+    rows, (idx,) = st.fetch([("big", torch.as_tensor(mine, device=dev))])
+    got = rows[idx.long()].cpu().numpy()
+    fetch_ok = bool(np.array_equal(got, _c5_values_np(mine)))
+    st.apply([(torch.as_tensor(_c5_grad(rank, b), device=dev), [(idx, 0)])], 0.05, 1e-7)
+    torch.cuda.synchronize()
+    owned = np.unique(ids[ids % world == rank]).astype(np.int64)  # this rank's touched rows, global ids
+    loc = torch.as_tensor(owned // world, device=dev)
+    out[rank] = (fetch_ok, idx.cpu().numpy(), owned, st.shard["big"][loc].cpu().numpy(),
+                 st.acc["big"][loc].cpu().numpy(), int(st.shard["big"].shape[0]))
+    dist.destroy_process_group()
+
+
+def test_c5_row_sharded_table_eight_ranks(cuda):
+    """configs[4] at its stated layout: a 100M x 128 fp32 table row-sharded
+    over 8 ranks (eight processes on cuda:0, gloo; global row r on rank r % 8,
+    each rank building ONLY its 12.5M rows and their accumulator), a global
+    batch of 65,536 Zipf + uniform ids split over the ranks.
+      * fetched rows (all_to_all of requests and rows) bit-exact;
+      * one Adagrad apply bit-exact against the restatement of the sharded
+        order: each rank's per-request sums (oracle.dedup_sum: the GPU dedup's
+        block order, tt_sparse_scatter_sum), sent to the owners, the owner's
+        sparse Adagrad over the requests in source-rank order
+        (oracle.sparse_adagrad on the owner's touched rows, compacted in
+        order)."""
+    from oracle import oracle
+
+    ids = _c5_ids()
+    out = mp.Manager().dict()
+    mp.spawn(_c5_worker, args=(C5_WORLD, _free_port(), ids, out), nprocs=C5_WORLD, join=True)
+    W, b = C5_WORLD, C5_BATCH // C5_WORLD
+    recv = {o: ([], []) for o in range(W)}  # owner -> (global rows, gradient rows) in arrival order
+    for s in range(W):
+        fetch_ok, idx, *_ = out[s]
+        assert fetch_ok, s
+        mine = ids[s * b:(s + 1) * b].astype(np.int64)
+        uniq, sums = oracle.dedup_sum(idx, _c5_grad(s, b), oracle.GPU_DEDUP_CHUNK)  # per-request sums
+        req_row = np.empty(len(uniq), np.int64)
+        req_row[idx] = mine  # request j <- the global row of its lookups
+        assert np.array_equal(uniq, np.arange(len(uniq)))
+        for o in range(W):  # requests are bucketed by owner, in request order within a bucket
+            sel = np.nonzero(req_row % W == o)[0]
+            recv[o][0].append(req_row[sel])
+            recv[o][1].append(sums[sel])
+    for o in range(W):
+        _, _, owned, t_got, a_got, n_local = out[o]
+        assert n_local == len(range(o, C5_ROWS, W)) and n_local < C5_ROWS
+        rows = np.concatenate(recv[o][0])
+        grads = np.concatenate(recv[o][1])
+        assert np.array_equal(np.unique(rows), owned)
+        t_ref = _c5_values_np(owned)
+        a_ref = np.full_like(t_ref, 0.1)
+        oracle.sparse_adagrad(t_ref, a_ref, np.searchsorted(owned, rows).astype(np.int32), grads, 0.05)
+        assert np.array_equal(t_got, t_ref), o
+        assert np.array_equal(a_got, a_ref), o

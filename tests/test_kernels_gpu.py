@@ -207,6 +207,13 @@ def _rel(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
+# The kernels' arithmetic contract (include/tt.h K5-K7): dq / dc within 1e-3
+# of its restatement (oracle.inbatch_softmax_xent_bf16; the residual is fp32
+# summation order and rare last-bit differences of the exp arguments), and
+# within 1e-2 of fp64 (the bf16 rounding of the negatives' scores itself).
+CONTRACT_RTOL = 1e-3
+
+
 def _check_loss(q, c, ref, lse, row_loss, pos_offset=0):
     """Loss within 1e-3 rel (B >= 32) and lse / loss within the certified bound."""
     bound = oracle.inbatch_error_bound(q, c, pos_offset)
@@ -232,10 +239,16 @@ def test_inbatch_softmax_xent(cuda, B, E, use_logq, scale):
     tq, tc = _t(q, cuda), _t(c, cuda)
     tl = _t(logq, cuda) if use_logq else None
     lse, row_loss, dq = hip_ops.inbatch_rows(tq, tc, tl)
-    dc = hip_ops.inbatch_cols(tq, lse, tc, tl)
+    dc = hip_ops.inbatch_cols(tq, lse, tc, tl, row_loss=row_loss)
+    dc_nl = hip_ops.inbatch_cols(tq, lse, tc, tl)  # 1 - P_pos from lse (no row_loss)
     _check_loss(q, c, ref, lse, row_loss)
     assert _rel(dq.cpu().numpy(), ref["dq"]) <= 1e-2
     assert _rel(dc.cpu().numpy(), ref["dc"]) <= 1e-2
+    con = oracle.inbatch_softmax_xent_bf16(q, c, logq)
+    assert _rel(dq.cpu().numpy(), con["dq"]) <= CONTRACT_RTOL
+    assert _rel(dc.cpu().numpy(), con["dc"]) <= CONTRACT_RTOL
+    assert _rel(dc_nl.cpu().numpy(), con["dc"]) <= 1e-2
+    np.testing.assert_allclose(row_loss.cpu().numpy(), con["row_loss"], rtol=1e-4, atol=1e-5)
 
 
 @pytest.mark.parametrize("B,E,use_logq,scale", [(8192, 128, True, 0.3), (4100, 64, True, 0.7), (2500, 32, False, 0.6),
@@ -253,6 +266,10 @@ def test_inbatch_fused_entry(cuda, B, E, use_logq, scale):
     ref = oracle.inbatch_softmax_xent(q, c, logq)
     lse, row_loss, dq, dc = hip_ops.inbatch_fused(_t(q, cuda), _t(c, cuda), _t(logq, cuda) if use_logq else None)
     _check_loss(q, c, ref, lse, row_loss)
+    con = oracle.inbatch_softmax_xent_bf16(q, c, logq)
+    assert _rel(dq.cpu().numpy(), con["dq"]) <= CONTRACT_RTOL
+    assert _rel(dc.cpu().numpy(), con["dc"]) <= CONTRACT_RTOL
+    np.testing.assert_allclose(row_loss.cpu().numpy(), con["row_loss"], rtol=1e-4, atol=1e-5)
     if B < 32:  # per-example gradients of a handful of rows: bounded by the same score error
         return
     assert _rel(dq.cpu().numpy(), ref["dq"]) <= 1e-2
@@ -267,16 +284,25 @@ def test_inbatch_row_blocks_with_offset(cuda):
     c = np.maximum(rng.standard_normal((B, E)) * 0.4, 0).astype(np.float32)
     logq = np.log(rng.uniform(1e-5, 1e-2, B)).astype(np.float32)
     ref = oracle.inbatch_softmax_xent(q, c, logq)
+    con = oracle.inbatch_softmax_xent_bf16(q, c, logq)
     tq, tc, tl = _t(q, cuda), _t(c, cuda), _t(logq, cuda)
-    lse_full, _, _ = hip_ops.inbatch_rows(tq, tc, tl)
+    lse_full, rl_full, _ = hip_ops.inbatch_rows(tq, tc, tl)
     b = B // G
     for r in range(G):
-        lse, rl, dq = hip_ops.inbatch_rows(tq[r * b:(r + 1) * b], tc, tl, pos_offset=r * b)
-        dc = hip_ops.inbatch_cols(tq, lse_full, tc[r * b:(r + 1) * b], tl[r * b:(r + 1) * b], pos_offset=r * b)
-        sub = {"lse": ref["lse"][r * b:(r + 1) * b], "row_loss": ref["row_loss"][r * b:(r + 1) * b]}
-        _check_loss(q[r * b:(r + 1) * b], c, sub, lse, rl, pos_offset=r * b)
-        assert _rel(dq.cpu().numpy(), ref["dq"][r * b:(r + 1) * b]) <= 1e-2
-        assert _rel(dc.cpu().numpy(), ref["dc"][r * b:(r + 1) * b]) <= 1e-2
+        sl = slice(r * b, (r + 1) * b)
+        lse, rl, dq = hip_ops.inbatch_rows(tq[sl], tc, tl, pos_offset=r * b)
+        dc = hip_ops.inbatch_cols(tq, lse_full, tc[sl], tl[sl], pos_offset=r * b, row_loss=rl_full)
+        sub = {"lse": ref["lse"][sl], "row_loss": ref["row_loss"][sl]}
+        _check_loss(q[sl], c, sub, lse, rl, pos_offset=r * b)
+        assert _rel(dq.cpu().numpy(), ref["dq"][sl]) <= 1e-2
+        assert _rel(dc.cpu().numpy(), ref["dc"][sl]) <= 1e-2
+        # the contract, with the column pass restated on the local block
+        con_r = oracle.inbatch_softmax_xent_bf16(q[sl], c, logq, pos_offset=r * b)
+        assert _rel(dq.cpu().numpy(), con_r["dq"]) <= CONTRACT_RTOL
+        assert _rel(dq.cpu().numpy(), con["dq"][sl]) <= CONTRACT_RTOL
+        dc_con = oracle.inbatch_cols_bf16(q, con["lse"], con["row_loss"], c[sl], logq[sl], pos_offset=r * b)
+        assert _rel(dc.cpu().numpy(), dc_con) <= CONTRACT_RTOL
+        assert _rel(dc.cpu().numpy(), con["dc"][sl]) <= CONTRACT_RTOL
 
 
 # --------------------------------------------------------------------------- brute force

@@ -97,7 +97,7 @@ def _batch(cuda, rng, B, zipf=True):
     return {"cust": z(301), "post": z(51), "art": z(301), "ptn": z(21)}
 
 
-def _cpu_mirror(m):
+def _cpu_mirror(m, inbatch="fp32"):
     def tables(layer):
         return [layer.embedding_layers[f.name].weight.cpu().numpy().copy() for f in layer.categorical_features]
 
@@ -105,7 +105,7 @@ def _cpu_mirror(m):
         return [(w.detach().cpu().numpy(), b.detach().cpu().numpy()) for w, b in t.dense.params()]
 
     ref = oracle.CpuTwoTower(tables(m.query_tower.input_layer), tables(m.candidate_tower.input_layer),
-                             dense(m.query_tower), dense(m.candidate_tower), 0.05)
+                             dense(m.query_tower), dense(m.candidate_tower), 0.05, inbatch=inbatch)
     # the duplicated name shares ONE table: alias the objects so both lookups update it
     ref.c_tables[2] = ref.c_tables[1]
     ref.c_acc[2] = ref.c_acc[1]
@@ -143,21 +143,30 @@ def test_train_steps_match_cpu_restatement(cuda, zipf):
         return {"art": ref.c_tables[0], "ptn": ref.c_tables[1], "cust": ref.q_tables[0], "post": ref.q_tables[1],
                 "qmlp": flat(ref.q_layers), "cmlp": flat(ref.c_layers)}
 
+    con = _cpu_mirror(m, inbatch="bf16")  # the kernels' arithmetic contract
     before = snapshot()
     for step in range(3):
         b = _batch(cuda, rng, 512, zipf)
         lq = m.candidate_logq(b).cpu().numpy()
-        rl = ref.step([b["cust"].cpu().numpy(), b["post"].cpu().numpy()],
-                      [b["art"].cpu().numpy(), b["ptn"].cpu().numpy(), b["ptn"].cpu().numpy()], lq)
+        ids = ([b["cust"].cpu().numpy(), b["post"].cpu().numpy()],
+               [b["art"].cpu().numpy(), b["ptn"].cpu().numpy(), b["ptn"].cpu().numpy()])
+        rl = ref.step(*ids, lq)
+        if step == 0:
+            con.step(*ids, lq)
         gl = float(m.train_step(b)["loss"].item())
         assert abs(gl - rl) <= 1e-3 * abs(rl), (step, gl, rl)
         if step == 0:
             after, r = snapshot(), ref_snapshot()
+            rc = {"art": con.c_tables[0], "ptn": con.c_tables[1], "cust": con.q_tables[0], "post": con.q_tables[1],
+                  "qmlp": np.concatenate([np.concatenate([w.reshape(-1), bb]) for w, bb in con.q_layers]),
+                  "cmlp": np.concatenate([np.concatenate([w.reshape(-1), bb]) for w, bb in con.c_layers])}
             for k in after:  # includes the shared ptn table (one combined update of both lookups)
-                d_gpu, d_ref = after[k] - before[k], r[k] - before[k]
+                d_gpu, d_ref, d_con = after[k] - before[k], r[k] - before[k], rc[k] - before[k]
                 err = np.linalg.norm(d_gpu - d_ref) / np.linalg.norm(d_ref)
-                print(f"first-step update {k}: rel err {err:.2e}")
+                err_c = np.linalg.norm(d_gpu - d_con) / np.linalg.norm(d_con)
+                print(f"first-step update {k}: rel err {err:.2e} (fp32), {err_c:.2e} (contract)")
                 assert err <= (1e-2 if k.endswith("mlp") else 3e-3), (k, err)
+                assert err_c <= 2e-3, (k, err_c)
 
 
 @pytest.mark.parametrize("B", [1, 2, 37, 1000])
@@ -426,12 +435,15 @@ def test_sharded_train_step_world1_matches_single_gpu(cuda):
         dist.destroy_process_group()
 
 
-def test_global_negatives_step_captures_rccl_collectives(cuda, monkeypatch):
+@pytest.mark.parametrize("B", [256, 4096])
+def test_global_negatives_step_captures_rccl_collectives(cuda, monkeypatch, B):
     """ShardedTrainStep's global-negatives middle with its collectives as real
     RCCL calls (a one-rank process group with BatchComm(always=True), so the
     all_gathers / reduce_scatters run even at world 1) captured into the
     step's hipGraph — the default over RCCL — trains bit-identically to the
-    same step run eagerly (TT_SHARDED_EAGER=1), step for step."""
+    same step run eagerly (TT_SHARDED_EAGER=1), step for step.  At 4096 rows
+    per rank (losses.GLOBAL_TOWER_STREAMS) the towers' two-stream fork/join is
+    captured together with the collectives."""
     import socket
 
     import torch.distributed as dist
@@ -450,8 +462,11 @@ def test_global_negatives_step_captures_rccl_collectives(cuda, monkeypatch):
         eager = ShardedTrainStep(b, shard_min_rows=300, global_negatives=True, comm=BatchComm(always=True))
         monkeypatch.delenv("TT_SHARDED_EAGER")
         assert graphed.use_graph and not eager.use_graph
+        from pkg.modelling import losses
+
+        assert (B >= losses.GLOBAL_TOWER_STREAMS) == (B == 4096)
         rng = np.random.default_rng(9)
-        batches = [_batch(cuda, rng, 256) for _ in range(5)]
+        batches = [_batch(cuda, rng, B) for _ in range(5)]
         for i, batch in enumerate(batches):  # call 1 eager, then graph replays
             la, lb = graphed(batch)["loss"], eager(batch)["loss"]
             assert torch.equal(la, lb), i
@@ -463,5 +478,50 @@ def test_global_negatives_step_captures_rccl_collectives(cuda, monkeypatch):
                 ga = graphed.tables.gather_full(mine._shard_key) if hasattr(mine, "_shard_key") else mine.weight
                 gb = eager.tables.gather_full(t._shard_key) if hasattr(t, "_shard_key") else t.weight
                 assert torch.equal(ga, gb), name
+        graphed.check_status()
+        eager.check_status()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_step_status_reports_stale_owner_keys(cuda):
+    """ShardedTrainStep.check_status reads the workspaces the sharded step's
+    sparse kernels write ("sparse_owner": the owners' Adagrad apply,
+    "sparse_mid": the per-request sums): a presorted owner apply that finds
+    another call's sorted keys there applies nothing and check_status raises
+    (the reference's legacy apply raises too, optimizer_factory.py:15-18);
+    the check clears it, so a second check is quiet."""
+    import socket
+
+    import torch.distributed as dist
+    from pkg._native import TTError
+    from pkg.modelling.distributed import ShardedTrainStep
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        m = _small_model(cuda, seed=6)
+        step = ShardedTrainStep(m, shard_min_rows=300, global_negatives=True)
+        rng = np.random.default_rng(4)
+        for _ in range(2):
+            step(_batch(cuda, rng, 256))
+        step.check_status()  # a clean run: nothing recorded
+        name = step.tables.names[0]
+        t, acc = step.tables.shard[name], step.tables.acc[name]
+        B, D = 128, t.shape[1]
+        ids_a = torch.as_tensor(rng.integers(0, t.shape[0], B).astype(np.int32), device=cuda)
+        ids_b = torch.as_tensor(rng.integers(0, t.shape[0], B).astype(np.int32), device=cuda)
+        g = torch.ones(B, D, dtype=torch.float32, device=cuda)
+        spec = lambda ids: [dict(table=t, slot0=acc, ids=[ids], grad_col_offset=[0], grad=g)]
+        before = t.clone()
+        hip_ops.sparse_sort(spec(ids_a), B, ws_tag="sparse_owner")
+        hip_ops.sparse_adagrad(spec(ids_b), B, None, 0.05, 1e-7, presorted=True, ws_tag="sparse_owner")
+        with pytest.raises(TTError, match="another call"):
+            step.check_status()
+        assert torch.equal(t, before)
+        step.check_status()
     finally:
         dist.destroy_process_group()

@@ -136,3 +136,42 @@ def test_vocab_value_counts_order():
     v = oracle.vocab_from_values(["b", "a", "b", "c", "a", "b"], max_vocab_size=2)
     assert v.tolist() == ["b", "a"]
     assert oracle.string_lookup(v, ["a", "zzz", "b"]).tolist() == [2, 0, 1]
+
+
+def test_bf16_round_is_round_to_nearest_even():
+    """oracle.bf16_round == torch's fp32 -> bfloat16 conversion (RNE), incl.
+    ties, infinities and values near the top of the range."""
+    import torch
+
+    rng = np.random.default_rng(0)
+    x = np.concatenate([rng.standard_normal(10000).astype(np.float32) * 10.0 ** rng.integers(-30, 30, 10000),
+                        np.array([1.0 + 2.0 ** -8, 1.0 + 3 * 2.0 ** -8, -(1.0 + 2.0 ** -8), np.inf, -np.inf, 0.0,
+                                  3.0e38], np.float32)]).astype(np.float32)
+    ref = torch.from_numpy(x).to(torch.bfloat16).float().numpy()
+    assert np.array_equal(oracle.bf16_round(x), ref)
+
+
+def test_inbatch_contract_oracle_properties():
+    """The kernels' arithmetic contract restated (oracle.inbatch_softmax_xent_bf16):
+    close to the fp64 loss/gradients (bf16 negatives only); row blocks with a
+    positive offset give the same rows as the full batch; a one-column batch
+    has loss 0 and zero gradients (P_pos = 1 exactly)."""
+    rng = np.random.default_rng(3)
+    B, E = 96, 32
+    q = np.maximum(rng.standard_normal((B, E)) * 0.5, 0).astype(np.float32)
+    c = np.maximum(rng.standard_normal((B, E)) * 0.5, 0).astype(np.float32)
+    lq = np.log(rng.uniform(1e-5, 1e-2, B)).astype(np.float32)
+    ref = oracle.inbatch_softmax_xent(q, c, lq)
+    con = oracle.inbatch_softmax_xent_bf16(q, c, lq)
+    rel = lambda a, b: np.linalg.norm(a - b) / np.linalg.norm(b)
+    assert abs(con["loss"] - ref["loss"]) <= 1e-3 * abs(ref["loss"])
+    assert rel(con["dq"], ref["dq"]) <= 1e-2 and rel(con["dc"], ref["dc"]) <= 1e-2
+    G, b = 4, B // 4
+    for r in range(G):
+        sl = slice(r * b, (r + 1) * b)
+        blk = oracle.inbatch_softmax_xent_bf16(q[sl], c, lq, pos_offset=r * b)
+        assert np.array_equal(blk["dq"], con["dq"][sl]) and np.array_equal(blk["row_loss"], con["row_loss"][sl])
+        dc = oracle.inbatch_cols_bf16(q, con["lse"], con["row_loss"], c[sl], lq[sl], pos_offset=r * b)
+        np.testing.assert_allclose(dc, con["dc"][sl], rtol=1e-6, atol=1e-7)
+    one = oracle.inbatch_softmax_xent_bf16(q[:1], c[:1], lq[:1])
+    assert one["loss"] == 0.0 and not one["dq"].any() and not one["dc"].any()
