@@ -102,6 +102,10 @@ class Adagrad(_Optimizer):
             with torch.cuda.stream(side), hip_ops.Workspace.scope(scope):
                 specs, batch = self._sparse_specs([tower], with_grad=False)  # new accumulators filled on `side`
                 if not specs or len(specs) > 16 or not batch:
+                    # not presorted: apply_tower sorts on the current stream,
+                    # which must first see the accumulators filled on `side`
+                    if specs:
+                        cur.wait_stream(side)
                     continue
                 hip_ops.sparse_sort(specs, batch)
                 key = hip_ops.Workspace._scope  # the apply must find its sorted keys in this scope's buffer
@@ -161,6 +165,8 @@ class Adagrad(_Optimizer):
             # anything ordered after the sort
             specs, batch = self._sparse_specs(towers, with_grad=False)
             if not specs or len(specs) > 16 or not batch:
+                if specs:  # the apply sorts on `cur`: order it after the accumulator fills
+                    cur.wait_stream(side)
                 return
             hip_ops.sparse_sort(specs, batch)
         done = torch.cuda.Event()
