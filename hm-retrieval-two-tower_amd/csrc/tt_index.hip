@@ -48,6 +48,7 @@
 //  Zero queries score exactly +0 against every candidate in both paths; their
 //  answer (indices 0..k-1 by the tie rule) is written directly.
 #include <cmath>
+#include <cstdlib>
 
 #include "tt_common.h"
 
@@ -793,122 +794,200 @@ __device__ __forceinline__ const uint2* seg_ptr(const Lists& L, int64_t q, int j
   return L.cap ? L.buf + (q * L.nseg + j) * static_cast<int64_t>(L.cap) : L.buf + L.off[q * L.cq + j * L.cj];
 }
 
-// Radix select with 8-bit digits and an LDS histogram (one wave) over keys
-// produced by `key_at(j)` for j < n (all lanes call with the same n).  After
+// Group primitives.  A "group" is the NW waves (NW * 64 threads) that work on
+// one query together: NW = 1 is one wave of a workgroup (the helpers are
+// wave-local then, so several waves of one workgroup may run them on their own
+// LDS regions: the fallback), NW > 1 is the whole workgroup.
+template <int NW>
+__device__ __forceinline__ void gsync() {
+  if constexpr (NW == 1) wsync();
+  else __syncthreads();
+}
+template <int NW>
+__device__ __forceinline__ int gtid() {
+  if constexpr (NW == 1) return lane_id();
+  else return static_cast<int>(threadIdx.x);
+}
+// Group-wide stream compaction of one chunk of NW * 64 items: returns the
+// output slot of this thread's item (meaningful when keep) and advances n by
+// the chunk's kept count (uniform over the group).  wcnt: 2 * NW ints of LDS
+// (double-buffered by chunk parity `par`).  For NW > 1 it contains a barrier,
+// so every thread of the group must call it; for NW = 1 the caller orders its
+// LDS reads before its writes (wsync).
+template <int NW>
+__device__ __forceinline__ int compact_slot(bool keep, int& n, int* wcnt, int& par) {
+  const uint64_t m = __ballot(keep);
+  const int before = __popcll(m & lanemask_lt64());
+  if constexpr (NW == 1) {
+    const int p = n + before;
+    n += __popcll(m);
+    return p;
+  } else {
+    int* wc = wcnt + (par & 1) * NW;
+    ++par;
+    const int wave = static_cast<int>(threadIdx.x) / kWave;
+    if (lane_id() == 0) wc[wave] = __popcll(m);
+    __syncthreads();
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const int c = wc[w];
+      off += w < wave ? c : 0;
+      tot += c;
+    }
+    const int p = n + off + before;
+    n += tot;
+    return p;
+  }
+}
+
+// Radix select with 8-bit digits and an LDS histogram over keys the group
+// adds with `fill(prefix, hi_mask, shift)` (LDS atomics, any thread).  After
 // `passes` digits, `prefix` holds the top 8*passes bits of the K-th largest
 // key, `above` = #keys whose top bits are greater, `at` = #keys sharing the
-// prefix (above < K <= above + at).
+// prefix (above < K <= above + at); at = -1: fewer than K keys.  The bin
+// search runs on the group's first wave; bc: 4 words of LDS (NW > 1).
 struct Kth {
   unsigned prefix;
   int above;
   int at;
 };
 
-template <class Hist>
-__device__ Kth radix_select(Hist&& fill, int K, int passes, unsigned* hist) {
+template <int NW = 1, class Hist>
+__device__ Kth radix_select(Hist&& fill, int K, int passes, unsigned* hist, unsigned* bc = nullptr) {
   const int lane = lane_id();
+  const int t = gtid<NW>();
+  const bool w0 = NW == 1 || t < kWave;
   unsigned prefix = 0;
   int above = 0, at = 0;
   for (int d = 0; d < passes; ++d) {
     const int shift = 24 - 8 * d;
     const unsigned hi_mask = d == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
-#pragma unroll
-    for (int u = 0; u < 4; ++u) hist[4 * lane + u] = 0;
-    wsync();
+    for (int u = t; u < 256; u += NW * kWave) hist[u] = 0;
+    gsync<NW>();
     fill(prefix, hi_mask, shift);
-    wsync();
-    // counts at or above each bin: lane L owns bins 4L..4L+3
-    unsigned h4[4];
+    gsync<NW>();
+    bool none = false;
+    if (w0) {
+      // counts at or above each bin: lane L owns bins 4L..4L+3
+      unsigned h4[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) h4[u] = hist[4 * lane + u];
-    const unsigned mine = h4[0] + h4[1] + h4[2] + h4[3];
-    unsigned suffix = mine;  // inclusive suffix sum over lanes >= L
+      for (int u = 0; u < 4; ++u) h4[u] = hist[4 * lane + u];
+      const unsigned mine = h4[0] + h4[1] + h4[2] + h4[3];
+      unsigned suffix = mine;  // inclusive suffix sum over lanes >= L
 #pragma unroll
-    for (int off = 1; off < kWave; off <<= 1) {
-      const unsigned o = __shfl_down(suffix, off, kWave);
-      if (lane + off < kWave) suffix += o;
+      for (int off = 1; off < kWave; off <<= 1) {
+        const unsigned o = __shfl_down(suffix, off, kWave);
+        if (lane + off < kWave) suffix += o;
+      }
+      unsigned cum[4];  // keys in bins >= 4L+u (within the prefix)
+      cum[3] = suffix - mine + h4[3];
+      cum[2] = cum[3] + h4[2];
+      cum[1] = cum[2] + h4[1];
+      cum[0] = cum[1] + h4[0];
+      const int need = K - above;
+      int best = -1;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (static_cast<int>(cum[u]) >= need) best = 4 * lane + u;
+      const uint64_t m = __ballot(best >= 0);
+      if (m == 0) {  // fewer than K keys
+        none = true;
+      } else {
+        const int src = 63 - __clzll(m);
+        const int b = __shfl(best, src, kWave);
+        const int u = b & 3;
+        const unsigned cb = __shfl(cum[0], src, kWave), cb1 = __shfl(cum[1], src, kWave),
+                       cb2 = __shfl(cum[2], src, kWave), cb3 = __shfl(cum[3], src, kWave);
+        const unsigned cumb = u == 0 ? cb : u == 1 ? cb1 : u == 2 ? cb2 : cb3;
+        const unsigned hb = hist[b];
+        above += static_cast<int>(cumb - hb);
+        at = static_cast<int>(hb);
+        prefix |= static_cast<unsigned>(b) << shift;
+      }
+      if (NW > 1 && lane == 0) {
+        bc[0] = prefix;
+        bc[1] = static_cast<unsigned>(above);
+        bc[2] = static_cast<unsigned>(at);
+        bc[3] = none ? 1u : 0u;
+      }
     }
-    unsigned cum[4];  // keys in bins >= 4L+u (within the prefix)
-    cum[3] = suffix - mine + h4[3];
-    cum[2] = cum[3] + h4[2];
-    cum[1] = cum[2] + h4[1];
-    cum[0] = cum[1] + h4[0];
-    const int need = K - above;
-    int best = -1;
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (static_cast<int>(cum[u]) >= need) best = 4 * lane + u;
-    const uint64_t m = __ballot(best >= 0);
-    if (m == 0) {  // fewer than K keys
-      wsync();
-      return Kth{0u, 0, -1};
+    gsync<NW>();
+    if constexpr (NW > 1) {
+      prefix = bc[0];
+      above = static_cast<int>(bc[1]);
+      at = static_cast<int>(bc[2]);
+      none = bc[3] != 0;
+      __syncthreads();  // bc read by all before the next pass's first wave rewrites it
     }
-    const int src = 63 - __clzll(m);
-    const int b = __shfl(best, src, kWave);
-    const int u = b & 3;
-    const unsigned cb = __shfl(cum[0], src, kWave), cb1 = __shfl(cum[1], src, kWave),
-                   cb2 = __shfl(cum[2], src, kWave), cb3 = __shfl(cum[3], src, kWave);
-    const unsigned cumb = u == 0 ? cb : u == 1 ? cb1 : u == 2 ? cb2 : cb3;
-    const unsigned hb = hist[b];
-    above += static_cast<int>(cumb - hb);
-    at = static_cast<int>(hb);
-    prefix |= static_cast<unsigned>(b) << shift;
-    wsync();
+    if (none) return Kth{0u, 0, -1};
   }
   return Kth{prefix, above, at};
 }
 
 // Exact selection in LDS: keeps exactly the K best entries by (score desc,
 // index asc); *thr = the K-th score (later candidates of an in-order scan need
-// a strictly larger score).
-__device__ int exact_select(float* sc, unsigned* id, int n, int K, float* thr, unsigned* hist) {
+// a strictly larger score).  aux (NW > 1): 2 * NW + 4 words of LDS.
+template <int NW = 1>
+__device__ int exact_select(float* sc, unsigned* id, int n, int K, float* thr, unsigned* hist,
+                            unsigned* aux = nullptr) {
   if (n <= K) {
     *thr = -INFINITY;
     return n;
   }
-  const Kth r = radix_select(
+  const int t = gtid<NW>();
+  constexpr int NT = NW * kWave;
+  const Kth r = radix_select<NW>(
       [&](unsigned prefix, unsigned hi_mask, int shift) {
-        for (int j = lane_id(); j < n; j += kWave) {
+        for (int j = t; j < n; j += NT) {
           const unsigned key = float_order_key(sc[j]);
           if ((key & hi_mask) == prefix) atomicAdd(&hist[(key >> shift) & 0xFFu], 1u);
         }
       },
-      K, 4, hist);
+      K, 4, hist, aux);
   const unsigned res = r.prefix;  // exact key of the K-th score
   const int need = K - r.above;   // ties at the K-th score to keep, lowest indices first
   unsigned cut = 0xFFFFFFFFu;
   if (need < r.at) {
     // need-th smallest index among the ties: largest v with #(idx < v) < need
-    unsigned v = 0;
+    // (the group's first wave; rare)
+    if (NW == 1 || t < kWave) {
+      unsigned v = 0;
 #pragma unroll 1
-    for (int bit = 31; bit >= 0; --bit) {
-      const unsigned c = v | (1u << bit);
-      int lt = 0;
-      for (int j0 = 0; j0 < n; j0 += kWave) {
-        const int j = j0 + lane_id();
-        lt += __popcll(__ballot(j < n && float_order_key(sc[j]) == res && id[j] < c));
+      for (int bit = 31; bit >= 0; --bit) {
+        const unsigned c = v | (1u << bit);
+        int lt = 0;
+        for (int j0 = 0; j0 < n; j0 += kWave) {
+          const int j = j0 + lane_id();
+          lt += __popcll(__ballot(j < n && float_order_key(sc[j]) == res && id[j] < c));
+        }
+        if (lt < need) v = c;
       }
-      if (lt < need) v = c;
+      cut = v;
+      if (NW > 1 && t == 0) aux[0] = v;
     }
-    cut = v;
+    if constexpr (NW > 1) {
+      __syncthreads();
+      cut = aux[0];
+      __syncthreads();
+    }
   }
-  int out = 0;
-  for (int j0 = 0; j0 < n; j0 += kWave) {
-    const int j = j0 + lane_id();
+  int out = 0, par = 0;
+  int* wcnt = reinterpret_cast<int*>(aux) + 4;
+  for (int j0 = 0; j0 < n; j0 += NT) {
+    const int j = j0 + t;
     const float s = j < n ? sc[j] : 0.0f;
     const unsigned i = j < n ? id[j] : 0u;
     const unsigned key = float_order_key(s);
     const bool keep = j < n && (key > res || (key == res && i <= cut));
-    const uint64_t m = __ballot(keep);
-    wsync();
-    if (keep) {
-      const int p = out + __popcll(m & lanemask_lt64());
+    const int p = compact_slot<NW>(keep, out, wcnt, par);
+    if constexpr (NW == 1) wsync();
+    if (keep) {  // p <= j: a chunk's writes never reach entries not yet read
       sc[p] = s;
       id[p] = i;
     }
-    out += __popcll(m);
   }
-  wsync();
+  gsync<NW>();
   *thr = order_key_float(res);
   return out;
 }
@@ -917,30 +996,33 @@ __device__ int exact_select(float* sc, unsigned* id, int n, int K, float* thr, u
 // Sort sizes up to kAliasP build their keys in registers, so the key array
 // may alias the (score, index) arrays it is built from (the finalize's LDS).
 constexpr int kAliasP = 1024;
+template <int NW = 1>
 __device__ void rank_and_write(const float* sc, const unsigned* id, int n, int k, int P, unsigned long long* sk,
                                float* out_s, int32_t* out_i) {
-  const int lane = lane_id();
+  const int t = gtid<NW>();
+  constexpr int NT = NW * kWave;
   if (P <= kAliasP) {
     // keys built in registers first: sk may alias sc / id
-    unsigned long long kv[kAliasP / kWave];
+    constexpr int PER = (kAliasP + NT - 1) / NT;
+    unsigned long long kv[PER];
 #pragma unroll
-    for (int u = 0; u < kAliasP / kWave; ++u) {
-      const int j = lane + kWave * u;
+    for (int u = 0; u < PER; ++u) {
+      const int j = t + NT * u;
       kv[u] = j < n ? make_key(sc[j], id[j]) : 0ull;
     }
-    wsync();
+    gsync<NW>();
 #pragma unroll
-    for (int u = 0; u < kAliasP / kWave; ++u) {
-      const int j = lane + kWave * u;
+    for (int u = 0; u < PER; ++u) {
+      const int j = t + NT * u;
       if (j < P) sk[j] = kv[u];
     }
   } else {
-    for (int j = lane; j < P; j += kWave) sk[j] = j < n ? make_key(sc[j], id[j]) : 0ull;
+    for (int j = t; j < P; j += NT) sk[j] = j < n ? make_key(sc[j], id[j]) : 0ull;
   }
   for (int size = 2; size <= P; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      wsync();
-      for (int i = lane; i < P / 2; i += kWave) {
+      gsync<NW>();
+      for (int i = t; i < P / 2; i += NT) {
         const int lo = 2 * i - (i & (stride - 1));
         const int hi = lo + stride;
         const bool desc = (lo & size) == 0;
@@ -952,11 +1034,11 @@ __device__ void rank_and_write(const float* sc, const unsigned* id, int n, int k
       }
     }
   }
-  wsync();
-  for (int t = lane; t < k; t += kWave) {
-    const unsigned long long key = sk[t];
-    out_s[t] = order_key_float(static_cast<unsigned>(key >> 32));
-    out_i[t] = static_cast<int32_t>(0xFFFFFFFFu - static_cast<unsigned>(key));
+  gsync<NW>();
+  for (int j = t; j < k; j += NT) {
+    const unsigned long long key = sk[j];
+    out_s[j] = order_key_float(static_cast<unsigned>(key >> 32));
+    out_i[j] = static_cast<int32_t>(0xFFFFFFFFu - static_cast<unsigned>(key));
   }
 }
 
@@ -986,12 +1068,20 @@ struct FinalArgs {
   const float* floor;   // rescore pass: per query lower bound on the GLOBAL k-th exact score
 };
 
-__host__ __device__ inline size_t final_lds_bytes(int L, int P) {
+// LDS of one finalize group: query row, (score, id) list of L, the ranking
+// keys when they cannot alias the list, 256 radix bins, 2 NW + 4 aux words
+__host__ __device__ inline size_t final_lds_bytes(int L, int P, int NW = 1) {
   return 128 * sizeof(float) + static_cast<size_t>(L) * 8 + (P <= kAliasP ? 0 : static_cast<size_t>(P) * 8) +
-         256 * sizeof(unsigned);
+         256 * sizeof(unsigned) + static_cast<size_t>(2 * NW + 4) * sizeof(unsigned);
 }
 
-__global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
+// One query per group of NW waves (the workgroup).  NW > 1 splits every
+// phase's loops over the waves (large k: long lists, many survivors, a
+// P-element sort), so a query's latency chain shrinks while its list stays
+// in LDS.
+template <int NW>
+__global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a) {
+  constexpr int NT = NW * kWave;
   extern __shared__ __attribute__((aligned(16))) char fsm[];
   float* qs = reinterpret_cast<float*>(fsm);  // query row (dim <= 128)
   float* sc = qs + 128;
@@ -1001,8 +1091,10 @@ __global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
   unsigned long long* sk = alias ? reinterpret_cast<unsigned long long*>(sc)
                                  : reinterpret_cast<unsigned long long*>(id + a.L);
   unsigned* hist = alias ? id + a.L : reinterpret_cast<unsigned*>(sk + a.P);  // 256 radix bins
+  unsigned* aux = hist + 256;                                                // 2 NW + 4 words
+  int* wcnt = reinterpret_cast<int*>(aux) + 4;
   const int64_t q = blockIdx.x;
-  const int lane = lane_id();
+  const int t = gtid<NW>();
   const int K = a.k;
   const Lists& Ls = a.lists;
 #ifdef TT_INDEX_NOINSERT
@@ -1013,12 +1105,12 @@ __global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
   const int fl = a.qflags[q];
   if (fl & kQZero) {  // every score is exactly +0: indices 0..k-1 by the tie rule
     if (a.kth_lb) {
-      if (lane == 0) a.kth_lb[q] = 0.0f;
+      if (t == 0) a.kth_lb[q] = 0.0f;
       return;
     }
-    for (int t = lane; t < K; t += kWave) {
-      out_s[t] = 0.0f;
-      out_i[t] = static_cast<int32_t>(a.zero_base + t);
+    for (int j = t; j < K; j += NT) {
+      out_s[j] = 0.0f;
+      out_i[j] = static_cast<int32_t>(a.zero_base + j);
     }
     return;
   }
@@ -1043,21 +1135,21 @@ __global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
     for (int j = 0; j < Ls.nseg; ++j) {
       const int c = seg_count(Ls, q, j);
       const uint2* e = seg_ptr(Ls, q, j);
-      for (int i = lane; i < c; i += kWave) {
+      for (int i = t; i < c; i += NT) {
         const uint2 en = e[i];
         sc[n0 + i] = __uint_as_float(en.x);
         id[n0 + i] = en.y;
       }
       n0 += c;
     }
-    wsync();
+    gsync<NW>();
   }
   if (!fail) {
     // K-th largest screened score to a 24-bit key prefix (rounded down)
-    const Kth r = radix_select(
+    const Kth r = radix_select<NW>(
         [&](unsigned prefix, unsigned hi_mask, int shift) {
           if (staged) {
-            for (int i = lane; i < ntot; i += kWave) {
+            for (int i = t; i < ntot; i += NT) {
               const unsigned key = float_order_key(sc[i]);
               if ((key & hi_mask) == prefix) atomicAdd(&hist[(key >> shift) & 0xFFu], 1u);
             }
@@ -1066,13 +1158,13 @@ __global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
           for (int j = 0; j < Ls.nseg; ++j) {
             const int c = seg_count(Ls, q, j);
             const uint2* e = seg_ptr(Ls, q, j);
-            for (int i = lane; i < c; i += kWave) {
+            for (int i = t; i < c; i += NT) {
               const unsigned key = float_order_key(__uint_as_float(e[i].x));
               if ((key & hi_mask) == prefix) atomicAdd(&hist[(key >> shift) & 0xFFu], 1u);
             }
           }
         },
-        K, 3, hist);
+        K, 3, hist, aux);
     fail = r.at < 0;
     if (!fail) {
       // certificate (below) is the only reason counted in stats[1]
@@ -1080,63 +1172,58 @@ __global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
       // certificate: every list kept all s~ > tau, and ub(s~) <= ub(tau) < X
       // rules a candidate out of the exact top-K (which has K members >= X).
       fail = !(X > ub_of(tmax, m, rel));
-      if (fail) TT_STAT0(1, 1);
+      if (fail && t == 0) TT_STAT(1, 1);
     }
   }
   if (a.kth_lb) {  // select pass: at least K rows of these candidates score >= X exactly
-    if (lane == 0) a.kth_lb[q] = fail ? -INFINITY : X;
+    if (t == 0) a.kth_lb[q] = fail ? -INFINITY : X;
     return;
   }
   // a member of the global top-K scores >= floor: only those can matter
   if (a.floor) X = fmaxf(X, a.floor[q]);
-  int n = 0;
+  int n = 0, par = 0;
   if (!fail && staged) {
-    for (int e = lane; e < a.dim; e += kWave) qs[e] = a.q[q * a.ldq + e];
+    for (int e = t; e < a.dim; e += NT) qs[e] = a.q[q * a.ldq + e];
     // in-place compaction of the kept ids (writes never pass the reads)
-    for (int i0 = 0; i0 < ntot; i0 += kWave) {
-      const int i = i0 + lane;
+    for (int i0 = 0; i0 < ntot; i0 += NT) {
+      const int i = i0 + t;
       const float sv = i < ntot ? sc[i] : 0.0f;
       const unsigned iv = i < ntot ? id[i] : 0u;
       const bool keepit = i < ntot && ub_of(sv, m, rel) >= X;
-      const uint64_t bm = __ballot(keepit);
-      wsync();
-      if (keepit) id[n + __popcll(bm & lanemask_lt64())] = iv;
-      n += __popcll(bm);
-      wsync();
+      const int p = compact_slot<NW>(keepit, n, wcnt, par);
+      if constexpr (NW == 1) wsync();
+      if (keepit) id[p] = iv;
+      if constexpr (NW == 1) wsync();
     }
   } else if (!fail) {
-    for (int e = lane; e < a.dim; e += kWave) qs[e] = a.q[q * a.ldq + e];
+    for (int e = t; e < a.dim; e += NT) qs[e] = a.q[q * a.ldq + e];
     for (int j = 0; j < Ls.nseg && !fail; ++j) {
       const int c = seg_count(Ls, q, j);
       const uint2* e = seg_ptr(Ls, q, j);
-      for (int i0 = 0; i0 < c; i0 += kWave) {
-        const int i = i0 + lane;
+      for (int i0 = 0; i0 < c; i0 += NT) {
+        const int i = i0 + t;
         const uint2 en = i < c ? e[i] : make_uint2(0u, 0u);
         const bool keepit = i < c && ub_of(__uint_as_float(en.x), m, rel) >= X;
-        const uint64_t bm = __ballot(keepit);
-        if (n + __popcll(bm) > a.L) {
+        const int p = compact_slot<NW>(keepit, n, wcnt, par);
+        if (n > a.L) {  // uniform over the group
           fail = true;
           break;
         }
-        if (keepit) {
-          const int p = n + __popcll(bm & lanemask_lt64());
-          id[p] = en.y;
-        }
-        n += __popcll(bm);
+        if (keepit) id[p] = en.y;
       }
     }
-    wsync();
   }
+  gsync<NW>();
   if (fail) {
-    if (lane == 0) {
+    if (t == 0) {
       const int slot = atomicAdd(a.fail_count, 1);
       a.fail_list[slot] = static_cast<int>(q);
+      TT_STAT(3, 1);
     }
-    TT_STAT0(3, 1);
     return;
   }
-  TT_STAT0(2, n);
-  for (int j = lane; j < n; j += kWave) {
+  if (t == 0) TT_STAT(2, n);
+  for (int j = t; j < n; j += NT) {
     const int64_t row = static_cast<int64_t>(id[j]) - a.cand_offset;
 #ifdef TT_FINAL_NORESCORE  // timing probe only: no candidate rows read (results wrong)
     sc[j] = static_cast<float>(row & 1023);
@@ -1144,14 +1231,14 @@ __global__ void __launch_bounds__(kWave) finalize_kernel(const FinalArgs a) {
     sc[j] = exact_score(qs, a.cand + row * a.ldc, a.dim, a.vec4 != 0) + 0.0f;
 #endif
   }
-  wsync();
+  gsync<NW>();
   float kth;
-  n = exact_select(sc, id, n, K, &kth, hist);
-  rank_and_write(sc, id, n, min(n, K), a.P, sk, out_s, out_i);
+  n = exact_select<NW>(sc, id, n, K, &kth, hist, aux);
+  rank_and_write<NW>(sc, id, n, min(n, K), a.P, sk, out_s, out_i);
   // with a floor fewer than K may remain: pad (sorts after every real entry)
-  for (int t = n + lane; t < K; t += kWave) {
-    out_s[t] = -INFINITY;
-    out_i[t] = 0x7FFFFFFF;
+  for (int j = n + t; j < K; j += NT) {
+    out_s[j] = -INFINITY;
+    out_i[j] = 0x7FFFFFFF;
   }
 }
 
@@ -1321,8 +1408,18 @@ __global__ void __launch_bounds__(kFbWaves * kWave) fallback_kernel(const Fallba
 #endif
 struct SearchPlan {
   int S, NS, jsel, cap, L, LF, P, k, parts;
+  int NW;  // waves per finalize workgroup (one query each)
   int64_t chunk;
 };
+
+// Finalize group size: one wave per query for small k (many queries in
+// flight hide each other's latency); four for large k, whose long lists,
+// ~1.3k rescored rows and P-element sort make one query's chain the latency.
+// TT_FINAL_WAVES (1 / 2 / 4) overrides, TT_FINAL_LF the staged list size.
+inline int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
 
 // R = target list entries per query over the whole candidate set (3k + 100),
 // split evenly over the S splits x `shards` ranks screening disjoint ranges;
@@ -1338,6 +1435,13 @@ SearchPlan plan_search(int64_t nq, int64_t n_rows, int k, int shards) {
 #define TT_INDEX_LF 1024
 #endif
   p.LF = p.L > TT_INDEX_LF ? p.L : TT_INDEX_LF;  // finalize: a query's whole list (~3k + 100 entries) fits
+  static const int nw_env = env_int("TT_FINAL_WAVES", 0), lf_env = env_int("TT_FINAL_LF", 0);
+  p.NW = nw_env == 1 || nw_env == 2 || nw_env == 4 ? nw_env : (k >= 512 ? 4 : 1);
+  if (p.NW > 1) {  // the whole list staged in the group's LDS
+    const int lf = static_cast<int>(round_up(static_cast<int64_t>(3.5 * k) + 128, kWave));
+    if (lf > p.LF) p.LF = lf;
+  }
+  if (lf_env >= p.L) p.LF = static_cast<int>(round_up(lf_env, kWave));
   const int64_t qblocks = ceil_div(nq > 0 ? nq : 1, kQPerWG);
   p.S = 1;  // enough workgroups for the 256 CUs: split the candidates of few query blocks
   while (p.S < kMaxSplits && qblocks * p.S < 256 && ntiles / (2 * p.S) >= TT_INDEX_SPLIT_TILES) p.S *= 2;
@@ -1456,19 +1560,33 @@ int run_scan(int D, const void* index, int64_t row0, int64_t row1, int64_t nq, c
   return run_pass(D, sa, nq_pad, false, st);
 }
 
-int run_finalize(const FinalArgs& fa, const FallbackArgs& fb, int64_t nq, const SearchPlan& p, hipStream_t st) {
-  const size_t shm = final_lds_bytes(p.LF, p.P);
+template <int NW>
+int launch_finalize_nw(const FinalArgs& fa, int64_t nq, const SearchPlan& p, hipStream_t st) {
+  const size_t shm = final_lds_bytes(p.LF, p.P, NW);
   if (shm > 65536)
-    TT_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(finalize_kernel),
+    TT_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(finalize_kernel<NW>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(shm)));
+  hipLaunchKernelGGL(finalize_kernel<NW>, dim3(nq), dim3(NW * kWave), shm, st, fa);
+  TT_CHECK_LAUNCH();
+  return TT_OK;
+}
+
+int launch_finalize(const FinalArgs& fa, int64_t nq, const SearchPlan& p, hipStream_t st) {
+  switch (p.NW) {
+    case 4: return launch_finalize_nw<4>(fa, nq, p, st);
+    case 2: return launch_finalize_nw<2>(fa, nq, p, st);
+    default: return launch_finalize_nw<1>(fa, nq, p, st);
+  }
+}
+
+int run_finalize(const FinalArgs& fa, const FallbackArgs& fb, int64_t nq, const SearchPlan& p, hipStream_t st) {
   const size_t fshm = fallback_lds_bytes(p.L, p.P, p.parts, p.k);
   if (fshm > 65536)
     TT_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fallback_kernel),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(fshm)));
   probe_begin(TT_PROBE_INDEX_FINALIZE, st);
-  hipLaunchKernelGGL(finalize_kernel, dim3(nq), dim3(kWave), shm, st, fa);
+  if (int rc = launch_finalize(fa, nq, p, st)) return rc;
   probe_end(TT_PROBE_INDEX_FINALIZE, st);
-  TT_CHECK_LAUNCH();
   hipLaunchKernelGGL(fallback_kernel, dim3(kFbGrid), dim3(kFbWaves * kWave), fshm, st, fb);
   TT_CHECK_LAUNCH();
   return TT_OK;
@@ -1642,13 +1760,7 @@ extern "C" int tt_bruteforce_shard_screen(const void* index, int64_t n_cand, int
   Lists ls{w.buf, w.count, w.tau, p.S, p.cap, nullptr, p.S, 1};
   FinalArgs fa{queries, ldq, nullptr, 0, n_cand, index_offset, index_offset, dim, k, p.LF, p.P, 0,
                n_queries, w.qflags, w.qmarg, ls, nullptr, nullptr, nullptr, nullptr, kth_lb, nullptr};
-  const size_t shm = final_lds_bytes(p.LF, p.P);
-  if (shm > 65536)
-    TT_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(finalize_kernel),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(shm)));
-  hipLaunchKernelGGL(finalize_kernel, dim3(n_queries), dim3(kWave), shm, st, fa);
-  TT_CHECK_LAUNCH();
-  return TT_OK;
+  return launch_finalize(fa, n_queries, p, st);
 }
 
 extern "C" int tt_bruteforce_shard_finalize(const void* index, const float* cand, int64_t ldc, int64_t n_cand,
