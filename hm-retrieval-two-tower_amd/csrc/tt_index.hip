@@ -549,8 +549,10 @@ __global__ void __launch_bounds__(kSThreads) scan_kernel(const ScreenArgs a) {
 
   // Filters nrows staged rows from the tail (one per lane) and appends their
   // hits to the lists: per register r, the lanes whose score r beats their
-  // row's tau store it at their list's next slot.  A store is issued only
-  // when some lane has a hit in r (and then counted into the vmcnt window).
+  // row's tau store it at their list's next slot.  Branch-free: 16 stores per
+  // flush, a lane without a hit in r addressing past the buffer resource's
+  // range (the store drops it; 4.53 -> 4.35 ms per 131k-query chunk against
+  // one branch per register).
   auto flush = [&](int nrows) {
     wsync();
     const float* row = srow + ((tail + lane) & (kStageRows - 1)) * kRowF;
@@ -573,22 +575,19 @@ __global__ void __launch_bounds__(kSThreads) scan_kernel(const ScreenArgs a) {
     }
     const unsigned lbase = static_cast<unsigned>((ql * a.S + split) * a.cap) * 8u;
     const int last = a.cap - 1;  // scratch slot: entries past it are dropped with the list
-    int stores = 0;
+    // branch-free: one store per register for the whole wave; a lane with no
+    // hit in it addresses past the resource's range, and the store drops it
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float v = x[r >> 2][r & 3];
       const bool keepit = v > tr;
-      if (__ballot(keepit)) {
-        if (keepit) {
-          typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-          const u32x2 e = {__float_as_uint(v), pcr + static_cast<unsigned>((r & 3) + 8 * (r >> 2))};
-          __builtin_amdgcn_raw_buffer_store_b64(e, lists, lbase + static_cast<unsigned>(min(pos, last)) * 8u, 0, 0);
-          ++pos;
-        }
-        ++stores;
-      }
+      const u32x2 e = {__float_as_uint(v), pcr + static_cast<unsigned>((r & 3) + 8 * (r >> 2))};
+      const unsigned off = keepit ? lbase + static_cast<unsigned>(min(pos, last)) * 8u : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b64(e, lists, off, 0, 0);
+      pos += keepit ? 1 : 0;
     }
-    wc += stores;
+    wc += 16;
     tail += nrows;
     wsync();
   };
