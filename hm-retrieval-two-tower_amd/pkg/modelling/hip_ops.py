@@ -669,6 +669,33 @@ def mlp_pack(w: torch.Tensor, trans: bool = False, out: Optional[torch.Tensor] =
     return out
 
 
+def score_matrix(q: torch.Tensor, c: torch.Tensor, chunk: int = 256) -> torch.Tensor:
+    """S = q . c^T [Q, N] fp32 (TwoTowerModel.call, two_tower_model.py:92)
+    on libtt's bf16x3 row GEMM: c in column chunks of `chunk` candidates, each
+    packed as the B image of one tt_mlp_rows call writing its columns of S."""
+    _req(q, "q", torch.float32, 2)
+    _req(c, "c", torch.float32, 2)
+    Q, E = q.shape
+    N = c.shape[0]
+    if c.shape[1] != E:
+        raise ValueError(f"q {tuple(q.shape)} and c {tuple(c.shape)} must share the embedding size")
+    n4 = (N + 3) // 4 * 4
+    out = torch.empty(Q, max(n4, 4), dtype=torch.float32, device=q.device)
+    if Q == 0 or N == 0:
+        return out[:, :N]
+    e4 = (E + 3) // 4 * 4
+    a = q.contiguous()
+    if e4 != E:  # 16-B rows for the kernel's vector loads
+        a = torch.zeros(Q, e4, dtype=torch.float32, device=q.device)
+        a[:, :E] = q
+    cc = c.contiguous()
+    for j0 in range(0, N, chunk):
+        j1 = min(N, j0 + chunk)
+        img = mlp_pack(cc[j0:j1], trans=True)
+        mlp_rows(a, img, E, j1 - j0, out[:, j0:j1])
+    return out[:, :N]
+
+
 def mlp_pack_many(jobs: Sequence[Tuple[torch.Tensor, bool, torch.Tensor]]) -> None:
     """Several mlp_pack images in one launch: jobs of (w, trans, image buffer)."""
     arr = (_native.MlpPackJob * len(jobs))()

@@ -105,10 +105,17 @@ class TwoTowerModel(AbstractKerasModel):
 
     def call(self, x: Dict[str, Any], training: bool = True) -> torch.Tensor:
         """[Q, C] scores of every query against every candidate of the batch
-        (two_tower_model.py:65-92); materialised, for inspection / small B."""
+        (two_tower_model.py:65-92); materialised, for inspection / small B
+        (the train step never forms it: losses.towers_inbatch_softmax_xent).
+        Without gradients the score matrix is libtt's (hip_ops.score_matrix,
+        bf16x3 MFMA: fp32-faithful); with gradients enabled it stays an
+        autograd matmul so callers can differentiate through it."""
         q, c = self._split(x)
         with torch.set_grad_enabled(training and torch.is_grad_enabled()):
-            return torch.matmul(self.query_tower.call(q), self.candidate_tower.call(c).t())
+            qe, ce = self.query_tower.call(q), self.candidate_tower.call(c)
+            if torch.is_grad_enabled() or not qe.is_cuda:
+                return torch.matmul(qe, ce.t())
+            return hip_ops.score_matrix(qe, ce)
 
     def candidate_logq(self, x: Dict[str, Any]) -> Optional[torch.Tensor]:
         """Per-example log p(candidate) [B] for the logQ correction, or None."""
