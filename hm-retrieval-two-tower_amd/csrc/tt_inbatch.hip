@@ -211,8 +211,11 @@ __device__ __forceinline__ void wait_vmcnt() {
 // Rows pass: lazy rescaling — the running max m only moves when a tile's max
 // exceeds it by more than 8 (log2 units), so p <= 2^8 and the 64-register O
 // rescale leaves the steady state (m, l, O stay consistent: lse = m + log l).
+// Two workgroups per CU (<= 256 registers per lane): the second hides the
+// first's barrier and DMA waits.  At one per CU (the mask_diag of the
+// contract commit in its 64-bit form needed 302) the passes ran 25 % slower.
 template <int D, int MODE>
-__global__ void __launch_bounds__(kThreads) inbatch_pass_kernel(const PassArgs a) {
+__global__ void __launch_bounds__(kThreads, 2) inbatch_pass_kernel(const PassArgs a) {
   using G = Geo<D>;
   extern __shared__ __attribute__((aligned(16))) char ring[];
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) / kWave);
@@ -337,15 +340,17 @@ __global__ void __launch_bounds__(kThreads) inbatch_pass_kernel(const PassArgs a
   // two tiles per wave and split; a wave-uniform test) its score becomes -inf,
   // so p = 0.  Score k of a lane is streamed row 32(k>>4) + 8((k&15)>>2) + 4h + (k&3).
   const int64_t wave_row0 = static_cast<int64_t>(blockIdx.x) * kRowsPerWG + wave * kRowsPerWave;
+  // (the test is on wave-uniform scalars; a lane holds its positive in at
+  // most one register, found from the row's digits: no 64-bit lane math)
   auto mask_diag = [&](f32x16* sacc, int tile) {
     const int64_t lo = wave_row0 + a.diag_off - (s_begin + static_cast<int64_t>(tile) * kTile);
     if (lo + kRowsPerWave <= 0 || lo >= kTile) return;
-    const int64_t d = lo + l32;  // this lane's positive, as a row of the tile
+    const int d = static_cast<int>(lo) + l32;  // this lane's positive, as a row of the tile
+    const bool mine = d >= 0 && d < kTile && ((d >> 2) & 1) == h;
+    const int kd = mine ? 16 * (d >> 5) + 4 * ((d >> 3) & 3) + (d & 3) : -1;  // its register
 #pragma unroll
-    for (int k = 0; k < 32; ++k) {
-      const int r = 32 * (k >> 4) + 8 * ((k & 15) >> 2) + 4 * h + (k & 3);
-      if (d == r) sacc[k >> 4][k & 15] = -INFINITY;
-    }
+    for (int k = 0; k < 32; ++k)
+      sacc[k >> 4][k & 15] = kd == k ? -INFINITY : sacc[k >> 4][k & 15];
   };
 
   const int pre = ntiles < kRingStages ? ntiles : kRingStages;

@@ -82,6 +82,12 @@ constexpr int kMaxSample = 128;                  // sample tiles per split
 #define TT_INDEX_SPLIT_TILES 32  // a split is halved only while each half keeps >= this many tiles
 #endif
 constexpr int kMaxSplits = TT_INDEX_MAX_SPLITS;
+#ifndef TT_INDEX_MAX_SCAN_SPLITS
+#define TT_INDEX_MAX_SCAN_SPLITS 64
+#endif
+#ifndef TT_INDEX_SCAN_TILES
+#define TT_INDEX_SCAN_TILES 16  // a scan split is halved only while each half keeps >= this many tiles
+#endif
 constexpr float kEps = 0.0087890625f;            // 2^-7 + 2^-10
 constexpr float kTiny = 1e-30f;
 #ifndef TT_LIST_BUDGET
@@ -840,6 +846,31 @@ __device__ __forceinline__ int compact_slot(bool keep, int& n, int* wcnt, int& p
   }
 }
 
+// Group-wide min / max of the threads' values (uniform result); ends with the
+// group's LDS writes ordered (gsync).  scratch: 2 * NW words (NW > 1).
+template <int NW>
+__device__ __forceinline__ void group_minmax(unsigned& mn, unsigned& mx, int* scratch) {
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    mn = min(mn, static_cast<unsigned>(__shfl_xor(static_cast<int>(mn), off, kWave)));
+    mx = max(mx, static_cast<unsigned>(__shfl_xor(static_cast<int>(mx), off, kWave)));
+  }
+  if constexpr (NW > 1) {
+    const int wave = static_cast<int>(threadIdx.x) / kWave;
+    if (lane_id() == 0) {
+      scratch[wave] = static_cast<int>(mn);
+      scratch[NW + wave] = static_cast<int>(mx);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      mn = min(mn, static_cast<unsigned>(scratch[w]));
+      mx = max(mx, static_cast<unsigned>(scratch[NW + w]));
+    }
+  }
+  gsync<NW>();
+}
+
 // Radix select with 8-bit digits and an LDS histogram over keys the group
 // adds with `fill(prefix, hi_mask, shift)` (LDS atomics, any thread).  After
 // `passes` digits, `prefix` holds the top 8*passes bits of the K-th largest
@@ -852,16 +883,25 @@ struct Kth {
   int at;
 };
 
+// The keys' common top bits, when the caller knows them (kmin / kmax: the
+// smallest and largest key), are skipped: resolution starts below them, and
+// the last digit may overlap resolved bits (their value is the same for every
+// counted key, so the bin order is the digit order).  Bits >= stop_lo are
+// resolved (stop_lo = 8: a 24-bit prefix; 0: the exact key).
 template <int NW = 1, class Hist>
-__device__ Kth radix_select(Hist&& fill, int K, int passes, unsigned* hist, unsigned* bc = nullptr) {
+__device__ Kth radix_select(Hist&& fill, int K, int stop_lo, unsigned* hist, unsigned* bc = nullptr,
+                            unsigned kmin = 0u, unsigned kmax = 0xFFFFFFFFu) {
   const int lane = lane_id();
   const int t = gtid<NW>();
   const bool w0 = NW == 1 || t < kWave;
-  unsigned prefix = 0;
+  const int kb = (kmin ^ kmax) == 0 ? 32 : __clz(kmin ^ kmax);  // common top bits
+  int lo = 32 - kb;                                               // bits below lo unresolved
+  if (lo <= stop_lo) lo = stop_lo + 1;                            // at least one digit pass
+  unsigned prefix = lo >= 32 ? 0u : (kmin & (0xFFFFFFFFu << lo));
   int above = 0, at = 0;
-  for (int d = 0; d < passes; ++d) {
-    const int shift = 24 - 8 * d;
-    const unsigned hi_mask = d == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
+  for (; lo > stop_lo;) {
+    const int shift = lo - 8 > 0 ? lo - 8 : 0;
+    const unsigned hi_mask = lo >= 32 ? 0u : (0xFFFFFFFFu << lo);
     for (int u = t; u < 256; u += NW * kWave) hist[u] = 0;
     gsync<NW>();
     fill(prefix, hi_mask, shift);
@@ -920,6 +960,7 @@ __device__ Kth radix_select(Hist&& fill, int K, int passes, unsigned* hist, unsi
       __syncthreads();  // bc read by all before the next pass's first wave rewrites it
     }
     if (none) return Kth{0u, 0, -1};
+    lo = shift;
   }
   return Kth{prefix, above, at};
 }
@@ -929,7 +970,7 @@ __device__ Kth radix_select(Hist&& fill, int K, int passes, unsigned* hist, unsi
 // a strictly larger score).  aux (NW > 1): 2 * NW + 4 words of LDS.
 template <int NW = 1>
 __device__ int exact_select(float* sc, unsigned* id, int n, int K, float* thr, unsigned* hist,
-                            unsigned* aux = nullptr) {
+                            unsigned* aux = nullptr, unsigned kmin = 0u, unsigned kmax = 0xFFFFFFFFu) {
   if (n <= K) {
     *thr = -INFINITY;
     return n;
@@ -943,7 +984,7 @@ __device__ int exact_select(float* sc, unsigned* id, int n, int K, float* thr, u
           if ((key & hi_mask) == prefix) atomicAdd(&hist[(key >> shift) & 0xFFu], 1u);
         }
       },
-      K, 4, hist, aux);
+      K, 0, hist, aux, kmin, kmax);
   const unsigned res = r.prefix;  // exact key of the K-th score
   const int need = K - r.above;   // ties at the K-th score to keep, lowest indices first
   unsigned cut = 0xFFFFFFFFu;
@@ -1000,6 +1041,58 @@ __device__ void rank_and_write(const float* sc, const unsigned* id, int n, int k
                                float* out_s, int32_t* out_i) {
   const int t = gtid<NW>();
   constexpr int NT = NW * kWave;
+  if (NW == 1 && P <= 4 * kWave) {
+    // one wave, P <= 256: the whole bitonic network in registers (element
+    // i = slot * 64 + lane; strides < 64 between lanes by shuffles, >= 64
+    // between a lane's slots) — no LDS round trip or wave barrier per stage
+    constexpr int EM = 4;
+    const int E = P / kWave > 0 ? P / kWave : 1;
+    const int lane = lane_id();
+    unsigned long long kv[EM];
+#pragma unroll
+    for (int e = 0; e < EM; ++e) {
+      const int j = e * kWave + lane;
+      kv[e] = (e < E && j < n) ? make_key(sc[j], id[j]) : 0ull;
+    }
+    const int PP = E * kWave;
+    for (int size = 2; size <= PP; size <<= 1) {
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        if (stride >= kWave) {
+          const int es = stride / kWave;
+#pragma unroll
+          for (int e = 0; e < EM; ++e) {
+            if (e >= E || (e & es)) continue;
+            const int i = e * kWave + lane;  // the lower element of the pair (e, e + es)
+            const bool desc = (i & size) == 0;
+            const unsigned long long x = kv[e], y = kv[e + es];
+            const bool sw = (x < y) == desc;
+            kv[e] = sw ? y : x;
+            kv[e + es] = sw ? x : y;
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < EM; ++e) {
+            if (e >= E) continue;
+            const int i = e * kWave + lane;
+            const unsigned long long o = __shfl_xor(kv[e], stride, kWave);
+            const bool lower = (i & stride) == 0;
+            const bool desc = (i & size) == 0;
+            const unsigned long long mx = kv[e] > o ? kv[e] : o, mn = kv[e] > o ? o : kv[e];
+            kv[e] = (lower == desc) ? mx : mn;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < EM; ++e) {
+      const int j = e * kWave + lane;
+      if (e < E && j < k) {
+        out_s[j] = order_key_float(static_cast<unsigned>(kv[e] >> 32));
+        out_i[j] = static_cast<int32_t>(0xFFFFFFFFu - static_cast<unsigned>(kv[e]));
+      }
+    }
+    return;
+  }
   if (P <= kAliasP) {
     // keys built in registers first: sk may alias sc / id
     constexpr int PER = (kAliasP + NT - 1) / NT;
@@ -1065,6 +1158,10 @@ struct FinalArgs {
   // candidate-sharded two-phase form (tt_bruteforce_shard_*):
   float* kth_lb;        // select pass: per query lb(k-th screened score) (-inf: certificate failed), then stop
   const float* floor;   // rescore pass: per query lower bound on the GLOBAL k-th exact score
+  // candidate-major rescoring (small query batches): hand the survivors over
+  // instead of rescoring them (cut_n[q] = 0: answered here or failed)
+  int* cut_n;
+  unsigned* cut_ids;    // [q * L + j]
 };
 
 // LDS of one finalize group: query row, (score, id) list of L, the ranking
@@ -1111,6 +1208,7 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
       out_s[j] = 0.0f;
       out_i[j] = static_cast<int32_t>(a.zero_base + j);
     }
+    if (a.cut_n && t == 0) a.cut_n[q] = 0;
     return;
   }
   const bool rel = (fl & kQRel) != 0;
@@ -1129,6 +1227,7 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
   // the whole list read once into LDS when it fits (the select's passes and
   // the cut then read LDS, not the lists in memory)
   const bool staged = !fail && ntot <= a.L;
+  unsigned kmin = 0xFFFFFFFFu, kmax = 0u;  // the staged list's key range (radix select skips its common bits)
   if (staged) {
     int n0 = 0;
     for (int j = 0; j < Ls.nseg; ++j) {
@@ -1138,10 +1237,13 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
         const uint2 en = e[i];
         sc[n0 + i] = __uint_as_float(en.x);
         id[n0 + i] = en.y;
+        const unsigned k = float_order_key(__uint_as_float(en.x));
+        kmin = min(kmin, k);
+        kmax = max(kmax, k);
       }
       n0 += c;
     }
-    gsync<NW>();
+    group_minmax<NW>(kmin, kmax, wcnt);
   }
   if (!fail) {
     // K-th largest screened score to a 24-bit key prefix (rounded down)
@@ -1163,7 +1265,7 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
             }
           }
         },
-        K, 3, hist, aux);
+        K, 8, hist, aux, staged ? kmin : 0u, staged ? kmax : 0xFFFFFFFFu);
     fail = r.at < 0;
     if (!fail) {
       // certificate (below) is the only reason counted in stats[1]
@@ -1218,10 +1320,17 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
       const int slot = atomicAdd(a.fail_count, 1);
       a.fail_list[slot] = static_cast<int>(q);
       TT_STAT(3, 1);
+      if (a.cut_n) a.cut_n[q] = 0;
     }
     return;
   }
   if (t == 0) TT_STAT(2, n);
+  if (a.cut_n) {
+    if (t == 0) a.cut_n[q] = n;
+    for (int j = t; j < n; j += NT) a.cut_ids[q * a.L + j] = id[j];
+    return;
+  }
+  unsigned emin = 0xFFFFFFFFu, emax = 0u;
   for (int j = t; j < n; j += NT) {
     const int64_t row = static_cast<int64_t>(id[j]) - a.cand_offset;
 #ifdef TT_FINAL_NORESCORE  // timing probe only: no candidate rows read (results wrong)
@@ -1229,16 +1338,215 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
 #else
     sc[j] = exact_score(qs, a.cand + row * a.ldc, a.dim, a.vec4 != 0) + 0.0f;
 #endif
+    const unsigned k = float_order_key(sc[j]);
+    emin = min(emin, k);
+    emax = max(emax, k);
   }
-  gsync<NW>();
+  group_minmax<NW>(emin, emax, wcnt);
   float kth;
-  n = exact_select<NW>(sc, id, n, K, &kth, hist, aux);
+  n = exact_select<NW>(sc, id, n, K, &kth, hist, aux, emin, emax);
   rank_and_write<NW>(sc, id, n, min(n, K), a.P, sk, out_s, out_i);
   // with a floor fewer than K may remain: pad (sorts after every real entry)
   for (int j = n + t; j < K; j += NT) {
     out_s[j] = -INFINITY;
     out_i[j] = 0x7FFFFFFF;
   }
+}
+
+// ---- candidate-major rescoring ----------------------------------------------
+// For a small query batch at large k (the reference runner's 2048 x k = 1000)
+// rescoring query by query reads ~1.3k fp32 candidate rows per query from
+// MALL / HBM, each used once.  The batch's query rows fit in L2 (1 MB), so
+// the survivors are bucketed by 64-row candidate block instead: a workgroup
+// stages its block's rows in LDS and runs every (query, candidate) pair of
+// the bucket, the query row read from L2.  Same fmaf chain, same scores.
+//   cm_count    per 16-query group: LDS histogram of the survivors' blocks,
+//               one global atomic per (group, block) reserves the group's run
+//   cm_scan     exclusive scan of the block counts
+//   cm_scatter  pairs (q * L + j) << 6 | row-in-block into the buckets
+//   cm_rescore  one workgroup per block
+//   cm_final    exact select + rank of each query's rescored survivors
+constexpr int kCmRows = 64;
+constexpr int kCmGroup = 16;
+constexpr int kCmMaxBlocks = 16384;  // LDS histogram of 64 KB
+
+struct CmArgs {
+  const float* q;
+  int64_t ldq;
+  const float* cand;
+  int64_t ldc;
+  int64_t n_rows;
+  int64_t cand_offset;
+  int dim;
+  int k;
+  int L;  // cut list stride per query
+  int P;
+  int nblk;
+  int vec4;
+  int64_t nq;
+  const int* cut_n;
+  const unsigned* cut_ids;
+  float* cut_sc;
+  int* blk_count;  // zeroed before cm_count
+  int* blk_start;  // nblk + 1
+  int* grp_off;    // [group * nblk + block]
+  unsigned* pairs;
+  float* out_s;
+  int32_t* out_i;
+};
+
+__global__ void __launch_bounds__(256) cm_count_kernel(const CmArgs a) {
+  extern __shared__ unsigned cmh[];
+  const int g = blockIdx.x;
+  for (int b = threadIdx.x; b < a.nblk; b += 256) cmh[b] = 0u;
+  __syncthreads();
+  const int64_t q1 = min(a.nq, static_cast<int64_t>(g + 1) * kCmGroup);
+  for (int64_t q = static_cast<int64_t>(g) * kCmGroup; q < q1; ++q) {
+    const int n = a.cut_n[q];
+    const unsigned* ids = a.cut_ids + q * a.L;
+    for (int j = threadIdx.x; j < n; j += 256)
+      atomicAdd(&cmh[(static_cast<int64_t>(ids[j]) - a.cand_offset) / kCmRows], 1u);
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < a.nblk; b += 256) {
+    const unsigned c = cmh[b];
+    a.grp_off[static_cast<int64_t>(g) * a.nblk + b] = c ? atomicAdd(&a.blk_count[b], static_cast<int>(c)) : 0;
+  }
+}
+
+__global__ void __launch_bounds__(1024) cm_scan_kernel(const CmArgs a) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x;
+  const int per = (a.nblk + 1023) / 1024;
+  const int b0 = t * per;
+  int s = 0;
+  for (int i = 0; i < per; ++i)
+    if (b0 + i < a.nblk) s += a.blk_count[b0 + i];
+  part[t] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int v = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = part[t] - s;
+  for (int i = 0; i < per; ++i)
+    if (b0 + i < a.nblk) {
+      a.blk_start[b0 + i] = run;
+      run += a.blk_count[b0 + i];
+    }
+  if (t == 1023) a.blk_start[a.nblk] = part[1023];
+}
+
+__global__ void __launch_bounds__(256) cm_scatter_kernel(const CmArgs a) {
+  extern __shared__ unsigned cmh[];
+  const int g = blockIdx.x;
+  for (int b = threadIdx.x; b < a.nblk; b += 256) cmh[b] = 0u;
+  __syncthreads();
+  const int64_t q1 = min(a.nq, static_cast<int64_t>(g + 1) * kCmGroup);
+  const int* off = a.grp_off + static_cast<int64_t>(g) * a.nblk;
+  for (int64_t q = static_cast<int64_t>(g) * kCmGroup; q < q1; ++q) {
+    const int n = a.cut_n[q];
+    const unsigned* ids = a.cut_ids + q * a.L;
+    for (int j = threadIdx.x; j < n; j += 256) {
+      const int64_t row = static_cast<int64_t>(ids[j]) - a.cand_offset;
+      const int b = static_cast<int>(row / kCmRows);
+      const unsigned r = atomicAdd(&cmh[b], 1u);
+      a.pairs[a.blk_start[b] + off[b] + r] =
+          (static_cast<unsigned>(q * a.L + j) << 6) | static_cast<unsigned>(row % kCmRows);
+    }
+  }
+}
+
+// LDS row stride of a staged candidate block: 16-byte rows offset by 4 banks
+__host__ __device__ inline int cm_stride(int dim) { return ((dim + 3) & ~3) + 4; }
+
+template <bool QV4>
+__global__ void __launch_bounds__(256) cm_rescore_kernel(const CmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float cms[];
+  const int b = blockIdx.x;
+  const int s0 = a.blk_start[b], s1 = a.blk_start[b + 1];
+  if (s0 == s1) return;
+  const int dim = a.dim, st = cm_stride(dim);
+  const int64_t r0 = static_cast<int64_t>(b) * kCmRows;
+  const int nr = static_cast<int>(min(static_cast<int64_t>(kCmRows), a.n_rows - r0));
+  if (a.vec4) {
+    const int d4 = dim / 4;
+    for (int i = threadIdx.x; i < nr * d4; i += 256) {
+      const int r = i / d4, e = (i - r * d4) * 4;
+      *reinterpret_cast<f32x4*>(cms + r * st + e) = *reinterpret_cast<const f32x4*>(a.cand + (r0 + r) * a.ldc + e);
+    }
+  } else {
+    for (int i = threadIdx.x; i < nr * dim; i += 256) {
+      const int r = i / dim, e = i - r * dim;
+      cms[r * st + e] = a.cand[(r0 + r) * a.ldc + e];
+    }
+  }
+  __syncthreads();
+  for (int s = s0 + static_cast<int>(threadIdx.x); s < s1; s += 256) {
+    const unsigned pr = a.pairs[s];
+    const unsigned pos = pr >> 6;
+    const float* cr = cms + (pr & 63u) * st;
+    const float* qr = a.q + static_cast<int64_t>(pos / static_cast<unsigned>(a.L)) * a.ldq;
+    float acc = 0.0f;  // the exact chain: fmaf(q[e], c[e], acc), e = 0 .. dim-1
+    if (QV4) {
+      for (int e0 = 0; e0 < dim; e0 += 64) {
+        f32x4 v[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (e0 + 4 * i < dim) v[i] = *reinterpret_cast<const f32x4*>(qr + e0 + 4 * i);
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (e0 + 4 * i < dim) {
+            const f32x4 c = *reinterpret_cast<const f32x4*>(cr + e0 + 4 * i);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc = __builtin_fmaf(v[i][u], c[u], acc);
+          }
+      }
+    } else {
+      for (int e0 = 0; e0 < dim; e0 += 16) {
+        float v[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = (e0 + i < dim) ? qr[e0 + i] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (e0 + i < dim) acc = __builtin_fmaf(v[i], cr[e0 + i], acc);
+      }
+    }
+    a.cut_sc[pos] = acc + 0.0f;
+  }
+}
+
+template <int NW>
+__global__ void __launch_bounds__(NW * kWave) cm_final_kernel(const CmArgs a) {
+  constexpr int NT = NW * kWave;
+  extern __shared__ __attribute__((aligned(16))) char fsm[];
+  float* sc = reinterpret_cast<float*>(fsm) + 128;  // the finalize's layout (final_lds_bytes)
+  unsigned* id = reinterpret_cast<unsigned*>(sc + a.L);
+  const bool alias = a.P <= kAliasP;
+  unsigned long long* sk = alias ? reinterpret_cast<unsigned long long*>(sc)
+                                 : reinterpret_cast<unsigned long long*>(id + a.L);
+  unsigned* hist = alias ? id + a.L : reinterpret_cast<unsigned*>(sk + a.P);
+  unsigned* aux = hist + 256;
+  int* wcnt = reinterpret_cast<int*>(aux) + 4;
+  const int64_t q = blockIdx.x;
+  const int t = gtid<NW>();
+  const int K = a.k;
+  const int n = a.cut_n[q];
+  if (n == 0) return;  // answered by the finalize or the fallback
+  unsigned emin = 0xFFFFFFFFu, emax = 0u;
+  for (int j = t; j < n; j += NT) {
+    sc[j] = a.cut_sc[q * a.L + j];
+    id[j] = a.cut_ids[q * a.L + j];
+    const unsigned k = float_order_key(sc[j]);
+    emin = min(emin, k);
+    emax = max(emax, k);
+  }
+  group_minmax<NW>(emin, emax, wcnt);
+  float kth;
+  const int m = exact_select<NW>(sc, id, n, K, &kth, hist, aux, emin, emax);
+  rank_and_write<NW>(sc, id, m, min(m, K), a.P, sk, a.out_s + q * K, a.out_i + q * K);
 }
 
 // Exact fallback for the queries the finalize could not certify.  A
@@ -1408,9 +1716,15 @@ __global__ void __launch_bounds__(kFbWaves * kWave) fallback_kernel(const Fallba
 #ifndef TT_INDEX_R_ADD
 #define TT_INDEX_R_ADD 100.0
 #endif
+#ifndef TT_INDEX_CM_MIN_K  // candidate-major rescoring from this k (small query batches)
+#define TT_INDEX_CM_MIN_K 100000
+#endif
 struct SearchPlan {
   int S, NS, jsel, cap, L, LF, P, k, parts;
+  int Ss;  // sample-pass splits (<= S): their estimates give one tau per query
   int NW;  // waves per finalize workgroup (one query each)
+  int cm;  // candidate-major rescoring (cm_* kernels), nblk 64-row blocks
+  int nblk;
   int64_t chunk;
 };
 
@@ -1447,6 +1761,7 @@ SearchPlan plan_search(int64_t nq, int64_t n_rows, int k, int shards) {
   const int64_t qblocks = ceil_div(nq > 0 ? nq : 1, kQPerWG);
   p.S = 1;  // enough workgroups for the 256 CUs: split the candidates of few query blocks
   while (p.S < kMaxSplits && qblocks * p.S < 256 && ntiles / (2 * p.S) >= TT_INDEX_SPLIT_TILES) p.S *= 2;
+  p.Ss = p.S;
   const int64_t nts = ceil_div(ntiles, p.S);  // tiles per split
   const double ns_cand = static_cast<double>(nts) * kCTile;
   // 3k + 100 below k = 512; 1.5k + 100 from there (at the runner's 2048 x
@@ -1472,6 +1787,16 @@ SearchPlan plan_search(int64_t nq, int64_t n_rows, int k, int shards) {
     p.jsel = j < 1 ? 1 : (j > 64 ? 64 : j);
     mu = R;
   }
+  if (p.NS > 0) {
+    // the scan needs only the per-query tau (the min over the sample
+    // splits), so it may split the candidates further than the sample pass
+    // (whose per-split estimates need enough tiles): a 2048-query batch gets
+    // 4 x 64 instead of 4 x 32 workgroups
+    while (p.S < TT_INDEX_MAX_SCAN_SPLITS && qblocks * p.S < 256 && ntiles / (2 * p.S) >= TT_INDEX_SCAN_TILES) {
+      p.S *= 2;
+      mu *= 0.5;
+    }
+  }
   // the lowest of S (x shards) estimates lands lower than each: room for it
   p.cap = next_pow2(static_cast<int>(3.0 * mu * (p.S > 1 ? 2.0 : 1.0)) + 64);
   const size_t per_query = static_cast<size_t>(p.S) * p.cap * sizeof(uint2);
@@ -1479,6 +1804,12 @@ SearchPlan plan_search(int64_t nq, int64_t n_rows, int k, int shards) {
   if (chunk < kQPerWG) chunk = kQPerWG;
   const int64_t need = round_up(nq > 0 ? nq : 1, kQPerWG);
   p.chunk = chunk < need ? chunk : need;
+  // candidate-major rescoring: the chunk's fp32 query rows stay in L2 (<= 2
+  // MB) and its survivor pairs are many (k >= 256); TT_INDEX_CM=0/1 overrides
+  static const int cm_env = env_int("TT_INDEX_CM", -1);
+  p.nblk = static_cast<int>(ceil_div(n_rows, kCmRows));
+  const bool cm_ok = shards <= 1 && p.nblk <= kCmMaxBlocks && p.chunk * p.LF < (1ll << 26);
+  p.cm = cm_ok && (cm_env >= 0 ? cm_env != 0 : (k >= TT_INDEX_CM_MIN_K && p.chunk * 128 * 4 <= (2 << 20)));
   return p;
 }
 
@@ -1494,6 +1825,13 @@ struct SearchWs {
   int* fail_list;
   uint2* fb_scratch;
   int* fb_scratch_n;
+  int* cut_n;  // candidate-major rescoring (p.cm)
+  unsigned* cut_ids;
+  float* cut_sc;
+  int* blk_count;
+  int* blk_start;
+  int* grp_off;
+  unsigned* pairs;
 };
 
 SearchWs carve_search(Carver& cv, int D, const SearchPlan& p, bool lists, bool finalize) {
@@ -1505,7 +1843,7 @@ SearchWs carve_search(Carver& cv, int D, const SearchPlan& p, bool lists, bool f
   if (lists) {
     w.buf = cv.take<uint2>(nq_pad * p.S * static_cast<int64_t>(p.cap));
     w.count = cv.take<int>(nq_pad * p.S);
-    w.tau_split = cv.take<float>(nq_pad * p.S);
+    w.tau_split = cv.take<float>(nq_pad * p.Ss);
     w.tau = cv.take<float>(nq_pad);
   }
   if (finalize) {
@@ -1513,6 +1851,16 @@ SearchWs carve_search(Carver& cv, int D, const SearchPlan& p, bool lists, bool f
     w.fail_list = cv.take<int>(nq_pad);
     w.fb_scratch = cv.take<uint2>(static_cast<int64_t>(kFbSlots) * p.parts * p.k);
     w.fb_scratch_n = cv.take<int>(static_cast<int64_t>(kFbSlots) * p.parts);
+    if (p.cm) {
+      const int64_t nc = nq_pad * p.LF;
+      w.cut_n = cv.take<int>(nq_pad);
+      w.cut_ids = cv.take<unsigned>(nc);
+      w.cut_sc = cv.take<float>(nc);
+      w.pairs = cv.take<unsigned>(nc);
+      w.blk_count = cv.take<int>(p.nblk);
+      w.blk_start = cv.take<int>(p.nblk + 1);
+      w.grp_off = cv.take<int>(ceil_div(nq_pad, kCmGroup) * p.nblk);
+    }
   }
   return w;
 }
@@ -1552,9 +1900,9 @@ int run_prep(const float* q, int64_t ldq, int64_t nq, int dim, int D, const void
 int run_estimate(int D, const void* index, int64_t row0, int64_t row1, int64_t nq, const SearchPlan& p,
                  const SearchWs& w, float* tau, hipStream_t st) {
   const int64_t nq_pad = round_up(nq, kQPerWG);
-  ScreenArgs sa{index, w.qb, nq, row0, row1, p.S, p.NS, p.jsel, p.cap, 0u, nullptr, nullptr, w.tau_split, nullptr};
+  ScreenArgs sa{index, w.qb, nq, row0, row1, p.Ss, p.NS, p.jsel, p.cap, 0u, nullptr, nullptr, w.tau_split, nullptr};
   if (int rc = run_pass(D, sa, nq_pad, true, st)) return rc;
-  hipLaunchKernelGGL(tau_min_kernel, dim3(ceil_div(nq, 256)), dim3(256), 0, st, w.tau_split, p.S, nq, tau);
+  hipLaunchKernelGGL(tau_min_kernel, dim3(ceil_div(nq, 256)), dim3(256), 0, st, w.tau_split, p.Ss, nq, tau);
   TT_CHECK_LAUNCH();
   return TT_OK;
 }
@@ -1585,13 +1933,52 @@ int launch_finalize(const FinalArgs& fa, int64_t nq, const SearchPlan& p, hipStr
   }
 }
 
-int run_finalize(const FinalArgs& fa, const FallbackArgs& fb, int64_t nq, const SearchPlan& p, hipStream_t st) {
+template <int NW>
+int launch_cm_final(const CmArgs& ca, int64_t nq, const SearchPlan& p, hipStream_t st) {
+  const size_t shm = final_lds_bytes(p.LF, p.P, NW);
+  if (shm > 65536)
+    TT_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(cm_final_kernel<NW>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(shm)));
+  hipLaunchKernelGGL(cm_final_kernel<NW>, dim3(nq), dim3(NW * kWave), shm, st, ca);
+  TT_CHECK_LAUNCH();
+  return TT_OK;
+}
+
+// after the finalize's select + cut (fa.cut_n): bucket, rescore, rank
+int run_cm(const CmArgs& ca, int64_t nq, const SearchPlan& p, bool qv4, hipStream_t st) {
+  const int ngrp = static_cast<int>(ceil_div(nq, kCmGroup));
+  const size_t hshm = static_cast<size_t>(p.nblk) * sizeof(unsigned);
+  if (hshm > 65536) return fail(TT_ERR_UNSUPPORTED, "candidate-major rescoring: %d blocks", p.nblk);
+  hipLaunchKernelGGL(cm_count_kernel, dim3(ngrp), dim3(256), hshm, st, ca);
+  TT_CHECK_LAUNCH();
+  hipLaunchKernelGGL(cm_scan_kernel, dim3(1), dim3(1024), 0, st, ca);
+  TT_CHECK_LAUNCH();
+  hipLaunchKernelGGL(cm_scatter_kernel, dim3(ngrp), dim3(256), hshm, st, ca);
+  TT_CHECK_LAUNCH();
+  const size_t rshm = static_cast<size_t>(kCmRows) * cm_stride(ca.dim) * sizeof(float);
+  if (qv4)
+    hipLaunchKernelGGL(cm_rescore_kernel<true>, dim3(p.nblk), dim3(256), rshm, st, ca);
+  else
+    hipLaunchKernelGGL(cm_rescore_kernel<false>, dim3(p.nblk), dim3(256), rshm, st, ca);
+  TT_CHECK_LAUNCH();
+  switch (p.NW) {
+    case 4: return launch_cm_final<4>(ca, nq, p, st);
+    case 2: return launch_cm_final<2>(ca, nq, p, st);
+    default: return launch_cm_final<1>(ca, nq, p, st);
+  }
+}
+
+int run_finalize(const FinalArgs& fa, const FallbackArgs& fb, int64_t nq, const SearchPlan& p, hipStream_t st,
+                 const CmArgs* ca = nullptr, bool qv4 = false) {
   const size_t fshm = fallback_lds_bytes(p.L, p.P, p.parts, p.k);
   if (fshm > 65536)
     TT_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fallback_kernel),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(fshm)));
   probe_begin(TT_PROBE_INDEX_FINALIZE, st);
+  if (ca) TT_CHECK_HIP(hipMemsetAsync(ca->blk_count, 0, static_cast<size_t>(p.nblk) * sizeof(int), st));
   if (int rc = launch_finalize(fa, nq, p, st)) return rc;
+  if (ca)
+    if (int rc = run_cm(*ca, nq, p, qv4, st)) return rc;
   probe_end(TT_PROBE_INDEX_FINALIZE, st);
   hipLaunchKernelGGL(fallback_kernel, dim3(kFbGrid), dim3(kFbWaves * kWave), fshm, st, fb);
   TT_CHECK_LAUNCH();
@@ -1674,11 +2061,15 @@ extern "C" int tt_bruteforce_search(const void* index, const float* cand, int64_
     Lists ls{w.buf, w.count, w.tau, p.S, p.cap, nullptr, p.S, 1};
     FinalArgs fa{qc, ldq, cand, ldc, n_cand, index_offset, index_offset, dim, k, p.LF, p.P, vec4,
                  nq, w.qflags, w.qmarg, ls, out_scores + q0 * k, out_idx + q0 * k, w.fail_count, w.fail_list,
-                 nullptr, nullptr};
+                 nullptr, nullptr, p.cm ? w.cut_n : nullptr, p.cm ? w.cut_ids : nullptr};
     FallbackArgs fb{qc, ldq, cand, ldc, n_cand, index_offset, dim, k, p.L, p.P, p.parts, vec4,
                     w.fail_count, w.fail_list, w.fail_count + 1, w.fb_scratch, w.fb_scratch_n,
                     out_scores + q0 * k, out_idx + q0 * k};
-    if (int rc = run_finalize(fa, fb, nq, p, st)) return rc;
+    const CmArgs ca{qc, ldq, cand, ldc, n_cand, index_offset, dim, k, p.LF, p.P, p.nblk, vec4, nq,
+                    w.cut_n, w.cut_ids, w.cut_sc, w.blk_count, w.blk_start, w.grp_off, w.pairs,
+                    out_scores + q0 * k, out_idx + q0 * k};
+    const bool qv4 = is_vec4(qc, ldq, dim);
+    if (int rc = run_finalize(fa, fb, nq, p, st, p.cm ? &ca : nullptr, qv4)) return rc;
   }
   return TT_OK;
 }
