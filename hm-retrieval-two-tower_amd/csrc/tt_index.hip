@@ -783,6 +783,7 @@ __device__ __forceinline__ float exact_score(const float* __restrict__ qs, const
 // buf + (q * nseg + j) * cap (region form) or at off[q * cq + j * cj] (CSR
 // form, cap == 0, entries as int64 = id << 32 | score bits, the same bytes as
 // uint2 {score bits, id}); their screens kept s~ > tau[q].
+static_assert(TT_INDEX_MAX_SCAN_SPLITS <= kWave, "the finalize prefixes at most 64 list segments");
 struct Lists {
   const uint2* buf;
   const int* count;
@@ -1158,10 +1159,6 @@ struct FinalArgs {
   // candidate-sharded two-phase form (tt_bruteforce_shard_*):
   float* kth_lb;        // select pass: per query lb(k-th screened score) (-inf: certificate failed), then stop
   const float* floor;   // rescore pass: per query lower bound on the GLOBAL k-th exact score
-  // candidate-major rescoring (small query batches): hand the survivors over
-  // instead of rescoring them (cut_n[q] = 0: answered here or failed)
-  int* cut_n;
-  unsigned* cut_ids;    // [q * L + j]
 };
 
 // LDS of one finalize group: query row, (score, id) list of L, the ranking
@@ -1208,42 +1205,65 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
       out_s[j] = 0.0f;
       out_i[j] = static_cast<int32_t>(a.zero_base + j);
     }
-    if (a.cut_n && t == 0) a.cut_n[q] = 0;
     return;
   }
   const bool rel = (fl & kQRel) != 0;
   const float m = a.qmarg[q];
-  bool fail = false;
-  int ntot = 0;
-  float tmax;
-  for (int j = 0; j < Ls.nseg; ++j) {
-    const int c = seg_count(Ls, q, j);
-    fail = fail || c < 0;
-    ntot += c;
+  // the segments' counts, one load each by the first wave, to an exclusive
+  // prefix pre[0..64] in LDS (the radix bins, cleared by the select later;
+  // padded with the total), so the list is read as one flat index space
+  // rather than segment by segment (64 dependent round trips at S = 64)
+  int* const pre = reinterpret_cast<int*>(hist);
+  if (t < kWave) {
+    const int c = t < Ls.nseg ? seg_count(Ls, q, t) : 0;
+    int v = c;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+      const int o = __shfl_up(v, off, kWave);
+      if (t >= off) v += o;
+    }
+    pre[t + 1] = v;
+    if (t == 0) pre[0] = 0;
+    const bool bad = __ballot(c < 0) != 0;
+    if (t == 0) pre[kWave + 1] = bad ? 1 : 0;
   }
-  tmax = Ls.tau[q];
-  fail = fail || ntot < K;
+  gsync<NW>();
+  const int ntot = pre[kWave];
+  bool fail = pre[kWave + 1] != 0 || ntot < K;
+  const float tmax = Ls.tau[q];
   float X = -INFINITY;
   // the whole list read once into LDS when it fits (the select's passes and
   // the cut then read LDS, not the lists in memory)
   const bool staged = !fail && ntot <= a.L;
   unsigned kmin = 0xFFFFFFFFu, kmax = 0u;  // the staged list's key range (radix select skips its common bits)
   if (staged) {
-    int n0 = 0;
-    for (int j = 0; j < Ls.nseg; ++j) {
-      const int c = seg_count(Ls, q, j);
-      const uint2* e = seg_ptr(Ls, q, j);
-      for (int i = t; i < c; i += NT) {
-        const uint2 en = e[i];
-        sc[n0 + i] = __uint_as_float(en.x);
-        id[n0 + i] = en.y;
-        const unsigned k = float_order_key(__uint_as_float(en.x));
-        kmin = min(kmin, k);
-        kmax = max(kmax, k);
+    for (int i0 = 0; i0 < ntot; i0 += 4 * NT) {
+      uint2 en[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * NT + t;
+        if (i < ntot) {
+          int j = 0;  // the segment holding flat entry i: the last j with pre[j] <= i
+#pragma unroll
+          for (int st = kWave / 2; st > 0; st >>= 1) j += pre[j + st] <= i ? st : 0;
+          en[u] = seg_ptr(Ls, q, j)[i - pre[j]];
+        }
       }
-      n0 += c;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * NT + t;
+        if (i < ntot) {
+          sc[i] = __uint_as_float(en[u].x);
+          id[i] = en[u].y;
+          const unsigned k = float_order_key(__uint_as_float(en[u].x));
+          kmin = min(kmin, k);
+          kmax = max(kmax, k);
+        }
+      }
     }
     group_minmax<NW>(kmin, kmax, wcnt);
+  } else {
+    gsync<NW>();  // pre read by all before the select clears the bins
   }
   if (!fail) {
     // K-th largest screened score to a 24-bit key prefix (rounded down)
@@ -1320,16 +1340,10 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
       const int slot = atomicAdd(a.fail_count, 1);
       a.fail_list[slot] = static_cast<int>(q);
       TT_STAT(3, 1);
-      if (a.cut_n) a.cut_n[q] = 0;
     }
     return;
   }
   if (t == 0) TT_STAT(2, n);
-  if (a.cut_n) {
-    if (t == 0) a.cut_n[q] = n;
-    for (int j = t; j < n; j += NT) a.cut_ids[q * a.L + j] = id[j];
-    return;
-  }
   unsigned emin = 0xFFFFFFFFu, emax = 0u;
   for (int j = t; j < n; j += NT) {
     const int64_t row = static_cast<int64_t>(id[j]) - a.cand_offset;
@@ -1351,202 +1365,6 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
     out_s[j] = -INFINITY;
     out_i[j] = 0x7FFFFFFF;
   }
-}
-
-// ---- candidate-major rescoring ----------------------------------------------
-// For a small query batch at large k (the reference runner's 2048 x k = 1000)
-// rescoring query by query reads ~1.3k fp32 candidate rows per query from
-// MALL / HBM, each used once.  The batch's query rows fit in L2 (1 MB), so
-// the survivors are bucketed by 64-row candidate block instead: a workgroup
-// stages its block's rows in LDS and runs every (query, candidate) pair of
-// the bucket, the query row read from L2.  Same fmaf chain, same scores.
-//   cm_count    per 16-query group: LDS histogram of the survivors' blocks,
-//               one global atomic per (group, block) reserves the group's run
-//   cm_scan     exclusive scan of the block counts
-//   cm_scatter  pairs (q * L + j) << 6 | row-in-block into the buckets
-//   cm_rescore  one workgroup per block
-//   cm_final    exact select + rank of each query's rescored survivors
-constexpr int kCmRows = 64;
-constexpr int kCmGroup = 16;
-constexpr int kCmMaxBlocks = 16384;  // LDS histogram of 64 KB
-
-struct CmArgs {
-  const float* q;
-  int64_t ldq;
-  const float* cand;
-  int64_t ldc;
-  int64_t n_rows;
-  int64_t cand_offset;
-  int dim;
-  int k;
-  int L;  // cut list stride per query
-  int P;
-  int nblk;
-  int vec4;
-  int64_t nq;
-  const int* cut_n;
-  const unsigned* cut_ids;
-  float* cut_sc;
-  int* blk_count;  // zeroed before cm_count
-  int* blk_start;  // nblk + 1
-  int* grp_off;    // [group * nblk + block]
-  unsigned* pairs;
-  float* out_s;
-  int32_t* out_i;
-};
-
-__global__ void __launch_bounds__(256) cm_count_kernel(const CmArgs a) {
-  extern __shared__ unsigned cmh[];
-  const int g = blockIdx.x;
-  for (int b = threadIdx.x; b < a.nblk; b += 256) cmh[b] = 0u;
-  __syncthreads();
-  const int64_t q1 = min(a.nq, static_cast<int64_t>(g + 1) * kCmGroup);
-  for (int64_t q = static_cast<int64_t>(g) * kCmGroup; q < q1; ++q) {
-    const int n = a.cut_n[q];
-    const unsigned* ids = a.cut_ids + q * a.L;
-    for (int j = threadIdx.x; j < n; j += 256)
-      atomicAdd(&cmh[(static_cast<int64_t>(ids[j]) - a.cand_offset) / kCmRows], 1u);
-  }
-  __syncthreads();
-  for (int b = threadIdx.x; b < a.nblk; b += 256) {
-    const unsigned c = cmh[b];
-    a.grp_off[static_cast<int64_t>(g) * a.nblk + b] = c ? atomicAdd(&a.blk_count[b], static_cast<int>(c)) : 0;
-  }
-}
-
-__global__ void __launch_bounds__(1024) cm_scan_kernel(const CmArgs a) {
-  __shared__ int part[1024];
-  const int t = threadIdx.x;
-  const int per = (a.nblk + 1023) / 1024;
-  const int b0 = t * per;
-  int s = 0;
-  for (int i = 0; i < per; ++i)
-    if (b0 + i < a.nblk) s += a.blk_count[b0 + i];
-  part[t] = s;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
-    const int v = t >= off ? part[t - off] : 0;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
-  }
-  int run = part[t] - s;
-  for (int i = 0; i < per; ++i)
-    if (b0 + i < a.nblk) {
-      a.blk_start[b0 + i] = run;
-      run += a.blk_count[b0 + i];
-    }
-  if (t == 1023) a.blk_start[a.nblk] = part[1023];
-}
-
-__global__ void __launch_bounds__(256) cm_scatter_kernel(const CmArgs a) {
-  extern __shared__ unsigned cmh[];
-  const int g = blockIdx.x;
-  for (int b = threadIdx.x; b < a.nblk; b += 256) cmh[b] = 0u;
-  __syncthreads();
-  const int64_t q1 = min(a.nq, static_cast<int64_t>(g + 1) * kCmGroup);
-  const int* off = a.grp_off + static_cast<int64_t>(g) * a.nblk;
-  for (int64_t q = static_cast<int64_t>(g) * kCmGroup; q < q1; ++q) {
-    const int n = a.cut_n[q];
-    const unsigned* ids = a.cut_ids + q * a.L;
-    for (int j = threadIdx.x; j < n; j += 256) {
-      const int64_t row = static_cast<int64_t>(ids[j]) - a.cand_offset;
-      const int b = static_cast<int>(row / kCmRows);
-      const unsigned r = atomicAdd(&cmh[b], 1u);
-      a.pairs[a.blk_start[b] + off[b] + r] =
-          (static_cast<unsigned>(q * a.L + j) << 6) | static_cast<unsigned>(row % kCmRows);
-    }
-  }
-}
-
-// LDS row stride of a staged candidate block: 16-byte rows offset by 4 banks
-__host__ __device__ inline int cm_stride(int dim) { return ((dim + 3) & ~3) + 4; }
-
-template <bool QV4>
-__global__ void __launch_bounds__(256) cm_rescore_kernel(const CmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float cms[];
-  const int b = blockIdx.x;
-  const int s0 = a.blk_start[b], s1 = a.blk_start[b + 1];
-  if (s0 == s1) return;
-  const int dim = a.dim, st = cm_stride(dim);
-  const int64_t r0 = static_cast<int64_t>(b) * kCmRows;
-  const int nr = static_cast<int>(min(static_cast<int64_t>(kCmRows), a.n_rows - r0));
-  if (a.vec4) {
-    const int d4 = dim / 4;
-    for (int i = threadIdx.x; i < nr * d4; i += 256) {
-      const int r = i / d4, e = (i - r * d4) * 4;
-      *reinterpret_cast<f32x4*>(cms + r * st + e) = *reinterpret_cast<const f32x4*>(a.cand + (r0 + r) * a.ldc + e);
-    }
-  } else {
-    for (int i = threadIdx.x; i < nr * dim; i += 256) {
-      const int r = i / dim, e = i - r * dim;
-      cms[r * st + e] = a.cand[(r0 + r) * a.ldc + e];
-    }
-  }
-  __syncthreads();
-  for (int s = s0 + static_cast<int>(threadIdx.x); s < s1; s += 256) {
-    const unsigned pr = a.pairs[s];
-    const unsigned pos = pr >> 6;
-    const float* cr = cms + (pr & 63u) * st;
-    const float* qr = a.q + static_cast<int64_t>(pos / static_cast<unsigned>(a.L)) * a.ldq;
-    float acc = 0.0f;  // the exact chain: fmaf(q[e], c[e], acc), e = 0 .. dim-1
-    if (QV4) {
-      for (int e0 = 0; e0 < dim; e0 += 64) {
-        f32x4 v[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          if (e0 + 4 * i < dim) v[i] = *reinterpret_cast<const f32x4*>(qr + e0 + 4 * i);
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          if (e0 + 4 * i < dim) {
-            const f32x4 c = *reinterpret_cast<const f32x4*>(cr + e0 + 4 * i);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) acc = __builtin_fmaf(v[i][u], c[u], acc);
-          }
-      }
-    } else {
-      for (int e0 = 0; e0 < dim; e0 += 16) {
-        float v[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = (e0 + i < dim) ? qr[e0 + i] : 0.0f;
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          if (e0 + i < dim) acc = __builtin_fmaf(v[i], cr[e0 + i], acc);
-      }
-    }
-    a.cut_sc[pos] = acc + 0.0f;
-  }
-}
-
-template <int NW>
-__global__ void __launch_bounds__(NW * kWave) cm_final_kernel(const CmArgs a) {
-  constexpr int NT = NW * kWave;
-  extern __shared__ __attribute__((aligned(16))) char fsm[];
-  float* sc = reinterpret_cast<float*>(fsm) + 128;  // the finalize's layout (final_lds_bytes)
-  unsigned* id = reinterpret_cast<unsigned*>(sc + a.L);
-  const bool alias = a.P <= kAliasP;
-  unsigned long long* sk = alias ? reinterpret_cast<unsigned long long*>(sc)
-                                 : reinterpret_cast<unsigned long long*>(id + a.L);
-  unsigned* hist = alias ? id + a.L : reinterpret_cast<unsigned*>(sk + a.P);
-  unsigned* aux = hist + 256;
-  int* wcnt = reinterpret_cast<int*>(aux) + 4;
-  const int64_t q = blockIdx.x;
-  const int t = gtid<NW>();
-  const int K = a.k;
-  const int n = a.cut_n[q];
-  if (n == 0) return;  // answered by the finalize or the fallback
-  unsigned emin = 0xFFFFFFFFu, emax = 0u;
-  for (int j = t; j < n; j += NT) {
-    sc[j] = a.cut_sc[q * a.L + j];
-    id[j] = a.cut_ids[q * a.L + j];
-    const unsigned k = float_order_key(sc[j]);
-    emin = min(emin, k);
-    emax = max(emax, k);
-  }
-  group_minmax<NW>(emin, emax, wcnt);
-  float kth;
-  const int m = exact_select<NW>(sc, id, n, K, &kth, hist, aux, emin, emax);
-  rank_and_write<NW>(sc, id, m, min(m, K), a.P, sk, a.out_s + q * K, a.out_i + q * K);
 }
 
 // Exact fallback for the queries the finalize could not certify.  A
@@ -1716,15 +1534,10 @@ __global__ void __launch_bounds__(kFbWaves * kWave) fallback_kernel(const Fallba
 #ifndef TT_INDEX_R_ADD
 #define TT_INDEX_R_ADD 100.0
 #endif
-#ifndef TT_INDEX_CM_MIN_K  // candidate-major rescoring from this k (small query batches)
-#define TT_INDEX_CM_MIN_K 100000
-#endif
 struct SearchPlan {
   int S, NS, jsel, cap, L, LF, P, k, parts;
   int Ss;  // sample-pass splits (<= S): their estimates give one tau per query
   int NW;  // waves per finalize workgroup (one query each)
-  int cm;  // candidate-major rescoring (cm_* kernels), nblk 64-row blocks
-  int nblk;
   int64_t chunk;
 };
 
@@ -1804,12 +1617,6 @@ SearchPlan plan_search(int64_t nq, int64_t n_rows, int k, int shards) {
   if (chunk < kQPerWG) chunk = kQPerWG;
   const int64_t need = round_up(nq > 0 ? nq : 1, kQPerWG);
   p.chunk = chunk < need ? chunk : need;
-  // candidate-major rescoring: the chunk's fp32 query rows stay in L2 (<= 2
-  // MB) and its survivor pairs are many (k >= 256); TT_INDEX_CM=0/1 overrides
-  static const int cm_env = env_int("TT_INDEX_CM", -1);
-  p.nblk = static_cast<int>(ceil_div(n_rows, kCmRows));
-  const bool cm_ok = shards <= 1 && p.nblk <= kCmMaxBlocks && p.chunk * p.LF < (1ll << 26);
-  p.cm = cm_ok && (cm_env >= 0 ? cm_env != 0 : (k >= TT_INDEX_CM_MIN_K && p.chunk * 128 * 4 <= (2 << 20)));
   return p;
 }
 
@@ -1825,13 +1632,6 @@ struct SearchWs {
   int* fail_list;
   uint2* fb_scratch;
   int* fb_scratch_n;
-  int* cut_n;  // candidate-major rescoring (p.cm)
-  unsigned* cut_ids;
-  float* cut_sc;
-  int* blk_count;
-  int* blk_start;
-  int* grp_off;
-  unsigned* pairs;
 };
 
 SearchWs carve_search(Carver& cv, int D, const SearchPlan& p, bool lists, bool finalize) {
@@ -1851,16 +1651,6 @@ SearchWs carve_search(Carver& cv, int D, const SearchPlan& p, bool lists, bool f
     w.fail_list = cv.take<int>(nq_pad);
     w.fb_scratch = cv.take<uint2>(static_cast<int64_t>(kFbSlots) * p.parts * p.k);
     w.fb_scratch_n = cv.take<int>(static_cast<int64_t>(kFbSlots) * p.parts);
-    if (p.cm) {
-      const int64_t nc = nq_pad * p.LF;
-      w.cut_n = cv.take<int>(nq_pad);
-      w.cut_ids = cv.take<unsigned>(nc);
-      w.cut_sc = cv.take<float>(nc);
-      w.pairs = cv.take<unsigned>(nc);
-      w.blk_count = cv.take<int>(p.nblk);
-      w.blk_start = cv.take<int>(p.nblk + 1);
-      w.grp_off = cv.take<int>(ceil_div(nq_pad, kCmGroup) * p.nblk);
-    }
   }
   return w;
 }
@@ -1933,52 +1723,13 @@ int launch_finalize(const FinalArgs& fa, int64_t nq, const SearchPlan& p, hipStr
   }
 }
 
-template <int NW>
-int launch_cm_final(const CmArgs& ca, int64_t nq, const SearchPlan& p, hipStream_t st) {
-  const size_t shm = final_lds_bytes(p.LF, p.P, NW);
-  if (shm > 65536)
-    TT_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(cm_final_kernel<NW>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(shm)));
-  hipLaunchKernelGGL(cm_final_kernel<NW>, dim3(nq), dim3(NW * kWave), shm, st, ca);
-  TT_CHECK_LAUNCH();
-  return TT_OK;
-}
-
-// after the finalize's select + cut (fa.cut_n): bucket, rescore, rank
-int run_cm(const CmArgs& ca, int64_t nq, const SearchPlan& p, bool qv4, hipStream_t st) {
-  const int ngrp = static_cast<int>(ceil_div(nq, kCmGroup));
-  const size_t hshm = static_cast<size_t>(p.nblk) * sizeof(unsigned);
-  if (hshm > 65536) return fail(TT_ERR_UNSUPPORTED, "candidate-major rescoring: %d blocks", p.nblk);
-  hipLaunchKernelGGL(cm_count_kernel, dim3(ngrp), dim3(256), hshm, st, ca);
-  TT_CHECK_LAUNCH();
-  hipLaunchKernelGGL(cm_scan_kernel, dim3(1), dim3(1024), 0, st, ca);
-  TT_CHECK_LAUNCH();
-  hipLaunchKernelGGL(cm_scatter_kernel, dim3(ngrp), dim3(256), hshm, st, ca);
-  TT_CHECK_LAUNCH();
-  const size_t rshm = static_cast<size_t>(kCmRows) * cm_stride(ca.dim) * sizeof(float);
-  if (qv4)
-    hipLaunchKernelGGL(cm_rescore_kernel<true>, dim3(p.nblk), dim3(256), rshm, st, ca);
-  else
-    hipLaunchKernelGGL(cm_rescore_kernel<false>, dim3(p.nblk), dim3(256), rshm, st, ca);
-  TT_CHECK_LAUNCH();
-  switch (p.NW) {
-    case 4: return launch_cm_final<4>(ca, nq, p, st);
-    case 2: return launch_cm_final<2>(ca, nq, p, st);
-    default: return launch_cm_final<1>(ca, nq, p, st);
-  }
-}
-
-int run_finalize(const FinalArgs& fa, const FallbackArgs& fb, int64_t nq, const SearchPlan& p, hipStream_t st,
-                 const CmArgs* ca = nullptr, bool qv4 = false) {
+int run_finalize(const FinalArgs& fa, const FallbackArgs& fb, int64_t nq, const SearchPlan& p, hipStream_t st) {
   const size_t fshm = fallback_lds_bytes(p.L, p.P, p.parts, p.k);
   if (fshm > 65536)
     TT_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fallback_kernel),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(fshm)));
   probe_begin(TT_PROBE_INDEX_FINALIZE, st);
-  if (ca) TT_CHECK_HIP(hipMemsetAsync(ca->blk_count, 0, static_cast<size_t>(p.nblk) * sizeof(int), st));
   if (int rc = launch_finalize(fa, nq, p, st)) return rc;
-  if (ca)
-    if (int rc = run_cm(*ca, nq, p, qv4, st)) return rc;
   probe_end(TT_PROBE_INDEX_FINALIZE, st);
   hipLaunchKernelGGL(fallback_kernel, dim3(kFbGrid), dim3(kFbWaves * kWave), fshm, st, fb);
   TT_CHECK_LAUNCH();
@@ -2061,15 +1812,11 @@ extern "C" int tt_bruteforce_search(const void* index, const float* cand, int64_
     Lists ls{w.buf, w.count, w.tau, p.S, p.cap, nullptr, p.S, 1};
     FinalArgs fa{qc, ldq, cand, ldc, n_cand, index_offset, index_offset, dim, k, p.LF, p.P, vec4,
                  nq, w.qflags, w.qmarg, ls, out_scores + q0 * k, out_idx + q0 * k, w.fail_count, w.fail_list,
-                 nullptr, nullptr, p.cm ? w.cut_n : nullptr, p.cm ? w.cut_ids : nullptr};
+                 nullptr, nullptr};
     FallbackArgs fb{qc, ldq, cand, ldc, n_cand, index_offset, dim, k, p.L, p.P, p.parts, vec4,
                     w.fail_count, w.fail_list, w.fail_count + 1, w.fb_scratch, w.fb_scratch_n,
                     out_scores + q0 * k, out_idx + q0 * k};
-    const CmArgs ca{qc, ldq, cand, ldc, n_cand, index_offset, dim, k, p.LF, p.P, p.nblk, vec4, nq,
-                    w.cut_n, w.cut_ids, w.cut_sc, w.blk_count, w.blk_start, w.grp_off, w.pairs,
-                    out_scores + q0 * k, out_idx + q0 * k};
-    const bool qv4 = is_vec4(qc, ldq, dim);
-    if (int rc = run_finalize(fa, fb, nq, p, st, p.cm ? &ca : nullptr, qv4)) return rc;
+    if (int rc = run_finalize(fa, fb, nq, p, st)) return rc;
   }
   return TT_OK;
 }
