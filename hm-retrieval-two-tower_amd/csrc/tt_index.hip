@@ -1265,6 +1265,11 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
   } else {
     gsync<NW>();  // pre read by all before the select clears the bins
   }
+#if defined(TT_FINAL_STOP) && TT_FINAL_STOP == 1  // timing probe: phases up to here only
+  for (int j = t; j < K; j += NT) out_s[j] = sc[j];
+  return;
+#endif
+
   if (!fail) {
     // K-th largest screened score to a 24-bit key prefix (rounded down)
     const Kth r = radix_select<NW>(
@@ -1300,6 +1305,11 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
     if (t == 0) a.kth_lb[q] = fail ? -INFINITY : X;
     return;
   }
+#if defined(TT_FINAL_STOP) && TT_FINAL_STOP == 2  // timing probe: phases up to here only
+  for (int j = t; j < K; j += NT) out_s[j] = sc[j];
+  return;
+#endif
+
   // a member of the global top-K scores >= floor: only those can matter
   if (a.floor) X = fmaxf(X, a.floor[q]);
   int n = 0, par = 0;
@@ -1344,11 +1354,15 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
     return;
   }
   if (t == 0) TT_STAT(2, n);
+#if defined(TT_FINAL_STOP) && TT_FINAL_STOP == 3  // timing probe: phases up to here only
+  for (int j = t; j < K; j += NT) out_s[j] = sc[j];
+  return;
+#endif
   unsigned emin = 0xFFFFFFFFu, emax = 0u;
   for (int j = t; j < n; j += NT) {
     const int64_t row = static_cast<int64_t>(id[j]) - a.cand_offset;
-#ifdef TT_FINAL_NORESCORE  // timing probe only: no candidate rows read (results wrong)
-    sc[j] = static_cast<float>(row & 1023);
+#ifdef TT_FINAL_NORESCORE  // timing probe only: no candidate rows read (results wrong, no ties)
+    sc[j] = static_cast<float>(row);
 #else
     sc[j] = exact_score(qs, a.cand + row * a.ldc, a.dim, a.vec4 != 0) + 0.0f;
 #endif
@@ -1357,8 +1371,17 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
     emax = max(emax, k);
   }
   group_minmax<NW>(emin, emax, wcnt);
+#if defined(TT_FINAL_STOP) && TT_FINAL_STOP == 4  // timing probe: phases up to here only
+  for (int j = t; j < K; j += NT) out_s[j] = sc[j];
+  return;
+#endif
   float kth;
   n = exact_select<NW>(sc, id, n, K, &kth, hist, aux, emin, emax);
+#if defined(TT_FINAL_STOP) && TT_FINAL_STOP == 5  // timing probe: phases up to here only
+  for (int j = t; j < K; j += NT) out_s[j] = sc[j];
+  return;
+#endif
+
   rank_and_write<NW>(sc, id, n, min(n, K), a.P, sk, out_s, out_i);
   // with a floor fewer than K may remain: pad (sorts after every real entry)
   for (int j = n + t; j < K; j += NT) {
