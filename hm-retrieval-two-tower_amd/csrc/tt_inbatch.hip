@@ -342,9 +342,15 @@ __global__ void __launch_bounds__(kThreads, 2) inbatch_pass_kernel(const PassArg
   const int64_t wave_row0 = static_cast<int64_t>(blockIdx.x) * kRowsPerWG + wave * kRowsPerWave;
   // (the test is on wave-uniform scalars; a lane holds its positive in at
   // most one register, found from the row's digits: no 64-bit lane math)
+  // The tiles [td_lo, td_hi] of the split that hold them (empty: td_lo > td_hi).
+  const int64_t dlo = wave_row0 + a.diag_off - s_begin;  // first positive, as a column of the split
+  const int64_t dhi = dlo + kRowsPerWave - 1, send = static_cast<int64_t>(ntiles) * kTile;
+  const bool dnone = dhi < 0 || dlo >= send;
+  const int td_lo = dnone ? 1 : static_cast<int>(max(dlo, int64_t{0}) / kTile);
+  const int td_hi = dnone ? 0 : static_cast<int>(min(dhi, send - 1) / kTile);
   auto mask_diag = [&](f32x16* sacc, int tile) {
-    const int64_t lo = wave_row0 + a.diag_off - (s_begin + static_cast<int64_t>(tile) * kTile);
-    if (lo + kRowsPerWave <= 0 || lo >= kTile) return;
+    if (tile < td_lo || tile > td_hi) return;
+    const int64_t lo = dlo - static_cast<int64_t>(tile) * kTile;
     const int d = static_cast<int>(lo) + l32;  // this lane's positive, as a row of the tile
     const bool mine = d >= 0 && d < kTile && ((d >> 2) & 1) == h;
     const int kd = mine ? 16 * (d >> 5) + 4 * ((d >> 3) & 3) + (d & 3) : -1;  // its register
@@ -434,8 +440,6 @@ __global__ void __launch_bounds__(kThreads, 2) inbatch_pass_kernel(const PassArg
       __builtin_amdgcn_sched_barrier(0);
     }
 
-    if (tile + 1 < ntiles) mask_diag(sn, tile + 1);
-
     // Region B: O^T += X^T . P^T of this tile || row sums, next tile's max.
     float mxa = -INFINITY;
 #pragma unroll
@@ -443,6 +447,10 @@ __global__ void __launch_bounds__(kThreads, 2) inbatch_pass_kernel(const PassArg
       prefetch(NS + j + AHEAD);
       o[j % G::DT] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[(NS + j) % (AHEAD + 1)], pf[j / G::DT], o[j % G::DT],
                                                               0, 0, 0);
+      // S(tile+1)'s positives out, half way through: its MFMAs have landed
+      // by now (masked right after region A the wave waited for them: +4 %
+      // per pass), and the next max below reads them after
+      if (j == MX0) mask_diag(sn, tile + 1);
       if constexpr (MODE == 0) {
 #pragma unroll
         for (int k = j * EPP; k < (j + 1) * EPP; ++k) l_run += sc[k >> 4][k & 15];
