@@ -540,7 +540,8 @@ class ShardedTables:
         _a2a(recv, pend["send"][:R], r_split, s_split, pend["group"])
         tags, rows, tids = self.ops.route_owner(recv, W, T)
         return _Route(s_split=s_split, r_split=r_split, R=R, n_recv=int(sum(r_split)), tags=tags, rows=rows,
-                      table_ids=list(tids.unbind(0)), idx=list(pend["idx"].unbind(0)), dev=pend["dev"])
+                      table_ids=list(tids.unbind(0)), idx=list(pend["idx"].unbind(0)), idx_all=pend["idx"],
+                      dev=pend["dev"])
 
     # -- forward -----------------------------------------------------------
     def fetch_routed(self, rt: _Route, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -629,12 +630,13 @@ class ShardedTrainStep:
          MLPs + fused in-batch loss forward and backward, the per-request
          gradient sums of the sharded tables and the dense gradients of the
          small ones (ONE tt_sparse_scatter_sum: one sort), packed with the MLP
-         gradients and the loss into one bucket — replayed as a hipGraph
-         from the second step on;
+         gradients and the loss into one bucket, one all_reduce of the bucket,
+         then tt_dense_adagrad on the two tower MLP buffers and on ONE flat
+         buffer holding every small table — replayed as a hipGraph from the
+         second step on;
       3. one all_to_all returns the per-request sums to the owners, which
-         apply tt_sparse_adagrad to their shards;
-      4. one all_reduce of the bucket, then tt_dense_adagrad on the two tower
-         MLP buffers and on ONE flat buffer holding every small table.
+         apply tt_sparse_adagrad to their shards (outside the graph: its
+         exchange sizes vary per batch).
     Routing (dedup + owner bucketing + request exchange; ids only) of the
     NEXT batch, when passed as `next_batch`, runs on a side stream over its
     own process group while this step computes, so its host sync does not
@@ -673,11 +675,12 @@ class ShardedTrainStep:
         self.lr, self.eps, self.init = opt.learning_rate, opt.epsilon, opt.initial_accumulator_value
         self.global_negatives = bool(global_negatives)
         self.comm = (comm or BatchComm(group)) if self.global_negatives else None
-        # the global-negatives middle holds collectives: over RCCL they are
+        # the middle holds collectives (the bucket's all_reduce; the global
+        # negatives' all_gathers and reduce_scatters): over RCCL they are
         # captured into the step's hipGraph with the kernels (the default;
         # TT_SHARDED_EAGER=1 runs the middle eagerly); over gloo, whose host
         # staging synchronises, the middle runs eagerly
-        collectives = self.global_negatives and (self.world > 1 or self.comm.always)
+        collectives = self.world > 1 or (self.global_negatives and self.comm.always)
         self.use_graph = use_graph and os.environ.get("TT_SHARDED_EAGER") != "1" and not (
             collectives and _staged(group))
         big: Dict[str, torch.Tensor] = {}
@@ -766,7 +769,9 @@ class ShardedTrainStep:
         dim = self.tables.dim if self.tables is not None else 1
         self._got = torch.zeros(cap, dim, dtype=torch.float32, device=dev)
         self._g_req = torch.zeros(cap, dim, dtype=torch.float32, device=dev)
-        self._idx = [torch.zeros(B, dtype=torch.int32, device=dev) for _ in lk]
+        self._idx_all = torch.zeros(max(len(lk), 1), B, dtype=torch.int32, device=dev)  # one copy per step
+        self._idx = list(self._idx_all[:len(lk)].unbind(0))
+        self._loss = torch.zeros((), dtype=torch.float32, device=dev)
         n_bucket = sum(t.dense.flat.numel() for t in m.towers) + self._small_grad.numel() + 1
         self._bucket = torch.zeros(n_bucket, dtype=torch.float32, device=dev)
 
@@ -839,6 +844,27 @@ class ShardedTrainStep:
             self.ops.scatter_sum(specs, self._B, grads[0])
         torch.cat([t.dense.flat.grad.reshape(-1) for t in m.towers]
                   + [self._small_grad, loss.detach().reshape(1)], out=self._bucket)
+        self._dense_update()
+
+    def _dense_update(self) -> None:
+        """One all_reduce of the bucket, then tt_dense_adagrad on both towers'
+        MLP buffers and the flat small-table buffer, and the loss into its
+        static scalar: the tail of the middle, so over RCCL it is captured into
+        the step's hipGraph with it (fixed shapes; the sparse tables' owner
+        apply, whose exchange sizes vary per batch, stays outside)."""
+        m = self.model
+        _all_reduce_sum(self._bucket, self.group)
+        off = 0
+        for ti, t in enumerate(m.towers):
+            n = t.dense.flat.numel()
+            self.ops.dense_adagrad(t.dense.flat.data, self._dense_acc[ti], self._bucket[off:off + n].view_as(t.dense.flat),
+                                   self.lr, self.eps)
+            off += n
+        n = self._small_grad.numel()
+        if self.small:
+            self.ops.dense_adagrad(self._small_flat, self._small_acc, self._bucket[off:off + n], self.lr, self.eps)
+        off += n
+        self._loss.copy_(self._bucket[off])
 
     # -- one step ----------------------------------------------------------
     def _route(self, batch) -> _Route:
@@ -904,8 +930,7 @@ class ShardedTrainStep:
             self._pending = None
             tm = self._tick("route_wait", tm)
             self.tables.fetch_routed(rt, out=self._got)
-            for buf, ix in zip(self._idx, rt.idx):
-                buf.copy_(ix)
+            self._idx_all[:len(self._idx)].copy_(rt.idx_all)
             tm = self._tick("fetch", tm)
         if self._graph is None and self.use_graph and self._calls >= 1 and cur is not None:
             try:
@@ -928,19 +953,7 @@ class ShardedTrainStep:
         if rt is not None:
             self.tables.apply_routed(rt, self._g_req, self.lr, self.eps)
         tm = self._tick("apply", tm)
-        _all_reduce_sum(self._bucket, self.group)
-        off = 0
-        for ti, t in enumerate(m.towers):
-            n = t.dense.flat.numel()
-            self.ops.dense_adagrad(t.dense.flat.data, self._dense_acc[ti], self._bucket[off:off + n].view_as(t.dense.flat),
-                                   self.lr, self.eps)
-            off += n
-        n = self._small_grad.numel()
-        if self.small:
-            self.ops.dense_adagrad(self._small_flat, self._small_acc, self._bucket[off:off + n], self.lr, self.eps)
-        off += n
-        loss = self._bucket[off:off + 1].reshape(()).clone()
-        tm = self._tick("dense", tm)
+        loss = self._loss.clone()
         if self._inflight:
             # routes begun in an earlier step: their counts landed long ago.  With
             # only one batch of look-ahead, finish this step's too (waits here).
