@@ -35,7 +35,12 @@ namespace tt {
 namespace {
 
 constexpr int kMlpThreads = 256;
-constexpr int kMlpBM = 64;       // rows per workgroup
+#ifndef TT_MLP_BM
+#define TT_MLP_BM 64
+#endif
+constexpr int kMlpBM = TT_MLP_BM;  // rows per workgroup (32 or 64)
+constexpr int kMlpRB = kMlpBM / 32;  // 32-row MFMA blocks per wave
+constexpr int kMlpUQ = kMlpBM / 16;  // A rows per thread per stage
 constexpr int kMlpBK = 64;       // depth per A stage (4 MFMA k-steps)
 constexpr int kMlpMaxCB = 3;     // 32-column blocks per wave (N <= 384)
 
@@ -111,11 +116,11 @@ __device__ __forceinline__ void mlp_rows_block(const MlpArgs& a, const int64_t b
   const int qrow = tid >> 4, qk = (tid & 15) * 4;
   const __amdgpu_buffer_rsrc_t da = mlp_desc(a.A + m0 * a.lda, static_cast<uint64_t>(a.M - m0) * a.lda * 4);
   const __amdgpu_buffer_rsrc_t dm = mlp_desc(HAS_MASK ? a.amask + m0 * a.ldam : a.A, static_cast<uint64_t>(a.M - m0) * a.ldam * 4);
-  f32x4 ra[2][4], rm[2][4];
+  f32x4 ra[2][kMlpUQ], rm[2][kMlpUQ];
   auto fetch_a = [&](int k0, auto slot_c) {
     constexpr int SL = decltype(slot_c)::value;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < kMlpUQ; ++u) {
       const int row = qrow + 16 * u;
       ra[SL][u] = mlp_load4(da, static_cast<unsigned>((row * a.lda + k0 + qk) * 4));
       if constexpr (HAS_MASK) rm[SL][u] = mlp_load4(dm, static_cast<unsigned>((row * a.ldam + k0 + qk) * 4));
@@ -125,7 +130,7 @@ __device__ __forceinline__ void mlp_rows_block(const MlpArgs& a, const int64_t b
     constexpr int SL = decltype(slot_c)::value;
     char* base = smem[buf];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < kMlpUQ; ++u) {
       const int row = qrow + 16 * u;
       unsigned hb[4], lb[4];
 #pragma unroll
@@ -158,9 +163,9 @@ __device__ __forceinline__ void mlp_rows_block(const MlpArgs& a, const int64_t b
     }
   };
 
-  f32x16 acc[2][NCB];
+  f32x16 acc[kMlpRB][NCB];
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb)
+  for (int rb = 0; rb < kMlpRB; ++rb)
 #pragma unroll
     for (int i = 0; i < NCB; ++i) acc[rb][i] = f32x16{};
 
@@ -188,9 +193,9 @@ __device__ __forceinline__ void mlp_rows_block(const MlpArgs& a, const int64_t b
       if (kk == 2) load_b(ks + 3, std::integral_constant<int, 1>());
       if (kk == 3) load_b(ks + 3, std::integral_constant<int, 2>());
       if (ks >= ks_end) continue;  // the zero padding of the last stage (uniform)
-      bf16x8 ah[2], al[2];
+      bf16x8 ah[kMlpRB], al[kMlpRB];
 #pragma unroll
-      for (int rb = 0; rb < 2; ++rb) {
+      for (int rb = 0; rb < kMlpRB; ++rb) {
         const int row = 32 * rb + l32, chunk = 2 * kk + h;
         ah[rb] = *reinterpret_cast<const bf16x8*>(base + a_lds_off(0, row, chunk));
         al[rb] = *reinterpret_cast<const bf16x8*>(base + a_lds_off(1, row, chunk));
@@ -198,7 +203,7 @@ __device__ __forceinline__ void mlp_rows_block(const MlpArgs& a, const int64_t b
 #pragma unroll
       for (int i = 0; i < NCB; ++i)
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb) {
+        for (int rb = 0; rb < kMlpRB; ++rb) {
           acc[rb][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[rb], bq[kk][i][0], acc[rb][i], 0, 0, 0);
           acc[rb][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[rb], bq[kk][i][1], acc[rb][i], 0, 0, 0);
           acc[rb][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[rb], bq[kk][i][0], acc[rb][i], 0, 0, 0);
@@ -225,7 +230,7 @@ __device__ __forceinline__ void mlp_rows_block(const MlpArgs& a, const int64_t b
     const int col = (wave + 4 * i) * 32 + l32;
     const float b = (a.bias && col < a.N) ? a.bias[col] : 0.0f;
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
+    for (int rb = 0; rb < kMlpRB; ++rb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         float v = acc[rb][i][r] + b;
