@@ -74,7 +74,10 @@ constexpr int kQPerWave = 64;                    // two 32-query sets
 constexpr int kQPerWG = kSWaves * kQPerWave;     // 512
 constexpr int kCTile = 64;                       // candidates per LDS tile
 constexpr int kStages = 4;                       // LDS ring depth
-constexpr int kMaxSample = 128;                  // sample tiles per split
+#ifndef TT_INDEX_MAX_SAMPLE
+#define TT_INDEX_MAX_SAMPLE 128
+#endif
+constexpr int kMaxSample = TT_INDEX_MAX_SAMPLE;  // sample tiles per split
 #ifndef TT_INDEX_MAX_SPLITS
 #define TT_INDEX_MAX_SPLITS 32
 #endif
