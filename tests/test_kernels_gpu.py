@@ -364,6 +364,23 @@ def test_bruteforce_signed_split_candidates(cuda):
     assert np.array_equal(s, rs)
 
 
+@pytest.mark.parametrize("k", [1000, 100])
+def test_bruteforce_runner_point_shape(cuda, k):
+    """The reference runner's index point at a smaller batch: the H&M article
+    count, k = max(IndexRecall ks) = 1000 (main.py:99,107; four-wave finalize
+    groups) and k = 100, one query block, so the scan runs 64 candidate splits
+    and the finalize reads 64 list segments per query as one flat index."""
+    rng = np.random.default_rng(k)
+    N, Q, E = 105542, 512, 128
+    c = np.maximum(rng.standard_normal((N, E)), 0).astype(np.float32)
+    q = np.maximum(rng.standard_normal((Q, E)), 0).astype(np.float32)
+    q[3] = 0.0
+    s, i = _search(cuda, c, q, k)
+    rs, ri, _ = oracle.bruteforce_topk(q, c, k)
+    assert np.array_equal(i, ri)
+    assert np.array_equal(s, rs)
+
+
 def test_bruteforce_zero_queries_many_splits(cuda):
     """All-zero queries against a large candidate set split across workgroups:
     every score ties at 0, the answer is the lowest k indices."""
