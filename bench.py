@@ -151,6 +151,17 @@ def dist_env():
     return ws, rank, local
 
 
+def max_over_ranks(x: float, device) -> float:
+    """The maximum of x over the ranks (the slowest rank's time); over gloo
+    (TT_BENCH_REHEARSE) through a host tensor."""
+    import torch.distributed as tdist
+
+    on = "cpu" if tdist.get_backend() == "gloo" else device
+    t = torch.tensor([x], device=on, dtype=torch.float64)
+    tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def build_model(device, rank, fused_apply: bool = False):
     from pkg.modelling.models.two_tower_model import TwoTowerModel
     from pkg.modelling.optimizer_factory import OptimizerFactory
@@ -202,9 +213,7 @@ def time_train(args, model, data, device, ws):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if ws > 1:
-        t = torch.tensor([dt], device=device, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        dt = float(t.item())
+        dt = max_over_ranks(dt, device)
     loss = float(out["loss"].item())
     # after the timed region: no sparse apply recorded refused keys
     if hasattr(step, "check_status"):
@@ -590,9 +599,7 @@ def time_index_sharded(device, n_queries: int, n_cand: int, k: int, ws: int, ran
     torch.distributed.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    t = torch.tensor([dt], device=device, dtype=torch.float64)
-    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    dt = float(t.item())
+    dt = max_over_ranks(dt, device)
     tf = 2.0 * n_queries * n_cand * E / dt / 1e12
     res = {"queries": n_queries, "candidates": n_cand, "k": k, "dim": E, "shards": ws, "seconds": dt,
            "qps": n_queries / dt, "scaling": "strong (candidates row-sharded over the ranks, all queries)",
@@ -613,9 +620,7 @@ def time_index_sharded(device, n_queries: int, n_cand: int, k: int, ws: int, ran
     torch.distributed.barrier()
     torch.cuda.synchronize()
     dq = time.perf_counter() - t0
-    t = torch.tensor([dq], device=device, dtype=torch.float64)
-    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    dq = float(t.item())
+    dq = max_over_ranks(dq, device)
     res["query_sharded"] = {"seconds": dq, "qps": n_queries / dq,
                             "scaling": "strong (queries split over the ranks, candidates replicated)",
                             "roofline_frac": 2.0 * n_queries * n_cand * E / dq / 1e12 / (MI355X_BF16_DENSE_TFLOPS * ws)}
@@ -688,9 +693,7 @@ def time_c5_sharded(device, ws: int, rank: int, steps: int = 10, rows: int = 100
             torch.cuda.synchronize()
             tdist.barrier()
             torch.cuda.synchronize()
-            t = torch.tensor([time.perf_counter() - t0], device=device, dtype=torch.float64)
-            tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-            return float(t.item()) / n
+            return max_over_ranks(time.perf_counter() - t0, device) / n
 
         sec = timed(step, steps)
         rt = st.route([("big", ids[0])])
@@ -864,14 +867,22 @@ def main():
     os.dup2(2, 1)
 
     ws, rank, local = dist_env()
+    # TT_BENCH_REHEARSE=1: a dry run of the N > 1 path on a box with fewer
+    # GPUs than ranks (ranks share the GPUs, collectives over gloo through the
+    # host); its line says so and is not a measurement
+    rehearse = os.environ.get("TT_BENCH_REHEARSE") == "1"
     if ws > 1 or args.train_mode == "sharded" or args.index_mode == "sharded":
-        torch.cuda.set_device(local)
+        dev_index = local % torch.cuda.device_count() if rehearse else local
+        torch.cuda.set_device(dev_index)
         if ws == 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29533")
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            torch.distributed.init_process_group("gloo")
+        else:
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", torch.cuda.current_device())
 
     model, data = build_model(device, rank, args.fused_apply)
@@ -935,6 +946,9 @@ def main():
         },
         "gather_roofline": gather,
     }
+    if rehearse:
+        result["rehearsal"] = "TT_BENCH_REHEARSE: ranks share GPUs over gloo; not a measurement"
+
     rp = rocprof_avg_ms("inbatch_pass_kernel<128, 0>")
     if rp is not None:
         # the profiler's dispatch timestamps (no event overhead around each launch)
