@@ -309,6 +309,8 @@ def pmc_traffic(kernel: str):
 def _graph_time(fn, reps: int) -> float:
     """ms per call of fn, `reps` calls replayed from one hipGraph between HIP
     events on the current stream (no host overhead between launches)."""
+    from pkg.modelling import hip_ops
+
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
@@ -316,7 +318,7 @@ def _graph_time(fn, reps: int) -> float:
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
-        with torch.cuda.graph(graph, stream=side):
+        with hip_ops.capture_guard(), torch.cuda.graph(graph, stream=side):
             for _ in range(reps):
                 fn()
     torch.cuda.current_stream().wait_stream(side)
@@ -426,7 +428,7 @@ def time_gather(model, data, device, B: int, reps: int = 50):
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
-            with torch.cuda.graph(graph, stream=side):
+            with hip_ops.capture_guard(), torch.cuda.graph(graph, stream=side):
                 for _ in range(reps):
                     hip_ops.gather_multi(launches, B)
         torch.cuda.current_stream().wait_stream(side)

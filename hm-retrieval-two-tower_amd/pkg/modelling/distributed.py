@@ -933,12 +933,14 @@ class ShardedTrainStep:
             self._idx_all[:len(self._idx)].copy_(rt.idx_all)
             tm = self._tick("fetch", tm)
         if self._graph is None and self.use_graph and self._calls >= 1 and cur is not None:
+            from pkg.modelling import hip_ops
+
             try:
                 g = torch.cuda.CUDAGraph()
                 # thread_local: the process group's watchdog thread polls its
                 # events during the capture; in the default global mode that
                 # poll invalidates the capture and the watchdog aborts the process
-                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                with hip_ops.capture_guard(), torch.cuda.graph(g, capture_error_mode="thread_local"):
                     self._middle()
                 self._graph = g
             except Exception as e:  # keep training eagerly (still the HIP kernels)

@@ -7,7 +7,9 @@ no CPU or eager fallback: a CPU tensor or a missing libtt.so is an error.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
+import gc
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -61,6 +63,22 @@ def _row_major(t: torch.Tensor, name: str) -> int:
     if t.dim() != 2 or (t.stride(1) != 1 and t.shape[1] > 1):
         raise ValueError(f"{name} must be 2-D with unit column stride")
     return max(t.stride(0), t.shape[1])
+
+
+@contextlib.contextmanager
+def capture_guard():
+    """Python's garbage collector off while a hipGraph is captured on this
+    thread (collected first): a collection mid-capture can run a finalizer
+    that frees device or pinned host memory or destroys an event, which the
+    runtime refuses during capture and the process aborts."""
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 class Workspace:

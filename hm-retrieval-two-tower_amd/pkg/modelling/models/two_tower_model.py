@@ -441,7 +441,7 @@ class GraphedTrainStep:
         self.graph = torch.cuda.CUDAGraph()
         # thread_local: other host threads (a process group's watchdog, the
         # dataset's order prefetch) may query events while this thread captures
-        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+        with hip_ops.capture_guard(), torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self.out = self._step()
         # what the captured pointers refer to (see reusable)
         self.optimizer = model.optimizer
