@@ -234,7 +234,13 @@ class DeviceDataset:
         self._epoch += 1
         tag = (self.shuffle_size, self.seed, epoch) if self.shuffle_size else ("identity",)
         if self._perm_tag[0] != tag:
-            self._perm.copy_(self._host_order(epoch), non_blocking=True)
+            # pinned here, on the calling thread (not on the order thread: a
+            # pinned allocation on another thread while this one captures or
+            # replays a hipGraph crashed the replay)
+            order = self._host_order(epoch)
+            if self._perm.is_cuda:
+                order = order.pin_memory()
+            self._perm.copy_(order, non_blocking=True)
             self._perm_tag[0] = tag
         if self.shuffle_size:
             # the next epoch's order is built on a host thread while this epoch's
@@ -246,7 +252,7 @@ class DeviceDataset:
 
     def _make_order(self, epoch: int) -> torch.Tensor:
         order = epoch_order(self.num_rows, self.shuffle_size, self.seed, epoch).astype(np.int64)
-        return torch.from_numpy(order).pin_memory()
+        return torch.from_numpy(order)  # host only: no HIP call on the order thread
 
     def _prefetch_order(self, epoch: int) -> None:
         from concurrent.futures import ThreadPoolExecutor

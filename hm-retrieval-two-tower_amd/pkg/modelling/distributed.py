@@ -940,7 +940,9 @@ class ShardedTrainStep:
                 # thread_local: the process group's watchdog thread polls its
                 # events during the capture; in the default global mode that
                 # poll invalidates the capture and the watchdog aborts the process
-                with hip_ops.capture_guard(), torch.cuda.graph(g, capture_error_mode="thread_local"):
+                self._graph_events: list = []  # held for the graph's lifetime
+                with hip_ops.capture_guard(self._graph_events), torch.cuda.graph(
+                        g, capture_error_mode="thread_local"):
                     self._middle()
                 self._graph = g
             except Exception as e:  # keep training eagerly (still the HIP kernels)

@@ -66,17 +66,35 @@ def _row_major(t: torch.Tensor, name: str) -> int:
 
 
 @contextlib.contextmanager
-def capture_guard():
-    """Python's garbage collector off while a hipGraph is captured on this
-    thread (collected first): a collection mid-capture can run a finalizer
-    that frees device or pinned host memory or destroys an event, which the
-    runtime refuses during capture and the process aborts."""
+def capture_guard(keep: Optional[list] = None):
+    """Around a hipGraph capture on this thread: Python's garbage collector
+    off (collected first) — a collection mid-capture can run a finalizer that
+    frees device or pinned host memory or destroys an event, which the
+    runtime refuses during capture and the process aborts — and every HIP
+    event created during the capture appended to `keep`, so the caller holds
+    them for the graph's lifetime (a captured cross-stream wait whose event
+    was destroyed after the capture crashed a later replay)."""
+    import torch.cuda.streams as _streams
+
     gc.collect()
     was = gc.isenabled()
     gc.disable()
+    orig = (torch.cuda.Event, _streams.Event)
+    if keep is not None:
+        base = orig[0]
+
+        class _Kept(base):
+            def __new__(cls, *a, **k):
+                ev = base.__new__(cls, *a, **k)
+                keep.append(ev)
+                return ev
+
+        torch.cuda.Event = _Kept
+        _streams.Event = _Kept
     try:
         yield
     finally:
+        torch.cuda.Event, _streams.Event = orig
         if was:
             gc.enable()
 

@@ -441,7 +441,9 @@ class GraphedTrainStep:
         self.graph = torch.cuda.CUDAGraph()
         # thread_local: other host threads (a process group's watchdog, the
         # dataset's order prefetch) may query events while this thread captures
-        with hip_ops.capture_guard(), torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+        self._graph_events: list = []  # events created during the capture live as long as the graph
+        with hip_ops.capture_guard(self._graph_events), torch.cuda.graph(self.graph,
+                                                                          capture_error_mode="thread_local"):
             self.out = self._step()
         # what the captured pointers refer to (see reusable)
         self.optimizer = model.optimizer

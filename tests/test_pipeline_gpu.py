@@ -12,6 +12,10 @@ rows 1 and 4).
   in-memory index gives and that the fp32 oracle top-k gives
   (brute_force.py:54-83).
 """
+import os
+import subprocess
+import sys
+
 import numpy as np
 import pytest
 import torch
@@ -79,7 +83,25 @@ def test_batch_take_past_the_epoch_is_flagged(cuda):
         dev.check_status()
 
 
+def _in_child(name: str) -> bool:
+    """Run test `name` in a fresh process (True: done here, the caller returns).
+    In the full suite on this pool (late round 4) a graphed DeviceDataset fit
+    segfaulted inside hipGraphLaunch after the earlier tests — with this tree
+    and with the library of the last tree that passed there
+    (tools/runs/gpu_s04_suite2.sh); alone it passes.  The cross-test cause is
+    open."""
+    if os.environ.get("TT_TEST_IN_CHILD") == "1":
+        return False
+    env = dict(os.environ, TT_TEST_IN_CHILD="1")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-p", "no:cacheprovider", f"{__file__}::{name}"],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    return True
+
+
 def test_graphed_device_fit_equals_eager_host_fit(cuda):
+    if _in_child("test_graphed_device_fit_equals_eager_host_fit"):
+        return
     cols = _columns(2600, 2)  # 5 full batches of 512 + a partial one
     a, b = _model(cuda, 3), _model(cuda, 3)
     ha = a.fit(EncodedDataset(cols, 512, 1000, seed=7, device=cuda), epochs=2, use_graph=False)
@@ -94,6 +116,8 @@ def test_graphed_device_fit_equals_eager_host_fit(cuda):
 
 
 def test_export_round_trip_and_retriever_on_raw_queries(cuda, tmp_path):
+    if _in_child("test_export_round_trip_and_retriever_on_raw_queries"):
+        return
     m = _model(cuda, 5)
     m.fit(DeviceDataset(_columns(2048, 5), 512, device=cuda), epochs=1, use_graph=True)
     m.save(str(tmp_path / "model") + "/")
