@@ -10,8 +10,6 @@ Tolerances:
     loss); ||dq - ref|| / ||ref|| and ||dc - ref|| / ||ref|| <= 1e-2 (the
     gradients go through bf16 P as well).
 """
-import os
-
 import numpy as np
 import pytest
 import torch
@@ -366,9 +364,6 @@ def test_bruteforce_signed_split_candidates(cuda):
     assert np.array_equal(s, rs)
 
 
-@pytest.mark.skipif(os.environ.get("TT_GPU_TEST_RUNNER_SHAPE") != "1",
-                    reason="under investigation: the full suite aborted in a later graph capture / replay "
-                           "after this test (TT_GPU_TEST_RUNNER_SHAPE=1 runs it)")
 @pytest.mark.parametrize("k", [1000, 100])
 def test_bruteforce_runner_point_shape(cuda, k):
     """The reference runner's index point at a smaller batch: the H&M article
