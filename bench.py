@@ -640,25 +640,30 @@ def time_index_sharded(device, n_queries: int, n_cand: int, k: int, ws: int, ran
     return res
 
 
-def time_c5_sharded(device, ws: int, rank: int, steps: int = 10, rows: int = 100_000_000, batch: int = 65536,
-                    D: int = 128):
+def time_c5_sharded(device, ws: int, rank: int, steps: int = 20, rows: int = 100_000_000,
+                    global_batch: int = 65536, D: int = 128):
     """BASELINE configs[4]: a 100M x 128 fp32 table row-sharded over the ranks
     (ShardedTables; global row r on rank r % G, each rank holding only its
-    rows and their Adagrad accumulator), each rank a batch of 65,536 uniform
-    ids per step (weak scaling): routing (dedup + owner buckets + count and
-    request all_to_alls), fetch (tt_gather_tagged on the owners + all_to_all
-    of rows), apply (tt_sparse_scatter_sum per request + all_to_all of the
-    sums + tt_sparse_adagrad on the owners).  Algorithmic HBM bytes per rank
-    and step: lookups x (4 B id + 2 x 4D row read/write + 4D gradient read)
-    + owner rows x 16D (param and accumulator read + write).  The
-    all_to_all share is the three data all_to_alls of the same sizes timed
-    alone."""
+    rows and their Adagrad accumulator) and a GLOBAL batch of 65,536 uniform
+    ids split over the ranks (65,536 / G per rank: the configuration as
+    stated).  A step, replayed as one hipGraph (fixed-capacity routing: no
+    host sync): routing (tt_route_requests dedup + owner buckets, tt_route_pad
+    into fixed per-owner slots, all_to_all of the requests), fetch
+    (tt_gather_tagged on the owners + all_to_all of the rows), apply
+    (tt_sparse_scatter_sum per request + all_to_all of the sums +
+    tt_sparse_adagrad on the owners).  Algorithmic HBM bytes per rank and
+    step: lookups x (4 B id + 2 x 4D row read/write + 4D gradient read) +
+    owner rows x 16D (param and accumulator read + write).  The all_to_all
+    share is the three data all_to_alls of the same sizes timed alone.  At
+    G > 1 `weak_per_rank` adds the weak-scaled variant (65,536 ids per rank)
+    as a labelled extra."""
     import torch.distributed as tdist
 
+    from pkg.modelling import hip_ops
     from pkg.modelling.distributed import ShardedTables, _a2a
 
     own = not tdist.is_initialized()
-    if own:  # N = 1: a one-rank RCCL group, so the all_to_alls are real calls
+    if own:  # N = 1: a one-rank RCCL group
         import socket
 
         sk = socket.socket()
@@ -676,59 +681,88 @@ def time_c5_sharded(device, ws: int, rank: int, steps: int = 10, rows: int = 100
             shard[s0:s0 + (1 << 24)].uniform_(-0.05, 0.05, generator=g)
         st = ShardedTables({"big": shard, "__rows__": {"big": rows}}, full_tables=False)
         del shard
-        ids = [torch.randint(0, rows, (batch,), generator=g, device=device, dtype=torch.int32) for _ in range(2)]
-        grad = torch.randn(batch, D, generator=g, device=device)
+        graphed = tdist.get_backend() == "nccl"
 
-        def step(i):
-            _, (idx,) = st.fetch([("big", ids[i % 2])])
-            st.apply([(grad, [(idx, 0)])], 0.05, 1e-7)
+        def leg(b: int) -> dict:
+            ids = [torch.randint(0, rows, (b,), generator=g, device=device, dtype=torch.int32) for _ in range(2)]
+            grad = torch.randn(b, D, generator=g, device=device)
+            sid = ids[0].clone()  # the static batch the graph reads
+            cap = st.route_capacity(1, b)
+            g_req = torch.zeros(ws * cap, D, device=device)
 
-        def timed(fn, n):
-            for i in range(2):
-                fn(i)
-            torch.cuda.synchronize()
-            tdist.barrier()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for i in range(n):
-                fn(i)
-            torch.cuda.synchronize()
-            tdist.barrier()
-            torch.cuda.synchronize()
-            return max_over_ranks(time.perf_counter() - t0, device) / n
+            def body():
+                rt = st.route_fixed([("big", sid)], cap)
+                st.fetch_routed(rt)
+                st.ops.scatter_sum([dict(table=g_req, ids=[rt.idx[0]], grad_col_offset=[0])], b, grad)
+                st.apply_routed(rt, g_req, 0.05, 1e-7)
 
-        sec = timed(step, steps)
-        rt = st.route([("big", ids[0])])
-        req = torch.zeros(rt.R, 2, dtype=torch.int32, device=device)
-        req_in = torch.empty(rt.n_recv, 2, dtype=torch.int32, device=device)
-        rows_out = torch.empty(rt.n_recv, D, device=device)
-        rows_in = torch.empty(rt.R, D, device=device)
-        grads_in = torch.empty(rt.n_recv, D, device=device)
-        group = st.group
+            body()  # eager: code, workspaces
+            graph = None
+            if graphed:
+                graph = torch.cuda.CUDAGraph()
+                with hip_ops.capture_guard(), torch.cuda.graph(graph, capture_error_mode="thread_local"):
+                    body()
 
-        def a2a(_):
-            _a2a(req_in, req, rt.r_split, rt.s_split, group)
-            _a2a(rows_in, rows_out, rt.s_split, rt.r_split, group)
-            _a2a(grads_in, rows_in, rt.r_split, rt.s_split, group)
+            def step(i):
+                sid.copy_(ids[i % 2])
+                graph.replay() if graph is not None else body()
 
-        a2a_sec = timed(a2a, steps)
-        nbytes = batch * (4 + 12 * D) + rt.n_recv * 16 * D
-        gbs = ws * nbytes / sec / 1e9
-        res = {"rows": rows, "dim": D, "ranks": ws, "batch_per_rank": batch, "rows_per_rank": n_local,
-               "requests_per_rank": rt.R, "owner_rows_per_rank": rt.n_recv, "ms_per_step": sec * 1e3,
-               "lookups_per_s": ws * batch / sec, "scaling": "weak (a batch of 65,536 ids per rank)",
-               "roofline": {"bound": "hbm", "achieved": gbs, "peak": MI355X_HBM_PEAK_GBS * ws, "unit": "GB/s",
-                            "frac": gbs / (MI355X_HBM_PEAK_GBS * ws),
-                            "algorithmic_bytes_per_rank_step": nbytes},
-               "all_to_all_ms": a2a_sec * 1e3, "all_to_all_share": a2a_sec / sec,
-               "note": "fetch + apply per step, eager (the route's one host sync per step included); "
-                       "uniform ids over the whole table"}
+            def timed(fn, n):
+                for i in range(2):
+                    fn(i)
+                torch.cuda.synchronize()
+                tdist.barrier()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for i in range(n):
+                    fn(i)
+                torch.cuda.synchronize()
+                tdist.barrier()
+                torch.cuda.synchronize()
+                return max_over_ranks(time.perf_counter() - t0, device) / n
+
+            sec = timed(step, steps)
+            if graph is not None:
+                graph.reset()
+            rt = st.route([("big", ids[0])])  # compact route: the real request / owner-row counts
+            rt_sizes = (rt.R, rt.n_recv)
+            slots = ws * cap
+            req = torch.zeros(slots, 2, dtype=torch.int32, device=device)
+            req_in = torch.empty(slots, 2, dtype=torch.int32, device=device)
+            rows_out = torch.empty(slots, D, device=device)
+            rows_in = torch.empty(slots, D, device=device)
+            grads_in = torch.empty(slots, D, device=device)
+            split = [cap] * ws
+
+            def a2a(_):
+                _a2a(req_in, req, split, split, st.group)
+                _a2a(rows_in, rows_out, split, split, st.group)
+                _a2a(grads_in, rows_in, split, split, st.group)
+
+            a2a_sec = timed(a2a, steps)
+            nbytes = b * (4 + 12 * D) + rt_sizes[1] * 16 * D
+            gbs = ws * nbytes / sec / 1e9
+            return {"batch_per_rank": b, "requests_per_rank": rt_sizes[0], "owner_rows_per_rank": rt_sizes[1],
+                    "slots_per_owner": cap, "ms_per_step": sec * 1e3, "lookups_per_s": ws * b / sec,
+                    "roofline": {"bound": "hbm", "achieved": gbs, "peak": MI355X_HBM_PEAK_GBS * ws, "unit": "GB/s",
+                                 "frac": gbs / (MI355X_HBM_PEAK_GBS * ws), "algorithmic_bytes_per_rank_step": nbytes},
+                    "all_to_all_ms": a2a_sec * 1e3, "all_to_all_share": a2a_sec / sec}
+
+        res = {"rows": rows, "dim": D, "ranks": ws, "rows_per_rank": n_local, "global_batch": global_batch,
+               "scaling": "strong (the global batch of 65,536 ids split over the ranks)",
+               "graphed": graphed, **leg(global_batch // ws),
+               "note": "route + fetch + apply per step as one hipGraph replay (fixed-capacity routing, no host "
+                       "sync); uniform ids over the whole table"}
+        if ws > 1:
+            res["weak_per_rank"] = {"scaling": "weak (65,536 ids per rank; labelled extra)", **leg(global_batch)}
         del st
         torch.cuda.empty_cache()
         return res
     finally:
         if own:
-            tdist.destroy_process_group()
+            from pkg.modelling.distributed import destroy_process_group
+
+            destroy_process_group()
 
 
 def time_pipeline(model, data, device, rows: int, B: int, encode_n: int = 2_000_000):
@@ -973,7 +1007,9 @@ def main():
         sys.stdout.flush()
         os.write(real_stdout, (json.dumps(result) + "\n").encode())
     if torch.distributed.is_initialized():
-        torch.distributed.destroy_process_group()
+        from pkg.modelling.distributed import destroy_process_group
+
+        destroy_process_group()  # captured step graphs (RCCL collectives) released first
 
 
 if __name__ == "__main__":

@@ -152,6 +152,53 @@ __global__ void __launch_bounds__(256) route_owner_kernel(const int32_t* recv, i
   for (int t = 0; t < num_tags; ++t) table_ids[t * n + j] = (t == tag) ? row : -1;
 }
 
+// Fixed per-owner slots (tt_route_pad): every block computes the owners'
+// start offsets in LDS from the device counts (world <= kMaxWorld), then one
+// thread per padded slot copies its request (or writes the (-1, -1) filler)
+// and one thread per lookup rewrites its request index to the padded slot.
+__global__ void __launch_bounds__(256) route_pad_kernel(const int32_t* send, const long long* counts,
+                                                        const int32_t* idx, int64_t num_lookups, int32_t world,
+                                                        int64_t cap, int32_t* send_padded, int32_t* idx_padded,
+                                                        int32_t* overflow) {
+  __shared__ long long start[kMaxWorld + 1];
+  if (threadIdx.x == 0) {
+    long long run = 0;
+    for (int o = 0; o < world; ++o) {
+      start[o] = run;
+      run += counts[o];
+    }
+    start[world] = run;
+  }
+  __syncthreads();
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  const int64_t slots = static_cast<int64_t>(world) * cap;
+  if (t < slots) {
+    const int o = static_cast<int>(t / cap);
+    const int64_t j = t - static_cast<int64_t>(o) * cap;
+    const long long n = start[o + 1] - start[o];
+    int32_t row = -1, tag = -1;
+    if (j < n) {
+      const long long u = start[o] + j;
+      row = send[2 * u];
+      tag = send[2 * u + 1];
+    }
+    send_padded[2 * t] = row;
+    send_padded[2 * t + 1] = tag;
+    if (j == cap - 1 && n > cap && overflow) atomicAdd(overflow, static_cast<int32_t>(n - cap));
+  }
+  if (t < num_lookups) {
+    const long long u = idx[t];
+    int lo = 0, hi = world - 1;  // the owner o with start[o] <= u < start[o + 1]
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (start[mid] <= u) lo = mid; else hi = mid - 1;
+    }
+    long long j = u - start[lo];
+    if (j >= cap) j = cap - 1;  // dropped request (counted in *overflow): a defined slot
+    idx_padded[t] = static_cast<int32_t>(static_cast<int64_t>(lo) * cap + j);
+  }
+}
+
 int bits_for(int64_t x) {  // bits needed to represent values in [0, x]
   int b = 1;
   while ((int64_t(1) << b) <= x) ++b;
@@ -280,6 +327,22 @@ extern "C" int tt_route_owner(const int32_t* recv, int64_t n, int32_t world, int
   TT_REQUIRE(recv && tags && rows && table_ids, "tt_route_owner: NULL pointer");
   hipLaunchKernelGGL(route_owner_kernel, dim3(static_cast<unsigned>(ceil_div(n, 256))), dim3(256), 0,
                      to_stream(stream), recv, n, world, num_tags, tags, rows, table_ids);
+  TT_CHECK_LAUNCH();
+  return TT_OK;
+}
+
+extern "C" int tt_route_pad(const int32_t* send, const long long* counts, const int32_t* idx, int64_t num_lookups,
+                            int32_t world, int64_t cap, int32_t* send_padded, int32_t* idx_padded, int32_t* overflow,
+                            tt_stream_t stream) {
+  clear_error();
+  TT_REQUIRE(send && counts && idx && send_padded && idx_padded, "tt_route_pad: NULL pointer");
+  TT_REQUIRE(world >= 1 && world <= kMaxWorld, "tt_route_pad: world %d out of range", world);
+  TT_REQUIRE(cap >= 1 && num_lookups >= 1, "tt_route_pad: cap %lld / lookups %lld must be >= 1",
+             static_cast<long long>(cap), static_cast<long long>(num_lookups));
+  TT_REQUIRE(static_cast<int64_t>(world) * cap < (int64_t(1) << 31), "tt_route_pad: world * cap exceeds int32");
+  const int64_t n = std::max<int64_t>(static_cast<int64_t>(world) * cap, num_lookups);
+  hipLaunchKernelGGL(route_pad_kernel, dim3(static_cast<unsigned>(ceil_div(n, 256))), dim3(256), 0, to_stream(stream),
+                     send, counts, idx, num_lookups, world, cap, send_padded, idx_padded, overflow);
   TT_CHECK_LAUNCH();
   return TT_OK;
 }

@@ -32,6 +32,7 @@ from __future__ import annotations
 import logging
 import os
 import time
+import weakref
 from dataclasses import dataclass
 from typing import Any, Callable, Dict, Iterable, List, Optional, Sequence, Tuple
 
@@ -42,7 +43,22 @@ import torch.distributed as dist
 logger = logging.getLogger(__name__)
 
 __all__ = ["IndexOps", "BatchComm", "ShardedBruteForceIndex", "QueryShardedBruteForceIndex", "shard_range", "all_gather_cat",
-           "EmbeddingOps", "ShardedTables", "ShardedTrainStep"]
+           "EmbeddingOps", "ShardedTables", "ShardedTrainStep", "destroy_process_group"]
+
+# every ShardedTrainStep alive: its captured graph may hold RCCL collectives
+# and must be destroyed while their communicator still exists
+_LIVE_STEPS: "weakref.WeakSet" = weakref.WeakSet()
+
+
+def destroy_process_group(group=None) -> None:
+    """torch.distributed.destroy_process_group, after releasing the captured
+    graphs of every live ShardedTrainStep (ShardedTrainStep.close).  A hipGraph
+    holding RCCL collectives that is destroyed after its communicator corrupted
+    the host heap: a later, unrelated graph replay segfaulted inside
+    hipGraphLaunch on a freed vector of the runtime."""
+    for step in list(_LIVE_STEPS):
+        step.close()
+    dist.destroy_process_group(group)
 
 
 def all_gather_cat(t: torch.Tensor, group=None) -> torch.Tensor:
@@ -350,6 +366,25 @@ def torch_route_requests(lookups: List[Tuple[torch.Tensor, int, int]], world: in
     return send, counts, torch.tensor([R], dtype=torch.int32, device=dev), idx
 
 
+def torch_route_pad(send: torch.Tensor, counts: torch.Tensor, idx: torch.Tensor, world: int, cap: int,
+                    overflow: Optional[torch.Tensor] = None):
+    """Restatement of tt_route_pad in torch ops (the CPU/gloo tests'
+    implementation): (send_padded [world*cap, 2], idx_padded)."""
+    c = [int(v) for v in counts.tolist()]
+    start = np.concatenate([[0], np.cumsum(c)]).astype(np.int64)
+    send_p = torch.full((world * cap, 2), -1, dtype=torch.int32, device=send.device)
+    for o in range(world):
+        n = min(c[o], cap)
+        send_p[o * cap:o * cap + n] = send[start[o]:start[o] + n]
+    st = torch.as_tensor(start[:-1], device=idx.device)
+    u = idx.reshape(-1).to(torch.int64)
+    own = torch.searchsorted(st, u, right=True) - 1
+    j = torch.clamp(u - st[own], max=cap - 1)
+    if overflow is not None:
+        overflow += sum(max(0, v - cap) for v in c)
+    return send_p, (own * cap + j).to(torch.int32).reshape(idx.shape)
+
+
 def torch_route_owner(recv: torch.Tensor, world: int, num_tags: int):
     tags = recv[:, 1].contiguous()
     gid = recv[:, 0]
@@ -369,6 +404,7 @@ class EmbeddingOps:
     dense_adagrad: Callable[..., None]
     route_requests: Callable[..., Any] = torch_route_requests
     route_owner: Callable[..., Any] = torch_route_owner
+    route_pad: Callable[..., Any] = torch_route_pad
 
     @staticmethod
     def hip() -> "EmbeddingOps":
@@ -381,10 +417,15 @@ class EmbeddingOps:
                             lambda specs, b, g: hip_ops.sparse_scatter_sum(specs, b, g, ws_tag="sparse_mid"),
                             lambda specs, b, g, lr, eps: hip_ops.sparse_adagrad(specs, b, g, lr, eps,
                                                                                 ws_tag="sparse_owner"),
-                            hip_ops.dense_adagrad, hip_ops.route_requests, hip_ops.route_owner)
+                            hip_ops.dense_adagrad, hip_ops.route_requests, hip_ops.route_owner,
+                            hip_ops.route_pad)
 
 
 def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits: List[int], in_splits: List[int], group) -> torch.Tensor:
+    if dist.get_world_size(group) == 1:  # one rank: the exchange is the identity
+        if out.numel():
+            out.copy_(inp)
+        return out
     if _staged(group) and inp.is_cuda:  # gloo: through the host
         h = torch.empty(out.shape, dtype=out.dtype)
         dist.all_to_all_single(h, inp.cpu(), out_splits, in_splits, group=group)
@@ -395,6 +436,8 @@ def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits: List[int], in_splits:
 
 
 def _all_reduce_sum(t: torch.Tensor, group) -> None:
+    if dist.get_world_size(group) == 1:  # one rank: the sum is the tensor
+        return
     if _staged(group) and t.is_cuda:
         h = t.cpu()
         dist.all_reduce(h, group=group)
@@ -543,6 +586,33 @@ class ShardedTables:
                       table_ids=list(tids.unbind(0)), idx=list(pend["idx"].unbind(0)), idx_all=pend["idx"],
                       dev=pend["dev"])
 
+    def route_capacity(self, num_lookups: int, batch: int) -> int:
+        """Requests one rank can send one owner, at most: every lookup
+        distinct, capped by the rows a table can have on one owner."""
+        return max(1, num_lookups * batch)
+
+    def route_fixed(self, lookups: List[Tuple[str, torch.Tensor]], cap: int, group=None,
+                    overflow: Optional[torch.Tensor] = None) -> _Route:
+        """route() with `cap` fixed request slots per owner (tt_route_pad):
+        every exchange has split sizes [cap] * world, known on the host
+        before the step, so routing, fetch and apply run with no host sync
+        and can be captured into a hipGraph.  Unused slots carry (-1, -1):
+        owners answer them with zero rows and apply nothing to them.  With
+        cap = route_capacity(...) no request is ever dropped; a smaller cap
+        counts dropped requests in `overflow`."""
+        group = self.group if group is None else group
+        W, T = self.world, len(self.names)
+        dev = lookups[0][1].device
+        tagged = [(ids.reshape(-1), self.rows[name], self.names.index(name)) for name, ids in lookups]
+        send, counts, _, idx = self.ops.route_requests(tagged, W, T)
+        send_p, idx_p = self.ops.route_pad(send, counts, idx, W, cap, overflow)
+        recv = torch.empty(W * cap, 2, dtype=torch.int32, device=dev)
+        split = [cap] * W
+        _a2a(recv, send_p, split, split, group)
+        tags, rows, tids = self.ops.route_owner(recv, W, T)
+        return _Route(s_split=split, r_split=split, R=W * cap, n_recv=W * cap, tags=tags, rows=rows,
+                      table_ids=list(tids.unbind(0)), idx=list(idx_p.unbind(0)), idx_all=idx_p, dev=dev)
+
     # -- forward -----------------------------------------------------------
     def fetch_routed(self, rt: _Route, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Rows of the routed requests, [R, dim] (into out[:R] when given)."""
@@ -552,9 +622,18 @@ class ShardedTables:
         _a2a(got, reply, rt.s_split, rt.r_split, self.group)
         return got
 
-    def fetch(self, lookups: List[Tuple[str, torch.Tensor]]) -> Tuple[torch.Tensor, List[torch.Tensor]]:
+    def fetch(self, lookups: List[Tuple[str, torch.Tensor]], capacity: Optional[int] = None,
+              overflow: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, List[torch.Tensor]]:
         """lookups: (table name, ids [B] int32) -> (rows [R, dim], row index per
-        lookup [B] int32): lookup l's embedding of batch row b is rows[idx_l[b]]."""
+        lookup [B] int32): lookup l's embedding of batch row b is rows[idx_l[b]].
+        capacity: route with that many fixed slots per owner (route_fixed: no
+        host sync; "full" = route_capacity, never overflows)."""
+        if capacity is not None:
+            if capacity == "full":
+                capacity = self.route_capacity(len(lookups), lookups[0][1].numel())
+            rt = self.route_fixed(lookups, int(capacity), overflow=overflow)
+            self._ctx = rt
+            return self.fetch_routed(rt), rt.idx
         rt = self.route(lookups)
         self._ctx = rt
         return self.fetch_routed(rt), rt.idx
@@ -584,12 +663,14 @@ class ShardedTables:
         self.apply_routed(rt, g_req, lr, eps)
         self._ctx = None
 
-    def gather_full(self, name: str) -> torch.Tensor:
-        """The full table reassembled on every rank (checks / export)."""
+    def gather_full(self, name: str, accumulator: bool = False) -> torch.Tensor:
+        """The full table (or its Adagrad accumulator) reassembled on every
+        rank (checks / export)."""
         rows, W = self.rows[name], self.world
+        src = self.acc[name] if accumulator else self.shard[name]
         per = (rows + W - 1) // W
-        mine = torch.zeros(per, self.dim, dtype=torch.float32, device=self.shard[name].device)
-        mine[:self.shard[name].shape[0]] = self.shard[name]
+        mine = torch.zeros(per, self.dim, dtype=torch.float32, device=src.device)
+        mine[:src.shape[0]] = src
         parts = _all_gather_any(mine, self.group)
         full = torch.empty(rows, self.dim, dtype=torch.float32, device=mine.device)
         for r in range(W):
@@ -623,24 +704,30 @@ class ShardedTrainStep:
     as ranks are added (each owner updates only its rows), unlike gathering
     every replica's sparse gradients.
 
-    Per step, on the compute stream:
-      1. owners answer the routed row requests (tt_gather_tagged) and one
-         all_to_all brings the rows back into a static buffer;
-      2. the static middle — both towers' gathers (one tt_gather_multi), the
-         MLPs + fused in-batch loss forward and backward, the per-request
-         gradient sums of the sharded tables and the dense gradients of the
-         small ones (ONE tt_sparse_scatter_sum: one sort), packed with the MLP
-         gradients and the loss into one bucket, one all_reduce of the bucket,
-         then tt_dense_adagrad on the two tower MLP buffers and on ONE flat
-         buffer holding every small table — replayed as a hipGraph from the
-         second step on;
-      3. one all_to_all returns the per-request sums to the owners, which
-         apply tt_sparse_adagrad to their shards (outside the graph: its
-         exchange sizes vary per batch).
-    Routing (dedup + owner bucketing + request exchange; ids only) of the
-    NEXT batch, when passed as `next_batch`, runs on a side stream over its
-    own process group while this step computes, so its host sync does not
-    stall the compute stream.
+    Per step, one hipGraph replay (over RCCL; the first call runs eagerly and
+    warms every buffer) on the compute stream, with no host work but the
+    batch copy:
+      1. routing: the rank's sharded lookups deduplicated and bucketed by
+         owner (tt_route_requests), laid into `route_capacity` fixed slots per
+         owner (tt_route_pad, no host sync), one all_to_all of the requests
+         with split sizes known before the step, the owners' local rows
+         (tt_route_owner);
+      2. fetch: owners answer (tt_gather_tagged), one all_to_all brings the
+         rows back into a static buffer;
+      3. the middle — both towers' gathers (one tt_gather_multi), the MLPs +
+         fused in-batch loss forward and backward, the per-request gradient
+         sums of the sharded tables and the dense gradients of the small ones
+         (ONE tt_sparse_scatter_sum: one sort), packed with the MLP gradients
+         and the loss into one bucket, one all_reduce of the bucket, then
+         tt_dense_adagrad on the two tower MLP buffers and on ONE flat buffer
+         holding every small table;
+      4. one all_to_all returns the per-request sums to the owners, which
+         apply tt_sparse_adagrad to their shards (padding slots: nothing).
+    route_capacity (default: num_sharded_lookups x batch, the most one rank
+    can ever send one owner) trades exchange bytes for safety: a smaller
+    value sends less padding, and a step that overflows it drops requests and
+    is reported by check_status().  At world 1 the exchanges are identities
+    and the bucket's all_reduce is skipped.
 
     global_negatives=True (the reference's semantics, two_tower_model.py:
     113-122: every query row's negatives are the candidates of the GLOBAL
@@ -662,7 +749,8 @@ class ShardedTrainStep:
     """
 
     def __init__(self, model, shard_min_rows: int = 100_000, group=None, ops: Optional[EmbeddingOps] = None,
-                 use_graph: bool = True, global_negatives: bool = True, comm: Optional[BatchComm] = None):
+                 use_graph: bool = True, global_negatives: bool = True, comm: Optional[BatchComm] = None,
+                 route_capacity: Optional[int] = None):
         from pkg.modelling.optimizer_factory import Adagrad
 
         opt = model.optimizer
@@ -675,11 +763,13 @@ class ShardedTrainStep:
         self.lr, self.eps, self.init = opt.learning_rate, opt.epsilon, opt.initial_accumulator_value
         self.global_negatives = bool(global_negatives)
         self.comm = (comm or BatchComm(group)) if self.global_negatives else None
-        # the middle holds collectives (the bucket's all_reduce; the global
-        # negatives' all_gathers and reduce_scatters): over RCCL they are
-        # captured into the step's hipGraph with the kernels (the default;
-        # TT_SHARDED_EAGER=1 runs the middle eagerly); over gloo, whose host
-        # staging synchronises, the middle runs eagerly
+        # the step holds collectives (the route's and the rows' all_to_alls,
+        # the bucket's all_reduce; the global negatives' all_gathers and
+        # reduce_scatters): over RCCL they are captured into the step's
+        # hipGraph with the kernels (the default; TT_SHARDED_EAGER=1 runs the
+        # step eagerly); over gloo, whose host staging synchronises, the step
+        # runs eagerly.  At world 1 every exchange is skipped.
+        self.route_capacity = None if route_capacity is None else int(route_capacity)
         collectives = self.world > 1 or (self.global_negatives and self.comm.always)
         self.use_graph = use_graph and os.environ.get("TT_SHARDED_EAGER") != "1" and not (
             collectives and _staged(group))
@@ -714,17 +804,30 @@ class ShardedTrainStep:
             off += n
         self._small_acc = torch.full_like(self._small_flat, self.init)
         self._dense_acc = [torch.full_like(t.dense.flat, self.init) for t in model.towers]
-        self._route_group = dist.new_group(list(range(self.world)), backend=dist.get_backend(group)) \
-            if self.world > 1 else group
-        self._side = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
-        self._pending = None     # (batch object id, _Route) routed ahead (prefetch())
-        self._inflight: List[Tuple[int, dict, int]] = []  # (batch id, route_begin state, step begun)
-        self._ready: Dict[int, _Route] = {}               # batch id -> finished route
         self._static = None      # static batch / request buffers (set up on the first call)
         self._graph = None
         self._calls = 0
         self._out_grads = None
         self.host_times: Optional[Dict[str, float]] = {} if os.environ.get("TT_HOST_PROFILE") else None
+        _LIVE_STEPS.add(self)
+
+    def close(self) -> None:
+        """Release the captured step graph (the next call captures again).
+        Call it before the process group is destroyed
+        (distributed.destroy_process_group does): the graph holds the
+        group's RCCL collectives."""
+        if self._graph is not None:
+            torch.cuda.synchronize(self.model.device)
+            self._graph.reset()
+            self._graph = None
+            self._graph_events = []
+
+    def __enter__(self) -> "ShardedTrainStep":
+        return self
+
+    def __exit__(self, *exc) -> bool:
+        self.close()
+        return False
 
     def _tick(self, name: str, t0: float) -> float:
         t1 = time.perf_counter()
@@ -765,10 +868,13 @@ class ShardedTrainStep:
         lk = self._lookups(self._static)
         B = next(iter(self._static.values())).numel()
         self._B = B
-        cap = max(len(lk) * B, 1)  # distinct requests <= lookups
+        full = self.tables.route_capacity(len(lk), B) if self.tables is not None else 1
+        self._cap = full if self.route_capacity is None else max(1, min(self.route_capacity, full))
+        slots = self.world * self._cap
         dim = self.tables.dim if self.tables is not None else 1
-        self._got = torch.zeros(cap, dim, dtype=torch.float32, device=dev)
-        self._g_req = torch.zeros(cap, dim, dtype=torch.float32, device=dev)
+        self._got = torch.zeros(slots, dim, dtype=torch.float32, device=dev)
+        self._g_req = torch.zeros(slots, dim, dtype=torch.float32, device=dev)
+        self._overflow = torch.zeros(1, dtype=torch.int32, device=dev)  # dropped requests (capacity)
         self._idx_all = torch.zeros(max(len(lk), 1), B, dtype=torch.int32, device=dev)  # one copy per step
         self._idx = list(self._idx_all[:len(lk)].unbind(0))
         self._loss = torch.zeros((), dtype=torch.float32, device=dev)
@@ -867,72 +973,32 @@ class ShardedTrainStep:
         self._loss.copy_(self._bucket[off])
 
     # -- one step ----------------------------------------------------------
-    def _route(self, batch) -> _Route:
-        return self.tables.route([(k, ids) for k, ids, _, _ in self._lookups(batch)], group=self._route_group)
-
-    def _route_begin(self, batch) -> dict:
-        return self.tables.route_begin([(k, ids) for k, ids, _, _ in self._lookups(batch)], group=self._route_group)
+    def _body(self) -> None:
+        """Route, fetch, middle, owner apply on the static batch: fixed shapes
+        and no host sync, so the whole of it is captured as one graph."""
+        rt = None
+        if self.tables is not None:
+            rt = self.tables.route_fixed([(k, ids) for k, ids, _, _ in self._lookups(self._static)], self._cap,
+                                         overflow=self._overflow)
+            self.tables.fetch_routed(rt, out=self._got)
+            self._idx_all[:len(self._idx)].copy_(rt.idx_all)
+        self._middle()
+        if rt is not None:
+            self.tables.apply_routed(rt, self._g_req, self.lr, self.eps)
 
     def prefetch(self, batch) -> None:
-        """Route `batch` (the next step's) on the side stream now."""
-        if self.tables is None:
-            return
-        ready = torch.cuda.Event()
-        ready.record()  # the batch's ids exist before the work already queued here
-        with torch.cuda.stream(self._side):
-            self._side.wait_event(ready)
-            rt = self._route(batch)
-            rt.event = torch.cuda.Event()
-            rt.event.record(self._side)
-        self._pending = (id(batch), rt)
+        """Kept for API compatibility: routing runs inside the step's graph."""
 
     def __call__(self, batch: Dict[str, Any], next_batch: Optional[Dict[str, Any]] = None,
                  ahead: Optional[Sequence[Dict[str, Any]]] = None) -> Dict[str, torch.Tensor]:
-        """One step on `batch`.  `ahead` (or `next_batch`): upcoming batches in
-        order.  Their routing (ids only) starts on the side stream at the start
-        of this step and is finished (the one host sync) at the end of a LATER
-        step, so the host never waits for routing work queued behind compute:
-        with ahead=[b+1, b+2] the route of b+2 begins now and completes at the
-        end of the next step."""
-        m = self.model
+        """One step on `batch` (next_batch / ahead: accepted for API
+        compatibility and ignored — routing is part of the step's graph)."""
         tm = time.perf_counter()
         if self._static is None:
             self._setup(batch)
-        cur = torch.cuda.current_stream() if self._side is not None else None
-        upcoming = list(ahead) if ahead is not None else ([next_batch] if next_batch is not None else [])
-        if upcoming and self._side is not None and self.tables is not None:
-            known = set(self._ready) | {k for k, _, _ in self._inflight}
-            todo = [b for b in upcoming if id(b) not in known and b is not batch]
-            if todo:
-                pre = torch.cuda.Event()
-                pre.record(cur)  # the batches' ids exist before the work queued here
-                with torch.cuda.stream(self._side):
-                    self._side.wait_event(pre)
-                    for b in todo:
-                        self._inflight.append((id(b), self._route_begin(b), self._calls))
         self._load(batch)
         tm = self._tick("load", tm)
-        rt = None
-        if self.tables is not None:
-            key = id(batch)
-            if key not in self._ready and any(k == key for k, _, _ in self._inflight):
-                self._finish_routes(lambda k, step: k == key)  # needed now
-            if key in self._ready:
-                rt = self._ready.pop(key)
-            elif self._pending is not None and self._pending[0] == key:
-                rt = self._pending[1]
-            if rt is not None:
-                cur.wait_event(rt.event)
-                for t in rt.tensors():  # made on the side stream, read on this one
-                    t.record_stream(cur)
-            else:
-                rt = self._route(batch)
-            self._pending = None
-            tm = self._tick("route_wait", tm)
-            self.tables.fetch_routed(rt, out=self._got)
-            self._idx_all[:len(self._idx)].copy_(rt.idx_all)
-            tm = self._tick("fetch", tm)
-        if self._graph is None and self.use_graph and self._calls >= 1 and cur is not None:
+        if self._graph is None and self.use_graph and self._calls >= 1 and self.model.device.type == "cuda":
             from pkg.modelling import hip_ops
 
             try:
@@ -943,28 +1009,19 @@ class ShardedTrainStep:
                 self._graph_events: list = []  # held for the graph's lifetime
                 with hip_ops.capture_guard(self._graph_events), torch.cuda.graph(
                         g, capture_error_mode="thread_local"):
-                    self._middle()
+                    self._body()
                 self._graph = g
+                hip_ops.Workspace.snapshot()  # its workspaces are never freed from now on
             except Exception as e:  # keep training eagerly (still the HIP kernels)
                 logger.warning(f"ShardedTrainStep: graph capture failed ({e!r}); running eagerly")
                 self.use_graph = False
         if self._graph is not None:
             self._graph.replay()
         else:
-            self._middle()
+            self._body()
         self._calls += 1
-        tm = self._tick("middle", tm)
-        if rt is not None:
-            self.tables.apply_routed(rt, self._g_req, self.lr, self.eps)
-        tm = self._tick("apply", tm)
-        loss = self._loss.clone()
-        if self._inflight:
-            # routes begun in an earlier step: their counts landed long ago.  With
-            # only one batch of look-ahead, finish this step's too (waits here).
-            now = self._calls - 1
-            self._finish_routes(lambda k, step: step < now or len(upcoming) < 2)
-        self._tick("prefetch", tm)
-        return {"loss": loss}
+        tm = self._tick("step", tm)
+        return {"loss": self._loss.clone()}
 
     # workspaces the sharded step's sparse kernels write (EmbeddingOps.hip)
     STATUS_TAGS = ("sparse_owner", "sparse_mid")
@@ -979,19 +1036,10 @@ class ShardedTrainStep:
             from pkg.modelling import hip_ops
 
             hip_ops.sparse_status_all(self.model.device, self.STATUS_TAGS)
-
-    def _finish_routes(self, which) -> None:
-        keep = []
-        for key, pend, step in self._inflight:
-            if which(key, step):
-                with torch.cuda.stream(self._side):
-                    rt = self.tables.route_finish(pend)
-                    rt.event = torch.cuda.Event()
-                    rt.event.record(self._side)
-                    rt.keep = pend  # its device buffers stay alive until the route is used
-                self._ready[key] = rt
-                if self.host_times is not None:
-                    self.host_times["route_sync"] = self.host_times.get("route_sync", 0.0) + pend["sync_s"]
-            else:
-                keep.append((key, pend, step))
-        self._inflight = keep
+        ov = getattr(self, "_overflow", None)
+        if ov is not None:
+            n = int(ov.item())
+            ov.zero_()
+            if n:
+                raise RuntimeError(f"ShardedTrainStep: {n} row requests overflowed route_capacity={self._cap} "
+                                   "and were dropped (use the default capacity for exact steps)")

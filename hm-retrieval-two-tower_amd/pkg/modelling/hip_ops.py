@@ -33,6 +33,7 @@ __all__ = [
     "probe_arm",
     "probe_arm_repeat",
     "route_requests",
+    "route_pad",
     "route_owner",
     "bruteforce_build",
     "bruteforce_search",
@@ -110,12 +111,18 @@ class Workspace:
 
     _bufs: Dict[Tuple[int, str], torch.Tensor] = {}
     _scope = ""
+    # device addresses a captured graph may hold (snapshot()), and the buffers
+    # a regrowth replaced while a graph could still address them: never freed
+    _captured: set = set()
+    _retired: List[torch.Tensor] = []
 
     @classmethod
     def get(cls, nbytes: int, device: torch.device, tag: str) -> torch.Tensor:
         key = (device.index if device.index is not None else torch.cuda.current_device(), cls._scope + tag)
         buf = cls._bufs.get(key)
         if buf is None or buf.numel() < nbytes:
+            if buf is not None and buf.data_ptr() in cls._captured:
+                cls._retired.append(buf)  # a live graph may replay into it
             # zeroed once (a fresh sparse workspace carries no recorded error)
             buf = torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=device)
             cls._bufs[key] = buf
@@ -136,14 +143,20 @@ class Workspace:
 
     @classmethod
     def clear(cls) -> None:
+        """Forget every buffer (those a captured graph may address stay alive)."""
+        cls._retired.extend(b for b in cls._bufs.values() if b.data_ptr() in cls._captured)
         cls._bufs.clear()
 
     @classmethod
     def snapshot(cls) -> Dict[Tuple[int, str], int]:
         """{key: device address} of every buffer now allocated.  A captured
-        hipGraph holds these addresses: it may be replayed only while
-        `unchanged(snapshot)` (no buffer it may use was regrown or cleared)."""
-        return {k: v.data_ptr() for k, v in cls._bufs.items()}
+        hipGraph holds these addresses: they are never freed from now on
+        (a regrowth retires the old buffer instead), and the graph should be
+        replayed only while `unchanged(snapshot)` — the host-side readers
+        (sparse_status) look at the current buffers."""
+        snap = {k: v.data_ptr() for k, v in cls._bufs.items()}
+        cls._captured.update(snap.values())
+        return snap
 
     @classmethod
     def unchanged(cls, snap: Dict[Tuple[int, str], int]) -> bool:
@@ -373,6 +386,25 @@ def route_requests(lookups: Sequence[Tuple[torch.Tensor, int, int]], world: int,
     check(lib_.tt_route_requests(arr, L, B, world, num_tags, send.data_ptr(), counts.data_ptr(), nreq.data_ptr(),
                                  idx.data_ptr(), ws.data_ptr(), ws.numel(), _stream()))
     return send, counts, nreq, idx
+
+
+def route_pad(send: torch.Tensor, counts: torch.Tensor, idx: torch.Tensor, world: int, cap: int,
+              overflow: Optional[torch.Tensor] = None):
+    """The compact requests of route_requests in `cap` fixed slots per owner
+    (tt_route_pad): (send_padded [world*cap, 2], idx_padded like idx).  No
+    host sync; `overflow` (int32 [1], optional) counts dropped requests."""
+    _req(send, "send", torch.int32, 2)
+    _req(counts, "counts", torch.int64, 1)
+    _req(idx, "idx", torch.int32)
+    if counts.numel() != world or not idx.is_contiguous():
+        raise ValueError("route_pad: counts must be [world], idx contiguous")
+    send_p = torch.empty(world * cap, 2, dtype=torch.int32, device=send.device)
+    idx_p = torch.empty_like(idx)
+    if overflow is not None:
+        _req(overflow, "overflow", torch.int32, 1)
+    check(lib().tt_route_pad(send.data_ptr(), counts.data_ptr(), idx.data_ptr(), idx.numel(), world, cap,
+                             send_p.data_ptr(), idx_p.data_ptr(), _ptr(overflow), _stream()))
+    return send_p, idx_p
 
 
 def route_owner(recv: torch.Tensor, world: int, num_tags: int):

@@ -311,12 +311,15 @@ class TwoTowerModel(AbstractKerasModel):
         history: Dict[str, List[float]] = {"loss": []}
         B, nfull = int(ds.batch_size), ds.full_batches
         rem = ds.num_rows - nfull * B
-        graphed = getattr(self, "_device_fit_graph", None)
-        if graphed is not None and not graphed.reusable(self, ds):
-            graphed = self._device_fit_graph = None
+        graphed = None
         for epoch in range(epochs):
             ds.begin_epoch()
             todo = nfull
+            # before every epoch's replays (the eager partial batch of the last
+            # one, or other work since, may have regrown a workspace)
+            graphed = getattr(self, "_device_fit_graph", None)
+            if graphed is not None and not graphed.reusable(self, ds):
+                graphed = self._device_fit_graph = None
             if todo and graphed is None:
                 graphed = GraphedTrainStep(self, None, warmup=1, source=ds)  # warm-up = this epoch's batch 0
                 self._device_fit_graph = graphed

@@ -141,6 +141,21 @@ int tt_route_owner(const int32_t* recv, int64_t n, int32_t world,
                    int32_t num_tags, int32_t* tags, int32_t* rows,
                    int32_t* table_ids, tt_stream_t stream);
 
+/* Fixed-capacity routing (no host sync, graph-capturable): the compact
+ * owner-major requests of tt_route_requests (send, counts on the device, idx
+ * [num_lookups]) laid into `cap` slots per owner: request j of owner o at
+ * slot o*cap + j of send_padded [world*cap, 2], unused slots (-1, -1) (an
+ * owner answers them with zero rows and applies nothing); idx_padded
+ * [num_lookups] = each lookup's slot.  Every exchange of the step then has
+ * the split sizes [cap]*world.  cap = num_lookups never overflows; a smaller
+ * cap drops an owner's requests past it, adds their number to *overflow
+ * (optional, zero it first) and points their lookups at the owner's last
+ * slot. */
+int tt_route_pad(const int32_t* send, const long long* counts, const int32_t* idx,
+                 int64_t num_lookups, int32_t world, int64_t cap,
+                 int32_t* send_padded, int32_t* idx_padded, int32_t* overflow,
+                 tt_stream_t stream);
+
 /* ------------------------------------------------------------------------ *
  * K8+K9  Sparse optimizer step on embedding tables.
  * Replaces the legacy Keras optimizer's sparse path reached from

@@ -20,6 +20,24 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libtt.so on cuda:0)")
 
 
+@pytest.fixture(autouse=True)
+def _segv_backtrace():
+    """TT_SEGV_BT=<file> (diagnostic): a native backtrace of a host crash
+    appended to <file> (tools/segv_bt.c), installed ahead of faulthandler at
+    every test."""
+    if os.environ.get("TT_SEGV_BT"):
+        import ctypes
+        import gc
+
+        import torch
+
+        graphs = sum(1 for o in gc.get_objects() if isinstance(o, torch.cuda.CUDAGraph))
+        with open(os.environ["TT_SEGV_BT"], "a") as f:
+            f.write(f"[segv_bt] test start: {graphs} live CUDAGraph objects\n")
+        ctypes.CDLL(os.path.join(ROOT, "tools", "pbin", "libsegv_bt.so")).tt_segv_bt_install(os.environ["TT_SEGV_BT"].encode())
+    yield
+
+
 @pytest.fixture(scope="session")
 def cuda():
     import torch

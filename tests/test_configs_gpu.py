@@ -5,9 +5,11 @@ restatement (oracle/).
   headline: emb 128, towers [256] -> 128, batch 16384): three full train
   steps (gather, towers, fused in-batch CE, MLP backward, dense + sparse
   Adagrad), each vs oracle.CpuTwoTower started from the model's state
-  before the step: loss within 1e-3 rel of the fp32 restatement, update of
-  every table and MLP buffer within 2e-3 rel of the restatement of the
-  kernels' arithmetic contract (bf16 in-batch negatives);
+  before the step: loss within 1e-3 rel of the fp32 restatement; the
+  gradient of every table and MLP buffer, and its update measured in
+  gradient units by Adagrad's steepest slope, within 2e-3 rel of the
+  restatement of the kernels' arithmetic contract (bf16 in-batch negatives)
+  at every step (the plain update norm at steps 0-1);
 - C4: 105,542 x 128 candidates, top-100 (and the reference runner's k = 1000
   at test_batch_size 2048, /root/reference/main.py:99,107): indices and
   scores bit-exact vs the fp32 fmaf-chain oracle;
@@ -114,6 +116,13 @@ def _train_steps_vs_cpu(cuda, emb, joint, B, steps, loss_rtol, upd_rtol):
                   for layer in (m.query_tower.input_layer, m.candidate_tower.input_layer)
                   for n in layer.embedding_layers}
         mlp_before = [t.dense.flat.detach().cpu().numpy().copy() for t in m.towers]
+        # accumulators before the step (the slope of this step's Adagrad update)
+        slot_of = lambda w: (m.optimizer._slots[id(w)][0].detach() if id(w) in m.optimizer._slots
+                             else torch.full_like(w.detach(), 0.1))
+        acc_before = {n: slot_of(layer.embedding_layers[n].weight)[torch.as_tensor(rows[n], device=cuda).long()]
+                      .cpu().numpy() for layer in (m.query_tower.input_layer, m.candidate_tower.input_layer)
+                      for n in layer.embedding_layers}
+        mlp_acc_before = [slot_of(t.dense.flat).cpu().numpy().reshape(-1) for t in m.towers]
         ids = ([b[f.name].cpu().numpy() for f in qf], [b[f.name].cpu().numpy() for f in cf])
         # the GPU's own tower activations (the kernels are deterministic: the
         # step computes the same ones): the forward is checked against the
@@ -140,39 +149,46 @@ def _train_steps_vs_cpu(cuda, emb, joint, B, steps, loss_rtol, upd_rtol):
             for f, t, a in zip(feats, tabs, accs):
                 refs[f.name], racc[f.name] = t, a
         opt = m.optimizer
-        # the step's gradient, recovered from Adagrad's update (g = -d (sqrt(acc') + eps) / lr):
-        # the update itself amplifies a gradient coordinate near 0 by up to
-        # 1/sqrt(0.1) (its steepest slope) and saturates large ones
+        # the step's gradient, recovered from Adagrad's update (g = -d (sqrt(acc') + eps) / lr)
         grad_of = lambda d, acc: -d * (np.sqrt(acc) + 1e-7) / 0.05
+
+        def compare(name, d_gpu, d_ref, acc_gpu, acc_ref, acc_before):
+            """update, recovered gradient, and the update measured in gradient
+            units by Adagrad's steepest slope: u(g) = -lr g / sqrt(a + g^2) has
+            |u'| <= lr / sqrt(a) (a = the accumulator before the step), so
+            |du_j| sqrt(a_j) / lr <= |dg_j| coordinate by coordinate — the
+            update held to the gradient's tolerance at every step, whatever
+            Adagrad's slope does to small coordinates."""
+            g_ref = grad_of(d_ref, acc_ref)
+            errs[(name, step)] = np.linalg.norm(d_gpu - d_ref) / np.linalg.norm(d_ref)
+            errs[(name + ":grad", step)] = np.linalg.norm(grad_of(d_gpu, acc_gpu) - g_ref) / np.linalg.norm(g_ref)
+            errs[(name + ":upd_slope", step)] = (np.linalg.norm((d_gpu - d_ref) * np.sqrt(acc_before) / 0.05)
+                                                 / np.linalg.norm(g_ref))
+
         for layer in (m.query_tower.input_layer, m.candidate_tower.input_layer):
             for n, tab in layer.embedding_layers.items():
                 r = rows[n]
                 rt = torch.as_tensor(r, device=cuda).long()
                 got = tab.weight[rt].cpu().numpy()
-                d_gpu, d_ref = got - before[n], refs[n][r] - before[n]
-                errs[(n, step)] = np.linalg.norm(d_gpu - d_ref) / np.linalg.norm(d_ref)
-                g_gpu = grad_of(d_gpu, opt._slots[id(tab.weight)][0][rt].cpu().numpy())
-                g_ref = grad_of(d_ref, racc[n][r])
-                errs[(n + ":grad", step)] = np.linalg.norm(g_gpu - g_ref) / np.linalg.norm(g_ref)
+                compare(n, got - before[n], refs[n][r] - before[n], opt._slots[id(tab.weight)][0][rt].cpu().numpy(),
+                        racc[n][r], acc_before[n])
         flat = lambda layers: np.concatenate([np.concatenate([w.reshape(-1), bb]) for w, bb in layers])
         for ti, (t, mb, rlay, ralay) in enumerate(zip(m.towers, mlp_before, (ref.q_layers, ref.c_layers),
                                                       (ref.ql_acc, ref.cl_acc))):
-            d_gpu = t.dense.flat.detach().cpu().numpy() - mb
-            d_ref = flat(rlay) - mb
-            errs[(f"mlp{ti}", step)] = np.linalg.norm(d_gpu - d_ref) / np.linalg.norm(d_ref)
-            g_gpu = grad_of(d_gpu, opt._slots[id(t.dense.flat)][0].detach().cpu().numpy().reshape(-1))
-            g_ref = grad_of(d_ref, flat(ralay))
-            errs[(f"mlp{ti}:grad", step)] = np.linalg.norm(g_gpu - g_ref) / np.linalg.norm(g_ref)
+            compare(f"mlp{ti}", t.dense.flat.detach().cpu().numpy() - mb, flat(rlay) - mb,
+                    opt._slots[id(t.dense.flat)][0].detach().cpu().numpy().reshape(-1), flat(ralay),
+                    mlp_acc_before[ti])
         del ref
     print({f"{k[0]}@{k[1]}": f"{v:.2e}" for k, v in errs.items()})
-    # every step's gradients, and the updates of the steps before the scores
-    # blow up (Adagrad at lr 0.05 on a SUM loss makes them O(100-1000) by the
-    # third step, where the bf16 weights of nearly tied negatives round
-    # differently under the two fp32 accumulation orders — a few 1e-4 of dq —
-    # and Adagrad's slope near 0 turns that into whole-lr changes of single
-    # coordinates)
+    # every step's gradients and slope-normalised updates; the plain relative
+    # update norm at the steps before the scores blow up (Adagrad at lr 0.05
+    # on a SUM loss makes them O(100-1000) by the third step, where the bf16
+    # weights of nearly tied negatives round differently under the two fp32
+    # accumulation orders — a few 1e-4 of dq — and Adagrad's slope near 0
+    # turns that into whole-lr changes of single coordinates: the
+    # ":upd_slope" metric holds those updates instead)
     bad = {k: v for k, v in errs.items() if k[0] not in ("loss", "fwd") and not v <= upd_rtol
-           and (k[0].endswith(":grad") or k[1] < 2)}
+           and (":" in k[0] or k[1] < 2)}
     assert not bad, bad
     m.optimizer.check_status(cuda)
     return errs
@@ -217,6 +233,8 @@ def test_c5_100m_row_table_world1(cuda):
     (bit-exact, same block summation order), untouched rows unchanged."""
     import torch.distributed as dist
 
+    from pkg.modelling.distributed import destroy_process_group
+
     from pkg.modelling.distributed import ShardedTables
 
     s = socket.socket()
@@ -257,5 +275,5 @@ def test_c5_100m_row_table_world1(cuda):
         assert torch.equal(st.shard["big"][:64][torch.as_tensor(mask, device=cuda)],
                            before_untouched[torch.as_tensor(mask, device=cuda)])
     finally:
-        dist.destroy_process_group()
+        destroy_process_group()  # the captured step graphs first, then the group
         torch.cuda.empty_cache()

@@ -196,14 +196,19 @@ def _sharded_worker(rank, world, port, tables, lookups, grads, out):
     _init(rank, world, port)
     from pkg.modelling.distributed import ShardedTables
 
-    st = ShardedTables({k: torch.from_numpy(v) for k, v in tables.items()}, 0.1, ops=_cpu_embedding_ops())
     lk = [(name, torch.from_numpy(ids[rank])) for name, ids in lookups]
-    got, idx = st.fetch(lk)
-    fwd = [got[i.long()].numpy() for i in idx]
-    # gradient matrix of this rank: one [B, 16 * L] block, lookup l at column 16 l
-    g = torch.from_numpy(grads[rank])
-    st.apply([(g, [(idx[l], 16 * l) for l in range(len(lk))])], lr=0.05, eps=1e-7)
-    out[rank] = (fwd, {k: st.gather_full(k).numpy() for k in tables})
+    g = torch.from_numpy(grads[rank])  # this rank's [B, 16 * L] gradients, lookup l at column 16 l
+    res = {}
+    # compact routing (host-known counts), the fixed-capacity routing at the
+    # never-overflowing capacity, and at a capacity too small for the batch
+    for mode, cap in (("compact", None), ("fixed", "full"), ("small", 5)):
+        st = ShardedTables({k: torch.from_numpy(v) for k, v in tables.items()}, 0.1, ops=_cpu_embedding_ops())
+        ov = torch.zeros(1, dtype=torch.int32)
+        got, idx = st.fetch(lk, capacity=cap, overflow=ov)
+        fwd = [got[i.long()].numpy() for i in idx]
+        st.apply([(g, [(idx[l], 16 * l) for l in range(len(lk))])], lr=0.05, eps=1e-7)
+        res[mode] = (fwd, {k: st.gather_full(k).numpy() for k in tables}, int(ov.item()))
+    out[rank] = res
     dist.destroy_process_group()
 
 
@@ -229,7 +234,7 @@ def test_sharded_tables_match_unsharded_adagrad(world):
             # forward rows equal the unsharded gather (zeros for invalid ids)
             exp = np.zeros((B, D), np.float32)
             exp[ok] = tables[name][idsl[r][ok]]
-            assert np.array_equal(out[r][0][l], exp)
+            assert np.array_equal(out[r]["compact"][0][l], exp)
             np.add.at(gsum[name], idsl[r][ok], grads[r][ok, 16 * l:16 * l + D])
     for k in ref:
         touched = np.abs(gsum[k]).sum(1) > 0
@@ -237,7 +242,23 @@ def test_sharded_tables_match_unsharded_adagrad(world):
         upd = ref[k] - 0.05 * gsum[k] / (np.sqrt(a) + 1e-7)
         ref[k] = np.where(touched[:, None], upd, ref[k])
         for r in range(world):
-            np.testing.assert_allclose(out[r][1][k], ref[k], rtol=0, atol=2e-6)
+            np.testing.assert_allclose(out[r]["compact"][1][k], ref[k], rtol=0, atol=2e-6)
+    for r in range(world):
+        # fixed slots per owner, no host-known counts: the same rows and updates, bit for bit
+        fc, ff = out[r]["compact"], out[r]["fixed"]
+        assert ff[2] == 0
+        assert all(np.array_equal(x, y) for x, y in zip(ff[0], fc[0]))
+        assert all(np.array_equal(ff[1][k], fc[1][k]) for k in tables)
+        # a capacity of 5 slots per owner drops requests and counts them: the
+        # distinct (table, row) requests of this rank per owner, minus 5
+        reqs = {}
+        for name, idsl in lookups:
+            n = tables[name].shape[0]
+            for v in np.unique(idsl[r]):
+                key = (name, int(v)) if 0 <= v < n else (name, -1)
+                reqs[key] = (int(v) % world) if 0 <= v < n else world - 1
+        per_owner = np.bincount(list(reqs.values()), minlength=world)
+        assert out[r]["small"][2] == int(np.maximum(per_owner - 5, 0).sum()) > 0
 
 
 def _global_loss_worker(rank, world, port, q, c, logq, out):

@@ -123,6 +123,26 @@ def _global_batches(steps, B):
     return [{"cust": z(301), "post": z(51), "art": z(301), "ptn": z(21)} for _ in range(steps)]
 
 
+def _sharded_state(step, m):
+    """Every parameter and Adagrad accumulator of the sharded step's model,
+    reassembled full-size on every rank: tower MLP buffers, small tables
+    (views of the step's flat buffers), row-sharded tables (gather_full)."""
+    flats = [(t.dense.flat.detach().cpu().numpy().copy(), step._dense_acc[ti].cpu().numpy().copy())
+             for ti, t in enumerate(m.towers)]
+    tables = {}
+    for ti, t in enumerate(m.towers):
+        for name, e in t.input_layer.embedding_layers.items():
+            if hasattr(e, "_shard_key"):
+                w = step.tables.gather_full(e._shard_key)
+                a = step.tables.gather_full(e._shard_key, accumulator=True)
+            else:
+                off = (e.weight.data_ptr() - step._small_flat.data_ptr()) // 4
+                w = e.weight
+                a = step._small_acc[off:off + w.numel()].view_as(w)
+            tables[(ti, name)] = (w.cpu().numpy().copy(), a.cpu().numpy().copy())
+    return flats, tables
+
+
 def _step_worker(rank, world, port, batches, out):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -133,43 +153,72 @@ def _step_worker(rank, world, port, batches, out):
     from pkg.modelling.distributed import ShardedTrainStep
 
     step = ShardedTrainStep(m, shard_min_rows=300, global_negatives=True)
-    losses = []
+    states, losses = [_sharded_state(step, m)], []
     for gb in batches:
         b = len(gb["cust"]) // world
         local = {k: torch.as_tensor(v[rank * b:(rank + 1) * b], device=dev) for k, v in gb.items()}
         losses.append(float(step(local)["loss"].item()))
-    tables = {}
-    for ti, t in enumerate(m.towers):
-        for name, e in t.input_layer.embedding_layers.items():
-            full = step.tables.gather_full(e._shard_key) if hasattr(e, "_shard_key") else e.weight
-            tables[(ti, name)] = full.cpu().numpy()
-    out[rank] = (losses, [t.dense.flat.detach().cpu().numpy() for t in m.towers], tables)
+        states.append(_sharded_state(step, m))
+    out[rank] = (losses, states)
     dist.destroy_process_group()
+
+
+def _load_state(ref, state):
+    """The single-GPU model `ref` set to a state of the sharded step
+    (parameters and Adagrad accumulators)."""
+    flats, tables = state
+    opt = ref.optimizer
+    with torch.no_grad():
+        for ti, t in enumerate(ref.towers):
+            t.dense.flat.copy_(torch.as_tensor(flats[ti][0]))
+            opt._slots[id(t.dense.flat)] = [torch.as_tensor(flats[ti][1], device=t.dense.flat.device)]
+            for name, e in t.input_layer.embedding_layers.items():
+                w, a = tables[(ti, name)]
+                e.weight.copy_(torch.as_tensor(w))
+                opt._slots[id(e.weight)] = [torch.as_tensor(a, device=e.weight.device)]
 
 
 @pytest.mark.parametrize("world", [2, 4])
 def test_global_negatives_sharded_step_matches_full_batch(cuda, world):
     """ShardedTrainStep(global_negatives=True) on `world` ranks (libtt
     kernels, row-sharded tables, gloo through the host, all on cuda:0) trains
-    like ONE model on the concatenated global batch: the loss of every step
-    and the final MLP and embedding parameters match the single-GPU step
-    within fp32 summation-order rounding (the reduce_scatter / all_reduce sum
-    the same terms in another order)."""
+    like ONE model on the concatenated global batch, step by step: the
+    single-GPU model, set to the sharded step's full state (parameters and
+    Adagrad accumulators, reassembled) before step s, takes one train step on
+    the global batch, and the sharded step's loss and state after step s must
+    match it.  The two differ only in fp32 summation order (the in-batch
+    passes' column splits, the MLP weight gradients' row splits, the
+    all_reduce): ~1e-7 relative per gradient.  One Adagrad update moves a
+    parameter by lr g / sqrt(a + g^2), whose slope in g is at most
+    lr / sqrt(a) <= 0.05 / sqrt(0.1) = 0.16, so the updates differ by
+    ~1e-8-1e-7 for the O(0.1-1) gradients here: atol 2e-6 per step.  Every
+    step restarts the reference from the sharded state, so nothing compounds
+    (a trajectory comparison would measure the drift of two chaotic runs)."""
     steps, B = 3, 64 * world
     batches = _global_batches(steps, B)
-    ref = _small_model(cuda, 3)
-    ref_losses = [float(ref.train_step({k: torch.as_tensor(v, device=cuda) for k, v in gb.items()})["loss"].item())
-                  for gb in batches]
     out = mp.Manager().dict()
     mp.spawn(_step_worker, args=(world, _free_port(), batches, out), nprocs=world, join=True)
-    for r in range(world):
-        losses, flats, tables = out[r]
-        np.testing.assert_allclose(losses, ref_losses, rtol=2e-5)
-        for fl, t in zip(flats, ref.towers):
-            np.testing.assert_allclose(fl, t.dense.flat.detach().cpu().numpy(), rtol=1e-4, atol=1e-5)
+    losses0, states0 = out[0]
+    for r in range(1, world):  # every rank reassembles the same state
+        losses, states = out[r]
+        assert losses == losses0
+        for (fa, ta), (fb, tb) in zip(states, states0):
+            assert all(np.array_equal(x[0], y[0]) and np.array_equal(x[1], y[1]) for x, y in zip(fa, fb))
+            assert all(np.array_equal(ta[k][0], tb[k][0]) and np.array_equal(ta[k][1], tb[k][1]) for k in ta)
+    ref = _small_model(cuda, 3)
+    for s, gb in enumerate(batches):
+        _load_state(ref, states0[s])
+        ref_loss = float(ref.train_step({k: torch.as_tensor(v, device=cuda) for k, v in gb.items()})["loss"].item())
+        np.testing.assert_allclose(losses0[s], ref_loss, rtol=2e-5)
+        flats, tables = states0[s + 1]
+        opt = ref.optimizer
         for ti, t in enumerate(ref.towers):
+            np.testing.assert_allclose(flats[ti][0], t.dense.flat.detach().cpu().numpy(), rtol=0, atol=2e-6)
+            np.testing.assert_allclose(flats[ti][1], opt._slots[id(t.dense.flat)][0].cpu().numpy(), rtol=1e-5)
             for name, e in t.input_layer.embedding_layers.items():
-                np.testing.assert_allclose(tables[(ti, name)], e.weight.cpu().numpy(), rtol=1e-4, atol=2e-6)
+                np.testing.assert_allclose(tables[(ti, name)][0], e.weight.cpu().numpy(), rtol=0, atol=2e-6)
+                np.testing.assert_allclose(tables[(ti, name)][1], opt._slots[id(e.weight)][0].cpu().numpy(),
+                                           rtol=1e-5)
 
 
 def _integration_worker(rank, world, port, code, C, batches, qemb, out):

@@ -405,6 +405,8 @@ def test_sharded_train_step_world1_matches_single_gpu(cuda):
     import socket
 
     import torch.distributed as dist
+
+    from pkg.modelling.distributed import destroy_process_group
     from pkg.modelling.distributed import ShardedTrainStep
 
     s = socket.socket()
@@ -432,7 +434,7 @@ def test_sharded_train_step_world1_matches_single_gpu(cuda):
                 full = step.tables.gather_full(mine._shard_key) if hasattr(mine, "_shard_key") else mine.weight
                 assert torch.equal(full, t.weight), name
     finally:
-        dist.destroy_process_group()
+        destroy_process_group()  # the captured step graphs first, then the group
 
 
 @pytest.mark.parametrize("B", [256, 4096])
@@ -447,6 +449,8 @@ def test_global_negatives_step_captures_rccl_collectives(cuda, monkeypatch, B):
     import socket
 
     import torch.distributed as dist
+
+    from pkg.modelling.distributed import destroy_process_group
     from pkg.modelling.distributed import BatchComm, ShardedTrainStep
 
     s = socket.socket()
@@ -481,7 +485,7 @@ def test_global_negatives_step_captures_rccl_collectives(cuda, monkeypatch, B):
         graphed.check_status()
         eager.check_status()
     finally:
-        dist.destroy_process_group()
+        destroy_process_group()  # the captured step graphs first, then the group
 
 
 def test_sharded_step_status_reports_stale_owner_keys(cuda):
@@ -494,6 +498,8 @@ def test_sharded_step_status_reports_stale_owner_keys(cuda):
     import socket
 
     import torch.distributed as dist
+
+    from pkg.modelling.distributed import destroy_process_group
     from pkg._native import TTError
     from pkg.modelling.distributed import ShardedTrainStep
 
@@ -524,7 +530,7 @@ def test_sharded_step_status_reports_stale_owner_keys(cuda):
         assert torch.equal(t, before)
         step.check_status()
     finally:
-        dist.destroy_process_group()
+        destroy_process_group()  # the captured step graphs first, then the group
 
 
 def test_model_call_score_matrix_on_libtt(cuda):

@@ -12,10 +12,6 @@ rows 1 and 4).
   in-memory index gives and that the fp32 oracle top-k gives
   (brute_force.py:54-83).
 """
-import os
-import subprocess
-import sys
-
 import numpy as np
 import pytest
 import torch
@@ -83,25 +79,7 @@ def test_batch_take_past_the_epoch_is_flagged(cuda):
         dev.check_status()
 
 
-def _in_child(name: str) -> bool:
-    """Run test `name` in a fresh process (True: done here, the caller returns).
-    In the full suite on this pool (late round 4) a graphed DeviceDataset fit
-    segfaulted inside hipGraphLaunch after the earlier tests — with this tree
-    and with the library of the last tree that passed there
-    (tools/runs/gpu_s04_suite2.sh); alone it passes.  The cross-test cause is
-    open."""
-    if os.environ.get("TT_TEST_IN_CHILD") == "1":
-        return False
-    env = dict(os.environ, TT_TEST_IN_CHILD="1")
-    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-p", "no:cacheprovider", f"{__file__}::{name}"],
-                       env=env, capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
-    return True
-
-
 def test_graphed_device_fit_equals_eager_host_fit(cuda):
-    if _in_child("test_graphed_device_fit_equals_eager_host_fit"):
-        return
     cols = _columns(2600, 2)  # 5 full batches of 512 + a partial one
     a, b = _model(cuda, 3), _model(cuda, 3)
     ha = a.fit(EncodedDataset(cols, 512, 1000, seed=7, device=cuda), epochs=2, use_graph=False)
@@ -116,8 +94,6 @@ def test_graphed_device_fit_equals_eager_host_fit(cuda):
 
 
 def test_export_round_trip_and_retriever_on_raw_queries(cuda, tmp_path):
-    if _in_child("test_export_round_trip_and_retriever_on_raw_queries"):
-        return
     m = _model(cuda, 5)
     m.fit(DeviceDataset(_columns(2048, 5), 512, device=cuda), epochs=1, use_graph=True)
     m.save(str(tmp_path / "model") + "/")
@@ -144,3 +120,34 @@ def test_export_round_trip_and_retriever_on_raw_queries(cuda, tmp_path):
     emb = m.query_tower(enc).cpu().numpy()
     rs, ri, _ = oracle.bruteforce_topk(emb, index._candidates.cpu().numpy(), 10)
     assert np.array_equal(got, ids[ri]) and np.array_equal(scores.cpu().numpy(), rs)
+
+
+def test_graphed_fits_back_to_back_after_a_larger_graph(cuda):
+    """In one process: a GraphedTrainStep of a third model at a LARGER batch
+    (its workspaces grow past what the fits need), then graphed
+    DeviceDataset fits of two different models on two different datasets
+    back to back (each recapturing, each with a partial last batch), each
+    bit-identical to the same model trained eagerly on the host batches."""
+    from pkg.modelling.models.two_tower_model import GraphedTrainStep
+
+    big = _model(cuda, 11)
+    cols_big = _columns(4096, 12)
+    g = GraphedTrainStep(big, {k: torch.as_tensor(v, device=cuda) for k, v in cols_big.items()}, warmup=1)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    for seed, (n, bs, shuffle) in ((21, (3000, 768, None)), (22, (2100, 256, 500))):
+        cols = _columns(n, seed)
+        a, b = _model(cuda, seed), _model(cuda, seed)
+        ha = a.fit(EncodedDataset(cols, bs, shuffle, seed=seed, device=cuda), epochs=2, use_graph=False)
+        hb = b.fit(DeviceDataset(cols, bs, shuffle, seed=seed, device=cuda), epochs=2, use_graph=True)
+        torch.cuda.synchronize()
+        assert b._device_fit_graph is not None
+        np.testing.assert_allclose(hb["loss"], ha["loss"], rtol=1e-12)
+        for ta, tb in zip(a.towers, b.towers):
+            assert torch.equal(ta.dense.flat, tb.dense.flat)
+            for name in ta.input_layer.embedding_layers:
+                assert torch.equal(ta.input_layer.embedding_layers[name].weight,
+                                   tb.input_layer.embedding_layers[name].weight), name
+    g.replay()  # the first graph still replays after the fits' captures
+    torch.cuda.synchronize()
