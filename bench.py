@@ -887,6 +887,7 @@ def main():
                     help="rows of the device-resident input-pipeline leg (0 skips it; N=1 only)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-c5", action="store_true", help="skip the row-sharded 100M-row table leg (configs[4])")
+    ap.add_argument("--c5-only", action="store_true", help="run only the configs[4] leg (profiling)")
     ap.add_argument("--train-mode", choices=("auto", "sharded"), default="auto",
                     help="sharded: run the N>1 row-sharded step (ShardedTrainStep) even on one rank")
     ap.add_argument("--negatives", choices=("global", "replica"), default="global",
@@ -920,6 +921,15 @@ def main():
         else:
             torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", torch.cuda.current_device())
+    if args.c5_only:
+        res = time_c5_sharded(device, ws, rank, steps=args.steps)
+        if rank == 0:
+            os.write(real_stdout, (json.dumps({"c5_sharded_table": res}) + "\n").encode())
+        if torch.distributed.is_initialized():
+            from pkg.modelling.distributed import destroy_process_group
+
+            destroy_process_group()
+        return
 
     model, data = build_model(device, rank, args.fused_apply)
     B = args.batch

@@ -107,7 +107,9 @@ struct IndexHeader {
   int32_t D;
   unsigned maxnorm_bits;  // max_c |c|_2 as float bits (non-negative)
   unsigned has_neg;       // some candidate coordinate < 0
-  unsigned pad[8];
+  unsigned maxcb_bits;    // max_c |bf16(c)|_2 (rounded up)
+  unsigned maxrc_bits;    // max_c |c - bf16(c)|_2 (rounded up)
+  unsigned pad[6];
 };
 static_assert(sizeof(IndexHeader) == 64, "header");
 
@@ -124,13 +126,36 @@ inline int next_pow2(int x) {
   return p;
 }
 
+// Index image: 64-B header, bf16 rows [n_pad, D], then per row the norms
+// (|bf16(c)|_2, |c - bf16(c)|_2) as float2 (rounded up) for the per-row
+// screen bound.
 size_t index_bytes(int64_t n, int dim) {
   const int D = pick_dpad(dim);
-  return 64 + static_cast<size_t>(round_up(n, kCTile)) * D * 2;
+  const size_t n_pad = static_cast<size_t>(round_up(n, kCTile));
+  return 64 + n_pad * D * 2 + n_pad * sizeof(float2);
 }
 
 __device__ __forceinline__ const __bf16* index_rows(const void* idx) {
   return reinterpret_cast<const __bf16*>(static_cast<const char*>(idx) + 64);
+}
+
+__host__ __device__ __forceinline__ size_t norms_offset(int64_t n_pad, int D) {
+  return 64 + static_cast<size_t>(n_pad) * D * 2;
+}
+
+// Per-row screen bound.  With qb = bf16(q), rq = q - qb, cb = bf16(c),
+// rc = c - cb (componentwise exact in fp32):
+//   q.c = qb.cb + qb.rc + rq.cb + rq.rc,
+//   |s~ - qb.cb|      <= g |qb| |cb|   (fp32 accumulation of the exact bf16
+//                                       products, any order, g = 2 D 2^-24),
+//   |s_chain - q.c|   <= g |q| |c|     (the exact fmaf chain's own rounding),
+// so |s~ - s_chain| <= |qb||rc| + |rq|(|cb| + |rc|) + 2g(|qb| + |rq|)(|cb| + |rc|)
+// (Cauchy-Schwarz; |q| <= |qb| + |rq|, |c| <= |cb| + |rc|).  The bf16
+// residuals are ~2^-9 of their vectors, so this is typically 2-3x tighter
+// than eps * s (relative form): fewer screened entries survive the cut.
+constexpr float kGam2 = 2.0f * 2.0f * 128.0f * 5.9604645e-8f;  // 2g at D <= 128
+__device__ __forceinline__ float row_err(float qb, float qr, float cb, float cr) {
+  return (qb * cr + qr * (cb + cr) + kGam2 * (qb + qr) * (cb + cr)) * (1.0f + 1e-5f) + kTiny;
 }
 
 __device__ __forceinline__ float lb_of(float s, float m, bool rel) {
@@ -165,40 +190,61 @@ __device__ __forceinline__ unsigned long long make_key(float s, unsigned idx) {
 constexpr int kBuildRowsPerWave = 16;
 __global__ void __launch_bounds__(256) build_kernel(const float* __restrict__ cand, int64_t ldc, int64_t n, int dim,
                                                     int64_t n_pad, int D, void* index) {
-  __shared__ float wmax[4];
+  __shared__ float wmax[3][4];
   __shared__ int wneg[4];
   IndexHeader* hdr = static_cast<IndexHeader*>(index);
   __bf16* rows = reinterpret_cast<__bf16*>(static_cast<char*>(index) + 64);
+  float2* norms = reinterpret_cast<float2*>(static_cast<char*>(index) + norms_offset(n_pad, D));
   const int wave = threadIdx.x / kWave;
   const int lane = lane_id();
-  float mx = 0.0f;
+  float mx = 0.0f, mcb = 0.0f, mrc = 0.0f;
   bool neg = false;
   for (int i = 0; i < kBuildRowsPerWave; ++i) {
     const int64_t r = (blockIdx.x * 4ll + wave) * kBuildRowsPerWave + i;
     if (r >= n_pad) break;
-    float ss = 0.0f;
+    float ss = 0.0f, sb = 0.0f, sr = 0.0f;
     for (int e2 = lane; e2 < D / 2; e2 += kWave) {
       const int e = 2 * e2;
       const float x0 = (r < n && e < dim) ? cand[r * ldc + e] : 0.0f;
       const float x1 = (r < n && e + 1 < dim) ? cand[r * ldc + e + 1] : 0.0f;
       ss = __builtin_fmaf(x0, x0, __builtin_fmaf(x1, x1, ss));
       neg = neg || x0 < 0.0f || x1 < 0.0f;
-      reinterpret_cast<unsigned*>(rows + r * D)[e2] = pack_bf16x2(x0, x1);
+      const unsigned pk = pack_bf16x2(x0, x1);
+      reinterpret_cast<unsigned*>(rows + r * D)[e2] = pk;
+      const float b0 = __uint_as_float(pk << 16), b1 = __uint_as_float(pk & 0xFFFF0000u);
+      const float d0 = x0 - b0, d1 = x1 - b1;  // exact in fp32
+      sb = __builtin_fmaf(b0, b0, __builtin_fmaf(b1, b1, sb));
+      sr = __builtin_fmaf(d0, d0, __builtin_fmaf(d1, d1, sr));
     }
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) ss += __shfl_xor(ss, m, kWave);
-    if (r < n) mx = fmaxf(mx, sqrtf(ss));
+    for (int m = 32; m >= 1; m >>= 1) {
+      ss += __shfl_xor(ss, m, kWave);
+      sb += __shfl_xor(sb, m, kWave);
+      sr += __shfl_xor(sr, m, kWave);
+    }
+    // rounded up (the sums of <= 128 squares and the sqrt: relative < 1e-5)
+    const float nb = sqrtf(sb) * (1.0f + 1e-5f), nr = sqrtf(sr) * (1.0f + 1e-5f);
+    if (lane == 0) norms[r] = make_float2(nb, nr);
+    if (r < n) {
+      mx = fmaxf(mx, sqrtf(ss));
+      mcb = fmaxf(mcb, nb);
+      mrc = fmaxf(mrc, nr);
+    }
   }
   const bool wn = __ballot(neg) != 0;
   if (lane == 0) {
-    wmax[wave] = mx;
+    wmax[0][wave] = mx;
+    wmax[1][wave] = mcb;
+    wmax[2][wave] = mrc;
     wneg[wave] = wn ? 1 : 0;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float m = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+    const float m = fmaxf(fmaxf(wmax[0][0], wmax[0][1]), fmaxf(wmax[0][2], wmax[0][3]));
     // round the norm up so the bound stays an upper bound
     atomicMax(&hdr->maxnorm_bits, __float_as_uint(m * (1.0f + 1e-5f)));
+    atomicMax(&hdr->maxcb_bits, __float_as_uint(fmaxf(fmaxf(wmax[1][0], wmax[1][1]), fmaxf(wmax[1][2], wmax[1][3]))));
+    atomicMax(&hdr->maxrc_bits, __float_as_uint(fmaxf(fmaxf(wmax[2][0], wmax[2][1]), fmaxf(wmax[2][2], wmax[2][3]))));
     if (wneg[0] | wneg[1] | wneg[2] | wneg[3]) atomicOr(&hdr->has_neg, 1u);
     if (blockIdx.x == 0) {
       hdr->n = n;
@@ -214,11 +260,11 @@ __global__ void __launch_bounds__(256) build_kernel(const float* __restrict__ ca
 // every candidate are non-negative), the absolute margin M_q, the zero flag.
 __global__ void query_prep_kernel(const float* __restrict__ q, int64_t ldq, int64_t nq, int dim, int64_t nq_pad,
                                   int D, const void* index, __bf16* __restrict__ qb, int* __restrict__ qflags,
-                                  float* __restrict__ qmarg) {
+                                  float* __restrict__ qmarg, float2* __restrict__ qnorm) {
   const int64_t r = blockIdx.x * 4ll + threadIdx.x / kWave;
   if (r >= nq_pad) return;
   const int lane = lane_id();
-  float ss = 0.0f;
+  float ss = 0.0f, sb = 0.0f, sr = 0.0f;
   bool nz = false, neg = false;
   for (int e2 = lane; e2 < D / 2; e2 += kWave) {
     const int e = 2 * e2;
@@ -227,10 +273,20 @@ __global__ void query_prep_kernel(const float* __restrict__ q, int64_t ldq, int6
     ss = __builtin_fmaf(x0, x0, __builtin_fmaf(x1, x1, ss));
     nz = nz || x0 != 0.0f || x1 != 0.0f;
     neg = neg || x0 < 0.0f || x1 < 0.0f;
-    if (qb) reinterpret_cast<unsigned*>(qb + r * D)[e2] = pack_bf16x2(x0, x1);
+    const unsigned pk = pack_bf16x2(x0, x1);
+    if (qb) reinterpret_cast<unsigned*>(qb + r * D)[e2] = pk;
+    const float b0 = __uint_as_float(pk << 16), b1 = __uint_as_float(pk & 0xFFFF0000u);
+    const float d0 = x0 - b0, d1 = x1 - b1;
+    sb = __builtin_fmaf(b0, b0, __builtin_fmaf(b1, b1, sb));
+    sr = __builtin_fmaf(d0, d0, __builtin_fmaf(d1, d1, sr));
   }
 #pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) ss += __shfl_xor(ss, m, kWave);
+  for (int m = 32; m >= 1; m >>= 1) {
+    ss += __shfl_xor(ss, m, kWave);
+    sb += __shfl_xor(sb, m, kWave);
+    sr += __shfl_xor(sr, m, kWave);
+  }
+  if (lane == 0) qnorm[r] = make_float2(sqrtf(sb) * (1.0f + 1e-5f), sqrtf(sr) * (1.0f + 1e-5f));
   const bool nonzero = __ballot(nz) != 0;
   const bool qneg = __ballot(neg) != 0;
   if (lane == 0) {
@@ -1156,6 +1212,9 @@ struct FinalArgs {
   int64_t nq;
   const int* qflags;
   const float* qmarg;
+  const float2* qnorm;      // per query (|bf16(q)|, |q - bf16(q)|)
+  const float2* cnorm;      // per candidate row of the index: (|bf16(c)|, |c - bf16(c)|)
+  const IndexHeader* hdr;   // the maxima of cnorm (the certificate's bound for unlisted rows)
   Lists lists;
   float* out_s;
   int32_t* out_i;
@@ -1214,6 +1273,12 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
   }
   const bool rel = (fl & kQRel) != 0;
   const float m = a.qmarg[q];
+  const float2 qn = a.qnorm[q];
+  // the per-row screen bound of list entry id (row_err)
+  auto err_row = [&](unsigned idv) {
+    const float2 cn = a.cnorm[static_cast<int64_t>(idv) - a.cand_offset];
+    return row_err(qn.x, qn.y, cn.x, cn.y);
+  };
   // the segments' counts, one load each by the first wave, to an exclusive
   // prefix pre[0..64] in LDS (the radix bins, cleared by the select later;
   // padded with the total), so the list is read as one flat index space
@@ -1300,9 +1365,34 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
     if (!fail) {
       // certificate (below) is the only reason counted in stats[1]
       X = lb_of(order_key_float(r.prefix), m, rel);
-      // certificate: every list kept all s~ > tau, and ub(s~) <= ub(tau) < X
-      // rules a candidate out of the exact top-K (which has K members >= X).
-      fail = !(X > ub_of(tmax, m, rel));
+      // per-row bounds: the >= K entries at or above the K-th key prefix each
+      // score at least max(lb(s~), s~ - err_row) exactly, so X = the least of
+      // those lower bounds has >= K candidates at or above it (and is >= the
+      // relative / absolute form's lb(prefix))
+      unsigned xk = 0xFFFFFFFFu, unused = 0u;
+      auto visit = [&](float sv, unsigned iv) {
+        if (float_order_key(sv) >= r.prefix)
+          xk = min(xk, float_order_key(fmaxf(lb_of(sv, m, rel), sv - err_row(iv))));
+      };
+      if (staged) {
+        for (int i = t; i < ntot; i += NT) visit(sc[i], id[i]);
+      } else {
+        for (int j = 0; j < Ls.nseg; ++j) {
+          const int c = seg_count(Ls, q, j);
+          const uint2* e = seg_ptr(Ls, q, j);
+          for (int i = t; i < c; i += NT) visit(__uint_as_float(e[i].x), e[i].y);
+        }
+      }
+      group_minmax<NW>(xk, unused, wcnt);
+      if (xk != 0xFFFFFFFFu) X = fmaxf(X, order_key_float(xk));
+      // certificate: every list kept all s~ > tau, and an unlisted row's
+      // exact score is <= min(ub(tau), tau + the per-row bound at the index's
+      // largest row norms) < X, which rules it out of the exact top-K (K
+      // members >= X)
+      const float ubt = fminf(ub_of(tmax, m, rel),
+                              tmax + row_err(qn.x, qn.y, __uint_as_float(a.hdr->maxcb_bits),
+                                             __uint_as_float(a.hdr->maxrc_bits)));
+      fail = !(X > ubt);
       if (fail && t == 0) TT_STAT(1, 1);
     }
   }
@@ -1325,7 +1415,9 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
       const int i = i0 + t;
       const float sv = i < ntot ? sc[i] : 0.0f;
       const unsigned iv = i < ntot ? id[i] : 0u;
-      const bool keepit = i < ntot && ub_of(sv, m, rel) >= X;
+      // ub = min(relative / absolute form, s~ + per-row bound): its row
+      // norms are read only for the entries the first form keeps
+      const bool keepit = i < ntot && ub_of(sv, m, rel) >= X && sv + err_row(iv) >= X;
       const int p = compact_slot<NW>(keepit, n, wcnt, par);
       if constexpr (NW == 1) wsync();
       if (keepit) id[p] = iv;
@@ -1339,7 +1431,8 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
       for (int i0 = 0; i0 < c; i0 += NT) {
         const int i = i0 + t;
         const uint2 en = i < c ? e[i] : make_uint2(0u, 0u);
-        const bool keepit = i < c && ub_of(__uint_as_float(en.x), m, rel) >= X;
+        const bool keepit = i < c && ub_of(__uint_as_float(en.x), m, rel) >= X &&
+                            __uint_as_float(en.x) + err_row(en.y) >= X;
         const int p = compact_slot<NW>(keepit, n, wcnt, par);
         if (n > a.L) {  // uniform over the group
           fail = true;
@@ -1652,6 +1745,7 @@ struct SearchWs {
   __bf16* qb;
   int* qflags;
   float* qmarg;
+  float2* qnorm;
   uint2* buf;
   int* count;
   float* tau_split;
@@ -1668,6 +1762,7 @@ SearchWs carve_search(Carver& cv, int D, const SearchPlan& p, bool lists, bool f
   w.qb = cv.take<__bf16>(nq_pad * D);
   w.qflags = cv.take<int>(nq_pad);
   w.qmarg = cv.take<float>(nq_pad);
+  w.qnorm = cv.take<float2>(nq_pad);
   if (lists) {
     w.buf = cv.take<uint2>(nq_pad * p.S * static_cast<int64_t>(p.cap));
     w.count = cv.take<int>(nq_pad * p.S);
@@ -1709,7 +1804,7 @@ int run_prep(const float* q, int64_t ldq, int64_t nq, int dim, int D, const void
              bool with_rows, hipStream_t st) {
   const int64_t nq_pad = round_up(nq, kQPerWG);
   hipLaunchKernelGGL(query_prep_kernel, dim3(ceil_div(nq_pad, 4)), dim3(256), 0, st, q, ldq, nq, dim, nq_pad, D, index,
-                     with_rows ? w.qb : nullptr, w.qflags, w.qmarg);
+                     with_rows ? w.qb : nullptr, w.qflags, w.qmarg, w.qnorm);
   TT_CHECK_LAUNCH();
   return TT_OK;
 }
@@ -1763,6 +1858,11 @@ int run_finalize(const FinalArgs& fa, const FallbackArgs& fb, int64_t nq, const 
   TT_CHECK_LAUNCH();
   return TT_OK;
 }
+
+inline const float2* index_norms(const void* index, int64_t n_cand, int D) {
+  return reinterpret_cast<const float2*>(static_cast<const char*>(index) + norms_offset(round_up(n_cand, kCTile), D));
+}
+inline const IndexHeader* index_header(const void* index) { return static_cast<const IndexHeader*>(index); }
 
 inline bool is_vec4(const float* cand, int64_t ldc, int dim) {
   return reinterpret_cast<uintptr_t>(cand) % 16 == 0 && ldc % 4 == 0 && dim % 4 == 0;
@@ -1839,7 +1939,8 @@ extern "C" int tt_bruteforce_search(const void* index, const float* cand, int64_
     if (int rc = run_scan(D, index, 0, n_cand, nq, p, w, w.tau, static_cast<unsigned>(index_offset), st)) return rc;
     Lists ls{w.buf, w.count, w.tau, p.S, p.cap, nullptr, p.S, 1};
     FinalArgs fa{qc, ldq, cand, ldc, n_cand, index_offset, index_offset, dim, k, p.LF, p.P, vec4,
-                 nq, w.qflags, w.qmarg, ls, out_scores + q0 * k, out_idx + q0 * k, w.fail_count, w.fail_list,
+                 nq, w.qflags, w.qmarg, w.qnorm, index_norms(index, n_cand, D), index_header(index), ls,
+                 out_scores + q0 * k, out_idx + q0 * k, w.fail_count, w.fail_list,
                  nullptr, nullptr};
     FallbackArgs fb{qc, ldq, cand, ldc, n_cand, index_offset, dim, k, p.L, p.P, p.parts, vec4,
                     w.fail_count, w.fail_list, w.fail_count + 1, w.fb_scratch, w.fb_scratch_n,
@@ -1931,7 +2032,8 @@ extern "C" int tt_bruteforce_shard_screen(const void* index, int64_t n_cand, int
     return rc;
   Lists ls{w.buf, w.count, w.tau, p.S, p.cap, nullptr, p.S, 1};
   FinalArgs fa{queries, ldq, nullptr, 0, n_cand, index_offset, index_offset, dim, k, p.LF, p.P, 0,
-               n_queries, w.qflags, w.qmarg, ls, nullptr, nullptr, nullptr, nullptr, kth_lb, nullptr};
+               n_queries, w.qflags, w.qmarg, w.qnorm, index_norms(index, n_cand, D), index_header(index), ls, nullptr,
+               nullptr, nullptr, nullptr, kth_lb, nullptr};
   return launch_finalize(fa, n_queries, p, st);
 }
 
@@ -1956,7 +2058,8 @@ extern "C" int tt_bruteforce_shard_finalize(const void* index, const float* cand
   TT_CHECK_HIP(hipMemsetAsync(w.fail_count, 0, (2 + kFbSlots) * sizeof(int), st));
   Lists ls{w.buf, w.count, w.tau, p.S, p.cap, nullptr, p.S, 1};
   FinalArgs fa{queries, ldq, cand, ldc, n_cand, index_offset, index_offset, dim, k, p.LF, p.P, vec4,
-               n_queries, w.qflags, w.qmarg, ls, out_scores, out_idx, w.fail_count, w.fail_list, nullptr, floor};
+               n_queries, w.qflags, w.qmarg, w.qnorm, index_norms(index, n_cand, pick_dpad(dim)), index_header(index), ls,
+               out_scores, out_idx, w.fail_count, w.fail_list, nullptr, floor};
   FallbackArgs fb{queries, ldq, cand, ldc, n_cand, index_offset, dim, k, p.L, p.P, p.parts, vec4,
                   w.fail_count, w.fail_list, w.fail_count + 1, w.fb_scratch, w.fb_scratch_n, out_scores, out_idx};
   return run_finalize(fa, fb, n_queries, p, st);

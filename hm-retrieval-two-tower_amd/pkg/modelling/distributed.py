@@ -606,9 +606,11 @@ class ShardedTables:
         tagged = [(ids.reshape(-1), self.rows[name], self.names.index(name)) for name, ids in lookups]
         send, counts, _, idx = self.ops.route_requests(tagged, W, T)
         send_p, idx_p = self.ops.route_pad(send, counts, idx, W, cap, overflow)
-        recv = torch.empty(W * cap, 2, dtype=torch.int32, device=dev)
         split = [cap] * W
-        _a2a(recv, send_p, split, split, group)
+        recv = send_p  # world 1: the exchange is the identity
+        if W > 1:
+            recv = torch.empty(W * cap, 2, dtype=torch.int32, device=dev)
+            _a2a(recv, send_p, split, split, group)
         tags, rows, tids = self.ops.route_owner(recv, W, T)
         return _Route(s_split=split, r_split=split, R=W * cap, n_recv=W * cap, tags=tags, rows=rows,
                       table_ids=list(tids.unbind(0)), idx=list(idx_p.unbind(0)), idx_all=idx_p, dev=dev)
@@ -616,9 +618,12 @@ class ShardedTables:
     # -- forward -----------------------------------------------------------
     def fetch_routed(self, rt: _Route, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Rows of the routed requests, [R, dim] (into out[:R] when given)."""
+        got = out[:rt.R] if out is not None else torch.empty(rt.R, self.dim, dtype=torch.float32, device=rt.dev)
+        if self.world == 1:  # the owner's answer IS the fetched rows
+            self.ops.gather_tagged([self.shard[n] for n in self.names], rt.tags, rt.rows, got)
+            return got
         reply = torch.empty(rt.n_recv, self.dim, dtype=torch.float32, device=rt.dev)
         self.ops.gather_tagged([self.shard[n] for n in self.names], rt.tags, rt.rows, reply)
-        got = out[:rt.R] if out is not None else torch.empty(rt.R, self.dim, dtype=torch.float32, device=rt.dev)
         _a2a(got, reply, rt.s_split, rt.r_split, self.group)
         return got
 
@@ -642,8 +647,11 @@ class ShardedTables:
     def apply_routed(self, rt: _Route, g_req: torch.Tensor, lr: float, eps: float) -> None:
         """g_req[:R]: the per-request gradient sums of the routed requests;
         returns them to the owners, which apply Adagrad to their shards."""
-        recv = torch.empty(rt.n_recv, self.dim, dtype=torch.float32, device=rt.dev)
-        _a2a(recv, g_req[:rt.R], rt.r_split, rt.s_split, self.group)
+        if self.world == 1:  # the per-request sums are already the owner's
+            recv = g_req[:rt.R]
+        else:
+            recv = torch.empty(rt.n_recv, self.dim, dtype=torch.float32, device=rt.dev)
+            _a2a(recv, g_req[:rt.R], rt.r_split, rt.s_split, self.group)
         specs = [dict(table=self.shard[name], slot0=self.acc[name], ids=[rt.table_ids[ti]], grad_col_offset=[0])
                  for ti, name in enumerate(self.names)]
         if recv.shape[0] > 0:

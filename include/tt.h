@@ -327,7 +327,9 @@ int tt_inbatch_softmax_xent(const float* q, int64_t ldq, const float* c,
  * in fp32 as a k-ordered fmaf chain and returns the exact top-k.  Indices
  * are candidate positions + index_offset (the global offset of a shard).
  * ------------------------------------------------------------------------ */
-/* Bytes of a prepared candidate image (bf16 copy + norms). */
+/* Bytes of a prepared candidate image: 64-B header (sizes, max row norms),
+ * bf16 copy [n_pad, D], then per row (|bf16(c)|_2, |c - bf16(c)|_2) for the
+ * finalize's per-row screen bound. */
 size_t tt_bruteforce_index_bytes(int64_t n_cand, int32_t dim);
 int tt_bruteforce_build(const float* cand, int64_t ldc, int64_t n_cand,
                         int32_t dim, void* index, size_t index_bytes,

@@ -277,3 +277,51 @@ def test_c5_100m_row_table_world1(cuda):
     finally:
         destroy_process_group()  # the captured step graphs first, then the group
         torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("B", [2048, 16384])
+def test_c3_sharded_step_world1_matches_single_gpu(cuda, B):
+    """C3's schema with its H&M vocabularies (customer, postal and article
+    tables row-sharded: 3 sharded lookups per row) through ShardedTrainStep
+    at world 1 over RCCL — routing, fetch, the step and the owner apply
+    captured as ONE hipGraph with fixed-capacity routing (3 x B slots) — is
+    bit-identical to the single-GPU train step, step for step, at the
+    per-rank batch of an 8-way split (2,048) and at the full C3 batch; no
+    request overflows (check_status)."""
+    import torch.distributed as dist
+
+    from pkg.modelling.distributed import ShardedTrainStep, destroy_process_group
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device(cuda))
+    try:
+        schema = bench.main_schema()
+        data = bench.SyntheticHM(cuda, seed=11)
+        schema.set_candidate_prob_lookup(data.prob_lookup())
+        models = []
+        for _ in range(2):
+            m = TwoTowerModel.create_from_schema(schema, "article_id", device=cuda, seed=0)
+            m.compile(optimizer=OptimizerFactory.get_optimizer("adagrad", {"learning_rate": 0.05}))
+            models.append(m)
+        a, b = models
+        step = ShardedTrainStep(a, shard_min_rows=100_000, global_negatives=False)
+        assert len(step.tables.names) == 3
+        for i in range(5):
+            batch = data.batch(B)
+            la, lb = step(batch)["loss"], b.train_step(batch)["loss"]
+            assert torch.equal(la, lb), i
+        assert step._graph is not None and step._cap == 3 * B
+        step.check_status()
+        for ta, tb in zip(a.towers, b.towers):
+            assert torch.equal(ta.dense.flat, tb.dense.flat)
+            for name, t in tb.input_layer.embedding_layers.items():
+                mine = ta.input_layer.embedding_layers[name]
+                full = step.tables.gather_full(mine._shard_key) if hasattr(mine, "_shard_key") else mine.weight
+                assert torch.equal(full, t.weight), name
+    finally:
+        destroy_process_group()
+        torch.cuda.empty_cache()

@@ -664,3 +664,64 @@ def test_mlp_wgrad_pair_equals_single(cuda, shapes, masked):
         single = torch.full_like(p["dwb"], float("nan"))
         hip_ops.mlp_wgrad(p["a"], p["g"], single, gmask=p.get("gmask"), scale=p.get("scale"))
         assert torch.equal(p["dwb"], single)
+
+
+@pytest.mark.parametrize("world,cap_frac", [(1, None), (3, None), (8, None), (8, 0.1)])
+def test_route_pad_matches_torch_restatement(cuda, world, cap_frac):
+    """tt_route_pad: the compact requests laid into fixed per-owner slots
+    equal distributed.torch_route_pad (slots, padding, each lookup's slot and
+    the overflow count), at the never-overflowing capacity (every lookup
+    distinct) and at one that drops requests."""
+    from pkg.modelling.distributed import torch_route_pad
+
+    rng = np.random.default_rng(10 + world)
+    B = 2048
+    rows = [5000, 1371980, 700]
+    spec = [(0, zipf_ids(rng, B, 5000)), (1, zipf_ids(rng, B, 1371980, 1.05)), (2, rng.integers(-3, 705, B).astype(np.int32))]
+    lookups = [(_t(ids, cuda), rows[tag], tag) for tag, ids in spec]
+    send, counts, nreq, idx = hip_ops.route_requests(lookups, world, 3)
+    cap = len(spec) * B if cap_frac is None else max(1, int(cap_frac * len(spec) * B / world))
+    ov = torch.zeros(1, dtype=torch.int32, device=cuda)
+    sp, ip = hip_ops.route_pad(send, counts, idx, world, cap, ov)
+    ov_ref = torch.zeros(1, dtype=torch.int32)
+    rsp, rip = torch_route_pad(send.cpu(), counts.cpu(), idx.cpu(), world, cap, ov_ref)
+    assert torch.equal(sp.cpu(), rsp) and torch.equal(ip.cpu(), rip)
+    assert int(ov.item()) == int(ov_ref.item()) == int(np.maximum(counts.cpu().numpy() - cap, 0).sum())
+    assert (int(ov.item()) > 0) == (cap_frac is not None)
+
+
+@pytest.mark.parametrize("B", [256, 2048, 16384])
+def test_route_fixed_captured_equals_eager(cuda, B):
+    """The fixed-capacity routing (tt_route_requests: key build + rocPRIM
+    radix sort + head scan; tt_route_pad) captured into a hipGraph and
+    replayed on new ids equals the same calls run eagerly on those ids — at
+    the ShardedTrainStep's sizes (3 sharded lookups x B rows, world 1)."""
+    rng = np.random.default_rng(B)
+    rows = [1371980, 352899, 105542]
+    ids = torch.zeros(3, B, dtype=torch.int32, device=cuda)
+
+    def route():
+        lk = [(ids[t], rows[t], t) for t in range(3)]
+        send, counts, _, idx = hip_ops.route_requests(lk, 1, 3)
+        ov = torch.zeros(1, dtype=torch.int32, device=cuda)
+        sp, ip = hip_ops.route_pad(send, counts, idx, 1, 3 * B, ov)
+        return counts, sp, ip, ov
+
+    def fill():
+        for t in range(3):
+            ids[t].copy_(_t(zipf_ids(rng, B, rows[t], 1.05), cuda))
+
+    fill()
+    route()  # warm: workspaces
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with hip_ops.capture_guard(), torch.cuda.graph(g):
+        out = route()
+    for _ in range(3):
+        fill()
+        g.replay()
+        ref = route()
+        torch.cuda.synchronize()
+        for a, b in zip(out, ref):
+            assert torch.equal(a, b)
+        assert int(out[3].item()) == 0
