@@ -74,7 +74,13 @@ __global__ void __launch_bounds__(256) route_keys_kernel(const RouteArgs a) {
 // its per-owner counts (LDS, then one atomic per owner per block into the
 // zeroed counts); the last block writes the request total.
 __global__ void __launch_bounds__(kScanThreads) route_heads_kernel(const unsigned long long* keys, int64_t total,
-                                                                   int32_t* block_heads) {
+                                                                   int32_t* block_heads, long long* counts,
+                                                                   int32_t world) {
+  // the per-owner counts route_write_kernel adds into are zeroed here, by a
+  // kernel: a captured hipMemsetAsync (a graph memset node) was seen to be
+  // ordered differently from the kernels around it on replay
+  if (blockIdx.x == 0)
+    for (int o = threadIdx.x; o < world; o += kScanThreads) counts[o] = 0;
   __shared__ int wsum[kScanThreads / kWave];
   const int64_t i = static_cast<int64_t>(blockIdx.x) * kScanThreads + threadIdx.x;
   const int head = (i < total && (i == 0 || keys[i] != keys[i - 1])) ? 1 : 0;
@@ -310,8 +316,8 @@ extern "C" int tt_route_requests(const tt_route_lookup* lookups, int32_t num_loo
   TT_CHECK_HIP(rocprim::radix_sort_pairs<SortConfig>(w.sort_tmp, sb, w.keys_in, w.keys, w.vals_in, w.vals,
                                          static_cast<unsigned>(p.total), 0, p.end_bit, st, false));
   const unsigned nb = static_cast<unsigned>(ceil_div(p.total, kScanThreads));
-  TT_CHECK_HIP(hipMemsetAsync(counts, 0, static_cast<size_t>(world) * sizeof(long long), st));
-  hipLaunchKernelGGL(route_heads_kernel, dim3(nb), dim3(kScanThreads), 0, st, w.keys, p.total, w.block_heads);
+  hipLaunchKernelGGL(route_heads_kernel, dim3(nb), dim3(kScanThreads), 0, st, w.keys, p.total, w.block_heads, counts,
+                     world);
   TT_CHECK_LAUNCH();
   hipLaunchKernelGGL(route_write_kernel, dim3(nb), dim3(kScanThreads), 0, st, w.keys, w.vals, p.total, world,
                      num_tags, p.id_bits, w.block_heads, send, idx, counts, num_requests);

@@ -1277,6 +1277,63 @@ __global__ void dense_adam_kernel(float* p, float* m, float* v, const float* g, 
   }
 }
 
+// Adagrad on rows that are distinct (tt_sparse_adagrad_rows): slot j applies
+// grad row j to row rows[j] of table tags[j]; one thread per 4 columns of a
+// slot (dim % 4 == 0) or per column.  g = 0 + (0 + grad): the block sums'
+// arithmetic for a segment of one lookup, so the result is bit-identical to
+// tt_sparse_adagrad on the same (distinct) rows.
+constexpr int kRowsMaxTables = 16;
+struct RowsArgs {
+  float* table[kRowsMaxTables];
+  float* slot0[kRowsMaxTables];
+  int64_t num_rows[kRowsMaxTables];
+  int num_tables;
+  int dim;
+  const int32_t* tags;
+  const int32_t* rows;
+  int64_t n;
+  const float* grad;
+  int64_t grad_ld;
+  float lr, eps;
+};
+
+__device__ __forceinline__ void adagrad_elem(float* tab, float* acc, float gsrc, float lr, float eps) {
+  const float g = ieee_op<'+'>(0.0f, ieee_op<'+'>(0.0f, gsrc));
+  const float a = ieee_op<'+'>(*acc, ieee_op<'*'>(g, g));
+  *acc = a;
+  *tab = ieee_op<'-'>(*tab, ieee_op<'/'>(ieee_op<'*'>(lr, g), ieee_op<'+'>(sqrtf(a), eps)));
+}
+
+template <bool V4>
+__global__ void __launch_bounds__(256) adagrad_rows_kernel(const RowsArgs a) {
+  const int per = V4 ? a.dim / 4 : a.dim;  // threads per slot
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  const int64_t j = i / per;
+  if (j >= a.n) return;
+  const int c = static_cast<int>(i - j * per) * (V4 ? 4 : 1);
+  const int t = a.tags[j];
+  const int64_t r = a.rows[j];
+  if (t < 0 || t >= a.num_tables || r < 0 || r >= a.num_rows[t]) return;
+  const int64_t o = r * a.dim + c;
+  const float* gp = a.grad + j * a.grad_ld + c;
+  if constexpr (V4) {
+    f32x4 tv = *reinterpret_cast<const f32x4*>(a.table[t] + o);
+    f32x4 av = *reinterpret_cast<const f32x4*>(a.slot0[t] + o);
+    const f32x4 gv = *reinterpret_cast<const f32x4*>(gp);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float tt = tv[e], aa = av[e];
+      adagrad_elem(&tt, &aa, gv[e], a.lr, a.eps);
+      tv[e] = tt;
+      av[e] = aa;
+    }
+    *reinterpret_cast<f32x4*>(a.slot0[t] + o) = av;
+    *reinterpret_cast<f32x4*>(a.table[t] + o) = tv;
+  } else {
+    adagrad_elem(a.table[t] + o, a.slot0[t] + o, *gp, a.lr, a.eps);
+  }
+}
+
 dim3 stride_grid(int64_t n) {
   int64_t b = ceil_div(n, 256);
   if (b > 8192) b = 8192;
@@ -1421,6 +1478,44 @@ extern "C" int tt_sparse_status(void* workspace, size_t workspace_bytes, tt_stre
   return fail(TT_ERR_BAD_ARG, "sparse: %s%s(error word 0x%x); those blocks applied nothing",
               (h.error & kErrStaleKeys) ? "an apply found sorted keys of another call (stale presorted workspace) " : "",
               (h.error & kErrOutOfCall) ? "a sorted lookup pointed outside the call's gradient " : "", h.error);
+}
+
+extern "C" int tt_sparse_adagrad_rows(const tt_sparse_table* tables, int32_t num_tables, const int32_t* tags,
+                                      const int32_t* rows, int64_t n, const float* grad, int64_t grad_ld, float lr,
+                                      float epsilon, tt_stream_t stream) {
+  clear_error();
+  TT_REQUIRE(n >= 0, "tt_sparse_adagrad_rows: negative n");
+  if (n == 0) return TT_OK;
+  TT_REQUIRE(tables && tags && rows && grad, "tt_sparse_adagrad_rows: NULL pointer");
+  TT_REQUIRE(num_tables >= 1 && num_tables <= kRowsMaxTables, "tt_sparse_adagrad_rows: 1..%d tables, got %d",
+             kRowsMaxTables, num_tables);
+  RowsArgs a{};
+  a.num_tables = num_tables;
+  a.dim = tables[0].dim;
+  for (int t = 0; t < num_tables; ++t) {
+    TT_REQUIRE(tables[t].table && tables[t].slot0, "tt_sparse_adagrad_rows: table %d NULL", t);
+    TT_REQUIRE(tables[t].dim == a.dim, "tt_sparse_adagrad_rows: tables must share one dim");
+    a.table[t] = tables[t].table;
+    a.slot0[t] = tables[t].slot0;
+    a.num_rows[t] = tables[t].num_rows;
+  }
+  TT_REQUIRE(a.dim >= 1 && grad_ld >= a.dim, "tt_sparse_adagrad_rows: bad dim %d / grad_ld", a.dim);
+  a.tags = tags;
+  a.rows = rows;
+  a.n = n;
+  a.grad = grad;
+  a.grad_ld = grad_ld;
+  a.lr = lr;
+  a.eps = epsilon;
+  bool v4 = a.dim % 4 == 0 && grad_ld % 4 == 0 && reinterpret_cast<uintptr_t>(grad) % 16 == 0;
+  for (int t = 0; t < num_tables; ++t)
+    v4 = v4 && reinterpret_cast<uintptr_t>(a.table[t]) % 16 == 0 && reinterpret_cast<uintptr_t>(a.slot0[t]) % 16 == 0;
+  const int64_t threads = n * (v4 ? a.dim / 4 : a.dim);
+  const dim3 grid(static_cast<unsigned>(ceil_div(threads, 256)));
+  if (v4) hipLaunchKernelGGL(adagrad_rows_kernel<true>, grid, dim3(256), 0, to_stream(stream), a);
+  else hipLaunchKernelGGL(adagrad_rows_kernel<false>, grid, dim3(256), 0, to_stream(stream), a);
+  TT_CHECK_LAUNCH();
+  return TT_OK;
 }
 
 extern "C" int tt_dense_adagrad(float* param, float* accum, const float* grad, int64_t n, float lr,

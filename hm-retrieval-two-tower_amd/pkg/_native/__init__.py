@@ -187,6 +187,8 @@ _PROTOS = {
         [POINTER(RouteLookup), c_int32, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          c_size_t, c_void_p]),
     "tt_route_owner": (c_int32, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "tt_sparse_adagrad_rows": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_float,
+                                         c_float, c_void_p]),
     "tt_route_pad": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int64, c_void_p, c_void_p, c_void_p,
                                c_void_p]),
     "tt_sum": (c_int32, [c_void_p, c_int64, c_float, c_void_p, c_void_p]),

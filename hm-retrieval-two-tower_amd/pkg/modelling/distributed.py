@@ -405,6 +405,8 @@ class EmbeddingOps:
     route_requests: Callable[..., Any] = torch_route_requests
     route_owner: Callable[..., Any] = torch_route_owner
     route_pad: Callable[..., Any] = torch_route_pad
+    # Adagrad on distinct rows (a one-rank owner's requests); None: sparse_adagrad
+    sparse_adagrad_rows: Optional[Callable[..., None]] = None
 
     @staticmethod
     def hip() -> "EmbeddingOps":
@@ -418,7 +420,7 @@ class EmbeddingOps:
                             lambda specs, b, g, lr, eps: hip_ops.sparse_adagrad(specs, b, g, lr, eps,
                                                                                 ws_tag="sparse_owner"),
                             hip_ops.dense_adagrad, hip_ops.route_requests, hip_ops.route_owner,
-                            hip_ops.route_pad)
+                            hip_ops.route_pad, hip_ops.sparse_adagrad_rows)
 
 
 def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits: List[int], in_splits: List[int], group) -> torch.Tensor:
@@ -613,7 +615,8 @@ class ShardedTables:
             _a2a(recv, send_p, split, split, group)
         tags, rows, tids = self.ops.route_owner(recv, W, T)
         return _Route(s_split=split, r_split=split, R=W * cap, n_recv=W * cap, tags=tags, rows=rows,
-                      table_ids=list(tids.unbind(0)), idx=list(idx_p.unbind(0)), idx_all=idx_p, dev=dev)
+                      table_ids=list(tids.unbind(0)), idx=list(idx_p.unbind(0)), idx_all=idx_p, dev=dev,
+                      counts=counts)
 
     # -- forward -----------------------------------------------------------
     def fetch_routed(self, rt: _Route, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -649,6 +652,11 @@ class ShardedTables:
         returns them to the owners, which apply Adagrad to their shards."""
         if self.world == 1:  # the per-request sums are already the owner's
             recv = g_req[:rt.R]
+            if self.ops.sparse_adagrad_rows is not None:
+                # one rank's requests are distinct (tag, row) pairs: no sort, no sums
+                self.ops.sparse_adagrad_rows([(self.shard[n], self.acc[n]) for n in self.names], rt.tags, rt.rows,
+                                             recv, lr, eps)
+                return
         else:
             recv = torch.empty(rt.n_recv, self.dim, dtype=torch.float32, device=rt.dev)
             _a2a(recv, g_req[:rt.R], rt.r_split, rt.s_split, self.group)
@@ -882,7 +890,10 @@ class ShardedTrainStep:
         dim = self.tables.dim if self.tables is not None else 1
         self._got = torch.zeros(slots, dim, dtype=torch.float32, device=dev)
         self._g_req = torch.zeros(slots, dim, dtype=torch.float32, device=dev)
-        self._overflow = torch.zeros(1, dtype=torch.int32, device=dev)  # dropped requests (capacity)
+        # dropped requests (capacity); TT_SHARDED_DEBUG=1: between two canary words
+        self._canary = torch.full((3,), 0x7EADBEEF, dtype=torch.int32, device=dev)
+        self._canary[1] = 0
+        self._overflow = self._canary[1:2]
         self._idx_all = torch.zeros(max(len(lk), 1), B, dtype=torch.int32, device=dev)  # one copy per step
         self._idx = list(self._idx_all[:len(lk)].unbind(0))
         self._loss = torch.zeros((), dtype=torch.float32, device=dev)
@@ -988,6 +999,12 @@ class ShardedTrainStep:
         if self.tables is not None:
             rt = self.tables.route_fixed([(k, ids) for k, ids, _, _ in self._lookups(self._static)], self._cap,
                                          overflow=self._overflow)
+            if os.environ.get("TT_SHARDED_KEEP", "1") == "1":
+                self._last_counts = rt.counts
+            if os.environ.get("TT_SHARDED_DEBUG") == "2":  # running max of the per-owner counts, in the graph
+                if getattr(self, "_cmax", None) is None:
+                    self._cmax = torch.zeros(1, dtype=torch.int64, device=rt.counts.device)
+                torch.maximum(self._cmax, rt.counts.max().reshape(1), out=self._cmax)
             self.tables.fetch_routed(rt, out=self._got)
             self._idx_all[:len(self._idx)].copy_(rt.idx_all)
         self._middle()
@@ -1029,6 +1046,13 @@ class ShardedTrainStep:
             self._body()
         self._calls += 1
         tm = self._tick("step", tm)
+        if os.environ.get("TT_SHARDED_DEBUG") == "1" and self.tables is not None:
+            torch.cuda.synchronize()
+            c = self._canary.tolist()
+            counts = self._last_counts.tolist()
+            if c[0] != 0x7EADBEEF or c[2] != 0x7EADBEEF or c[1] != 0 or max(counts) > self._cap:
+                raise RuntimeError(f"ShardedTrainStep debug: call {self._calls}, canary/overflow {c}, counts {counts}, "
+                                   f"cap {self._cap}, graph {self._graph is not None}")
         return {"loss": self._loss.clone()}
 
     # workspaces the sharded step's sparse kernels write (EmbeddingOps.hip)
@@ -1045,6 +1069,10 @@ class ShardedTrainStep:
 
             hip_ops.sparse_status_all(self.model.device, self.STATUS_TAGS)
         ov = getattr(self, "_overflow", None)
+        if os.environ.get("TT_SHARDED_DEBUG") == "2" and ov is not None:
+            torch.cuda.synchronize()
+            logger.warning(f"ShardedTrainStep debug: canary/overflow {self._canary.tolist()}, max owner count "
+                           f"{int(self._cmax.item())} (cap {self._cap}), last counts {self._last_counts.tolist()}")
         if ov is not None:
             n = int(ov.item())
             ov.zero_()

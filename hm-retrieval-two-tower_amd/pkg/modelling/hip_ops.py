@@ -21,6 +21,7 @@ __all__ = [
     "loss_sum",
     "gather_grouped",
     "sparse_adagrad",
+    "sparse_adagrad_rows",
     "sparse_sort",
     "sparse_status",
     "sparse_adam",
@@ -298,6 +299,28 @@ def sparse_adagrad(tables: Sequence[dict], batch: int, grad: Optional[torch.Tens
     fn = L.tt_sparse_adagrad_sorted if presorted else L.tt_sparse_adagrad
     check(fn(arr, len(tables), batch, grad.data_ptr() if grad is not None else None, ld, lr, epsilon,
              ws.data_ptr(), ws.numel(), _stream()))
+
+
+def sparse_adagrad_rows(tables: Sequence[Tuple[torch.Tensor, torch.Tensor]], tags: torch.Tensor, rows: torch.Tensor,
+                        grad: torch.Tensor, lr: float, epsilon: float) -> None:
+    """Adagrad on DISTINCT rows (tt_sparse_adagrad_rows): slot j applies
+    grad[j] to row rows[j] of tables[tags[j]] = (table, accumulator);
+    invalid tags / rows are skipped.  Each (tag, row) at most once."""
+    _req(tags, "tags", torch.int32, 1)
+    _req(rows, "rows", torch.int32, 1)
+    _req(grad, "grad", torch.float32, 2)
+    n = tags.numel()
+    if rows.numel() != n or grad.shape[0] < n:
+        raise ValueError("tags / rows / grad sizes disagree")
+    arr = (SparseTable * len(tables))()
+    for i, (t, a) in enumerate(tables):
+        _req(t, f"table[{i}]", torch.float32, 2)
+        _req(a, f"slot0[{i}]", torch.float32, 2)
+        if not (t.is_contiguous() and a.is_contiguous()) or a.shape != t.shape:
+            raise ValueError(f"table/slot0[{i}] must be contiguous and of equal shape")
+        arr[i].table, arr[i].slot0, arr[i].num_rows, arr[i].dim = t.data_ptr(), a.data_ptr(), t.shape[0], t.shape[1]
+    check(lib().tt_sparse_adagrad_rows(arr, len(tables), tags.data_ptr(), rows.data_ptr(), n, grad.data_ptr(),
+                                       _row_major(grad, "grad"), lr, epsilon, _stream()))
 
 
 def sparse_status(device: torch.device, ws_tag: str = "sparse", scope: Optional[str] = None) -> None:

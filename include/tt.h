@@ -213,6 +213,17 @@ int tt_sparse_adagrad_sorted(const tt_sparse_table* tables, int32_t num_tables,
                              float lr, float epsilon, void* workspace,
                              size_t workspace_bytes, tt_stream_t stream);
 
+/* Adagrad on DISTINCT rows (no sort, no duplicate sums): slot j (< n) applies
+ * grad row j (grad + j*grad_ld, tables[*].dim columns) to row rows[j] of
+ * tables[tags[j]] (tags[j] < 0 or a row outside the table: nothing).  Every
+ * (tag, row) must occur at most once — e.g. the requests a one-rank owner
+ * receives from tt_route_requests.  Bit-identical to tt_sparse_adagrad on
+ * those rows.  Tables share one dim; ids / grad_col_offset are ignored. */
+int tt_sparse_adagrad_rows(const tt_sparse_table* tables, int32_t num_tables,
+                           const int32_t* tags, const int32_t* rows, int64_t n,
+                           const float* grad, int64_t grad_ld, float lr,
+                           float epsilon, tt_stream_t stream);
+
 /* The sparse calls never fault on a mismatched workspace: the sort stage
  * stamps the first 256 bytes of the workspace with a fingerprint of the
  * lookups it sorted, and the apply passes (of every sparse entry point above

@@ -725,3 +725,36 @@ def test_route_fixed_captured_equals_eager(cuda, B):
         for a, b in zip(out, ref):
             assert torch.equal(a, b)
         assert int(out[3].item()) == 0
+
+
+@pytest.mark.parametrize("dim", [128, 6])
+def test_sparse_adagrad_rows_equals_sorted_apply_on_distinct_rows(cuda, dim):
+    """tt_sparse_adagrad_rows (no sort) on distinct (table, row) slots equals
+    tt_sparse_adagrad (sort + block sums) on the same rows bit for bit;
+    slots with tag -1 or a row outside the table change nothing."""
+    rng = np.random.default_rng(dim)
+    rows_t = [5000, 777]
+    tabs = [torch.as_tensor(rng.standard_normal((r, dim)).astype(np.float32), device=cuda) for r in rows_t]
+    accs = [torch.full_like(t, 0.1) + torch.rand_like(t) for t in tabs]
+    n = 3000
+    tags = rng.integers(0, 2, n).astype(np.int32)
+    rws = np.where(tags == 0, rng.permutation(5000)[:n], rng.integers(0, 777, n)).astype(np.int32)
+    # make (tag, row) distinct: keep first occurrences, invalidate the rest
+    seen, keep = set(), np.ones(n, bool)
+    for j in range(n):
+        if (tags[j], rws[j]) in seen:
+            keep[j] = False
+        seen.add((tags[j], rws[j]))
+    tags[~keep] = -1
+    rws[::97] = 100000  # out of every table
+    grad = torch.as_tensor(rng.standard_normal((n, dim)).astype(np.float32), device=cuda)
+    t1, a1 = [t.clone() for t in tabs], [a.clone() for a in accs]
+    hip_ops.sparse_adagrad_rows(list(zip(t1, a1)), _t(tags, cuda), _t(rws, cuda), grad, 0.05, 1e-7)
+    t2, a2 = [t.clone() for t in tabs], [a.clone() for a in accs]
+    specs = []
+    for ti in range(2):
+        ids = np.where(tags == ti, rws, -1).astype(np.int32)
+        specs.append(dict(table=t2[ti], slot0=a2[ti], ids=[_t(ids, cuda)], grad_col_offset=[0]))
+    hip_ops.sparse_adagrad(specs, n, grad, 0.05, 1e-7)
+    for x, y in zip(t1 + a1, t2 + a2):
+        assert torch.equal(x, y)

@@ -326,6 +326,29 @@ def test_graph_replay_equals_eager(cuda):
             assert torch.equal(ta.input_layer.embedding_layers[n].weight, tb.input_layer.embedding_layers[n].weight)
 
 
+def test_graph_replays_back_to_back_equal_eager(cuda):
+    """40 replays of the captured train step queued back to back (one sync at
+    the end, as bench.py and fit run them) leave the state bit-identical to
+    40 eager steps: a replay never overlaps the previous one, whose freed
+    and re-used temporaries the next replay's first nodes would otherwise
+    clobber."""
+    a, b = _small_model(cuda, seed=8), _small_model(cuda, seed=8)
+    rng = np.random.default_rng(21)
+    batches = [_batch(cuda, rng, 4096) for _ in range(41)]
+    for x in batches:
+        a.train_step(x)
+    g = GraphedTrainStep(b, batches[0], warmup=1)
+    packed = [g.pack(x) for x in batches[1:]]
+    torch.cuda.synchronize()
+    for p in packed:
+        g(packed=p)
+    torch.cuda.synchronize()
+    for ta, tb in zip(a.towers, b.towers):
+        assert torch.equal(ta.dense.flat, tb.dense.flat)
+        for n in ta.input_layer.embedding_layers:
+            assert torch.equal(ta.input_layer.embedding_layers[n].weight, tb.input_layer.embedding_layers[n].weight)
+
+
 def test_c3_shape_inbatch_passes_vs_torch_fp64(cuda):
     """Full C3 size (B=16384, E=128): rows/cols passes against a torch fp64
     reference evaluated in row blocks on the GPU."""
