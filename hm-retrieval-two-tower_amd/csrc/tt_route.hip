@@ -77,8 +77,11 @@ __global__ void __launch_bounds__(kScanThreads) route_heads_kernel(const unsigne
                                                                    int32_t* block_heads, long long* counts,
                                                                    int32_t world) {
   // the per-owner counts route_write_kernel adds into are zeroed here, by a
-  // kernel: a captured hipMemsetAsync (a graph memset node) was seen to be
-  // ordered differently from the kernels around it on replay
+  // kernel, not by a captured hipMemsetAsync: with the memset node (and the
+  // counts' block recycled inside the step's graph) the overflow word picked
+  // up garbage in 2 of 2 graphed runs; a standalone probe of memset nodes
+  // (tools/graph_replay_overlap_probe.py) stayed ordered, so that cause is
+  // not pinned down, and the kernel-zeroed version has run clean since
   if (blockIdx.x == 0)
     for (int o = threadIdx.x; o < world; o += kScanThreads) counts[o] = 0;
   __shared__ int wsum[kScanThreads / kWave];
