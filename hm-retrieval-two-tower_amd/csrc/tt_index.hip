@@ -1369,6 +1369,10 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
       // score at least max(lb(s~), s~ - err_row) exactly, so X = the least of
       // those lower bounds has >= K candidates at or above it (and is >= the
       // relative / absolute form's lb(prefix))
+#ifndef TT_INDEX_ROW_X
+#define TT_INDEX_ROW_X 0
+#endif
+      if (TT_INDEX_ROW_X) {
       unsigned xk = 0xFFFFFFFFu, unused = 0u;
       auto visit = [&](float sv, unsigned iv) {
         if (float_order_key(sv) >= r.prefix)
@@ -1385,6 +1389,7 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
       }
       group_minmax<NW>(xk, unused, wcnt);
       if (xk != 0xFFFFFFFFu) X = fmaxf(X, order_key_float(xk));
+      }
       // certificate: every list kept all s~ > tau, and an unlisted row's
       // exact score is <= min(ub(tau), tau + the per-row bound at the index's
       // largest row norms) < X, which rules it out of the exact top-K (K
