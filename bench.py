@@ -693,8 +693,7 @@ def time_c5_sharded(device, ws: int, rank: int, steps: int = 20, rows: int = 100
             def body():
                 rt = st.route_fixed([("big", sid)], cap)
                 st.fetch_routed(rt)
-                st.ops.scatter_sum([dict(table=g_req, ids=[rt.idx[0]], grad_col_offset=[0])], b, grad)
-                st.apply_routed(rt, g_req, 0.05, 1e-7)
+                st.apply_lookups(rt, [(grad, 0)], 0.05, 1e-7, g_req=g_req if ws > 1 else None)
 
             body()  # eager: code, workspaces
             graph = None

@@ -24,6 +24,8 @@
 // 49k lookups: every load instruction touched 64 lines and each thread's
 // loop was a chain of dependent misses.)
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "tt_common.h"
@@ -75,7 +77,8 @@ __global__ void __launch_bounds__(256) route_keys_kernel(const RouteArgs a) {
 // zeroed counts); the last block writes the request total.
 __global__ void __launch_bounds__(kScanThreads) route_heads_kernel(const unsigned long long* keys, int64_t total,
                                                                    int32_t* block_heads, long long* counts,
-                                                                   int32_t world) {
+                                                                   int32_t world, int32_t* grp_first, int32_t* grp_last,
+                                                                   int32_t groups) {
   // the per-owner counts route_write_kernel adds into are zeroed here, by a
   // kernel, not by a captured hipMemsetAsync: with the memset node (and the
   // counts' block recycled inside the step's graph) the overflow word picked
@@ -84,6 +87,12 @@ __global__ void __launch_bounds__(kScanThreads) route_heads_kernel(const unsigne
   // not pinned down, and the kernel-zeroed version has run clean since
   if (blockIdx.x == 0)
     for (int o = threadIdx.x; o < world; o += kScanThreads) counts[o] = 0;
+  // (owner, tag) group bounds (optional): empty groups read [0, -1]
+  if (grp_first && blockIdx.x == gridDim.x - 1)
+    for (int g = threadIdx.x; g < groups; g += kScanThreads) {
+      grp_first[g] = 0;
+      grp_last[g] = -1;
+    }
   __shared__ int wsum[kScanThreads / kWave];
   const int64_t i = static_cast<int64_t>(blockIdx.x) * kScanThreads + threadIdx.x;
   const int head = (i < total && (i == 0 || keys[i] != keys[i - 1])) ? 1 : 0;
@@ -101,7 +110,8 @@ __global__ void __launch_bounds__(kScanThreads) route_write_kernel(const unsigne
                                                                    int64_t total, int32_t world, int32_t num_tags,
                                                                    int32_t id_bits, const int32_t* block_heads,
                                                                    int32_t* send, int32_t* idx, long long* counts,
-                                                                   int32_t* num_requests) {
+                                                                   int32_t* num_requests, int32_t* order,
+                                                                   int32_t* grp_first, int32_t* grp_last) {
   __shared__ int wsum[kScanThreads / kWave + 1];
   __shared__ int cnt[kMaxWorld];
   __shared__ int base_s;
@@ -142,6 +152,12 @@ __global__ void __launch_bounds__(kScanThreads) route_write_kernel(const unsigne
       atomicAdd(&cnt[static_cast<int>(ot / num_tags)], 1);
     }
     idx[vals[i]] = u;
+    if (order) order[i] = static_cast<int32_t>(vals[i]);
+    if (grp_first) {  // first / last sorted position of each (owner, tag) group
+      const unsigned long long g = k >> id_bits;
+      if (i == 0 || (keys[i - 1] >> id_bits) != g) grp_first[g] = static_cast<int32_t>(i);
+      if (i == total - 1 || (keys[i + 1] >> id_bits) != g) grp_last[g] = static_cast<int32_t>(i);
+    }
   }
   __syncthreads();
   for (int o = threadIdx.x; o < world; o += kScanThreads)
@@ -165,10 +181,13 @@ __global__ void __launch_bounds__(256) route_owner_kernel(const int32_t* recv, i
 // start offsets in LDS from the device counts (world <= kMaxWorld), then one
 // thread per padded slot copies its request (or writes the (-1, -1) filler)
 // and one thread per lookup rewrites its request index to the padded slot.
+// own_tags / own_rows / own_tids (optional, world 1): tt_route_owner's view
+// of the slots written in the same pass.
 __global__ void __launch_bounds__(256) route_pad_kernel(const int32_t* send, const long long* counts,
                                                         const int32_t* idx, int64_t num_lookups, int32_t world,
                                                         int64_t cap, int32_t* send_padded, int32_t* idx_padded,
-                                                        int32_t* overflow) {
+                                                        int32_t* overflow, int32_t num_tags, int32_t* own_tags,
+                                                        int32_t* own_rows, int32_t* own_tids) {
   __shared__ long long start[kMaxWorld + 1];
   if (threadIdx.x == 0) {
     long long run = 0;
@@ -193,6 +212,11 @@ __global__ void __launch_bounds__(256) route_pad_kernel(const int32_t* send, con
     }
     send_padded[2 * t] = row;
     send_padded[2 * t + 1] = tag;
+    if (own_tags) {  // world 1: the local row is the row
+      own_tags[t] = tag;
+      own_rows[t] = row;
+      for (int q = 0; q < num_tags; ++q) own_tids[static_cast<int64_t>(q) * slots + t] = q == tag ? row : -1;
+    }
     if (j == cap - 1 && n > cap && overflow) atomicAdd(overflow, static_cast<int32_t>(n - cap));
   }
   if (t < num_lookups) {
@@ -206,6 +230,308 @@ __global__ void __launch_bounds__(256) route_pad_kernel(const int32_t* send, con
     if (j >= cap) j = cap - 1;  // dropped request (counted in *overflow): a defined slot
     idx_padded[t] = static_cast<int32_t>(static_cast<int64_t>(lo) * cap + j);
   }
+}
+
+// ---- fused fixed-capacity route for small batches (tt_route_fixed) --------
+// One 1024-thread workgroup does the whole route of <= kRsMax lookups whose
+// keys fit 32 bits: key build into LDS, a stable LSD radix sort of the
+// positions (8-bit-or-narrower digits; per wave a contiguous slice, ranks by
+// ballots of equal digits, so equal keys keep lookup order — the rocPRIM
+// path's order), the request scan, then the padded slots, each lookup's slot,
+// the per-owner counts and overflow, optionally the sorted order / group
+// bounds, and at world 1 the owner view (tags / rows / table_ids) of the
+// slots — the outputs of tt_route_requests_ordered + tt_route_pad (+
+// tt_route_owner) in one launch instead of ~11 (key build, ~6 sort
+// launches, heads, write, pad, owner: each a few microseconds of launch
+// and drain at a 2048-row step).
+#ifdef TT_ROUTE_STAMPS
+__device__ unsigned long long g_route_stamps[8];  // phase end times (wall clock), thread 0
+#define TT_RS_STAMP(i)                                            \
+  if (threadIdx.x == 0) g_route_stamps[i] = wall_clock64();
+#else
+#define TT_RS_STAMP(i)
+#endif
+constexpr int kRsThreads = 1024;
+constexpr int kRsWaves = kRsThreads / kWave;
+constexpr int kRsMax = 16384;
+// the one-workgroup route wins only at small batches (one CU's LDS radix
+// passes: 25 vs 31 us per call at 3 x 1024 lookups, 44 vs 46 at 3 x 2048,
+// 108 vs 46 at 3 x 5461 — tools/time_route.py, profiles/r05_route_fused.txt)
+constexpr int kRsFusedMax = 8192;
+constexpr int kRsTiles = kRsMax / kRsWaves / kWave;  // 64-lane tiles per wave at the maximum
+constexpr int kRsHistStride = kRsWaves + 1;
+constexpr size_t kRsLdsBytes = size_t(kRsMax) * 4 + size_t(2) * kRsMax * 2 + size_t(256) * kRsHistStride * 4 +
+                               size_t(2) * (kMaxWorld + 1) * 4;
+
+struct RouteFixedArgs {
+  RouteLookup lk[kMaxRouteLookups];
+  int32_t num;
+  int64_t batch;
+  int32_t world, num_tags, id_bits, end_bit;
+  int64_t cap;
+  int32_t* send_padded;
+  int32_t* idx_padded;
+  long long* counts;
+  int32_t* overflow;
+  int32_t* order;
+  int32_t* grp_first;
+  int32_t* grp_last;
+  int32_t* own_tags;
+  int32_t* own_rows;
+  int32_t* own_tids;
+};
+
+// lanes of this wave holding the same digit among the active lanes (one
+// ballot per digit bit, nbits <= 8, wave-uniform)
+__device__ __forceinline__ uint64_t rs_peers(uint32_t d, bool act, int nbits) {
+  const uint64_t a = __ballot(act);
+  uint32_t lo = static_cast<uint32_t>(a), hi = static_cast<uint32_t>(a >> 32);
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    if (b >= nbits) break;
+    const uint32_t bit = (d >> b) & 1u;
+    const uint64_t bal = __ballot(bit);
+    const uint32_t flip = bit - 1u;
+    lo &= static_cast<uint32_t>(bal) ^ flip;
+    hi &= static_cast<uint32_t>(bal >> 32) ^ flip;
+  }
+  return act ? (static_cast<uint64_t>(hi) << 32 | lo) : 0;
+}
+
+// block-wide exclusive scan of one int per thread; *total = the sum
+__device__ __forceinline__ int rs_scan(int v, int* wsum, int* total) {
+  const int lane = lane_id(), w = threadIdx.x / kWave;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int y = __shfl_up(x, o, kWave);
+    if (lane >= o) x += y;
+  }
+  __syncthreads();  // wsum free (an earlier scan's readers are done)
+  if (lane == kWave - 1) wsum[w] = x;
+  __syncthreads();
+  int ex = x - v, t = 0;
+  for (int q = 0; q < kRsWaves; ++q) {
+    const int c = wsum[q];
+    ex += q < w ? c : 0;
+    t += c;
+  }
+  *total = t;
+  return ex;
+}
+
+__global__ void __launch_bounds__(kRsThreads) route_fixed_small_kernel(const RouteFixedArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char rsm[];
+  uint32_t* lkey = reinterpret_cast<uint32_t*>(rsm);
+  uint16_t* pb0 = reinterpret_cast<uint16_t*>(rsm + kRsMax * 4);
+  uint16_t* pb1 = pb0 + kRsMax;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(rsm + kRsMax * 8);  // [256][kRsHistStride]
+  int* cnt = reinterpret_cast<int*>(rsm + kRsMax * 8 + 256 * kRsHistStride * 4);
+  int* start = cnt + (kMaxWorld + 1);
+  __shared__ int wsum[kRsWaves];
+  TT_RS_STAMP(5)
+  const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
+  const int n = static_cast<int>(a.batch * a.num);
+  const int W = a.world, T = a.num_tags;
+  // keys: (owner, tag, row + 1) as in route_keys_kernel, 32 bits
+  for (int i = tid; i < n; i += kRsThreads) {
+    const int l = static_cast<int>(i / a.batch);
+    const int b = i - static_cast<int>(l * a.batch);
+    const RouteLookup& L = a.lk[l];
+    const int32_t r = L.ids[b];
+    const bool ok = r >= 0 && r < L.num_rows;
+    const uint32_t owner = ok ? static_cast<uint32_t>(r % W) : static_cast<uint32_t>(W - 1);
+    const uint32_t rowp1 = ok ? static_cast<uint32_t>(r) + 1u : 0u;
+    lkey[i] = ((owner * static_cast<uint32_t>(T) + static_cast<uint32_t>(L.tag)) << a.id_bits) | rowp1;
+    pb0[i] = static_cast<uint16_t>(i);
+  }
+  for (int o = tid; o <= W; o += kRsThreads) cnt[o] = 0;
+  if (a.grp_first)
+    for (int g = tid; g < W * T; g += kRsThreads) {
+      a.grp_first[g] = 0;
+      a.grp_last[g] = -1;
+    }
+  TT_RS_STAMP(0)
+  // stable LSD radix sort of the positions by key
+  const int per = ((n + kRsWaves - 1) / kRsWaves + kWave - 1) / kWave * kWave;
+  const int wbeg = w * per, wend = min(n, wbeg + per);
+  const uint64_t lt = (uint64_t(1) << lane) - 1u;
+  const int passes = (a.end_bit + 7) / 8;
+  const int width = (a.end_bit + passes - 1) / passes;
+  const uint32_t dmask = (1u << width) - 1u;
+  uint16_t* src = pb0;
+  uint16_t* dst = pb1;
+  for (int p = 0; p < passes; ++p) {
+    const int sh = p * width;
+    for (int e = tid; e < 256 * kRsHistStride; e += kRsThreads) hist[e] = 0u;
+    __syncthreads();
+    uint16_t pos[kRsTiles];
+    uint32_t dig[kRsTiles];
+    uint64_t peer[kRsTiles];
+#pragma unroll
+    for (int q = 0; q < kRsTiles; ++q) {
+      const int i = wbeg + q * kWave + lane;
+      pos[q] = 0;
+      dig[q] = 0;
+      if (i < wend) {
+        pos[q] = src[i];
+        dig[q] = (lkey[pos[q]] >> sh) & dmask;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kRsTiles; ++q) {
+      peer[q] = 0;
+      if (wbeg + q * kWave < wend) {  // wave-uniform
+        peer[q] = rs_peers(dig[q], wbeg + q * kWave + lane < wend, width);
+        if (peer[q] != 0 && __builtin_ctzll(peer[q]) == lane) hist[dig[q] * kRsHistStride + w] += __popcll(peer[q]);
+      }
+    }
+    __syncthreads();
+    {  // counts -> exclusive offsets in (digit, wave) order: 4 words per thread
+      uint32_t h[4], run = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int L = 4 * tid + u;
+        h[u] = hist[(L / kRsWaves) * kRsHistStride + L % kRsWaves];
+        run += h[u];
+      }
+      int tot;
+      uint32_t ex = static_cast<uint32_t>(rs_scan(static_cast<int>(run), wsum, &tot));
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int L = 4 * tid + u;
+        hist[(L / kRsWaves) * kRsHistStride + L % kRsWaves] = ex;
+        ex += h[u];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kRsTiles; ++q) {
+      if (wbeg + q * kWave < wend) {  // wave-uniform
+        const uint64_t m = peer[q];
+        if (m != 0) {
+          uint32_t* slot = &hist[dig[q] * kRsHistStride + w];
+          const uint32_t off = *slot;
+          dst[off + __popcll(m & lt)] = pos[q];
+          if (__builtin_ctzll(m) == lane) *slot = off + __popcll(m);
+        }
+      }
+    }
+    __syncthreads();
+    uint16_t* t = src;
+    src = dst;
+    dst = t;
+  }
+  TT_RS_STAMP(1)
+  // requests: heads of the sorted key runs; each thread a contiguous run of
+  // sorted positions
+  const int E = (n + kRsThreads - 1) / kRsThreads;
+  const int p0 = min(n, tid * E), p1 = min(n, p0 + E);
+  const uint32_t omask = (1u << a.id_bits) - 1u;
+  // (a thread's sorted keys have non-decreasing owners: one LDS atomic per
+  // owner run, not per request — at world 1 every request has owner 0)
+  int heads = 0, run_owner = -1, run_n = 0;
+  uint32_t kprev = p0 > 0 ? lkey[src[p0 - 1]] : ~0u;
+  for (int p = p0; p < p1; ++p) {
+    const uint32_t k = lkey[src[p]];
+    if (p == 0 || k != kprev) {
+      ++heads;
+      const int o = static_cast<int>((k >> a.id_bits) / static_cast<uint32_t>(T));
+      if (o != run_owner) {
+        if (run_n) atomicAdd(&cnt[run_owner], run_n);
+        run_owner = o;
+        run_n = 0;
+      }
+      ++run_n;
+    }
+    kprev = k;
+  }
+  if (run_n) atomicAdd(&cnt[run_owner], run_n);
+  int nreq;
+  const int ubase = rs_scan(heads, wsum, &nreq);
+  {  // owners' first request: exclusive scan of cnt (W <= kRsThreads)
+    int tot;
+    const int c = tid < W ? cnt[tid] : 0;
+    const int ex = rs_scan(c, wsum, &tot);
+    if (tid < W) start[tid] = ex;
+  }
+  __syncthreads();
+  TT_RS_STAMP(2)
+  int u = ubase - 1;
+  for (int p = p0; p < p1; ++p) {
+    const int pos = src[p];
+    const uint32_t k = lkey[pos];
+    const uint32_t kp = p > 0 ? lkey[src[p - 1]] : ~0u;
+    const bool head = p == 0 || k != kp;
+    u += head ? 1 : 0;
+    const uint32_t g = k >> a.id_bits;
+    const int o = static_cast<int>(g / static_cast<uint32_t>(T));
+    const int tag = static_cast<int>(g - static_cast<uint32_t>(o * T));
+    const int64_t j = u - start[o];
+    const int64_t slot = static_cast<int64_t>(o) * a.cap + (j < a.cap ? j : a.cap - 1);
+    a.idx_padded[pos] = static_cast<int32_t>(slot);
+    if (a.order) a.order[p] = pos;
+    if (a.grp_first) {
+      if (p == 0 || (kp >> a.id_bits) != g) a.grp_first[g] = p;
+      if (p == n - 1 || (lkey[src[p + 1]] >> a.id_bits) != g) a.grp_last[g] = p;
+    }
+    if (head && j < a.cap) {
+      const int32_t row = static_cast<int32_t>(static_cast<int64_t>(k & omask) - 1);
+      a.send_padded[2 * slot] = row;
+      a.send_padded[2 * slot + 1] = tag;
+      if (a.own_tags) {  // world 1: the owner's local row is the row
+        a.own_tags[slot] = tag;
+        a.own_rows[slot] = row;
+        for (int t = 0; t < T; ++t) a.own_tids[static_cast<int64_t>(t) * W * a.cap + slot] = t == tag ? row : -1;
+      }
+    }
+  }
+  TT_RS_STAMP(3)
+  // unused slots, counts, overflow
+  const int64_t slots = static_cast<int64_t>(W) * a.cap;
+  for (int64_t t = tid; t < slots; t += kRsThreads) {
+    const int o = static_cast<int>(t / a.cap);
+    if (t - static_cast<int64_t>(o) * a.cap >= cnt[o]) {
+      a.send_padded[2 * t] = -1;
+      a.send_padded[2 * t + 1] = -1;
+      if (a.own_tags) {
+        a.own_tags[t] = -1;
+        a.own_rows[t] = -1;
+        for (int q = 0; q < T; ++q) a.own_tids[static_cast<int64_t>(q) * slots + t] = -1;
+      }
+    }
+  }
+  if (tid < W) {
+    a.counts[tid] = cnt[tid];
+    if (a.overflow && cnt[tid] > a.cap) atomicAdd(a.overflow, static_cast<int32_t>(cnt[tid] - a.cap));
+  }
+  TT_RS_STAMP(4)
+}
+
+// The route's device sort: rocPRIM's merge path below TT_SORT_MERGE_LIMIT
+// (block sort + ~6 merge launches at 65,536 keys) or, TT_ROUTE_SORT=onesweep,
+// its onesweep radix path (histogram + one launch per 8-bit digit of the key
+// bits in use: 4 at C5's 27-bit keys).
+using RouteOnesweep = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                 rocprim::default_config, 0>;
+bool route_onesweep() {
+  static const bool v = [] {
+    const char* e = std::getenv("TT_ROUTE_SORT");
+    return e && std::strcmp(e, "onesweep") == 0;
+  }();
+  return v;
+}
+size_t route_sort_bytes(int64_t total, int end_bit) {
+  size_t a = 0, b = 0;
+  unsigned long long* kp = nullptr;
+  uint32_t* vp = nullptr;
+  const hipError_t ea = rocprim::radix_sort_pairs<SortConfig>(nullptr, a, kp, kp, vp, vp, static_cast<unsigned>(total),
+                                                              0, end_bit, nullptr, false);
+  const hipError_t eb = rocprim::radix_sort_pairs<RouteOnesweep>(nullptr, b, kp, kp, vp, vp,
+                                                                 static_cast<unsigned>(total), 0, end_bit, nullptr,
+                                                                 false);
+  if (ea != hipSuccess || eb != hipSuccess) return static_cast<size_t>(total) * 24 + (size_t(4) << 20);
+  return std::max(a, b);
 }
 
 int bits_for(int64_t x) {  // bits needed to represent values in [0, x]
@@ -238,12 +564,7 @@ int plan_route(const tt_route_lookup* lookups, int32_t num, int64_t batch, int32
   p->id_bits = bits_for(max_rows);
   p->end_bit = p->id_bits + bits_for(static_cast<int64_t>(world) * num_tags - 1);
   TT_REQUIRE(p->end_bit <= 64, "route: key does not fit 64 bits");
-  size_t sb = 0;
-  unsigned long long* kp = nullptr;
-  uint32_t* vp = nullptr;
-  hipError_t e = rocprim::radix_sort_pairs<SortConfig>(nullptr, sb, kp, kp, vp, vp, static_cast<unsigned>(p->total), 0,
-                                           p->end_bit, nullptr, false);
-  p->sort_bytes = (e == hipSuccess) ? sb : static_cast<size_t>(p->total) * 24 + (size_t(4) << 20);
+  p->sort_bytes = route_sort_bytes(p->total, p->end_bit);
   return TT_OK;
 }
 
@@ -277,22 +598,20 @@ extern "C" size_t tt_route_workspace_size(int32_t num_lookups, int64_t batch, in
   p.total = batch * num_lookups;
   p.id_bits = bits_for(max_rows > 0 ? max_rows : 1);
   p.end_bit = p.id_bits + bits_for(static_cast<int64_t>(world) * num_tags - 1);
-  size_t sb = 0;
-  unsigned long long* kp = nullptr;
-  uint32_t* vp = nullptr;
-  hipError_t e = rocprim::radix_sort_pairs<SortConfig>(nullptr, sb, kp, kp, vp, vp, static_cast<unsigned>(p.total), 0,
-                                           p.end_bit, nullptr, false);
-  p.sort_bytes = (e == hipSuccess) ? sb : static_cast<size_t>(p.total) * 24 + (size_t(4) << 20);
+  p.sort_bytes = route_sort_bytes(p.total, p.end_bit);
   Carver cv(nullptr, 0);
   carve_route(cv, p);
   return cv.used();
 }
 
-extern "C" int tt_route_requests(const tt_route_lookup* lookups, int32_t num_lookups, int64_t batch, int32_t world,
-                                 int32_t num_tags, int32_t* send, long long* counts, int32_t* num_requests,
-                                 int32_t* idx, void* workspace, size_t workspace_bytes, tt_stream_t stream) {
+extern "C" int tt_route_requests_ordered(const tt_route_lookup* lookups, int32_t num_lookups, int64_t batch,
+                                         int32_t world, int32_t num_tags, int32_t* send, long long* counts,
+                                         int32_t* num_requests, int32_t* idx, int32_t* order, int32_t* grp_first,
+                                         int32_t* grp_last, void* workspace, size_t workspace_bytes,
+                                         tt_stream_t stream) {
   clear_error();
   TT_REQUIRE(lookups && send && counts && num_requests && idx, "tt_route_requests: NULL pointer");
+  TT_REQUIRE((grp_first == nullptr) == (grp_last == nullptr), "tt_route_requests: grp_first / grp_last: both or neither");
   for (int l = 0; l < num_lookups && l < kMaxRouteLookups; ++l)
     TT_REQUIRE(lookups[l].ids && lookups[l].num_rows >= 1 && lookups[l].num_rows < (int64_t(1) << 31),
                "tt_route_requests: lookup %d ids/num_rows invalid", l);
@@ -316,16 +635,27 @@ extern "C" int tt_route_requests(const tt_route_lookup* lookups, int32_t num_loo
   hipLaunchKernelGGL(route_keys_kernel, dim3(static_cast<unsigned>(ceil_div(p.total, 256))), dim3(256), 0, st, a);
   TT_CHECK_LAUNCH();
   size_t sb = p.sort_bytes;
-  TT_CHECK_HIP(rocprim::radix_sort_pairs<SortConfig>(w.sort_tmp, sb, w.keys_in, w.keys, w.vals_in, w.vals,
-                                         static_cast<unsigned>(p.total), 0, p.end_bit, st, false));
+  if (route_onesweep())
+    TT_CHECK_HIP(rocprim::radix_sort_pairs<RouteOnesweep>(w.sort_tmp, sb, w.keys_in, w.keys, w.vals_in, w.vals,
+                                                          static_cast<unsigned>(p.total), 0, p.end_bit, st, false));
+  else
+    TT_CHECK_HIP(rocprim::radix_sort_pairs<SortConfig>(w.sort_tmp, sb, w.keys_in, w.keys, w.vals_in, w.vals,
+                                                       static_cast<unsigned>(p.total), 0, p.end_bit, st, false));
   const unsigned nb = static_cast<unsigned>(ceil_div(p.total, kScanThreads));
   hipLaunchKernelGGL(route_heads_kernel, dim3(nb), dim3(kScanThreads), 0, st, w.keys, p.total, w.block_heads, counts,
-                     world);
+                     world, grp_first, grp_last, world * num_tags);
   TT_CHECK_LAUNCH();
   hipLaunchKernelGGL(route_write_kernel, dim3(nb), dim3(kScanThreads), 0, st, w.keys, w.vals, p.total, world,
-                     num_tags, p.id_bits, w.block_heads, send, idx, counts, num_requests);
+                     num_tags, p.id_bits, w.block_heads, send, idx, counts, num_requests, order, grp_first, grp_last);
   TT_CHECK_LAUNCH();
   return TT_OK;
+}
+
+extern "C" int tt_route_requests(const tt_route_lookup* lookups, int32_t num_lookups, int64_t batch, int32_t world,
+                                 int32_t num_tags, int32_t* send, long long* counts, int32_t* num_requests,
+                                 int32_t* idx, void* workspace, size_t workspace_bytes, tt_stream_t stream) {
+  return tt_route_requests_ordered(lookups, num_lookups, batch, world, num_tags, send, counts, num_requests, idx,
+                                   nullptr, nullptr, nullptr, workspace, workspace_bytes, stream);
 }
 
 extern "C" int tt_route_owner(const int32_t* recv, int64_t n, int32_t world, int32_t num_tags, int32_t* tags,
@@ -351,7 +681,117 @@ extern "C" int tt_route_pad(const int32_t* send, const long long* counts, const 
   TT_REQUIRE(static_cast<int64_t>(world) * cap < (int64_t(1) << 31), "tt_route_pad: world * cap exceeds int32");
   const int64_t n = std::max<int64_t>(static_cast<int64_t>(world) * cap, num_lookups);
   hipLaunchKernelGGL(route_pad_kernel, dim3(static_cast<unsigned>(ceil_div(n, 256))), dim3(256), 0, to_stream(stream),
-                     send, counts, idx, num_lookups, world, cap, send_padded, idx_padded, overflow);
+                     send, counts, idx, num_lookups, world, cap, send_padded, idx_padded, overflow, 1, nullptr,
+                     nullptr, nullptr);
   TT_CHECK_LAUNCH();
   return TT_OK;
 }
+
+namespace tt {
+namespace {
+// the multi-launch path's scratch after the route workspace: compact send,
+// idx and the request count
+struct FixedWs {
+  RouteWs rw;
+  int32_t* send;
+  int32_t* idx;
+  int32_t* nreq;
+};
+FixedWs carve_fixed(Carver& cv, const RoutePlan& p) {
+  FixedWs f;
+  f.rw = carve_route(cv, p);
+  f.send = cv.take<int32_t>(2 * p.total);
+  f.idx = cv.take<int32_t>(p.total);
+  f.nreq = cv.take<int32_t>(1);
+  return f;
+}
+bool route_fused(const RoutePlan& p) {
+  static const bool off = [] {
+    const char* e = std::getenv("TT_ROUTE_FUSED");
+    return e && e[0] == '0';
+  }();
+  return !off && p.total <= kRsFusedMax && p.end_bit <= 32;
+}
+}  // namespace
+}  // namespace tt
+
+extern "C" size_t tt_route_fixed_workspace_size(int32_t num_lookups, int64_t batch, int32_t world, int64_t max_rows,
+                                                int32_t num_tags) {
+  if (num_lookups < 1 || batch < 1 || world < 1 || num_tags < 1) return 0;
+  const size_t base = tt_route_workspace_size(num_lookups, batch, world, max_rows, num_tags);
+  const int64_t total = batch * num_lookups;
+  return base + ((static_cast<size_t>(total) * 12 + 4 + 3 * 256) & ~size_t(255)) + 256;
+}
+
+extern "C" int tt_route_fixed(const tt_route_lookup* lookups, int32_t num_lookups, int64_t batch, int32_t world,
+                              int32_t num_tags, int64_t cap, int32_t* send_padded, int32_t* idx_padded,
+                              long long* counts, int32_t* overflow, int32_t* order, int32_t* grp_first,
+                              int32_t* grp_last, int32_t* owner_tags, int32_t* owner_rows, int32_t* owner_table_ids,
+                              void* workspace, size_t workspace_bytes, tt_stream_t stream) {
+  clear_error();
+  TT_REQUIRE(lookups && send_padded && idx_padded && counts, "tt_route_fixed: NULL pointer");
+  TT_REQUIRE((grp_first == nullptr) == (grp_last == nullptr), "tt_route_fixed: grp_first / grp_last: both or neither");
+  const bool owner = owner_tags != nullptr;
+  TT_REQUIRE(owner == (owner_rows != nullptr) && owner == (owner_table_ids != nullptr),
+             "tt_route_fixed: owner_tags / owner_rows / owner_table_ids: all or none");
+  TT_REQUIRE(!owner || world == 1, "tt_route_fixed: the owner view is the world-1 shortcut (world %d)", world);
+  TT_REQUIRE(cap >= 1 && static_cast<int64_t>(world) * cap < (int64_t(1) << 31), "tt_route_fixed: bad cap");
+  for (int l = 0; l < num_lookups && l < kMaxRouteLookups; ++l)
+    TT_REQUIRE(lookups[l].ids && lookups[l].num_rows >= 1 && lookups[l].num_rows < (int64_t(1) << 31),
+               "tt_route_fixed: lookup %d ids/num_rows invalid", l);
+  RoutePlan p;
+  int rc = plan_route(lookups, num_lookups, batch, world, num_tags, &p);
+  if (rc) return rc;
+  hipStream_t st = to_stream(stream);
+  if (route_fused(p)) {
+    RouteFixedArgs a{};
+    for (int l = 0; l < num_lookups; ++l) a.lk[l] = RouteLookup{lookups[l].ids, lookups[l].num_rows, lookups[l].tag};
+    a.num = num_lookups;
+    a.batch = batch;
+    a.world = world;
+    a.num_tags = num_tags;
+    a.id_bits = p.id_bits;
+    a.end_bit = p.end_bit;
+    a.cap = cap;
+    a.send_padded = send_padded;
+    a.idx_padded = idx_padded;
+    a.counts = counts;
+    a.overflow = overflow;
+    a.order = order;
+    a.grp_first = grp_first;
+    a.grp_last = grp_last;
+    a.own_tags = owner_tags;
+    a.own_rows = owner_rows;
+    a.own_tids = owner_table_ids;
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(route_fixed_small_kernel),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       static_cast<int>(kRsLdsBytes));
+    TT_CHECK_HIP(attr);
+    hipLaunchKernelGGL(route_fixed_small_kernel, dim3(1), dim3(kRsThreads), kRsLdsBytes, st, a);
+    TT_CHECK_LAUNCH();
+    return TT_OK;
+  }
+  Carver cv(workspace, workspace_bytes);
+  FixedWs f = carve_fixed(cv, p);
+  if (!workspace || cv.used() > workspace_bytes)
+    return fail(TT_ERR_WORKSPACE, "tt_route_fixed: workspace %zu < required %zu", workspace_bytes, cv.used());
+  const size_t rbytes = static_cast<size_t>(reinterpret_cast<char*>(f.send) - static_cast<char*>(workspace));
+  rc = tt_route_requests_ordered(lookups, num_lookups, batch, world, num_tags, f.send, counts, f.nreq, f.idx, order,
+                                 grp_first, grp_last, workspace, rbytes, stream);
+  if (rc) return rc;
+  // tt_route_pad, with the world-1 owner view written by the same pass
+  const int64_t n = std::max<int64_t>(static_cast<int64_t>(world) * cap, p.total);
+  hipLaunchKernelGGL(route_pad_kernel, dim3(static_cast<unsigned>(ceil_div(n, 256))), dim3(256), 0, st, f.send,
+                     counts, f.idx, p.total, world, cap, send_padded, idx_padded, overflow, num_tags, owner_tags,
+                     owner_rows, owner_table_ids);
+  TT_CHECK_LAUNCH();
+  return TT_OK;
+}
+
+#ifdef TT_ROUTE_STAMPS
+// timing builds only: the fused route kernel's phase stamps (wall clock ticks)
+extern "C" int tt_route_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_route_stamps), sizeof(g_route_stamps)) == hipSuccess ? TT_OK
+                                                                                                      : TT_ERR_BAD_ARG;
+}
+#endif

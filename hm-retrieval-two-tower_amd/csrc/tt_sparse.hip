@@ -1265,6 +1265,32 @@ __global__ void dense_adagrad_kernel(float* p, float* acc, const float* g, int64
 
 // ResourceApplyAdam (use_nesterov=false):
 //   m += (g - m)*(1-b1); v += (g*g - v)*(1-b2); var -= m*alpha / (sqrt(v) + eps)
+// tt_dense_adagrad on up to kDenseMaxJobs buffers in one launch: a
+// grid-stride loop over their concatenation (the same per-element arithmetic)
+constexpr int kDenseMaxJobs = 8;
+struct DenseJobs {
+  float* p[kDenseMaxJobs];
+  float* acc[kDenseMaxJobs];
+  const float* g[kDenseMaxJobs];
+  int64_t begin[kDenseMaxJobs + 1];
+  int num;
+  float lr, eps;
+};
+__global__ void dense_adagrad_many_kernel(const DenseJobs d) {
+  const int64_t total = d.begin[d.num];
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int t = 0;
+#pragma unroll 1
+    for (int q = 1; q < d.num; ++q)
+      if (i >= d.begin[q]) t = q;
+    const int64_t k = i - d.begin[t];
+    const float gi = d.g[t][k];
+    const float a = ieee_op<'+'>(d.acc[t][k], ieee_op<'*'>(gi, gi));
+    d.acc[t][k] = a;
+    d.p[t][k] = ieee_op<'-'>(d.p[t][k], ieee_op<'/'>(ieee_op<'*'>(gi, d.lr), ieee_op<'+'>(sqrtf(a), d.eps)));
+  }
+}
+
 __global__ void dense_adam_kernel(float* p, float* m, float* v, const float* g, int64_t n, float alpha,
                                   float omb1, float omb2, float eps) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -1331,6 +1357,97 @@ __global__ void __launch_bounds__(256) adagrad_rows_kernel(const RowsArgs a) {
     *reinterpret_cast<f32x4*>(a.table[t] + o) = tv;
   } else {
     adagrad_elem(a.table[t] + o, a.slot0[t] + o, *gp, a.lr, a.eps);
+  }
+}
+
+// Keys of a routed call (tt_sparse_routed) taken from the route's own sort:
+// the route lists lookups by (owner, tag, row, lookup), so table i's lookups
+// (one tag) in slot order are that tag's route positions in order, and a
+// lookup's sorted position in the table's region is its rank among them:
+// (lookups of the tag at earlier owners) + (its offset in its (owner, tag)
+// group).  One thread per route position writes the (table | key, source |
+// batch row) pair the sort stage would have written; the trailing threads
+// write each region's padding.  Every block first turns the group sizes into
+// per-tag prefixes over the owners in LDS (world <= 1024, world * tags <=
+// kRoutedMaxGroups).
+constexpr int kRoutedMaxLookups = TT_ROUTE_MAX_LOOKUPS;
+constexpr int kRoutedMaxGroups = 4096;
+constexpr int kRoutedThreads = 1024;
+struct RoutedArgs {
+  const int32_t* order;
+  const int32_t* grp_first;
+  const int32_t* grp_last;
+  const int32_t* slot;
+  const int32_t* slot_row;
+  int64_t cap;
+  int64_t total;  // routed lookups = num_lookups * batch
+  int32_t world, num_tags, num_lookups, num_tables;
+  int32_t lk_tag[kRoutedMaxLookups];
+  uint32_t lk_khi[kRoutedMaxLookups];   // table index << id_bits
+  uint32_t lk_shi[kRoutedMaxLookups];   // source << kSrcShift
+  int32_t lk_base[kRoutedMaxLookups];   // region start of the lookup's table
+  int32_t pad_begin[kTablesPerLaunch + 1];  // prefix of the regions' padding entries
+  int32_t pad_dst[kTablesPerLaunch];        // first padding position of each region
+  uint32_t pad_key[kTablesPerLaunch];       // (table << id_bits) | invalid
+};
+
+__global__ void __launch_bounds__(kRoutedThreads) routed_keys_kernel(const Job j, const RoutedArgs r) {
+  __shared__ int pre[kRoutedMaxGroups];
+  __shared__ int wsum[kRoutedThreads / kWave];
+  const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
+  const int T = r.num_tags, G = r.world * r.num_tags;
+  for (int g = tid; g < G; g += kRoutedThreads) pre[g] = r.grp_last[g] - r.grp_first[g] + 1;
+  for (int t = 0; t < T; ++t) {  // exclusive prefix over the owners, per tag
+    __syncthreads();
+    const int v = tid < r.world ? pre[tid * T + t] : 0;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const int y = __shfl_up(x, o, kWave);
+      if (lane >= o) x += y;
+    }
+    if (lane == kWave - 1) wsum[w] = x;
+    __syncthreads();
+    int ex = x - v;
+    for (int q = 0; q < w; ++q) ex += wsum[q];
+    if (tid < r.world) pre[tid * T + t] = ex;
+  }
+  __syncthreads();
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kRoutedThreads + tid;
+  const uint32_t invalid = (1u << j.id_bits) - 1u;
+  if (i < r.total) {
+    const int lk = r.order[i];
+    const int l = static_cast<int>(lk / j.batch);
+    const int b = static_cast<int>(lk - static_cast<int64_t>(l) * j.batch);
+    const int s = r.slot[lk];
+    const int g = static_cast<int>(s / r.cap) * T + r.lk_tag[l];
+    const int dst = r.lk_base[l] + pre[g] + static_cast<int>(i - r.grp_first[g]);
+    uint32_t id = static_cast<uint32_t>(s);
+    if (r.slot_row) {
+      const int32_t row = r.slot_row[s];
+      id = row >= 0 ? static_cast<uint32_t>(row) : invalid;
+    }
+    const_cast<uint32_t*>(j.keys)[dst] = r.lk_khi[l] | id;
+    const_cast<uint32_t*>(j.vals)[dst] = id == invalid ? 0xFFFFFFFFu : (r.lk_shi[l] | static_cast<uint32_t>(b));
+  } else {
+    const int k = static_cast<int>(i - r.total);
+    int t = 0;
+#pragma unroll 1
+    for (int q = 1; q < r.num_tables; ++q)
+      if (k >= r.pad_begin[q]) t = q;
+    if (k < r.pad_begin[r.num_tables]) {
+      const int dst = r.pad_dst[t] + (k - r.pad_begin[t]);
+      const_cast<uint32_t*>(j.keys)[dst] = r.pad_key[t];
+      const_cast<uint32_t*>(j.vals)[dst] = 0xFFFFFFFFu;
+    }
+  }
+  if (i == 0) {  // stamp the workspace with this call's fingerprint
+    if (j.hdr->magic != kHdrMagic) {
+      j.hdr->error = 0u;
+      j.hdr->magic = kHdrMagic;
+    }
+    j.hdr->fp0 = j.fp0;
+    j.hdr->fp1 = j.fp1;
   }
 }
 
@@ -1530,6 +1647,33 @@ extern "C" int tt_dense_adagrad(float* param, float* accum, const float* grad, i
   return TT_OK;
 }
 
+extern "C" int tt_dense_adagrad_many(const tt_dense_job* jobs, int32_t num_jobs, float lr, float epsilon,
+                                     tt_stream_t stream) {
+  clear_error();
+  TT_REQUIRE(jobs && num_jobs >= 1 && num_jobs <= kDenseMaxJobs, "tt_dense_adagrad_many: 1..%d jobs, got %d",
+             kDenseMaxJobs, num_jobs);
+  DenseJobs d{};
+  d.num = num_jobs;
+  d.lr = lr;
+  d.eps = epsilon;
+  int64_t total = 0;
+  for (int i = 0; i < num_jobs; ++i) {
+    TT_REQUIRE(jobs[i].n >= 0, "tt_dense_adagrad_many: job %d negative n", i);
+    TT_REQUIRE(jobs[i].n == 0 || (jobs[i].param && jobs[i].accum && jobs[i].grad),
+               "tt_dense_adagrad_many: job %d NULL pointer", i);
+    d.p[i] = jobs[i].param;
+    d.acc[i] = jobs[i].accum;
+    d.g[i] = jobs[i].grad;
+    d.begin[i] = total;
+    total += jobs[i].n;
+  }
+  d.begin[num_jobs] = total;
+  if (total == 0) return TT_OK;
+  hipLaunchKernelGGL(dense_adagrad_many_kernel, stride_grid(total), dim3(256), 0, to_stream(stream), d);
+  TT_CHECK_LAUNCH();
+  return TT_OK;
+}
+
 extern "C" int tt_dense_adam(float* param, float* m, float* v, const float* grad, int64_t n, float lr,
                              float beta1, float beta2, float epsilon, int64_t step, tt_stream_t stream) {
   clear_error();
@@ -1559,4 +1703,95 @@ extern "C" int tt_sparse_scatter_sum(const tt_sparse_table* tables, int32_t num_
   ApplyParams ap{};
   return run_sparse<kScatterSum>(tables, num_tables, batch, grad, grad_stride, ap, workspace, workspace_bytes,
                                  to_stream(stream));
+}
+
+extern "C" int tt_sparse_routed(const tt_sparse_table* tables, int32_t num_tables, int64_t batch, const float* grad,
+                                int64_t grad_stride, const tt_route_sorted* rs, int32_t op, float lr, float epsilon,
+                                void* workspace, size_t workspace_bytes, tt_stream_t stream) {
+  clear_error();
+  TT_REQUIRE(rs && rs->order && rs->grp_first && rs->grp_last && rs->slot, "tt_sparse_routed: NULL route pointer");
+  TT_REQUIRE(op == 0 || op == 1, "tt_sparse_routed: op must be 0 (scatter sum) or 1 (Adagrad), got %d", op);
+  TT_REQUIRE(num_tables >= 1 && num_tables <= kTablesPerLaunch, "tt_sparse_routed: 1..%d tables, got %d",
+             kTablesPerLaunch, num_tables);
+  int rc = validate_tables(tables, num_tables, batch, false, op == 1);
+  if (rc) return rc;
+  if (batch == 0) return TT_OK;
+  const int L = rs->num_lookups, W = rs->world, T = rs->num_tags;
+  TT_REQUIRE(L >= 1 && L <= kRoutedMaxLookups, "tt_sparse_routed: 1..%d lookups, got %d", kRoutedMaxLookups, L);
+  TT_REQUIRE(W >= 1 && W <= kRoutedThreads && T >= 1 && static_cast<int64_t>(W) * T <= kRoutedMaxGroups,
+             "tt_sparse_routed: world %d x tags %d out of range", W, T);
+  TT_REQUIRE(rs->cap >= 1, "tt_sparse_routed: cap must be >= 1");
+  // every lookup belongs to one (table, source); each table takes one tag and
+  // lists exactly its lookups as sources 0..num_sources-1
+  int tag_of_table[kTablesPerLaunch], seen[kTablesPerLaunch][TT_MAX_SOURCES] = {};
+  for (int t = 0; t < num_tables; ++t) tag_of_table[t] = -1;
+  for (int l = 0; l < L; ++l) {
+    const int t = rs->lookup_table[l], s = rs->lookup_source[l], g = rs->lookup_tag[l];
+    TT_REQUIRE(t >= 0 && t < num_tables && s >= 0 && s < tables[t].num_sources && g >= 0 && g < T,
+               "tt_sparse_routed: lookup %d maps to table %d source %d tag %d: out of range", l, t, s, g);
+    TT_REQUIRE(tag_of_table[t] < 0 || tag_of_table[t] == g, "tt_sparse_routed: table %d takes two tags", t);
+    TT_REQUIRE(!seen[t][s], "tt_sparse_routed: table %d source %d listed twice", t, s);
+    tag_of_table[t] = g;
+    seen[t][s] = 1;
+  }
+  for (int t = 0; t < num_tables; ++t)
+    for (int s = 0; s < tables[t].num_sources; ++s)
+      TT_REQUIRE(seen[t][s], "tt_sparse_routed: table %d source %d has no routed lookup", t, s);
+  for (int t = 0; t < num_tables; ++t)
+    for (int u = t + 1; u < num_tables; ++u)
+      TT_REQUIRE(tag_of_table[t] != tag_of_table[u], "tt_sparse_routed: tables %d and %d take one tag", t, u);
+  const size_t need = tables_ws_bytes(tables, num_tables, batch, 0);
+  if (!workspace || workspace_bytes < need)
+    return fail(TT_ERR_WORKSPACE, "tt_sparse_routed: workspace %zu < required %zu", workspace_bytes, need);
+  TT_REQUIRE(batch < (int64_t(1) << kSrcShift), "tt_sparse_routed: batch too large");
+  Plan p;
+  rc = make_plan(tables, num_tables, batch, grad, grad_stride, &p);
+  if (rc) return rc;
+  Carver cv(workspace, workspace_bytes);
+  PlanWs w = carve_plan(cv, p, 0);
+  Job& j = p.job;
+  j.keys = w.keys;
+  j.vals = w.vals;
+  j.hdr = w.hdr;
+  RoutedArgs a{};
+  a.order = rs->order;
+  a.grp_first = rs->grp_first;
+  a.grp_last = rs->grp_last;
+  a.slot = rs->slot;
+  a.slot_row = rs->slot_row;
+  a.cap = rs->cap;
+  a.total = static_cast<int64_t>(L) * batch;
+  a.world = W;
+  a.num_tags = T;
+  a.num_lookups = L;
+  a.num_tables = num_tables;
+  for (int l = 0; l < L; ++l) {
+    const int t = rs->lookup_table[l];
+    a.lk_tag[l] = rs->lookup_tag[l];
+    a.lk_khi[l] = static_cast<uint32_t>(t) << j.id_bits;
+    a.lk_shi[l] = static_cast<uint32_t>(rs->lookup_source[l]) << kSrcShift;
+    a.lk_base[l] = j.t[t].base;
+  }
+  int pads = 0;
+  for (int t = 0; t < num_tables; ++t) {
+    a.pad_begin[t] = pads;
+    a.pad_dst[t] = j.t[t].base + j.t[t].n;
+    a.pad_key[t] = (static_cast<uint32_t>(t) << j.id_bits) | ((1u << j.id_bits) - 1u);
+    pads += j.t[t].n_pad - j.t[t].n;
+  }
+  a.pad_begin[num_tables] = pads;
+  TT_REQUIRE(a.total + pads == p.total, "tt_sparse_routed: %lld routed lookups + %d padding != %d sorted entries",
+             static_cast<long long>(a.total), pads, p.total);
+  hipStream_t st = to_stream(stream);
+  hipLaunchKernelGGL(routed_keys_kernel, dim3(static_cast<unsigned>(ceil_div(p.total, kRoutedThreads))),
+                     dim3(kRoutedThreads), 0, st, j, a);
+  TT_CHECK_LAUNCH();
+  ApplyParams ap{};
+  ap.lr = lr;
+  ap.eps = epsilon;
+  if (op == 1)
+    return run_sparse<kAdagrad>(tables, num_tables, batch, grad, grad_stride, ap, workspace, workspace_bytes, st,
+                                nullptr, nullptr, nullptr, kStageApply);
+  return run_sparse<kScatterSum>(tables, num_tables, batch, grad, grad_stride, ap, workspace, workspace_bytes, st,
+                                 nullptr, nullptr, nullptr, kStageApply);
 }

@@ -148,6 +148,35 @@ class SparseTable(ctypes.Structure):
     ]
 
 
+class DenseJob(ctypes.Structure):
+    _fields_ = [
+        ("param", c_void_p),
+        ("accum", c_void_p),
+        ("grad", c_void_p),
+        ("n", c_int64),
+    ]
+
+
+ROUTE_MAX_LOOKUPS = 32  # TT_ROUTE_MAX_LOOKUPS
+
+
+class RouteSorted(ctypes.Structure):
+    _fields_ = [
+        ("order", c_void_p),
+        ("grp_first", c_void_p),
+        ("grp_last", c_void_p),
+        ("slot", c_void_p),
+        ("slot_row", c_void_p),
+        ("cap", c_int64),
+        ("world", c_int32),
+        ("num_tags", c_int32),
+        ("num_lookups", c_int32),
+        ("lookup_tag", c_int32 * ROUTE_MAX_LOOKUPS),
+        ("lookup_table", c_int32 * ROUTE_MAX_LOOKUPS),
+        ("lookup_source", c_int32 * ROUTE_MAX_LOOKUPS),
+    ]
+
+
 # name -> (restype, argtypes); mirrors include/tt.h one to one.
 _PROTOS = {
     "tt_version": (c_char_p, []),
@@ -186,6 +215,19 @@ _PROTOS = {
         c_int32,
         [POINTER(RouteLookup), c_int32, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          c_size_t, c_void_p]),
+    "tt_route_requests_ordered": (
+        c_int32,
+        [POINTER(RouteLookup), c_int32, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "tt_route_fixed_workspace_size": (c_size_t, [c_int32, c_int64, c_int32, c_int64, c_int32]),
+    "tt_route_fixed": (
+        c_int32,
+        [POINTER(RouteLookup), c_int32, c_int64, c_int32, c_int32, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "tt_sparse_routed": (
+        c_int32,
+        [POINTER(SparseTable), c_int32, c_int64, c_void_p, c_int64, POINTER(RouteSorted), c_int32, c_float, c_float,
+         c_void_p, c_size_t, c_void_p]),
     "tt_route_owner": (c_int32, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "tt_sparse_adagrad_rows": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_float,
                                          c_float, c_void_p]),
@@ -193,6 +235,7 @@ _PROTOS = {
                                c_void_p]),
     "tt_sum": (c_int32, [c_void_p, c_int64, c_float, c_void_p, c_void_p]),
     "tt_dense_adagrad": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p]),
+    "tt_dense_adagrad_many": (c_int32, [POINTER(DenseJob), c_int32, c_float, c_float, c_void_p]),
     "tt_dense_adam": (
         c_int32,
         [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float, c_float, c_int64, c_void_p],

@@ -407,6 +407,14 @@ class EmbeddingOps:
     route_pad: Callable[..., Any] = torch_route_pad
     # Adagrad on distinct rows (a one-rank owner's requests); None: sparse_adagrad
     sparse_adagrad_rows: Optional[Callable[..., None]] = None
+    # per-request sums / Adagrad keyed by the route's own sort (no second
+    # sort; needs route_requests(..., ordered=True)); None: scatter_sum
+    sparse_routed: Optional[Callable[..., None]] = None
+    # the whole fixed route in one call (tt_route_fixed); None: route_requests
+    # + route_pad + route_owner
+    route_fixed: Optional[Callable[..., Any]] = None
+    # dense_adagrad on several (param, accum, grad) buffers in one launch
+    dense_adagrad_many: Optional[Callable[..., None]] = None
 
     @staticmethod
     def hip() -> "EmbeddingOps":
@@ -420,7 +428,8 @@ class EmbeddingOps:
                             lambda specs, b, g, lr, eps: hip_ops.sparse_adagrad(specs, b, g, lr, eps,
                                                                                 ws_tag="sparse_owner"),
                             hip_ops.dense_adagrad, hip_ops.route_requests, hip_ops.route_owner,
-                            hip_ops.route_pad, hip_ops.sparse_adagrad_rows)
+                            hip_ops.route_pad, hip_ops.sparse_adagrad_rows, hip_ops.sparse_routed,
+                            hip_ops.route_fixed, hip_ops.dense_adagrad_many)
 
 
 def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits: List[int], in_splits: List[int], group) -> torch.Tensor:
@@ -594,29 +603,42 @@ class ShardedTables:
         return max(1, num_lookups * batch)
 
     def route_fixed(self, lookups: List[Tuple[str, torch.Tensor]], cap: int, group=None,
-                    overflow: Optional[torch.Tensor] = None) -> _Route:
+                    overflow: Optional[torch.Tensor] = None, idx_out: Optional[torch.Tensor] = None) -> _Route:
         """route() with `cap` fixed request slots per owner (tt_route_pad):
         every exchange has split sizes [cap] * world, known on the host
         before the step, so routing, fetch and apply run with no host sync
         and can be captured into a hipGraph.  Unused slots carry (-1, -1):
         owners answer them with zero rows and apply nothing to them.  With
         cap = route_capacity(...) no request is ever dropped; a smaller cap
-        counts dropped requests in `overflow`."""
+        counts dropped requests in `overflow`.  idx_out ([L, B] int32):
+        where the lookups' slots are written (rt.idx_all is then idx_out)."""
         group = self.group if group is None else group
         W, T = self.world, len(self.names)
         dev = lookups[0][1].device
         tagged = [(ids.reshape(-1), self.rows[name], self.names.index(name)) for name, ids in lookups]
-        send, counts, _, idx = self.ops.route_requests(tagged, W, T)
-        send_p, idx_p = self.ops.route_pad(send, counts, idx, W, cap, overflow)
+        order = own = None
+        ordered = self.ops.sparse_routed is not None  # keep the route's sort for apply_lookups
+        if self.ops.route_fixed is not None:  # one call (one launch for small batches)
+            send_p, idx_p, counts, order, own = self.ops.route_fixed(tagged, W, T, cap, overflow, ordered=ordered,
+                                                                     owner=W == 1, idx_out=idx_out)
+        else:
+            if ordered:
+                send, counts, _, idx, order = self.ops.route_requests(tagged, W, T, ordered=True)
+            else:
+                send, counts, _, idx = self.ops.route_requests(tagged, W, T)
+            send_p, idx_p = self.ops.route_pad(send, counts, idx, W, cap, overflow)
+            if idx_out is not None:
+                idx_out.copy_(idx_p)
+                idx_p = idx_out
         split = [cap] * W
         recv = send_p  # world 1: the exchange is the identity
         if W > 1:
             recv = torch.empty(W * cap, 2, dtype=torch.int32, device=dev)
             _a2a(recv, send_p, split, split, group)
-        tags, rows, tids = self.ops.route_owner(recv, W, T)
+        tags, rows, tids = own if own is not None else self.ops.route_owner(recv, W, T)
         return _Route(s_split=split, r_split=split, R=W * cap, n_recv=W * cap, tags=tags, rows=rows,
                       table_ids=list(tids.unbind(0)), idx=list(idx_p.unbind(0)), idx_all=idx_p, dev=dev,
-                      counts=counts)
+                      counts=counts, order=order, cap=cap, lookup_tags=[t for _, _, t in tagged])
 
     # -- forward -----------------------------------------------------------
     def fetch_routed(self, rt: _Route, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -664,6 +686,57 @@ class ShardedTables:
                  for ti, name in enumerate(self.names)]
         if recv.shape[0] > 0:
             self.ops.sparse_adagrad(specs, recv.shape[0], recv, lr, eps)
+
+    def apply_lookups(self, rt: _Route, grads: List[Tuple[torch.Tensor, int]], lr: float, eps: float,
+                      g_req: Optional[torch.Tensor] = None) -> None:
+        """Adagrad on the shards from the gradients of a route_fixed batch's
+        lookups: grads[l] = (gradient matrix [B, width], column) of routed
+        lookup l.  With ops.sparse_routed (libtt) the per-request sums reuse
+        the route's sort (tt_sparse_routed): at world 1 they go straight into
+        the Adagrad update of the shard (the single-GPU tt_sparse_adagrad on the
+        same keys, no per-request buffer), otherwise into g_req (default: a
+        fresh [world*cap, dim] buffer) for apply_routed.  Without it:
+        scatter_sum, then apply_routed."""
+        if len(grads) != len(rt.idx):
+            raise ValueError(f"apply_lookups: {len(grads)} gradients for {len(rt.idx)} routed lookups")
+        B = rt.idx[0].numel()
+        specs, tables_of_tag, lk_table, lk_source = [], {}, [], []
+        for l, (gmat, col) in enumerate(grads):
+            tag = rt.lookup_tags[l]
+            if tag not in tables_of_tag:
+                tables_of_tag[tag] = len(specs)
+                specs.append(dict(ids=[], grad_col_offset=[], grad=gmat, tag=tag))
+            sp = specs[tables_of_tag[tag]]
+            if sp["grad"] is not gmat:
+                raise ValueError("apply_lookups: the lookups of one table must share one gradient matrix")
+            lk_table.append(tables_of_tag[tag])
+            lk_source.append(len(sp["ids"]))
+            sp["ids"].append(rt.idx[l])
+            sp["grad_col_offset"].append(int(col))
+        routed = self.ops.sparse_routed is not None and getattr(rt, "order", None) is not None
+        if g_req is None and not (self.world == 1 and routed):
+            g_req = torch.zeros(rt.R, self.dim, dtype=torch.float32, device=rt.dev)
+        if not routed:
+            for sp in specs:
+                sp["table"] = g_req
+            self.ops.scatter_sum([{k: v for k, v in sp.items() if k != "tag"} for sp in specs], B, grads[0][0])
+            self.apply_routed(rt, g_req, lr, eps)
+            return
+        route = dict(order=rt.order[0], grp_first=rt.order[1], grp_last=rt.order[2], slot=rt.idx_all, cap=rt.cap,
+                     world=self.world, num_tags=len(self.names), lookup_tag=rt.lookup_tags, lookup_table=lk_table,
+                     lookup_source=lk_source)
+        if self.world == 1:  # the owner is this rank: Adagrad on the shard, keyed by local row
+            route["slot_row"] = rt.rows
+            for sp in specs:
+                name = self.names[sp["tag"]]
+                sp["table"], sp["slot0"] = self.shard[name], self.acc[name]
+            self.ops.sparse_routed([{k: v for k, v in sp.items() if k != "tag"} for sp in specs], B, None, route,
+                                   "adagrad", lr, eps)
+            return
+        for sp in specs:
+            sp["table"] = g_req
+        self.ops.sparse_routed([{k: v for k, v in sp.items() if k != "tag"} for sp in specs], B, None, route, "sum")
+        self.apply_routed(rt, g_req, lr, eps)
 
     def apply(self, grads: List[Tuple[torch.Tensor, List[Tuple[torch.Tensor, int]]]], lr: float, eps: float) -> None:
         """grads: per gradient matrix [B, width] its (row index from fetch, column)
@@ -894,7 +967,7 @@ class ShardedTrainStep:
         self._canary = torch.full((3,), 0x7EADBEEF, dtype=torch.int32, device=dev)
         self._canary[1] = 0
         self._overflow = self._canary[1:2]
-        self._idx_all = torch.zeros(max(len(lk), 1), B, dtype=torch.int32, device=dev)  # one copy per step
+        self._idx_all = torch.zeros(max(len(lk), 1), B, dtype=torch.int32, device=dev)  # route_fixed writes the slots here
         self._idx = list(self._idx_all[:len(lk)].unbind(0))
         self._loss = torch.zeros((), dtype=torch.float32, device=dev)
         n_bucket = sum(t.dense.flat.numel() for t in m.towers) + self._small_grad.numel() + 1
@@ -967,29 +1040,38 @@ class ShardedTrainStep:
                               grad_col_offset=[s[1] for s in srcs], grad=grads[li]))
         if specs:
             self.ops.scatter_sum(specs, self._B, grads[0])
-        torch.cat([t.dense.flat.grad.reshape(-1) for t in m.towers]
-                  + [self._small_grad, loss.detach().reshape(1)], out=self._bucket)
-        self._dense_update()
+        self._dense_update([t.dense.flat.grad for t in m.towers], loss.detach())
 
-    def _dense_update(self) -> None:
-        """One all_reduce of the bucket, then tt_dense_adagrad on both towers'
-        MLP buffers and the flat small-table buffer, and the loss into its
-        static scalar: the tail of the middle, so over RCCL it is captured into
-        the step's hipGraph with it (fixed shapes; the sparse tables' owner
-        apply, whose exchange sizes vary per batch, stays outside)."""
+    def _dense_update(self, flat_grads: List[torch.Tensor], loss: torch.Tensor) -> None:
+        """The tail of the middle: the towers' MLP gradients, the flat
+        small-table gradient and the loss packed into one bucket, one
+        all_reduce of it (world 1: no bucket, the gradients are used in
+        place), then tt_dense_adagrad_many on both towers' MLP buffers and the
+        flat small-table buffer, and the loss into its static scalar — fixed
+        shapes, captured into the step's hipGraph."""
         m = self.model
-        _all_reduce_sum(self._bucket, self.group)
-        off = 0
-        for ti, t in enumerate(m.towers):
-            n = t.dense.flat.numel()
-            self.ops.dense_adagrad(t.dense.flat.data, self._dense_acc[ti], self._bucket[off:off + n].view_as(t.dense.flat),
-                                   self.lr, self.eps)
-            off += n
-        n = self._small_grad.numel()
+        if self.world == 1:
+            grads, small, loss_out = [g.view_as(t.dense.flat) for g, t in zip(flat_grads, m.towers)], \
+                self._small_grad, loss.reshape(())
+        else:
+            torch.cat([g.reshape(-1) for g in flat_grads] + [self._small_grad, loss.reshape(1)], out=self._bucket)
+            _all_reduce_sum(self._bucket, self.group)
+            grads, off = [], 0
+            for t in m.towers:
+                n = t.dense.flat.numel()
+                grads.append(self._bucket[off:off + n].view_as(t.dense.flat))
+                off += n
+            small = self._bucket[off:off + self._small_grad.numel()]
+            loss_out = self._bucket[off + self._small_grad.numel()]
+        jobs = [(t.dense.flat.data, self._dense_acc[ti], g) for ti, (t, g) in enumerate(zip(m.towers, grads))]
         if self.small:
-            self.ops.dense_adagrad(self._small_flat, self._small_acc, self._bucket[off:off + n], self.lr, self.eps)
-        off += n
-        self._loss.copy_(self._bucket[off])
+            jobs.append((self._small_flat, self._small_acc, small))
+        if self.ops.dense_adagrad_many is not None:  # one launch for every buffer
+            self.ops.dense_adagrad_many(jobs, self.lr, self.eps)
+        else:
+            for p, a, g in jobs:
+                self.ops.dense_adagrad(p, a, g, self.lr, self.eps)
+        self._loss.copy_(loss_out)
 
     # -- one step ----------------------------------------------------------
     def _body(self) -> None:
@@ -998,15 +1080,14 @@ class ShardedTrainStep:
         rt = None
         if self.tables is not None:
             rt = self.tables.route_fixed([(k, ids) for k, ids, _, _ in self._lookups(self._static)], self._cap,
-                                         overflow=self._overflow)
+                                         overflow=self._overflow, idx_out=self._idx_all[:len(self._idx)])
             if os.environ.get("TT_SHARDED_KEEP", "1") == "1":
                 self._last_counts = rt.counts
             if os.environ.get("TT_SHARDED_DEBUG") == "2":  # running max of the per-owner counts, in the graph
                 if getattr(self, "_cmax", None) is None:
                     self._cmax = torch.zeros(1, dtype=torch.int64, device=rt.counts.device)
                 torch.maximum(self._cmax, rt.counts.max().reshape(1), out=self._cmax)
-            self.tables.fetch_routed(rt, out=self._got)
-            self._idx_all[:len(self._idx)].copy_(rt.idx_all)
+            self.tables.fetch_routed(rt, out=self._got)  # rt.idx_all IS self._idx_all[:L]
         self._middle()
         if rt is not None:
             self.tables.apply_routed(rt, self._g_req, self.lr, self.eps)

@@ -27,6 +27,7 @@ __all__ = [
     "sparse_adam",
     "dedup_sum",
     "dense_adagrad",
+    "dense_adagrad_many",
     "dense_adam",
     "inbatch_rows",
     "inbatch_cols",
@@ -35,6 +36,8 @@ __all__ = [
     "probe_arm_repeat",
     "route_requests",
     "route_pad",
+    "route_fixed",
+    "sparse_routed",
     "route_owner",
     "bruteforce_build",
     "bruteforce_search",
@@ -383,10 +386,13 @@ def sparse_scatter_sum(tables: Sequence[dict], batch: int, grad: torch.Tensor, w
                                   _stream()))
 
 
-def route_requests(lookups: Sequence[Tuple[torch.Tensor, int, int]], world: int, num_tags: int):
+def route_requests(lookups: Sequence[Tuple[torch.Tensor, int, int]], world: int, num_tags: int,
+                   ordered: bool = False):
     """lookups: (ids [B] int32, table rows, tag).  Returns (send [L*B, 2] int32
     capacity, counts [world] int64, num_requests [1] int32, idx [L, B] int32)
-    from tt_route_requests (owner-major deduplicated requests)."""
+    from tt_route_requests (owner-major deduplicated requests); ordered=True
+    appends the route's sorted order (order [L*B], grp_first / grp_last
+    [world*num_tags] int32, tt_route_requests_ordered) for sparse_routed."""
     L = len(lookups)
     B = lookups[0][0].numel()
     dev = lookups[0][0].device
@@ -406,9 +412,111 @@ def route_requests(lookups: Sequence[Tuple[torch.Tensor, int, int]], world: int,
     idx = torch.empty(L, B, dtype=torch.int32, device=dev)
     lib_ = lib()
     ws = Workspace.get(lib_.tt_route_workspace_size(L, B, world, max_rows, num_tags), dev, "route")
-    check(lib_.tt_route_requests(arr, L, B, world, num_tags, send.data_ptr(), counts.data_ptr(), nreq.data_ptr(),
-                                 idx.data_ptr(), ws.data_ptr(), ws.numel(), _stream()))
-    return send, counts, nreq, idx
+    if not ordered:
+        check(lib_.tt_route_requests(arr, L, B, world, num_tags, send.data_ptr(), counts.data_ptr(), nreq.data_ptr(),
+                                     idx.data_ptr(), ws.data_ptr(), ws.numel(), _stream()))
+        return send, counts, nreq, idx
+    order = torch.empty(L * B, dtype=torch.int32, device=dev)
+    grp = torch.empty(2, world * num_tags, dtype=torch.int32, device=dev)
+    check(lib_.tt_route_requests_ordered(arr, L, B, world, num_tags, send.data_ptr(), counts.data_ptr(),
+                                         nreq.data_ptr(), idx.data_ptr(), order.data_ptr(), grp[0].data_ptr(),
+                                         grp[1].data_ptr(), ws.data_ptr(), ws.numel(), _stream()))
+    return send, counts, nreq, idx, (order, grp[0], grp[1])
+
+
+def route_fixed(lookups: Sequence[Tuple[torch.Tensor, int, int]], world: int, num_tags: int, cap: int,
+                overflow: Optional[torch.Tensor] = None, ordered: bool = False, owner: bool = False,
+                idx_out: Optional[torch.Tensor] = None):
+    """The fixed-capacity route in one call (tt_route_fixed; one launch for
+    <= 16384 lookups): (send_padded [world*cap, 2], idx_padded [L, B],
+    counts [world] int64, (order, grp_first, grp_last) if ordered, and at
+    world 1 with owner=True (tags, rows, table_ids [num_tags, cap]) of the
+    slots) — equal to route_requests + route_pad (+ route_owner).  idx_out:
+    an [L, B] int32 buffer for idx_padded (e.g. a captured step's static one)."""
+    L = len(lookups)
+    B = lookups[0][0].numel()
+    dev = lookups[0][0].device
+    arr = (_native.RouteLookup * L)()
+    max_rows = 1
+    for i, (ids, rows, tag) in enumerate(lookups):
+        _req(ids, f"ids[{i}]", torch.int32, 1)
+        if ids.numel() != B or not ids.is_contiguous():
+            raise ValueError("route: every lookup needs a contiguous [B] int32 id tensor")
+        arr[i].ids = ids.data_ptr()
+        arr[i].num_rows = int(rows)
+        arr[i].tag = int(tag)
+        max_rows = max(max_rows, int(rows))
+    if owner and world != 1:
+        raise ValueError("route_fixed: owner=True is the world-1 shortcut")
+    slots = world * cap
+    send_p = torch.empty(slots, 2, dtype=torch.int32, device=dev)
+    if idx_out is not None:
+        _req(idx_out, "idx_out", torch.int32, 2)
+        if tuple(idx_out.shape) != (L, B) or not idx_out.is_contiguous():
+            raise ValueError(f"route_fixed: idx_out must be a contiguous [{L}, {B}] int32 buffer")
+    idx_p = idx_out if idx_out is not None else torch.empty(L, B, dtype=torch.int32, device=dev)
+    counts = torch.empty(world, dtype=torch.int64, device=dev)
+    if overflow is not None:
+        _req(overflow, "overflow", torch.int32, 1)
+    order = grp = own = None
+    if ordered:
+        order = torch.empty(L * B, dtype=torch.int32, device=dev)
+        grp = torch.empty(2, world * num_tags, dtype=torch.int32, device=dev)
+    if owner:
+        own = (torch.empty(slots, dtype=torch.int32, device=dev), torch.empty(slots, dtype=torch.int32, device=dev),
+               torch.empty(num_tags, slots, dtype=torch.int32, device=dev))
+    lib_ = lib()
+    ws = Workspace.get(lib_.tt_route_fixed_workspace_size(L, B, world, max_rows, num_tags), dev, "route")
+    check(lib_.tt_route_fixed(arr, L, B, world, num_tags, cap, send_p.data_ptr(), idx_p.data_ptr(), counts.data_ptr(),
+                              _ptr(overflow), _ptr(order), _ptr(grp[0] if grp is not None else None),
+                              _ptr(grp[1] if grp is not None else None), *(_ptr(t) for t in (own or (None,) * 3)),
+                              ws.data_ptr(), ws.numel(), _stream()))
+    return send_p, idx_p, counts, (order, grp[0], grp[1]) if ordered else None, own
+
+
+def sparse_routed(tables: Sequence[dict], batch: int, grad: Optional[torch.Tensor], route: dict, op: str,
+                  lr: float = 0.0, epsilon: float = 0.0, ws_tag: str = "sparse_routed") -> None:
+    """Per-request sums (op "sum", tt_sparse_scatter_sum semantics) or the
+    Adagrad update (op "adagrad", tables need slot0) of routed lookups, keyed
+    by the route's own sort (tt_sparse_routed: no second sort).  tables: as
+    for sparse_scatter_sum / sparse_adagrad (ids = each source lookup's slots).
+    route: order, grp_first, grp_last (route_requests(..., ordered=True)),
+    slot ([L, B] slots of every routed lookup), slot_row (optional [world*cap]
+    keys per slot), cap, world, num_tags and per routed lookup l its
+    lookup_tag / lookup_table / lookup_source."""
+    ld = 0
+    if grad is not None:
+        _req(grad, "grad", torch.float32, 2)
+        ld = _row_major(grad, "grad")
+    elif any(t.get("grad") is None for t in tables):
+        raise ValueError("grad is None but some table has no per-table grad")
+    if op not in ("sum", "adagrad"):
+        raise ValueError(f"sparse_routed: op must be 'sum' or 'adagrad', got {op!r}")
+    arr = _sparse_tables(tables, batch, adam=False, slots=op == "adagrad")
+    rs = _native.RouteSorted()
+    for name in ("order", "grp_first", "grp_last", "slot"):
+        t = route[name]
+        _req(t, name, torch.int32)
+        if not t.is_contiguous():
+            raise ValueError(f"sparse_routed: {name} must be contiguous")
+        setattr(rs, name, t.data_ptr())
+    rs.slot_row = _ptr(route.get("slot_row"))
+    rs.cap, rs.world, rs.num_tags = int(route["cap"]), int(route["world"]), int(route["num_tags"])
+    L = len(route["lookup_tag"])
+    if L > _native.ROUTE_MAX_LOOKUPS:
+        raise ValueError(f"sparse_routed: at most {_native.ROUTE_MAX_LOOKUPS} routed lookups, got {L}")
+    rs.num_lookups = L
+    for i in range(L):
+        rs.lookup_tag[i] = int(route["lookup_tag"][i])
+        rs.lookup_table[i] = int(route["lookup_table"][i])
+        rs.lookup_source[i] = int(route["lookup_source"][i])
+    lib_ = lib()
+    need = lib_.tt_sparse_workspace_size(arr, len(tables), batch)
+    dev = grad.device if grad is not None else tables[0]["grad"].device
+    ws = Workspace.get(need, dev, ws_tag)
+    check(lib_.tt_sparse_routed(arr, len(tables), batch, grad.data_ptr() if grad is not None else None, ld,
+                                ctypes.byref(rs), 1 if op == "adagrad" else 0, lr, epsilon, ws.data_ptr(), ws.numel(),
+                                _stream()))
 
 
 def route_pad(send: torch.Tensor, counts: torch.Tensor, idx: torch.Tensor, world: int, cap: int,
@@ -502,6 +610,20 @@ def dense_adagrad(param: torch.Tensor, accum: torch.Tensor, grad: torch.Tensor, 
             raise ValueError(f"{n} must be contiguous with param's numel")
     check(lib().tt_dense_adagrad(param.data_ptr(), accum.data_ptr(), grad.data_ptr(), param.numel(), lr, epsilon,
                                  _stream()))
+
+
+def dense_adagrad_many(jobs: Sequence[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]], lr: float,
+                       epsilon: float) -> None:
+    """dense_adagrad on up to 8 (param, accum, grad) buffers in one launch
+    (tt_dense_adagrad_many; bit-identical to one call each)."""
+    arr = (_native.DenseJob * len(jobs))()
+    for i, (p, a, g) in enumerate(jobs):
+        for name, t in (("param", p), ("accum", a), ("grad", g)):
+            _req(t, f"{name}[{i}]", torch.float32)
+            if not t.is_contiguous() or t.numel() != p.numel():
+                raise ValueError(f"dense_adagrad_many: {name}[{i}] must be contiguous with param's size")
+        arr[i].param, arr[i].accum, arr[i].grad, arr[i].n = p.data_ptr(), a.data_ptr(), g.data_ptr(), p.numel()
+    check(lib().tt_dense_adagrad_many(arr, len(jobs), lr, epsilon, _stream()))
 
 
 def dense_adam(param, m, v, grad, lr, beta1, beta2, epsilon, step) -> None:

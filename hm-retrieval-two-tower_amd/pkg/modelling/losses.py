@@ -201,8 +201,11 @@ def global_inbatch_grads(q: torch.Tensor, c: torch.Tensor, logq: Optional[torch.
     L = comm.all_gather(logq) if logq is not None else None   # [G b]
     lse, row_loss, dq = rows(q, C, L, pos_offset=off)
     Qa = comm.all_gather(q)                                    # [G b, E]
-    st = comm.all_gather(torch.stack([lse, row_loss], 1))      # [G b, 2]: every row's lse and loss
-    lse_a, loss_a = st[:, 0].contiguous(), st[:, 1].contiguous()
+    if comm.world == 1 and not getattr(comm, "always", False):
+        lse_a, loss_a = lse, row_loss  # one rank: its rows are every row (no stack / split copies)
+    else:
+        st = comm.all_gather(torch.stack([lse, row_loss], 1))  # [G b, 2]: every row's lse and loss
+        lse_a, loss_a = st[:, 0].contiguous(), st[:, 1].contiguous()
     dc = cols(Qa, lse_a, c, logq, pos_offset=off, row_loss=loss_a)  # local columns, every row
     return row_loss, dq, dc
 

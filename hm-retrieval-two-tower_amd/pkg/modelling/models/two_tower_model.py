@@ -105,11 +105,14 @@ class TwoTowerModel(AbstractKerasModel):
 
     def call(self, x: Dict[str, Any], training: bool = True) -> torch.Tensor:
         """[Q, C] scores of every query against every candidate of the batch
-        (two_tower_model.py:65-92); materialised, for inspection / small B
-        (the train step never forms it: losses.towers_inbatch_softmax_xent).
-        Without gradients the score matrix is libtt's (hip_ops.score_matrix,
-        bf16x3 MFMA: fp32-faithful); with gradients enabled it stays an
-        autograd matmul so callers can differentiate through it."""
+        (two_tower_model.py:65-92); materialised.  An INSPECTION path, not
+        the hot path: fit / train_step / the graphed and sharded steps never
+        call it (they never form [B, B]: losses.towers_inbatch_softmax_xent,
+        the fused tt_inbatch kernels).  Without gradients the score matrix is
+        libtt's (hip_ops.score_matrix, bf16x3 MFMA: fp32-faithful); with
+        gradients enabled it is a plain autograd matmul (the reference's
+        tf.matmul semantics) so a caller can differentiate through it — a
+        vendor GEMM, kept off the measured path on purpose."""
         q, c = self._split(x)
         with torch.set_grad_enabled(training and torch.is_grad_enabled()):
             qe, ce = self.query_tower.call(q), self.candidate_tower.call(c)

@@ -137,6 +137,19 @@ int tt_route_requests(const tt_route_lookup* lookups, int32_t num_lookups,
                       int32_t* send, long long* counts, int32_t* num_requests,
                       int32_t* idx, void* workspace, size_t workspace_bytes,
                       tt_stream_t stream);
+/* tt_route_requests plus the route's sorted order, so a sparse sum / update
+ * keyed by the requests needs no second sort (tt_sparse_routed):
+ *   order [num_lookups*batch] = the lookup (l*batch + b) at each sorted
+ *   position (owner, tag, row ascending; a request's lookups in lookup
+ *   order), grp_first / grp_last [world*num_tags] = the first / last sorted
+ *   position of each (owner, tag) group (empty: 0 / -1).  Any of the three
+ *   may be NULL (grp_first and grp_last together). */
+int tt_route_requests_ordered(const tt_route_lookup* lookups, int32_t num_lookups,
+                              int64_t batch, int32_t world, int32_t num_tags,
+                              int32_t* send, long long* counts, int32_t* num_requests,
+                              int32_t* idx, int32_t* order, int32_t* grp_first,
+                              int32_t* grp_last, void* workspace,
+                              size_t workspace_bytes, tt_stream_t stream);
 int tt_route_owner(const int32_t* recv, int64_t n, int32_t world,
                    int32_t num_tags, int32_t* tags, int32_t* rows,
                    int32_t* table_ids, tt_stream_t stream);
@@ -155,6 +168,24 @@ int tt_route_pad(const int32_t* send, const long long* counts, const int32_t* id
                  int64_t num_lookups, int32_t world, int64_t cap,
                  int32_t* send_padded, int32_t* idx_padded, int32_t* overflow,
                  tt_stream_t stream);
+
+/* The whole fixed-capacity route in one call: the outputs of
+ * tt_route_requests_ordered (counts, optional order / grp_first / grp_last)
+ * and tt_route_pad (send_padded, idx_padded, optional overflow), and at world
+ * 1 optionally tt_route_owner's view of the slots (owner_tags / owner_rows
+ * [cap], owner_table_ids [num_tags, cap]: at one rank the slots ARE the
+ * owner's requests).  Up to 16384 lookups whose keys fit 32 bits run as ONE
+ * workgroup launch (LDS radix sort + scan + slot writes; TT_ROUTE_FUSED=0
+ * forces the multi-launch path); otherwise the three calls above.  Results
+ * are identical either way.  Workspace: tt_route_fixed_workspace_size. */
+size_t tt_route_fixed_workspace_size(int32_t num_lookups, int64_t batch, int32_t world,
+                                     int64_t max_rows, int32_t num_tags);
+int tt_route_fixed(const tt_route_lookup* lookups, int32_t num_lookups, int64_t batch,
+                   int32_t world, int32_t num_tags, int64_t cap, int32_t* send_padded,
+                   int32_t* idx_padded, long long* counts, int32_t* overflow,
+                   int32_t* order, int32_t* grp_first, int32_t* grp_last,
+                   int32_t* owner_tags, int32_t* owner_rows, int32_t* owner_table_ids,
+                   void* workspace, size_t workspace_bytes, tt_stream_t stream);
 
 /* ------------------------------------------------------------------------ *
  * K8+K9  Sparse optimizer step on embedding tables.
@@ -254,6 +285,38 @@ int tt_sparse_scatter_sum(const tt_sparse_table* tables, int32_t num_tables,
                           void* workspace, size_t workspace_bytes,
                           tt_stream_t stream);
 
+/* The per-request sums / updates of routed lookups, keyed by the route's own
+ * sort (tt_route_requests_ordered + tt_route_pad): no second sort.  Table i
+ * lists its lookups as sources (ids = the lookups' slots, idx_padded rows, in
+ * lookup order) exactly as for tt_sparse_scatter_sum; `rs` maps every routed
+ * lookup l to (tag, table, source).  Each table must take the lookups of one
+ * tag.  Keys: the lookup's slot, or slot_row[slot] when slot_row is given
+ * (e.g. tt_route_owner's local rows at world 1; -1 = nothing).  op 0: the
+ * duplicate-summed rows written into each table (tt_sparse_scatter_sum);
+ * op 1: Adagrad on them (tt_sparse_adagrad, lr / epsilon).  Results equal
+ * those calls' on the same keys whenever the route lists each table's
+ * lookups in the order that call sorts them (world 1: always). */
+#define TT_ROUTE_MAX_LOOKUPS 32
+typedef struct {
+  const int32_t* order;     /* [num_lookups*batch], tt_route_requests_ordered */
+  const int32_t* grp_first; /* [world*num_tags]                              */
+  const int32_t* grp_last;
+  const int32_t* slot;      /* [num_lookups*batch] slot of each lookup (idx_padded) */
+  const int32_t* slot_row;  /* optional [world*cap]: key = slot_row[slot]     */
+  int64_t cap;
+  int32_t world;
+  int32_t num_tags;
+  int32_t num_lookups;
+  int32_t lookup_tag[TT_ROUTE_MAX_LOOKUPS];
+  int32_t lookup_table[TT_ROUTE_MAX_LOOKUPS];
+  int32_t lookup_source[TT_ROUTE_MAX_LOOKUPS];
+} tt_route_sorted;
+
+int tt_sparse_routed(const tt_sparse_table* tables, int32_t num_tables, int64_t batch,
+                     const float* grad, int64_t grad_stride, const tt_route_sorted* rs,
+                     int32_t op, float lr, float epsilon, void* workspace,
+                     size_t workspace_bytes, tt_stream_t stream);
+
 /* Dedup only (K8), for parity checks: writes the U distinct ids of
  * ids[0..n) in ascending order, the per-id gradient sums [U, dim] (rows of
  * `grad` summed in index order) and U (device int32).  Capacity n rows. */
@@ -267,6 +330,16 @@ int tt_dedup_sum(const int32_t* ids, int64_t n, int64_t num_rows,
  * ResourceApplyAdagradV2 / ResourceApplyAdam (optimizer_factory.py:15-18). */
 int tt_dense_adagrad(float* param, float* accum, const float* grad, int64_t n,
                      float lr, float epsilon, tt_stream_t stream);
+/* tt_dense_adagrad on up to 8 buffers in one launch (bit-identical to one
+ * call per buffer). */
+typedef struct {
+  float* param;
+  float* accum;
+  const float* grad;
+  int64_t n;
+} tt_dense_job;
+int tt_dense_adagrad_many(const tt_dense_job* jobs, int32_t num_jobs, float lr, float epsilon,
+                          tt_stream_t stream);
 int tt_dense_adam(float* param, float* m, float* v, const float* grad,
                   int64_t n, float lr, float beta1, float beta2, float epsilon,
                   int64_t step, tt_stream_t stream);

@@ -208,6 +208,13 @@ def _sharded_worker(rank, world, port, tables, lookups, grads, out):
         fwd = [got[i.long()].numpy() for i in idx]
         st.apply([(g, [(idx[l], 16 * l) for l in range(len(lk))])], lr=0.05, eps=1e-7)
         res[mode] = (fwd, {k: st.gather_full(k).numpy() for k in tables}, int(ov.item()))
+    # route_fixed + fetch_routed + apply_lookups (per-lookup gradients): the
+    # same update as apply() on the fixed route
+    st = ShardedTables({k: torch.from_numpy(v) for k, v in tables.items()}, 0.1, ops=_cpu_embedding_ops())
+    rt = st.route_fixed(lk, st.route_capacity(len(lk), lk[0][1].numel()))
+    got = st.fetch_routed(rt)
+    st.apply_lookups(rt, [(g, 16 * l) for l in range(len(lk))], lr=0.05, eps=1e-7)
+    res["lookups"] = ([got[i.long()].numpy() for i in rt.idx], {k: st.gather_full(k).numpy() for k in tables}, 0)
     out[rank] = res
     dist.destroy_process_group()
 
@@ -249,6 +256,9 @@ def test_sharded_tables_match_unsharded_adagrad(world):
         assert ff[2] == 0
         assert all(np.array_equal(x, y) for x, y in zip(ff[0], fc[0]))
         assert all(np.array_equal(ff[1][k], fc[1][k]) for k in tables)
+        fl = out[r]["lookups"]
+        assert all(np.array_equal(x, y) for x, y in zip(fl[0], fc[0]))
+        assert all(np.array_equal(fl[1][k], fc[1][k]) for k in tables)
         # a capacity of 5 slots per owner drops requests and counts them: the
         # distinct (table, row) requests of this rank per owner, minus 5
         reqs = {}

@@ -758,3 +758,115 @@ def test_sparse_adagrad_rows_equals_sorted_apply_on_distinct_rows(cuda, dim):
     hip_ops.sparse_adagrad(specs, n, grad, 0.05, 1e-7)
     for x, y in zip(t1 + a1, t2 + a2):
         assert torch.equal(x, y)
+
+
+def _routed_case(cuda, world, B, seed, invalid=False):
+    """Three sharded tables, five lookups (two tables with two sources each,
+    Zipf ids with long duplicate runs), routed with tt_route_requests_ordered
+    + tt_route_pad at `world`: the lookups, the route tensors and per table
+    its (lookup, source) list."""
+    rng = np.random.default_rng(seed)
+    rows = [5000, 1371980, 700]
+    tags = [0, 1, 1, 2, 0]
+    ids = [zipf_ids(rng, B, rows[t], 1.05) for t in tags]
+    if invalid:
+        ids[3][::53] = -1
+        ids[3][::71] = 700 + 5
+    lookups = [(_t(x, cuda), rows[t], t) for x, t in zip(ids, tags)]
+    send, counts, _, idx, order = hip_ops.route_requests(lookups, world, 3, ordered=True)
+    cap = len(tags) * B
+    sp, ip = hip_ops.route_pad(send, counts, idx, world, cap)
+    _, rws, _ = hip_ops.route_owner(sp, world, 3)
+    tab_of_tag = {0: 0, 1: 1, 2: 2}
+    src = {}
+    lk_table, lk_source = [], []
+    for l, t in enumerate(tags):
+        src.setdefault(t, []).append(l)
+        lk_table.append(tab_of_tag[t])
+        lk_source.append(len(src[t]) - 1)
+    route = dict(order=order[0], grp_first=order[1], grp_last=order[2], slot=ip, cap=cap, world=world, num_tags=3,
+                 lookup_tag=tags, lookup_table=lk_table, lookup_source=lk_source)
+    return rows, tags, ids, ip, rws, route, src
+
+
+@pytest.mark.parametrize("world", [1, 3, 8])
+def test_sparse_routed_sum_equals_scatter_sum(cuda, world):
+    """tt_sparse_routed (op sum: keys from the route's own sort, no second
+    sort) writes the same per-request sums as tt_sparse_scatter_sum keyed by
+    each lookup's slot, bit for bit, at 1, 3 and 8 owners (one table with one
+    source, two with two), Zipf duplicate runs longer than a block included,
+    and an invalid id's request like any other."""
+    B, D = 4096, 64
+    rows, tags, ids, ip, _, route, src = _routed_case(cuda, world, B, 40 + world, invalid=True)
+    rng = np.random.default_rng(world)
+    grads = [torch.as_tensor(rng.standard_normal((B, 3 * D)).astype(np.float32), device=cuda) for _ in range(3)]
+    slots = world * route["cap"]
+
+    def specs(g_req):
+        return [dict(table=g_req, ids=[ip[l] for l in src[t]], grad_col_offset=[D * (l % 3) for l in src[t]],
+                     grad=grads[t]) for t in range(3)]
+
+    g1 = torch.full((slots, D), 7.0, device=cuda)
+    hip_ops.sparse_routed(specs(g1), B, None, route, "sum")
+    g2 = torch.full((slots, D), 7.0, device=cuda)
+    hip_ops.sparse_scatter_sum(specs(g2), B, grads[0])
+    torch.cuda.synchronize()
+    assert torch.equal(g1, g2)
+    assert (g1 != 7.0).any()
+
+
+@pytest.mark.parametrize("B", [512, 16384])
+def test_sparse_routed_adagrad_world1_equals_sparse_adagrad(cuda, B):
+    """At world 1 tt_sparse_routed (op Adagrad, keys = the owner's local rows
+    per slot) is the single-GPU tt_sparse_adagrad on the raw ids: tables and
+    accumulators bit-identical, two sources per table included."""
+    D = 128
+    rows, tags, ids, ip, rws, route, src = _routed_case(cuda, 1, B, B)
+    route["slot_row"] = rws
+    rng = np.random.default_rng(B + 1)
+    grads = [torch.as_tensor(rng.standard_normal((B, 2 * D)).astype(np.float32), device=cuda) for _ in range(3)]
+    tabs = [torch.as_tensor(rng.standard_normal((r, D)).astype(np.float32) * 0.05, device=cuda) for r in rows]
+    accs = [torch.full_like(t, 0.1) for t in tabs]
+
+    def specs(tt, aa, per_lookup):
+        return [dict(table=tt[t], slot0=aa[t], ids=[per_lookup[l] for l in src[t]],
+                     grad_col_offset=[D * (k % 2) for k in range(len(src[t]))], grad=grads[t]) for t in range(3)]
+
+    t1, a1 = [t.clone() for t in tabs], [a.clone() for a in accs]
+    hip_ops.sparse_routed(specs(t1, a1, list(ip.unbind(0))), B, None, route, "adagrad", 0.05, 1e-7)
+    t2, a2 = [t.clone() for t in tabs], [a.clone() for a in accs]
+    hip_ops.sparse_adagrad(specs(t2, a2, [_t(x, cuda) for x in ids]), B, None, 0.05, 1e-7)
+    torch.cuda.synchronize()
+    for x, y in zip(t1 + a1, t2 + a2):
+        assert torch.equal(x, y)
+    assert not torch.equal(t1[1], tabs[1])
+
+
+@pytest.mark.parametrize("world,B", [(1, 2048), (3, 2048), (8, 1024), (1, 16384), (2, 16384)])
+def test_route_fixed_equals_composed_route(cuda, world, B):
+    """tt_route_fixed (one workgroup for <= 16384 lookups; the multi-launch
+    path above that) equals tt_route_requests_ordered + tt_route_pad (+
+    tt_route_owner at world 1) on every output, bit for bit: padded requests,
+    slots, counts, sorted order, group bounds and the owner view — Zipf ids
+    with an invalid id, at a never-overflowing capacity and at one that
+    drops requests (same overflow count)."""
+    rng = np.random.default_rng(world * 7 + B)
+    rows = [1371980, 352899, 700]
+    ids = [zipf_ids(rng, B, rows[t], 1.05) for t in range(3)]
+    ids[2][::101] = -1
+    lookups = [(_t(x, cuda), rows[t], t) for t, x in enumerate(ids)]
+    for cap in (3 * B, max(1, B // (2 * world))):
+        ov1 = torch.zeros(1, dtype=torch.int32, device=cuda)
+        sp1, ip1, c1, (o1, gf1, gl1), own1 = hip_ops.route_fixed(lookups, world, 3, cap, ov1, ordered=True,
+                                                                 owner=world == 1)
+        send, c2, _, idx, (o2, gf2, gl2) = hip_ops.route_requests(lookups, world, 3, ordered=True)
+        ov2 = torch.zeros(1, dtype=torch.int32, device=cuda)
+        sp2, ip2 = hip_ops.route_pad(send, c2, idx, world, cap, ov2)
+        torch.cuda.synchronize()
+        for a, b in ((sp1, sp2), (ip1, ip2), (c1, c2), (o1, o2), (gf1, gf2), (gl1, gl2), (ov1, ov2)):
+            assert torch.equal(a, b)
+        if cap == 3 * B:
+            assert int(ov1.item()) == 0
+        if world == 1:
+            for a, b in zip(own1, hip_ops.route_owner(sp2, 1, 3)):
+                assert torch.equal(a, b)
