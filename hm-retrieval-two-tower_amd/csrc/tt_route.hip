@@ -25,7 +25,6 @@
 // loop was a chain of dependent misses.)
 #include <algorithm>
 #include <cstdlib>
-#include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "tt_common.h"
@@ -50,10 +49,13 @@ struct RouteArgs {
   int32_t world;
   int32_t num_tags;
   int32_t id_bits;
-  unsigned long long* keys_in;
+  void* keys_in;  // KeyT [total]
   uint32_t* vals_in;
 };
 
+// KeyT: uint32_t when the key bits in use fit 32 (every config here: the
+// sort then moves and compares half the key bytes), else 64-bit
+template <typename KeyT>
 __global__ void __launch_bounds__(256) route_keys_kernel(const RouteArgs a) {
   const int64_t i = blockIdx.x * 256ll + threadIdx.x;
   const int64_t total = a.batch * a.num;
@@ -63,9 +65,10 @@ __global__ void __launch_bounds__(256) route_keys_kernel(const RouteArgs a) {
   const RouteLookup& L = a.lk[l];
   const int32_t r = L.ids[b];
   const bool ok = r >= 0 && r < L.num_rows;
-  const unsigned long long owner = ok ? static_cast<unsigned long long>(r % a.world) : a.world - 1;
-  const unsigned long long rowp1 = ok ? static_cast<unsigned long long>(r) + 1ull : 0ull;
-  a.keys_in[i] = ((owner * a.num_tags + static_cast<unsigned long long>(L.tag)) << a.id_bits) | rowp1;
+  const KeyT owner = ok ? static_cast<KeyT>(r % a.world) : static_cast<KeyT>(a.world - 1);
+  const KeyT rowp1 = ok ? static_cast<KeyT>(r) + KeyT(1) : KeyT(0);
+  static_cast<KeyT*>(a.keys_in)[i] = ((owner * static_cast<KeyT>(a.num_tags) + static_cast<KeyT>(L.tag)) << a.id_bits) |
+                                     rowp1;
   a.vals_in[i] = static_cast<uint32_t>(i);
 }
 
@@ -75,7 +78,8 @@ __global__ void __launch_bounds__(256) route_keys_kernel(const RouteArgs a) {
 // before it (wave-parallel), scans its own heads and writes send / idx and
 // its per-owner counts (LDS, then one atomic per owner per block into the
 // zeroed counts); the last block writes the request total.
-__global__ void __launch_bounds__(kScanThreads) route_heads_kernel(const unsigned long long* keys, int64_t total,
+template <typename KeyT>
+__global__ void __launch_bounds__(kScanThreads) route_heads_kernel(const KeyT* keys, int64_t total,
                                                                    int32_t* block_heads, long long* counts,
                                                                    int32_t world, int32_t* grp_first, int32_t* grp_last,
                                                                    int32_t groups) {
@@ -106,7 +110,8 @@ __global__ void __launch_bounds__(kScanThreads) route_heads_kernel(const unsigne
   }
 }
 
-__global__ void __launch_bounds__(kScanThreads) route_write_kernel(const unsigned long long* keys, const uint32_t* vals,
+template <typename KeyT>
+__global__ void __launch_bounds__(kScanThreads) route_write_kernel(const KeyT* keys, const uint32_t* vals,
                                                                    int64_t total, int32_t world, int32_t num_tags,
                                                                    int32_t id_bits, const int32_t* block_heads,
                                                                    int32_t* send, int32_t* idx, long long* counts,
@@ -125,7 +130,7 @@ __global__ void __launch_bounds__(kScanThreads) route_write_kernel(const unsigne
     if (lane == 0) base_s = t;
   }
   const int64_t i = static_cast<int64_t>(blockIdx.x) * kScanThreads + threadIdx.x;
-  const unsigned long long k = i < total ? keys[i] : 0ull;
+  const KeyT k = i < total ? keys[i] : KeyT(0);
   const int head = (i < total && (i == 0 || k != keys[i - 1])) ? 1 : 0;
   const uint64_t m = __ballot(head);
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
@@ -145,8 +150,8 @@ __global__ void __launch_bounds__(kScanThreads) route_write_kernel(const unsigne
   if (i < total) {
     const int u = base_s + wsum[w] + incl - 1;  // request index of this key's run
     if (head) {
-      const unsigned long long mask = (1ull << id_bits) - 1ull;
-      const unsigned long long ot = k >> id_bits;
+      const KeyT mask = (KeyT(1) << id_bits) - KeyT(1);
+      const KeyT ot = k >> id_bits;
       send[2 * static_cast<int64_t>(u)] = static_cast<int32_t>(static_cast<long long>(k & mask) - 1);
       send[2 * static_cast<int64_t>(u) + 1] = static_cast<int32_t>(ot % num_tags);
       atomicAdd(&cnt[static_cast<int>(ot / num_tags)], 1);
@@ -154,7 +159,7 @@ __global__ void __launch_bounds__(kScanThreads) route_write_kernel(const unsigne
     idx[vals[i]] = u;
     if (order) order[i] = static_cast<int32_t>(vals[i]);
     if (grp_first) {  // first / last sorted position of each (owner, tag) group
-      const unsigned long long g = k >> id_bits;
+      const KeyT g = k >> id_bits;
       if (i == 0 || (keys[i - 1] >> id_bits) != g) grp_first[g] = static_cast<int32_t>(i);
       if (i == total - 1 || (keys[i + 1] >> id_bits) != g) grp_last[g] = static_cast<int32_t>(i);
     }
@@ -253,11 +258,11 @@ __device__ unsigned long long g_route_stamps[8];  // phase end times (wall clock
 #endif
 constexpr int kRsThreads = 1024;
 constexpr int kRsWaves = kRsThreads / kWave;
-constexpr int kRsMax = 16384;
 // the one-workgroup route wins only at small batches (one CU's LDS radix
 // passes: 25 vs 31 us per call at 3 x 1024 lookups, 44 vs 46 at 3 x 2048,
 // 108 vs 46 at 3 x 5461 — tools/time_route.py, profiles/r05_route_fused.txt)
-constexpr int kRsFusedMax = 8192;
+constexpr int kRsMax = 8192;
+constexpr int kRsPer = kRsMax / kRsThreads;  // lookups staged per thread
 constexpr int kRsTiles = kRsMax / kRsWaves / kWave;  // 64-lane tiles per wave at the maximum
 constexpr int kRsHistStride = kRsWaves + 1;
 constexpr size_t kRsLdsBytes = size_t(kRsMax) * 4 + size_t(2) * kRsMax * 2 + size_t(256) * kRsHistStride * 4 +
@@ -333,17 +338,31 @@ __global__ void __launch_bounds__(kRsThreads) route_fixed_small_kernel(const Rou
   const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
   const int n = static_cast<int>(a.batch * a.num);
   const int W = a.world, T = a.num_tags;
-  // keys: (owner, tag, row + 1) as in route_keys_kernel, 32 bits
-  for (int i = tid; i < n; i += kRsThreads) {
-    const int l = static_cast<int>(i / a.batch);
-    const int b = i - static_cast<int>(l * a.batch);
-    const RouteLookup& L = a.lk[l];
-    const int32_t r = L.ids[b];
-    const bool ok = r >= 0 && r < L.num_rows;
-    const uint32_t owner = ok ? static_cast<uint32_t>(r % W) : static_cast<uint32_t>(W - 1);
-    const uint32_t rowp1 = ok ? static_cast<uint32_t>(r) + 1u : 0u;
-    lkey[i] = ((owner * static_cast<uint32_t>(T) + static_cast<uint32_t>(L.tag)) << a.id_bits) | rowp1;
-    pb0[i] = static_cast<uint16_t>(i);
+  // keys: (owner, tag, row + 1) as in route_keys_kernel, 32 bits; every id
+  // load of the thread issued before the first is used
+  {
+    const int B = static_cast<int>(a.batch);
+    int32_t r[kRsPer];
+    int lk[kRsPer];
+#pragma unroll
+    for (int u = 0; u < kRsPer; ++u) {
+      const int i = tid + u * kRsThreads;
+      const int l = i < n ? i / B : 0;
+      lk[u] = l;
+      r[u] = i < n ? a.lk[l].ids[i - l * B] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kRsPer; ++u) {
+      const int i = tid + u * kRsThreads;
+      if (i < n) {
+        const RouteLookup& L = a.lk[lk[u]];
+        const bool ok = r[u] >= 0 && r[u] < L.num_rows;
+        const uint32_t owner = ok ? static_cast<uint32_t>(r[u] % W) : static_cast<uint32_t>(W - 1);
+        const uint32_t rowp1 = ok ? static_cast<uint32_t>(r[u]) + 1u : 0u;
+        lkey[i] = ((owner * static_cast<uint32_t>(T) + static_cast<uint32_t>(L.tag)) << a.id_bits) | rowp1;
+        pb0[i] = static_cast<uint16_t>(i);
+      }
+    }
   }
   for (int o = tid; o <= W; o += kRsThreads) cnt[o] = 0;
   if (a.grp_first)
@@ -509,29 +528,23 @@ __global__ void __launch_bounds__(kRsThreads) route_fixed_small_kernel(const Rou
 }
 
 // The route's device sort: rocPRIM's merge path below TT_SORT_MERGE_LIMIT
-// (block sort + ~6 merge launches at 65,536 keys) or, TT_ROUTE_SORT=onesweep,
-// its onesweep radix path (histogram + one launch per 8-bit digit of the key
-// bits in use: 4 at C5's 27-bit keys).
-using RouteOnesweep = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                                 rocprim::default_config, 0>;
-bool route_onesweep() {
-  static const bool v = [] {
-    const char* e = std::getenv("TT_ROUTE_SORT");
-    return e && std::strcmp(e, "onesweep") == 0;
-  }();
-  return v;
-}
+// (block sort + ~6 merge launches at 65,536 keys).  Its onesweep radix path
+// (histogram + one launch per 8-bit digit) measured slower at C5: 0.19 vs
+// 0.13 ms per step (tools/runs/gpu_s05_route3.sh).
 size_t route_sort_bytes(int64_t total, int end_bit) {
-  size_t a = 0, b = 0;
-  unsigned long long* kp = nullptr;
+  size_t a = 0;
   uint32_t* vp = nullptr;
-  const hipError_t ea = rocprim::radix_sort_pairs<SortConfig>(nullptr, a, kp, kp, vp, vp, static_cast<unsigned>(total),
-                                                              0, end_bit, nullptr, false);
-  const hipError_t eb = rocprim::radix_sort_pairs<RouteOnesweep>(nullptr, b, kp, kp, vp, vp,
-                                                                 static_cast<unsigned>(total), 0, end_bit, nullptr,
-                                                                 false);
-  if (ea != hipSuccess || eb != hipSuccess) return static_cast<size_t>(total) * 24 + (size_t(4) << 20);
-  return std::max(a, b);
+  hipError_t e;
+  if (end_bit <= 32) {
+    uint32_t* kp = nullptr;
+    e = rocprim::radix_sort_pairs<SortConfig>(nullptr, a, kp, kp, vp, vp, static_cast<unsigned>(total), 0, end_bit,
+                                              nullptr, false);
+  } else {
+    unsigned long long* kp = nullptr;
+    e = rocprim::radix_sort_pairs<SortConfig>(nullptr, a, kp, kp, vp, vp, static_cast<unsigned>(total), 0, end_bit,
+                                              nullptr, false);
+  }
+  return e == hipSuccess ? a : static_cast<size_t>(total) * 24 + (size_t(4) << 20);
 }
 
 int bits_for(int64_t x) {  // bits needed to represent values in [0, x]
@@ -632,23 +645,27 @@ extern "C" int tt_route_requests_ordered(const tt_route_lookup* lookups, int32_t
   a.id_bits = p.id_bits;
   a.keys_in = w.keys_in;
   a.vals_in = w.vals_in;
-  hipLaunchKernelGGL(route_keys_kernel, dim3(static_cast<unsigned>(ceil_div(p.total, 256))), dim3(256), 0, st, a);
-  TT_CHECK_LAUNCH();
-  size_t sb = p.sort_bytes;
-  if (route_onesweep())
-    TT_CHECK_HIP(rocprim::radix_sort_pairs<RouteOnesweep>(w.sort_tmp, sb, w.keys_in, w.keys, w.vals_in, w.vals,
-                                                          static_cast<unsigned>(p.total), 0, p.end_bit, st, false));
-  else
-    TT_CHECK_HIP(rocprim::radix_sort_pairs<SortConfig>(w.sort_tmp, sb, w.keys_in, w.keys, w.vals_in, w.vals,
+  const auto run = [&](auto key_tag) -> int {
+    using KeyT = decltype(key_tag);
+    KeyT* kin = reinterpret_cast<KeyT*>(w.keys_in);
+    KeyT* kout = reinterpret_cast<KeyT*>(w.keys);
+    hipLaunchKernelGGL(route_keys_kernel<KeyT>, dim3(static_cast<unsigned>(ceil_div(p.total, 256))), dim3(256), 0, st,
+                       a);
+    TT_CHECK_LAUNCH();
+    size_t sb = p.sort_bytes;
+    TT_CHECK_HIP(rocprim::radix_sort_pairs<SortConfig>(w.sort_tmp, sb, kin, kout, w.vals_in, w.vals,
                                                        static_cast<unsigned>(p.total), 0, p.end_bit, st, false));
-  const unsigned nb = static_cast<unsigned>(ceil_div(p.total, kScanThreads));
-  hipLaunchKernelGGL(route_heads_kernel, dim3(nb), dim3(kScanThreads), 0, st, w.keys, p.total, w.block_heads, counts,
-                     world, grp_first, grp_last, world * num_tags);
-  TT_CHECK_LAUNCH();
-  hipLaunchKernelGGL(route_write_kernel, dim3(nb), dim3(kScanThreads), 0, st, w.keys, w.vals, p.total, world,
-                     num_tags, p.id_bits, w.block_heads, send, idx, counts, num_requests, order, grp_first, grp_last);
-  TT_CHECK_LAUNCH();
-  return TT_OK;
+    const unsigned nb = static_cast<unsigned>(ceil_div(p.total, kScanThreads));
+    hipLaunchKernelGGL(route_heads_kernel<KeyT>, dim3(nb), dim3(kScanThreads), 0, st, kout, p.total, w.block_heads,
+                       counts, world, grp_first, grp_last, world * num_tags);
+    TT_CHECK_LAUNCH();
+    hipLaunchKernelGGL(route_write_kernel<KeyT>, dim3(nb), dim3(kScanThreads), 0, st, kout, w.vals, p.total, world,
+                       num_tags, p.id_bits, w.block_heads, send, idx, counts, num_requests, order, grp_first,
+                       grp_last);
+    TT_CHECK_LAUNCH();
+    return TT_OK;
+  };
+  return p.end_bit <= 32 ? run(uint32_t{}) : run(static_cast<unsigned long long>(0));
 }
 
 extern "C" int tt_route_requests(const tt_route_lookup* lookups, int32_t num_lookups, int64_t batch, int32_t world,
@@ -710,7 +727,7 @@ bool route_fused(const RoutePlan& p) {
     const char* e = std::getenv("TT_ROUTE_FUSED");
     return e && e[0] == '0';
   }();
-  return !off && p.total <= kRsFusedMax && p.end_bit <= 32;
+  return !off && p.total <= kRsMax && p.end_bit <= 32;
 }
 }  // namespace
 }  // namespace tt

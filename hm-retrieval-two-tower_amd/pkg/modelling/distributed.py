@@ -326,10 +326,12 @@ class QueryShardedBruteForceIndex:
 
 
 # --------------------------------------------------------------------------- row-sharded tables
-def torch_route_requests(lookups: List[Tuple[torch.Tensor, int, int]], world: int, num_tags: int):
+def torch_route_requests(lookups: List[Tuple[torch.Tensor, int, int]], world: int, num_tags: int,
+                         ordered: bool = False):
     """Restatement of tt_route_requests in torch ops (the CPU/gloo tests'
     implementation): (send [R, 2], counts [world] int64, num_requests [1],
-    idx [L, B])."""
+    idx [L, B]); ordered=True appends tt_route_requests_ordered's (order,
+    grp_first, grp_last)."""
     dev = lookups[0][0].device
     B = lookups[0][0].numel()
     by_tag: Dict[int, List[int]] = {}
@@ -363,7 +365,26 @@ def torch_route_requests(lookups: List[Tuple[torch.Tensor, int, int]], world: in
         u = inverse[tag][k:k + B]
         pos[tag] = k + B
         idx[i] = inv_perm[starts[tag] + u].to(torch.int32)
-    return send, counts, torch.tensor([R], dtype=torch.int32, device=dev), idx
+    nreq = torch.tensor([R], dtype=torch.int32, device=dev)
+    if not ordered:
+        return send, counts, nreq, idx
+    # the route's sort: lookups by (owner, tag, row + 1), stable in lookup order
+    keys = []
+    for ids, rows, tag in lookups:
+        r = ids.reshape(-1).to(torch.int64)
+        ok = (r >= 0) & (r < rows)
+        owner = torch.where(ok, torch.remainder(r, world), torch.full_like(r, world - 1))
+        keys.append(((owner * num_tags + tag) << 32) | torch.where(ok, r + 1, torch.zeros_like(r)))
+    keys = torch.cat(keys)
+    order = torch.sort(keys, stable=True)[1]
+    g = (keys[order] >> 32).tolist()
+    first = torch.zeros(world * num_tags, dtype=torch.int32)
+    last = torch.full((world * num_tags,), -1, dtype=torch.int32)
+    for p, gg in enumerate(g):
+        if p == 0 or g[p - 1] != gg:
+            first[gg] = p
+        last[gg] = p
+    return send, counts, nreq, idx, (order.to(torch.int32).to(dev), first.to(dev), last.to(dev))
 
 
 def torch_route_pad(send: torch.Tensor, counts: torch.Tensor, idx: torch.Tensor, world: int, cap: int,
@@ -961,7 +982,8 @@ class ShardedTrainStep:
         self._cap = full if self.route_capacity is None else max(1, min(self.route_capacity, full))
         slots = self.world * self._cap
         dim = self.tables.dim if self.tables is not None else 1
-        self._got = torch.zeros(slots, dim, dtype=torch.float32, device=dev)
+        # the fetched rows (world 1: unused, the middle reads the shard)
+        self._got = torch.zeros(slots if self.world > 1 else 1, dim, dtype=torch.float32, device=dev)
         self._g_req = torch.zeros(slots, dim, dtype=torch.float32, device=dev)
         # dropped requests (capacity); TT_SHARDED_DEBUG=1: between two canary words
         self._canary = torch.full((3,), 0x7EADBEEF, dtype=torch.int32, device=dev)
@@ -1001,7 +1023,10 @@ class ShardedTrainStep:
             for f, off in zip(layer.categorical_features, layer.column_offsets()):
                 t = layer.embedding_layers[f.name]
                 if hasattr(t, "_shard_key"):
-                    segs.append((self._got, self._idx[j], off))
+                    if self.world == 1:  # one rank: the shard IS the fetched rows, read by id directly
+                        segs.append((self.tables.shard[t._shard_key], layer._ids(xx[f.name]), off))
+                    else:
+                        segs.append((self._got, self._idx[j], off))
                     big_srcs.setdefault(t._shard_key, (li, []))[1].append((self._idx[j], off))
                     j += 1
                 else:
@@ -1087,7 +1112,8 @@ class ShardedTrainStep:
                 if getattr(self, "_cmax", None) is None:
                     self._cmax = torch.zeros(1, dtype=torch.int64, device=rt.counts.device)
                 torch.maximum(self._cmax, rt.counts.max().reshape(1), out=self._cmax)
-            self.tables.fetch_routed(rt, out=self._got)  # rt.idx_all IS self._idx_all[:L]
+            if self.world > 1:  # world 1: the middle gathers from the shard itself
+                self.tables.fetch_routed(rt, out=self._got)  # rt.idx_all IS self._idx_all[:L]
         self._middle()
         if rt is not None:
             self.tables.apply_routed(rt, self._g_req, self.lr, self.eps)

@@ -174,7 +174,7 @@ int tt_route_pad(const int32_t* send, const long long* counts, const int32_t* id
  * and tt_route_pad (send_padded, idx_padded, optional overflow), and at world
  * 1 optionally tt_route_owner's view of the slots (owner_tags / owner_rows
  * [cap], owner_table_ids [num_tags, cap]: at one rank the slots ARE the
- * owner's requests).  Up to 16384 lookups whose keys fit 32 bits run as ONE
+ * owner's requests).  Up to 8192 lookups whose keys fit 32 bits run as ONE
  * workgroup launch (LDS radix sort + scan + slot writes; TT_ROUTE_FUSED=0
  * forces the multi-launch path); otherwise the three calls above.  Results
  * are identical either way.  Workspace: tt_route_fixed_workspace_size. */

@@ -130,8 +130,9 @@ def test_sharded_index_equals_unsharded(world):
 
 
 # --------------------------------------------------------------------------- row-sharded tables (C5)
-def _cpu_embedding_ops():
-    """CPU restatement of the libtt kernels the sharded path calls (test-only)."""
+def _cpu_embedding_ops(routed: bool = False):
+    """CPU restatement of the libtt kernels the sharded path calls (test-only);
+    routed: with the route-keyed sparse op (tt_sparse_routed's semantics)."""
     from pkg.modelling.distributed import EmbeddingOps
 
     def gather_multi(calls, batch):
@@ -161,10 +162,11 @@ def _cpu_embedding_ops():
             d = tab.shape[1]
             acc = torch.zeros_like(tab, dtype=torch.float64)
             touched = torch.zeros(tab.shape[0], dtype=torch.bool)
+            g_s = s.get("grad") if s.get("grad") is not None else grad
             for ids, off in zip(s["ids"], s["grad_col_offset"]):
                 ii = ids.long()
                 ok = (ii >= 0) & (ii < tab.shape[0])
-                acc.index_add_(0, ii[ok], grad[ok, off:off + d].double())
+                acc.index_add_(0, ii[ok], g_s[ok, off:off + d].double())
                 touched[ii[ok]] = True
             tab[touched] = acc[touched].float()
 
@@ -174,10 +176,11 @@ def _cpu_embedding_ops():
             d = tab.shape[1]
             g = torch.zeros_like(tab, dtype=torch.float64)
             touched = torch.zeros(tab.shape[0], dtype=torch.bool)
+            g_s = s.get("grad") if s.get("grad") is not None else grad
             for ids, off in zip(s["ids"], s["grad_col_offset"]):
                 ii = ids.long()
                 ok = (ii >= 0) & (ii < tab.shape[0])
-                g.index_add_(0, ii[ok], grad[ok, off:off + d].double())
+                g.index_add_(0, ii[ok], g_s[ok, off:off + d].double())
                 touched[ii[ok]] = True
             gt = g[touched]
             a = accum[touched].double() + gt * gt
@@ -189,7 +192,16 @@ def _cpu_embedding_ops():
         acc.copy_(a.float())
         p.copy_((p.double() - lr * g.double() / (a.sqrt() + eps)).float())
 
-    return EmbeddingOps(gather_multi, gather_tagged, scatter_sum, sparse_adagrad, dense_adagrad)
+    def sparse_routed(specs, batch, grad, route, op, lr=0.0, eps=0.0):
+        # keyed by slot: the per-request sums; keyed by slot_row (world 1):
+        # the owner's Adagrad on its local rows
+        if op == "sum":
+            return scatter_sum(specs, batch, grad)
+        rows = route["slot_row"]
+        return sparse_adagrad([dict(sp, ids=[rows[i.long()] for i in sp["ids"]]) for sp in specs], batch, grad, lr, eps)
+
+    return EmbeddingOps(gather_multi, gather_tagged, scatter_sum, sparse_adagrad, dense_adagrad,
+                        sparse_routed=sparse_routed if routed else None)
 
 
 def _sharded_worker(rank, world, port, tables, lookups, grads, out):
@@ -210,16 +222,17 @@ def _sharded_worker(rank, world, port, tables, lookups, grads, out):
         res[mode] = (fwd, {k: st.gather_full(k).numpy() for k in tables}, int(ov.item()))
     # route_fixed + fetch_routed + apply_lookups (per-lookup gradients): the
     # same update as apply() on the fixed route
-    st = ShardedTables({k: torch.from_numpy(v) for k, v in tables.items()}, 0.1, ops=_cpu_embedding_ops())
-    rt = st.route_fixed(lk, st.route_capacity(len(lk), lk[0][1].numel()))
-    got = st.fetch_routed(rt)
-    st.apply_lookups(rt, [(g, 16 * l) for l in range(len(lk))], lr=0.05, eps=1e-7)
-    res["lookups"] = ([got[i.long()].numpy() for i in rt.idx], {k: st.gather_full(k).numpy() for k in tables}, 0)
+    for mode, routed in (("lookups", False), ("routed", True)):
+        st = ShardedTables({k: torch.from_numpy(v) for k, v in tables.items()}, 0.1, ops=_cpu_embedding_ops(routed))
+        rt = st.route_fixed(lk, st.route_capacity(len(lk), lk[0][1].numel()))
+        got = st.fetch_routed(rt)
+        st.apply_lookups(rt, [(g, 16 * l) for l in range(len(lk))], lr=0.05, eps=1e-7)
+        res[mode] = ([got[i.long()].numpy() for i in rt.idx], {k: st.gather_full(k).numpy() for k in tables}, 0)
     out[rank] = res
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3])
 def test_sharded_tables_match_unsharded_adagrad(world):
     rng = np.random.default_rng(1)
     B, D = 40, 16
@@ -256,9 +269,16 @@ def test_sharded_tables_match_unsharded_adagrad(world):
         assert ff[2] == 0
         assert all(np.array_equal(x, y) for x, y in zip(ff[0], fc[0]))
         assert all(np.array_equal(ff[1][k], fc[1][k]) for k in tables)
-        fl = out[r]["lookups"]
-        assert all(np.array_equal(x, y) for x, y in zip(fl[0], fc[0]))
-        assert all(np.array_equal(fl[1][k], fc[1][k]) for k in tables)
+        for mode in ("lookups", "routed"):
+            fl = out[r][mode]
+            assert all(np.array_equal(x, y) for x, y in zip(fl[0], fc[0]))
+            if mode == "routed" and world == 1:
+                # one rank: the routed op IS the owner's Adagrad (this CPU
+                # restatement sums in fp64 without the per-request fp32 buffer;
+                # on the GPU both are fp32 in one order: test_kernels_gpu)
+                assert all(np.allclose(fl[1][k], fc[1][k], rtol=0, atol=1e-7) for k in tables)
+            else:
+                assert all(np.array_equal(fl[1][k], fc[1][k]) for k in tables)
         # a capacity of 5 slots per owner drops requests and counts them: the
         # distinct (table, row) requests of this rank per owner, minus 5
         reqs = {}
