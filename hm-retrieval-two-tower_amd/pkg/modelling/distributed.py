@@ -1063,6 +1063,7 @@ class ShardedTrainStep:
         for key, (li, srcs) in small_srcs.items():
             specs.append(dict(table=self._small_views[key][1], ids=[s[0] for s in srcs],
                               grad_col_offset=[s[1] for s in srcs], grad=grads[li]))
+        self._join_route()  # the per-request sums read the route's slots
         if specs:
             self.ops.scatter_sum(specs, self._B, grads[0])
         self._dense_update([t.dense.flat.grad for t in m.towers], loss.detach())
@@ -1103,20 +1104,50 @@ class ShardedTrainStep:
         """Route, fetch, middle, owner apply on the static batch: fixed shapes
         and no host sync, so the whole of it is captured as one graph."""
         rt = None
+        self._route_side = None
         if self.tables is not None:
-            rt = self.tables.route_fixed([(k, ids) for k, ids, _, _ in self._lookups(self._static)], self._cap,
-                                         overflow=self._overflow, idx_out=self._idx_all[:len(self._idx)])
-            if os.environ.get("TT_SHARDED_KEEP", "1") == "1":
-                self._last_counts = rt.counts
-            if os.environ.get("TT_SHARDED_DEBUG") == "2":  # running max of the per-owner counts, in the graph
-                if getattr(self, "_cmax", None) is None:
-                    self._cmax = torch.zeros(1, dtype=torch.int64, device=rt.counts.device)
-                torch.maximum(self._cmax, rt.counts.max().reshape(1), out=self._cmax)
-            if self.world > 1:  # world 1: the middle gathers from the shard itself
-                self.tables.fetch_routed(rt, out=self._got)  # rt.idx_all IS self._idx_all[:L]
+            lookups = [(k, ids) for k, ids, _, _ in self._lookups(self._static)]
+            idx_out = self._idx_all[:len(self._idx)]
+            if self.world == 1 and idx_out.is_cuda:
+                # one rank: the route has no collective and the middle reads the
+                # shard by id, so the route only feeds the backward's per-request
+                # sums and the owner apply — it runs on a side stream beside the
+                # forward, joined (from the origin stream) before the sums
+                main = torch.cuda.current_stream()
+                if getattr(self, "_side", None) is None:
+                    self._side = torch.cuda.Stream(device=idx_out.device)
+                self._side.wait_stream(main)
+                with torch.cuda.stream(self._side):
+                    rt = self.tables.route_fixed(lookups, self._cap, overflow=self._overflow, idx_out=idx_out)
+                self._route_side = (self._side, rt)
+            else:
+                rt = self.tables.route_fixed(lookups, self._cap, overflow=self._overflow, idx_out=idx_out)
+                self._route_joined(rt)
+                if self.world > 1:
+                    self.tables.fetch_routed(rt, out=self._got)  # rt.idx_all IS self._idx_all[:L]
         self._middle()
         if rt is not None:
             self.tables.apply_routed(rt, self._g_req, self.lr, self.eps)
+
+    def _join_route(self) -> None:
+        """Join the side-stream route (world 1) before its outputs are read."""
+        if getattr(self, "_route_side", None) is None:
+            return
+        side, rt = self._route_side
+        self._route_side = None
+        main = torch.cuda.current_stream()
+        main.wait_stream(side)
+        for t in (rt.tags, rt.rows, rt.counts, *rt.table_ids):
+            t.record_stream(main)
+        self._route_joined(rt)
+
+    def _route_joined(self, rt: _Route) -> None:
+        if os.environ.get("TT_SHARDED_KEEP", "1") == "1":
+            self._last_counts = rt.counts
+        if os.environ.get("TT_SHARDED_DEBUG") == "2":  # running max of the per-owner counts, in the graph
+            if getattr(self, "_cmax", None) is None:
+                self._cmax = torch.zeros(1, dtype=torch.int64, device=rt.counts.device)
+            torch.maximum(self._cmax, rt.counts.max().reshape(1), out=self._cmax)
 
     def prefetch(self, batch) -> None:
         """Kept for API compatibility: routing runs inside the step's graph."""
