@@ -647,11 +647,13 @@ def time_c5_sharded(device, ws: int, rank: int, steps: int = 20, rows: int = 100
     rows and their Adagrad accumulator) and a GLOBAL batch of 65,536 uniform
     ids split over the ranks (65,536 / G per rank: the configuration as
     stated).  A step, replayed as one hipGraph (fixed-capacity routing: no
-    host sync): routing (tt_route_requests dedup + owner buckets, tt_route_pad
-    into fixed per-owner slots, all_to_all of the requests), fetch
-    (tt_gather_tagged on the owners + all_to_all of the rows), apply
-    (tt_sparse_scatter_sum per request + all_to_all of the sums +
-    tt_sparse_adagrad on the owners).  Algorithmic HBM bytes per rank and
+    host sync): routing (tt_route_fixed: dedup + owner buckets + fixed
+    per-owner slots; all_to_all of the requests), fetch (tt_gather_tagged on
+    the owners + all_to_all of the rows), apply (per-request sums on the
+    route's own sort, tt_sparse_routed + all_to_all of the sums +
+    tt_sparse_adagrad on the owners).  At one rank the exchanges are
+    identities: the fetch is the shard read by id with the route beside it on
+    a second stream, and the per-request sums are the Adagrad update itself.  Algorithmic HBM bytes per rank and
     step: lookups x (4 B id + 2 x 4D row read/write + 4D gradient read) +
     owner rows x 16D (param and accumulator read + write).  The all_to_all
     share is the three data all_to_alls of the same sizes timed alone.  At
@@ -690,9 +692,26 @@ def time_c5_sharded(device, ws: int, rank: int, steps: int = 20, rows: int = 100
             cap = st.route_capacity(1, b)
             g_req = torch.zeros(ws * cap, D, device=device)
 
+            rows_out = torch.empty(b, D, device=device)
+            side = torch.cuda.Stream(device=device)
+
             def body():
-                rt = st.route_fixed([("big", sid)], cap)
-                st.fetch_routed(rt)
+                if ws == 1:
+                    # one rank: the shard IS the owner's answer — the fetch is a
+                    # read by id (tt_gather_grouped), and the route (which then
+                    # only feeds the apply) runs beside it on a second stream,
+                    # joined from the origin stream (as ShardedTrainStep)
+                    main = torch.cuda.current_stream()
+                    side.wait_stream(main)
+                    with torch.cuda.stream(side):
+                        rt = st.route_fixed([("big", sid)], cap)
+                    hip_ops.gather_grouped([(st.shard["big"], sid, 0)], b, rows_out)
+                    main.wait_stream(side)
+                    for t in (rt.tags, rt.rows, rt.counts, rt.idx_all, *rt.table_ids, *(rt.order or ())):
+                        t.record_stream(main)
+                else:
+                    rt = st.route_fixed([("big", sid)], cap)
+                    st.fetch_routed(rt)
                 st.apply_lookups(rt, [(grad, 0)], 0.05, 1e-7, g_req=g_req if ws > 1 else None)
 
             body()  # eager: code, workspaces
