@@ -1474,7 +1474,8 @@ int sparse_adagrad_stage(const tt_sparse_table* tables, int32_t num_tables, int6
                          int64_t grad_stride, float lr, float epsilon, void* workspace, size_t workspace_bytes,
                          tt_stream_t stream, int stage, const char* name) {
   clear_error();
-  int rc = validate_tables(tables, num_tables, batch, false);
+  // the sort stage reads only the ids: no slot needed (also sorts for a scatter sum)
+  int rc = validate_tables(tables, num_tables, batch, false, stage != kStageSort);
   if (rc) return rc;
   if (batch == 0) return TT_OK;
   const size_t need = tables_ws_bytes(tables, num_tables, batch, 0);
@@ -1794,4 +1795,21 @@ extern "C" int tt_sparse_routed(const tt_sparse_table* tables, int32_t num_table
                                 nullptr, nullptr, nullptr, kStageApply);
   return run_sparse<kScatterSum>(tables, num_tables, batch, grad, grad_stride, ap, workspace, workspace_bytes, st,
                                  nullptr, nullptr, nullptr, kStageApply);
+}
+
+extern "C" int tt_sparse_scatter_sum_sorted(const tt_sparse_table* tables, int32_t num_tables, int64_t batch,
+                                            const float* grad, int64_t grad_stride, void* workspace,
+                                            size_t workspace_bytes, tt_stream_t stream) {
+  clear_error();
+  TT_REQUIRE(num_tables <= kTablesPerLaunch, "tt_sparse_scatter_sum_sorted: at most %d tables", kTablesPerLaunch);
+  int rc = validate_tables(tables, num_tables, batch, false, false);
+  if (rc) return rc;
+  if (batch == 0) return TT_OK;
+  const size_t need = tables_ws_bytes(tables, num_tables, batch, 0);
+  if (!workspace || workspace_bytes < need)
+    return fail(TT_ERR_WORKSPACE, "tt_sparse_scatter_sum_sorted: workspace %zu < required %zu", workspace_bytes,
+                need);
+  ApplyParams ap{};
+  return run_sparse<kScatterSum>(tables, num_tables, batch, grad, grad_stride, ap, workspace, workspace_bytes,
+                                 to_stream(stream), nullptr, nullptr, nullptr, kStageApply);
 }

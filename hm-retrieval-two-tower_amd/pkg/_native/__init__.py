@@ -197,6 +197,8 @@ _PROTOS = {
         [POINTER(SparseTable), c_int32, c_int64, c_void_p, c_int64, c_float, c_float, c_float, c_float, c_int64,
          c_void_p, c_size_t, c_void_p],
     ),
+    "tt_sparse_scatter_sum_sorted": (
+        c_int32, [POINTER(SparseTable), c_int32, c_int64, c_void_p, c_int64, c_void_p, c_size_t, c_void_p]),
     "tt_sparse_scatter_sum": (
         c_int32, [POINTER(SparseTable), c_int32, c_int64, c_void_p, c_int64, c_void_p, c_size_t, c_void_p]),
     "tt_dedup_workspace_size": (c_size_t, [c_int64, c_int32]),

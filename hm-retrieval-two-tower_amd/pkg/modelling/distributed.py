@@ -436,6 +436,9 @@ class EmbeddingOps:
     route_fixed: Optional[Callable[..., Any]] = None
     # dense_adagrad on several (param, accum, grad) buffers in one launch
     dense_adagrad_many: Optional[Callable[..., None]] = None
+    # scatter_sum in two stages: the key sort (ids only) early, the sums later
+    scatter_sort: Optional[Callable[..., None]] = None
+    scatter_sum_sorted: Optional[Callable[..., None]] = None
 
     @staticmethod
     def hip() -> "EmbeddingOps":
@@ -450,7 +453,10 @@ class EmbeddingOps:
                                                                                 ws_tag="sparse_owner"),
                             hip_ops.dense_adagrad, hip_ops.route_requests, hip_ops.route_owner,
                             hip_ops.route_pad, hip_ops.sparse_adagrad_rows, hip_ops.sparse_routed,
-                            hip_ops.route_fixed, hip_ops.dense_adagrad_many)
+                            hip_ops.route_fixed, hip_ops.dense_adagrad_many,
+                            lambda specs, b: hip_ops.sparse_sort(specs, b, ws_tag="sparse_mid", slots=False),
+                            lambda specs, b, g: hip_ops.sparse_scatter_sum(specs, b, g, ws_tag="sparse_mid",
+                                                                           presorted=True))
 
 
 def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits: List[int], in_splits: List[int], group) -> torch.Tensor:
@@ -1014,7 +1020,7 @@ class ShardedTrainStep:
         x = self._static
         q, c = m._split(x)
         layers = [t.input_layer for t in m.towers]
-        calls, widths, big_srcs, small_srcs = [], [], {}, {}
+        calls, widths = [], []
         j = 0
         for li, (layer, xx) in enumerate(zip(layers, [q, c])):
             segs = []
@@ -1027,12 +1033,9 @@ class ShardedTrainStep:
                         segs.append((self.tables.shard[t._shard_key], layer._ids(xx[f.name]), off))
                     else:
                         segs.append((self._got, self._idx[j], off))
-                    big_srcs.setdefault(t._shard_key, (li, []))[1].append((self._idx[j], off))
                     j += 1
                 else:
-                    ids = layer._ids(xx[f.name])
-                    segs.append((t.weight, ids, off))
-                    small_srcs.setdefault((id(m.towers[li]), f.name), (li, []))[1].append((ids, off))
+                    segs.append((t.weight, layer._ids(xx[f.name]), off))
             out = torch.empty(self._B, layer.row_stride, dtype=torch.float32, device=layer.device)
             calls.append((segs, out))
             widths.append(layer.output_dim)
@@ -1056,17 +1059,44 @@ class ShardedTrainStep:
         # one scatter-sum call: per-request sums of the sharded tables' lookups
         # (rows of g_req, disjoint per table) and dense small-table gradients
         self._small_grad.zero_()
+        specs = [dict(sp, grad=grads[li]) for sp, li in self._scatter_specs()]
+        self._join_route()  # the per-request sums read the route's slots (and its sorted keys)
+        if specs:
+            if self._presorted:
+                self.ops.scatter_sum_sorted(specs, self._B, grads[0])
+            else:
+                self.ops.scatter_sum(specs, self._B, grads[0])
+        self._dense_update([t.dense.flat.grad for t in m.towers], loss.detach())
+
+    def _scatter_specs(self) -> List[Tuple[dict, int]]:
+        """(scatter-sum table spec without its gradient, tower index) of every
+        table the step's sums write: the sharded tables' per-request sums
+        (ids = the lookups' slots) and the small tables' dense gradients
+        (ids = the batch's ids).  Static buffers only, so computed once."""
+        if getattr(self, "_sspecs", None) is not None:
+            return self._sspecs
+        m = self.model
+        q, c = m._split(self._static)
+        big_srcs, small_srcs = {}, {}
+        j = 0
+        for li, (layer, xx) in enumerate(zip([t.input_layer for t in m.towers], [q, c])):
+            for f, off in zip(layer.categorical_features, layer.column_offsets()):
+                t = layer.embedding_layers[f.name]
+                if hasattr(t, "_shard_key"):
+                    big_srcs.setdefault(t._shard_key, (li, []))[1].append((self._idx[j], off))
+                    j += 1
+                else:
+                    small_srcs.setdefault((id(m.towers[li]), f.name), (li, []))[1].append(
+                        (layer._ids(xx[f.name]), off))
         specs = []
         for key, (li, srcs) in big_srcs.items():
-            specs.append(dict(table=self._g_req, ids=[s[0] for s in srcs], grad_col_offset=[s[1] for s in srcs],
-                              grad=grads[li]))
+            specs.append((dict(table=self._g_req, ids=[s[0] for s in srcs], grad_col_offset=[s[1] for s in srcs]),
+                          li))
         for key, (li, srcs) in small_srcs.items():
-            specs.append(dict(table=self._small_views[key][1], ids=[s[0] for s in srcs],
-                              grad_col_offset=[s[1] for s in srcs], grad=grads[li]))
-        self._join_route()  # the per-request sums read the route's slots
-        if specs:
-            self.ops.scatter_sum(specs, self._B, grads[0])
-        self._dense_update([t.dense.flat.grad for t in m.towers], loss.detach())
+            specs.append((dict(table=self._small_views[key][1], ids=[s[0] for s in srcs],
+                               grad_col_offset=[s[1] for s in srcs]), li))
+        self._sspecs = specs
+        return specs
 
     def _dense_update(self, flat_grads: List[torch.Tensor], loss: torch.Tensor) -> None:
         """The tail of the middle: the towers' MLP gradients, the flat
@@ -1105,6 +1135,7 @@ class ShardedTrainStep:
         and no host sync, so the whole of it is captured as one graph."""
         rt = None
         self._route_side = None
+        self._presorted = False
         if self.tables is not None:
             lookups = [(k, ids) for k, ids, _, _ in self._lookups(self._static)]
             idx_out = self._idx_all[:len(self._idx)]
@@ -1119,6 +1150,10 @@ class ShardedTrainStep:
                 self._side.wait_stream(main)
                 with torch.cuda.stream(self._side):
                     rt = self.tables.route_fixed(lookups, self._cap, overflow=self._overflow, idx_out=idx_out)
+                    # ... and the sums' key sort, which reads only the slots and ids
+                    if self.ops.scatter_sort is not None and self._scatter_specs():
+                        self.ops.scatter_sort([sp for sp, _ in self._scatter_specs()], self._B)
+                        self._presorted = True
                 self._route_side = (self._side, rt)
             else:
                 rt = self.tables.route_fixed(lookups, self._cap, overflow=self._overflow, idx_out=idx_out)

@@ -350,10 +350,12 @@ def sparse_status_all(device: torch.device, ws_tags: Sequence[str]) -> None:
         raise err
 
 
-def sparse_sort(tables: Sequence[dict], batch: int, ws_tag: str = "sparse") -> None:
-    """First stage of sparse_adagrad(..., presorted=True): build and sort the lookup keys
-    (reads only the ids; no gradient needed), on the current stream."""
-    arr = _sparse_tables(tables, batch, adam=False)
+def sparse_sort(tables: Sequence[dict], batch: int, ws_tag: str = "sparse", slots: bool = True) -> None:
+    """First stage of sparse_adagrad(..., presorted=True) or
+    sparse_scatter_sum(..., presorted=True) (slots=False: tables without
+    accumulators): build and sort the lookup keys (reads only the ids; no
+    gradient needed), on the current stream."""
+    arr = _sparse_tables(tables, batch, adam=False, slots=slots)
     L = lib()
     need = L.tt_sparse_workspace_size(arr, len(tables), batch)
     ws = Workspace.get(need, tables[0]["table"].device, ws_tag)
@@ -372,18 +374,21 @@ def sparse_adam(tables: Sequence[dict], batch: int, grad: torch.Tensor, lr: floa
                            ws.data_ptr(), ws.numel(), _stream()))
 
 
-def sparse_scatter_sum(tables: Sequence[dict], batch: int, grad: torch.Tensor, ws_tag: str = "sparse") -> None:
+def sparse_scatter_sum(tables: Sequence[dict], batch: int, grad: torch.Tensor, ws_tag: str = "sparse",
+                       presorted: bool = False) -> None:
     """tables: dicts with table (zero-filled dense gradient [rows, dim]), ids
     [list], grad_col_offset [list]; every touched row receives its
-    duplicate-summed gradient (tt_sparse_scatter_sum)."""
+    duplicate-summed gradient (tt_sparse_scatter_sum).  presorted: the keys
+    were sorted by sparse_sort(tables, batch, ws_tag, slots=False) earlier
+    (tt_sparse_scatter_sum_sorted)."""
     _req(grad, "grad", torch.float32, 2)
     ld = _row_major(grad, "grad")
     arr = _sparse_tables(tables, batch, adam=False, slots=False)
     L = lib()
     need = L.tt_sparse_workspace_size(arr, len(tables), batch)
     ws = Workspace.get(need, grad.device, ws_tag)
-    check(L.tt_sparse_scatter_sum(arr, len(tables), batch, grad.data_ptr(), ld, ws.data_ptr(), ws.numel(),
-                                  _stream()))
+    fn = L.tt_sparse_scatter_sum_sorted if presorted else L.tt_sparse_scatter_sum
+    check(fn(arr, len(tables), batch, grad.data_ptr(), ld, ws.data_ptr(), ws.numel(), _stream()))
 
 
 def route_requests(lookups: Sequence[Tuple[torch.Tensor, int, int]], world: int, num_tags: int,

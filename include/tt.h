@@ -317,6 +317,14 @@ int tt_sparse_routed(const tt_sparse_table* tables, int32_t num_tables, int64_t 
                      int32_t op, float lr, float epsilon, void* workspace,
                      size_t workspace_bytes, tt_stream_t stream);
 
+/* tt_sparse_scatter_sum's block / join passes on keys tt_sparse_sort sorted
+ * earlier (same tables, batch and workspace; the sort reads only the ids and
+ * accepts tables without slots): the sort can run beside other work. */
+int tt_sparse_scatter_sum_sorted(const tt_sparse_table* tables, int32_t num_tables,
+                                 int64_t batch, const float* grad, int64_t grad_stride,
+                                 void* workspace, size_t workspace_bytes,
+                                 tt_stream_t stream);
+
 /* Dedup only (K8), for parity checks: writes the U distinct ids of
  * ids[0..n) in ascending order, the per-id gradient sums [U, dim] (rows of
  * `grad` summed in index order) and U (device int32).  Capacity n rows. */
