@@ -870,3 +870,33 @@ def test_route_fixed_equals_composed_route(cuda, world, B):
         if world == 1:
             for a, b in zip(own1, hip_ops.route_owner(sp2, 1, 3)):
                 assert torch.equal(a, b)
+
+
+def test_scatter_sum_presorted_equals_one_call(cuda):
+    """tt_sparse_sort (tables without slots) on one stream, then
+    tt_sparse_scatter_sum_sorted on another after a join, equals one
+    tt_sparse_scatter_sum bit for bit (two tables, one with two sources,
+    Zipf duplicates and invalid ids)."""
+    rng = np.random.default_rng(5)
+    B, D = 4096, 32
+    grad = torch.as_tensor(rng.standard_normal((B, 3 * D)).astype(np.float32), device=cuda)
+    ids = [zipf_ids(rng, B, 5000), zipf_ids(rng, B, 5000), rng.integers(-2, 305, B).astype(np.int32)]
+
+    def specs(t0, t1):
+        return [dict(table=t0, ids=[_t(ids[0], cuda), _t(ids[1], cuda)], grad_col_offset=[0, D]),
+                dict(table=t1, ids=[_t(ids[2], cuda)], grad_col_offset=[2 * D])]
+
+    a0, a1 = torch.zeros(5000, D, device=cuda), torch.zeros(300, D, device=cuda)
+    hip_ops.sparse_scatter_sum(specs(a0, a1), B, grad, ws_tag="t_one")
+    b0, b1 = torch.zeros(5000, D, device=cuda), torch.zeros(300, D, device=cuda)
+    sp = specs(b0, b1)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        hip_ops.sparse_sort(sp, B, ws_tag="t_two", slots=False)
+    torch.cuda.current_stream().wait_stream(side)
+    hip_ops.sparse_scatter_sum(sp, B, grad, ws_tag="t_two", presorted=True)
+    hip_ops.sparse_status(grad.device, "t_two")
+    torch.cuda.synchronize()
+    assert torch.equal(a0, b0) and torch.equal(a1, b1)
+    assert (a0 != 0).any() and (a1 != 0).any()
