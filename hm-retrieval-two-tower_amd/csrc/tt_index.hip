@@ -326,18 +326,31 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 // Waits until at most n of this wave's vector-memory ops are in flight (n
 // rounded down to a bucket: waiting for more is always safe).
+// n is read as a wave-uniform (scalar) value: the tests are scalar compares
+// and branches, the small counts (the scan's steady state) first.
 __device__ __forceinline__ void wait_vmcnt_atmost(int n) {
-  if (n >= 63) wait_vmcnt<63>();
-  else if (n >= 48) wait_vmcnt<48>();
-  else if (n >= 32) wait_vmcnt<32>();
-  else if (n >= 24) wait_vmcnt<24>();
-  else if (n >= 16) wait_vmcnt<16>();
-  else if (n >= 12) wait_vmcnt<12>();
-  else if (n >= 8) wait_vmcnt<8>();
-  else if (n >= 6) wait_vmcnt<6>();
-  else if (n >= 4) wait_vmcnt<4>();
-  else if (n >= 2) wait_vmcnt<2>();
-  else wait_vmcnt<0>();
+  n = __builtin_amdgcn_readfirstlane(n);
+  if (n < 16) {
+    if (n >= 8) {
+      if (n >= 12) wait_vmcnt<12>();
+      else wait_vmcnt<8>();
+    } else if (n >= 4) {
+      if (n >= 6) wait_vmcnt<6>();
+      else wait_vmcnt<4>();
+    } else if (n >= 2) {
+      wait_vmcnt<2>();
+    } else {
+      wait_vmcnt<0>();
+    }
+  } else if (n >= 32) {
+    if (n >= 63) wait_vmcnt<63>();
+    else if (n >= 48) wait_vmcnt<48>();
+    else wait_vmcnt<32>();
+  } else if (n >= 24) {
+    wait_vmcnt<24>();
+  } else {
+    wait_vmcnt<16>();
+  }
 }
 
 // jsel-th largest of the 64 values {bins of this lane, bins of lane ^ 32},
@@ -652,7 +665,7 @@ __global__ void __launch_bounds__(kSThreads) scan_kernel(const ScreenArgs a) {
       __builtin_amdgcn_raw_buffer_store_b64(e, lists, off, 0, 0);
       pos += keepit ? 1 : 0;
     }
-    wc += 16;
+    wc = __builtin_amdgcn_readfirstlane(wc + 16);
     tail += nrows;
     wsync();
   };
@@ -722,9 +735,13 @@ __global__ void __launch_bounds__(kSThreads) scan_kernel(const ScreenArgs a) {
     unsigned pc;
     float m0, m1;
   };
+  // the split's only tiles that can reach outside [row0, row1): its first and
+  // last (scalar tile indices, -1 when that tile is whole)
+  const int ue0 = (nv > 0 && edge(static_cast<int64_t>(tb) * kCTile)) ? 0 : -1;
+  const int ue1 = (nv > 0 && edge(static_cast<int64_t>(tb + nv - 1) * kCTile)) ? nv - 1 : -1;
   auto prep = [&](f32x16& x0, f32x16& x1, int u, int t) {
     const int64_t cb = static_cast<int64_t>(tb + u) * kCTile + 32 * t;
-    if (edge(cb - 32 * t)) {
+    if (u == ue0 || u == ue1) {
       mask_pad(x0, cb + 4 * h);
       mask_pad(x1, cb + 4 * h);
     }
