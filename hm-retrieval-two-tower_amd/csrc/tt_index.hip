@@ -25,7 +25,7 @@
 //  screen   one workgroup = 8 waves x 64 queries (two 32-query sets per wave,
 //           their bf16 fragments in VGPRs as the B operand); 64-candidate bf16
 //           tiles stream through a 4-stage LDS ring filled by LDS-DMA
-//           (global_load_lds, XOR-swizzled 16-B chunks) and are scored with
+//           (global_load_lds, chunk-pair planes: tile_frag_lane_off) and are scored with
 //           v_mfma_f32_32x32x16_bf16 (S^T: each lane holds 16 candidates of one
 //           query).  Phase 1 scans a spread sample of the split's tiles and
 //           keeps per-register running maxima ("bins": 64 per query, each over
@@ -353,6 +353,24 @@ __device__ __forceinline__ void wait_vmcnt_atmost(int n) {
   }
 }
 
+// LDS image of one 64-candidate bf16 tile (sample and scan rings), in 16-B
+// chunks: plane s holds chunks 2s and 2s + 1 of every row (64 rows x 32 B =
+// 2 KiB at s * 2048); row r's pair sits at r * 32 with its two chunks swapped
+// when bit 3 of r is set.  A lane's fragment of k-step s is then at a
+// lane-constant offset + s * 2048 + t * 1024 (an instruction immediate, no
+// address arithmetic per read), and the 16 lanes of each ds_read_b128 lane
+// group ({0-3, 12-15, 20-27}, ...) hit 16 distinct 16-B bank slots.
+__device__ __forceinline__ int tile_frag_lane_off(int l32, int h) {
+  return l32 * 32 + ((h ^ ((l32 >> 3) & 1)) << 4);
+}
+// Source chunk of the 16 B that LDS-DMA piece p's lane writes (piece = 1 KiB
+// = half a plane: 32 rows x 32 B): its row in the tile and chunk in the row.
+__device__ __forceinline__ void tile_piece_src(int p, int lane, int& row, int& ch) {
+  const int plane = p >> 1, w = (p & 1) * 1024 + lane * 16;
+  row = w >> 5;
+  ch = 2 * plane + (((w >> 4) & 1) ^ ((row >> 3) & 1));
+}
+
 // jsel-th largest of the 64 values {bins of this lane, bins of lane ^ 32},
 // to a 16-bit order-key prefix (rounded down); -inf if fewer than jsel bins.
 __device__ float bins_select(const float (&ba)[16], const float (&bb)[16], int jsel) {
@@ -376,13 +394,13 @@ __device__ float bins_select(const float (&ba)[16], const float (&bb)[16], int j
 template <int D>
 __global__ void __launch_bounds__(kSThreads) sample_kernel(const ScreenArgs a) {
   constexpr bool SAMPLE = true;
-  constexpr int KS = D / 16, CH = D / 8, RB = D * 2;
+  constexpr int KS = D / 16, RB = D * 2;
   constexpr int TILE_BYTES = kCTile * RB;                 // 16 KiB at D = 128
   constexpr int PIECES = TILE_BYTES / 1024;               // 1 KiB LDS-DMA pieces per tile
   constexpr int PPW = PIECES >= kSWaves ? PIECES / kSWaves : 1;
   __shared__ __attribute__((aligned(1024))) char smem[kStages * TILE_BYTES];
   const int tid = threadIdx.x;
-  const int wave = tid / kWave;
+  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);  // wave-uniform (scalar)
   const int lane = lane_id();
   const int h = lane >> 5, l32 = lane & 31;
   const int split = static_cast<int>(blockIdx.x % a.S);
@@ -415,9 +433,8 @@ __global__ void __launch_bounds__(kSThreads) sample_kernel(const ScreenArgs a) {
     for (int u = 0; u < PPW; ++u) {
       const int p = wave * PPW + u;
       if (p < PIECES) {
-        const int off = p * 1024 + lane * 16;
-        const int row = off / RB, chp = (off % RB) / 16;
-        const int ch = chp ^ ((row * CH / 16) % CH);
+        int row, ch;
+        tile_piece_src(p, lane, row, ch);
         const __bf16* src = crow + (base + row) * D + ch * 8;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src),
                                          (__attribute__((address_space(3))) void*)(smem + stage * TILE_BYTES + p * 1024),
@@ -434,10 +451,9 @@ __global__ void __launch_bounds__(kSThreads) sample_kernel(const ScreenArgs a) {
       wait_vmcnt<2 * PPW>();
     }
   };
+  const int frag_off = tile_frag_lane_off(l32, h);
   auto frag = [&](const char* B, int t, int s) {
-    const int row = 32 * t + l32, ch = 2 * s + h;
-    const int swz = (row * CH / 16) % CH;
-    return *reinterpret_cast<const bf16x8*>(B + row * RB + ((ch ^ swz) << 4));
+    return *reinterpret_cast<const bf16x8*>(B + frag_off + s * 2048 + t * 1024);
   };
   auto mask_pad = [&](f32x16& acc, int64_t cfirst) {  // rows outside [row0, row1) (edge tiles only)
 #pragma unroll
@@ -518,19 +534,24 @@ struct ScanGeo {
   static constexpr int RING = kStages * TILE_BYTES;
 };
 
+// (IEEE maximum: v_maximum3_f32, no NaN-quieting canonicalisations as fmaxf
+// needs; a NaN score makes the max NaN, which stages nothing.)
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
+}
 __device__ __forceinline__ float max16(const f32x16& c) {
-  const float x0 = fmaxf(fmaxf(c[0], c[1]), c[2]);
-  float x1 = fmaxf(fmaxf(c[3], c[4]), c[5]);
-  float x2 = fmaxf(fmaxf(c[6], c[7]), c[8]);
-  float x3 = fmaxf(fmaxf(c[9], c[10]), c[11]);
-  float x4 = fmaxf(fmaxf(c[12], c[13]), c[14]);
-  return fmaxf(fmaxf(fmaxf(x0, x1), x2), fmaxf(fmaxf(x3, x4), c[15]));
+  const float x0 = max3f(c[0], c[1], c[2]);
+  const float x1 = max3f(c[3], c[4], c[5]);
+  const float x2 = max3f(c[6], c[7], c[8]);
+  const float x3 = max3f(c[9], c[10], c[11]);
+  const float x4 = max3f(c[12], c[13], c[14]);
+  return max3f(max3f(x0, x1, x2), max3f(x3, x4, c[15]), -INFINITY);
 }
 
 template <int D>
 __global__ void __launch_bounds__(kSThreads) scan_kernel(const ScreenArgs a) {
   using G = ScanGeo<D>;
-  constexpr int KS = D / 16, CH = D / 8, RB = D * 2;
+  constexpr int KS = D / 16;
   constexpr int TILE_BYTES = G::TILE_BYTES;
   constexpr int PIECES = TILE_BYTES / 1024;               // 1 KiB LDS-DMA pieces per tile
   constexpr int PPW = PIECES >= kSWaves ? PIECES / kSWaves : 1;
@@ -541,7 +562,7 @@ __global__ void __launch_bounds__(kSThreads) scan_kernel(const ScreenArgs a) {
   __shared__ float s_tau[kQPerWG];
   __shared__ int s_cnt[kQPerWG];
   const int tid = threadIdx.x;
-  const int wave = tid / kWave;
+  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);  // wave-uniform (scalar)
   const int lane = lane_id();
   const int h = lane >> 5, l32 = lane & 31;
   const int split = static_cast<int>(blockIdx.x % a.S);
@@ -586,9 +607,8 @@ __global__ void __launch_bounds__(kSThreads) scan_kernel(const ScreenArgs a) {
     for (int u = 0; u < PPW; ++u) {
       const int p = wave * PPW + u;
       if (p < PIECES) {
-        const int off = p * 1024 + lane * 16;
-        const int row = off / RB, chp = (off % RB) / 16;
-        const int ch = chp ^ ((row * CH / 16) % CH);
+        int row, ch;
+        tile_piece_src(p, lane, row, ch);
         const __bf16* src = crow + (base + row) * D + ch * 8;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src),
                                          (__attribute__((address_space(3))) void*)(smem + stage * TILE_BYTES + p * 1024),
@@ -596,10 +616,9 @@ __global__ void __launch_bounds__(kSThreads) scan_kernel(const ScreenArgs a) {
       }
     }
   };
+  const int frag_off = tile_frag_lane_off(l32, h);
   auto frag = [&](const char* B, int t, int s) {
-    const int row = 32 * t + l32, ch = 2 * s + h;
-    const int swz = (row * CH / 16) % CH;
-    return *reinterpret_cast<const bf16x8*>(B + row * RB + ((ch ^ swz) << 4));
+    return *reinterpret_cast<const bf16x8*>(B + frag_off + s * 2048 + t * 1024);
   };
   auto load_frags = [&](bf16x8 (&f)[KS], const char* B, int t) {
 #pragma unroll
@@ -670,11 +689,45 @@ __global__ void __launch_bounds__(kSThreads) scan_kernel(const ScreenArgs a) {
     wsync();
   };
   // Stages the rows of this block's lanes whose max beats their tau.
+#ifndef TT_SCAN_STAGE_ALL
+#define TT_SCAN_STAGE_ALL 0
+#endif
   auto stage = [&](const f32x16& c, bool hit, int ql, unsigned pc) {
     const uint64_t m = __ballot(hit);
-    if (m) {
+    if (TT_SCAN_STAGE_ALL) {
+      // (Probe, off: 1M x k=100 43.2 vs 41.8 ms with the branches below, 3
+      // interleaved pairs, profiles/r05_index_scan_ab.txt.)
+      // Branch-free: EVERY lane writes its row, the n hit lanes into slots
+      // head .. head + n - 1, the others after them (slots the ring does not
+      // hold yet: < 64 pending + 64 <= kStageRows), and head advances by n.
+      // The wave's five stores issue whatever the hits (as before: a block
+      // has some hit lane ~98 % of the time), with no exec-mask branches, so
+      // they schedule among the MFMAs and their count is static.  (As inline
+      // asm: the compiler, seeing these stores unconditional, put a vmcnt(0)
+      // — a wait for the whole LDS-DMA ring — before them and before the
+      // flush's reads; the rows are a separate LDS object from the ring.
+      // LDS executes a wave's operations in order, so the flush's reads see
+      // them, and any lgkmcnt wait the compiler counts stays conservative.)
+      const unsigned n = static_cast<unsigned>(__popcll(m));
+      const unsigned bh = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), 0u));
+      const unsigned slot = hit ? head + bh : head + n + static_cast<unsigned>(lane) - bh;
+      const unsigned addr = static_cast<unsigned>(reinterpret_cast<uintptr_t>(
+          (__attribute__((address_space(3))) float*)(srow + (slot & (kStageRows - 1)) * kRowF)));
+      const f32x4 v0 = {c[0], c[1], c[2], c[3]}, v1 = {c[4], c[5], c[6], c[7]};
+      const f32x4 v2 = {c[8], c[9], c[10], c[11]}, v3 = {c[12], c[13], c[14], c[15]};
+      const uint2 mt = make_uint2(pc, static_cast<unsigned>(ql));
+      asm volatile("ds_write_b128 %0, %1\n\tds_write_b128 %0, %2 offset:16\n\tds_write_b128 %0, %3 offset:32\n\t"
+                   "ds_write_b128 %0, %4 offset:48\n\tds_write_b64 %0, %5 offset:64"
+                   :: "v"(addr), "v"(v0), "v"(v1), "v"(v2), "v"(v3), "v"(mt) : "memory");
+      head += static_cast<int>(n);
+      if (head - tail >= kWave) flush(kWave);
+    } else if (m) {
       if (hit) {
-        f32x4* d = reinterpret_cast<f32x4*>(srow + ((head + __popcll(m & lanemask_lt64())) & (kStageRows - 1)) * kRowF);
+        // slot = head + #hit lanes below this one (v_mbcnt adds head in)
+        const unsigned slot = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), head));
+        f32x4* d = reinterpret_cast<f32x4*>(srow + (slot & (kStageRows - 1)) * kRowF);
         d[0] = f32x4{c[0], c[1], c[2], c[3]};
         d[1] = f32x4{c[4], c[5], c[6], c[7]};
         d[2] = f32x4{c[8], c[9], c[10], c[11]};
@@ -767,9 +820,14 @@ __global__ void __launch_bounds__(kSThreads) scan_kernel(const ScreenArgs a) {
   for (int u = 0; u < nv; ++u) {
     // half A: MFMAs (u, 0) into A (F0 read during the previous half), then
     // read F1 <- (u, 1), then filter (u - 1, 1) from B
+#ifndef TT_SCAN_LATE_B
+#define TT_SCAN_LATE_B 1
+#endif
+    // (TT_SCAN_LATE_B: filter B after the ring barrier, so the LDS drain the
+    // barrier needs covers the fragment reads only, not B's row stores)
     mfmas(f0, a0, a1);
     load_frags(f1, smem + (u % kStages) * TILE_BYTES, 1);
-    if (u > 0) stage_pair(b0, b1, prep(b0, b1, u - 1, 1));
+    if (!TT_SCAN_LATE_B && u > 0) stage_pair(b0, b1, prep(b0, b1, u - 1, 1));
     if (u + 1 < nv) {  // next tile: landed, every wave done with tile u, refill its stage
       wait_vmcnt_atmost((wa - da) + wb + wc);
       // compiler-visible wait + barrier: it then knows the fragment reads
@@ -787,6 +845,7 @@ __global__ void __launch_bounds__(kSThreads) scan_kernel(const ScreenArgs a) {
       }
       wc = dc;
     }
+    if (TT_SCAN_LATE_B && u > 0) stage_pair(b0, b1, prep(b0, b1, u - 1, 1));
     // half B: MFMAs (u, 1) into B, then read F0 <- (u + 1, 0) (stale after the
     // last tile: unused), then filter (u, 0) from A
     mfmas(f1, b0, b1);
