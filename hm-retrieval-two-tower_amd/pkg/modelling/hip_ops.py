@@ -914,6 +914,56 @@ def score_matrix(q: torch.Tensor, c: torch.Tensor, chunk: int = 256) -> torch.Te
     return out[:, :N]
 
 
+def matmul_rows(a: torch.Tensor, b: torch.Tensor, chunk: int = 256) -> torch.Tensor:
+    """a [M, K] . b [K, N] fp32 on libtt's bf16x3 row GEMM (tt_mlp_rows) for
+    any K and N: b in (K-chunk x N-chunk) blocks of <= `chunk`, each packed as
+    one B image; the K-chunk partials of an output block are added in chunk
+    order (deterministic).  The backward GEMMs of ScoreMatrix."""
+    _req(a, "a", torch.float32, 2)
+    _req(b, "b", torch.float32, 2)
+    M, K = a.shape
+    if b.shape[0] != K:
+        raise ValueError(f"a {tuple(a.shape)} and b {tuple(b.shape)} do not chain")
+    N = b.shape[1]
+    out = torch.zeros(M, max((N + 3) // 4 * 4, 4), dtype=torch.float32, device=a.device)
+    if M == 0 or N == 0 or K == 0:
+        return out[:, :N]
+    k4 = (K + 3) // 4 * 4
+    aa = a.contiguous()
+    if k4 != K:  # 16-B rows (and 16-B aligned column chunks) for the kernel's vector loads
+        aa = torch.zeros(M, k4, dtype=torch.float32, device=a.device)
+        aa[:, :K] = a
+    bb = b.contiguous()
+    part = torch.empty(M, min(chunk, (N + 3) // 4 * 4), dtype=torch.float32, device=a.device)
+    for n0 in range(0, N, chunk):
+        n1 = min(N, n0 + chunk)
+        for k0 in range(0, K, chunk):
+            k1 = min(K, k0 + chunk)
+            img = mlp_pack(bb[k0:k1, n0:n1].contiguous())
+            mlp_rows(aa[:, k0:], img, k1 - k0, n1 - n0, part)
+            out[:, n0:n1] += part[:, :n1 - n0]
+    return out[:, :N]
+
+
+class ScoreMatrix(torch.autograd.Function):
+    """S = q . c^T with its gradients, every product on libtt (score_matrix
+    forward; dq = G . c and dc = G^T . q by matmul_rows): the differentiable
+    form of TwoTowerModel.call (two_tower_model.py:92, tf.matmul)."""
+
+    @staticmethod
+    def forward(ctx, q, c):
+        ctx.save_for_backward(q, c)
+        return score_matrix(q.detach(), c.detach())
+
+    @staticmethod
+    def backward(ctx, g):
+        q, c = ctx.saved_tensors
+        g = g.contiguous()
+        dq = matmul_rows(g, c.detach()) if ctx.needs_input_grad[0] else None
+        dc = matmul_rows(g.t().contiguous(), q.detach()) if ctx.needs_input_grad[1] else None
+        return dq, dc
+
+
 def mlp_pack_many(jobs: Sequence[Tuple[torch.Tensor, bool, torch.Tensor]]) -> None:
     """Several mlp_pack images in one launch: jobs of (w, trans, image buffer)."""
     arr = (_native.MlpPackJob * len(jobs))()

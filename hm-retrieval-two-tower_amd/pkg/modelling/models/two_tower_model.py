@@ -108,16 +108,19 @@ class TwoTowerModel(AbstractKerasModel):
         (two_tower_model.py:65-92); materialised.  An INSPECTION path, not
         the hot path: fit / train_step / the graphed and sharded steps never
         call it (they never form [B, B]: losses.towers_inbatch_softmax_xent,
-        the fused tt_inbatch kernels).  Without gradients the score matrix is
-        libtt's (hip_ops.score_matrix, bf16x3 MFMA: fp32-faithful); with
-        gradients enabled it is a plain autograd matmul (the reference's
-        tf.matmul semantics) so a caller can differentiate through it — a
-        vendor GEMM, kept off the measured path on purpose."""
+        the fused tt_inbatch kernels).  The score matrix is libtt's
+        (hip_ops.score_matrix, bf16x3 MFMA: fp32-faithful); with gradients
+        enabled it is hip_ops.ScoreMatrix, whose backward GEMMs (dQ = G.C,
+        dC = G^T.Q) run on the same kernel, so a caller can differentiate
+        through it (the reference's tf.matmul semantics).  Host tensors
+        (no GPU) take torch.matmul."""
         q, c = self._split(x)
         with torch.set_grad_enabled(training and torch.is_grad_enabled()):
             qe, ce = self.query_tower.call(q), self.candidate_tower.call(c)
-            if torch.is_grad_enabled() or not qe.is_cuda:
+            if not qe.is_cuda:
                 return torch.matmul(qe, ce.t())
+            if torch.is_grad_enabled():
+                return hip_ops.ScoreMatrix.apply(qe, ce)
             return hip_ops.score_matrix(qe, ce)
 
     def candidate_logq(self, x: Dict[str, Any]) -> Optional[torch.Tensor]:

@@ -577,3 +577,56 @@ def test_model_call_score_matrix_on_libtt(cuda):
     b = torch.rand(300, 13, device=cuda)
     r = hip_ops.score_matrix(a, b)
     assert torch.allclose(r.double(), a.double() @ b.double().t(), rtol=2e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("nq,nc,e", [(601, 601, 64), (37, 517, 13), (300, 5, 130)])
+def test_score_matrix_autograd_on_libtt(cuda, nq, nc, e):
+    """hip_ops.ScoreMatrix (TwoTowerModel.call with gradients): S = q.c^T and
+    its gradients dq = G.c, dc = G^T.q all on tt_mlp_rows (bf16x3, K and N
+    chunked by 256, partials added in chunk order) — within 2e-5 (relative to
+    the largest entry) of the fp64 autograd product, ragged and odd sizes
+    included; deterministic."""
+    g0 = torch.Generator(device=cuda)
+    g0.manual_seed(nq + nc + e)
+    q = torch.randn(nq, e, device=cuda, generator=g0).requires_grad_()
+    c = torch.randn(nc, e, device=cuda, generator=g0).requires_grad_()
+    w = torch.randn(nq, nc, device=cuda, generator=g0)
+    s = hip_ops.ScoreMatrix.apply(q, c)
+    (s * w).sum().backward()
+    q64, c64 = q.detach().double().requires_grad_(), c.detach().double().requires_grad_()
+    s64 = q64 @ c64.t()
+    (s64 * w.double()).sum().backward()
+    for got, ref in ((s, s64), (q.grad, q64.grad), (c.grad, c64.grad)):
+        err = (got.detach().double() - ref.detach()).abs().max().item() / ref.detach().abs().max().item()
+        assert err <= 2e-5, err
+    dq1 = q.grad.clone()
+    q.grad = None
+    hip_ops.ScoreMatrix.apply(q, c).mul(w).sum().backward()
+    assert torch.equal(q.grad, dq1)
+
+
+def test_model_call_with_gradients_on_libtt(cuda):
+    """TwoTowerModel.call with gradients enabled differentiates through the
+    libtt score matrix (no torch.matmul): the towers' flat MLP gradients of
+    sum(S * W) within 1e-4 (relative norm) of the same towers with the
+    product taken by a torch fp32 matmul (the test's reference only)."""
+    m = _small_model(cuda, seed=32)
+    rng = np.random.default_rng(13)
+    x = _batch(cuda, rng, 300, True)
+    w = torch.randn(300, 300, device=cuda, generator=torch.Generator(device=cuda).manual_seed(5))
+    flats = [t.dense.flat for t in m.towers]
+    for f in flats:
+        f.grad = None
+    s = m.call(x, training=True)
+    assert s.requires_grad and "ScoreMatrix" in type(s.grad_fn).__name__
+    (s * w).sum().backward()
+    got = [f.grad.clone() for f in flats]
+    for f in flats:
+        f.grad = None
+    q, c = m._split(x)
+    qe, ce = m.query_tower.call(q), m.candidate_tower.call(c)
+    ((qe @ ce.t()) * w).sum().backward()
+    for g, f in zip(got, flats):
+        assert torch.isfinite(g).all()
+        err = ((g - f.grad).norm() / f.grad.norm()).item()
+        assert err <= 1e-4, err
