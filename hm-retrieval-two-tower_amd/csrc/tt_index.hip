@@ -661,9 +661,13 @@ __global__ void __launch_bounds__(kSThreads) scan_kernel(const ScreenArgs a) {
     const unsigned pcr = __float_as_uint(tg4[0]);
     const int ql = valid ? static_cast<int>(__float_as_uint(tg4[1])) : 0;
     const float tr = valid ? tau_l[ql] : INFINITY;
-    int n = 0;
+#ifndef TT_SCAN_FLUSH_LOOP
+#define TT_SCAN_FLUSH_LOOP 1
+#endif
+    unsigned hm = 0;  // the row's registers above tau
 #pragma unroll
-    for (int r = 0; r < 16; ++r) n += (x[r >> 2][r & 3] > tr) ? 1 : 0;
+    for (int r = 0; r < 16; ++r) hm |= (x[r >> 2][r & 3] > tr) ? (1u << r) : 0u;
+    const int n = __popc(hm);
     int pos = 0;
     if (n) {  // reserve n list slots (an LDS atomic the compiler would order behind the ring's loads)
       const unsigned addr = static_cast<unsigned>(
@@ -675,16 +679,35 @@ __global__ void __launch_bounds__(kSThreads) scan_kernel(const ScreenArgs a) {
     // branch-free: one store per register for the whole wave; a lane with no
     // hit in it addresses past the resource's range, and the store drops it
     typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+    if (TT_SCAN_FLUSH_LOOP) {
+      // one store per round for the whole wave, each lane storing its next
+      // hit (lowest register first: the same entries at the same slots as
+      // the per-register form), the score re-read from the staged row in
+      // LDS; rounds = the most hits in one row (usually 2), not 16
+      int rounds = 0;
+      while (__ballot(hm != 0u)) {
+        const int r = __builtin_ctz(hm | 0x10000u);  // 16 (the row's tag word) when none is left
+        const float v = row[r];
+        const u32x2 e = {__float_as_uint(v), pcr + static_cast<unsigned>((r & 3) + 8 * (r >> 2))};
+        const unsigned off = hm != 0u ? lbase + static_cast<unsigned>(min(pos, last)) * 8u : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b64(e, lists, off, 0, 0);
+        pos += hm != 0u ? 1 : 0;
+        hm &= hm - 1u;
+        ++rounds;
+      }
+      wc = __builtin_amdgcn_readfirstlane(wc + rounds);
+    } else {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float v = x[r >> 2][r & 3];
-      const bool keepit = v > tr;
-      const u32x2 e = {__float_as_uint(v), pcr + static_cast<unsigned>((r & 3) + 8 * (r >> 2))};
-      const unsigned off = keepit ? lbase + static_cast<unsigned>(min(pos, last)) * 8u : 0x80000000u;
-      __builtin_amdgcn_raw_buffer_store_b64(e, lists, off, 0, 0);
-      pos += keepit ? 1 : 0;
+      for (int r = 0; r < 16; ++r) {
+        const float v = x[r >> 2][r & 3];
+        const bool keepit = v > tr;
+        const u32x2 e = {__float_as_uint(v), pcr + static_cast<unsigned>((r & 3) + 8 * (r >> 2))};
+        const unsigned off = keepit ? lbase + static_cast<unsigned>(min(pos, last)) * 8u : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b64(e, lists, off, 0, 0);
+        pos += keepit ? 1 : 0;
+      }
+      wc = __builtin_amdgcn_readfirstlane(wc + 16);
     }
-    wc = __builtin_amdgcn_readfirstlane(wc + 16);
     tail += nrows;
     wsync();
   };

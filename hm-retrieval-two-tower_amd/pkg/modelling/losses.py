@@ -134,8 +134,9 @@ class _TowersInBatchXent(torch.autograd.Function):
     a device scalar (no separate scaling pass over dQ, dC)."""
 
     @staticmethod
-    def forward(ctx, qi, ci, flat_q, flat_c, logq, stack_q, stack_c, scale, on_tower=None):
+    def forward(ctx, qi, ci, flat_q, flat_c, logq, stack_q, stack_c, scale, on_tower=None, on_dx=None):
         ctx.pair = _paired(qi, stack_q, stack_c)
+        ctx.on_dx = on_dx
         if ctx.pair:
             qa, ca = _pair_forward(qi, ci, flat_q, flat_c, stack_q, stack_c)
             return _TowersInBatchXent._finish(ctx, qa, ca, flat_q, flat_c, logq, stack_q, stack_c, scale, on_tower)
@@ -164,21 +165,26 @@ class _TowersInBatchXent(torch.autograd.Function):
         qa, ca = acts[:ctx.nq], acts[ctx.nq:]
         s = (g * ctx.scale if ctx.scale != 1.0 else g).reshape(1).float().contiguous()
         stack_q, stack_c = ctx.stacks
-        if ctx.pair:
+        if ctx.pair:  # (on_dx unused: on_tower then applies each tower's whole update)
             return (*_pair_backward(ctx, qa, ca, flat_q, flat_c, dq, dc, s, ctx.on_tower),
-                    None, None, None, None, None)
+                    None, None, None, None, None, None)
+        on_dx = ctx.on_dx
         main = torch.cuda.current_stream()
         side = _tower_stream(dq.device) if TOWER_STREAMS else main
         side.wait_stream(main)
         with torch.cuda.stream(side), hip_ops.Workspace.scope(TOWER_C_SCOPE):
-            gci, gflat_c = stack_c.backward_acts(ca, flat_c, dc, s, ctx.needs_input_grad[1])
-            if ctx.on_tower is not None:  # this tower's updates, beside the other tower's backward
+            # this tower's updates (on_dx: the embedding update once its input
+            # gradient exists; on_tower: the rest), beside the other tower's backward
+            gci, gflat_c = stack_c.backward_acts(ca, flat_c, dc, s, ctx.needs_input_grad[1],
+                                                 on_dx=(lambda dx: on_dx(1, dx)) if on_dx is not None else None)
+            if ctx.on_tower is not None:
                 ctx.on_tower(1, gci, gflat_c)
-        gqi, gflat_q = stack_q.backward_acts(qa, flat_q, dq, s, ctx.needs_input_grad[0])
+        gqi, gflat_q = stack_q.backward_acts(qa, flat_q, dq, s, ctx.needs_input_grad[0],
+                                             on_dx=(lambda dx: on_dx(0, dx)) if on_dx is not None else None)
         if ctx.on_tower is not None:
             ctx.on_tower(0, gqi, gflat_q)
         main.wait_stream(side)
-        return gqi, gci, gflat_q, gflat_c, None, None, None, None, None
+        return gqi, gci, gflat_q, gflat_c, None, None, None, None, None, None
 
 
 def global_inbatch_grads(q: torch.Tensor, c: torch.Tensor, logq: Optional[torch.Tensor], comm,
@@ -257,7 +263,7 @@ def global_towers_inbatch_softmax_xent(qi: torch.Tensor, ci: torch.Tensor, stack
 
 def towers_inbatch_softmax_xent(qi: torch.Tensor, ci: torch.Tensor, stack_q, stack_c,
                                 logq: Optional[torch.Tensor] = None, reduction: str = "sum",
-                                on_tower=None) -> torch.Tensor:
+                                on_tower=None, on_dx=None) -> torch.Tensor:
     """Loss of the query tower on qi against the candidate tower on ci (tower
     inputs [B, *]), fused into one autograd node; stack_* are DenseStacks.
     on_tower(i, input_grad, flat_grad), if given, is called in the backward as
@@ -267,7 +273,8 @@ def towers_inbatch_softmax_xent(qi: torch.Tensor, ci: torch.Tensor, stack_q, sta
     if reduction not in ("sum", "sum_over_batch_size", "mean"):
         raise ValueError(f"unsupported reduction {reduction}")
     scale = 1.0 if reduction == "sum" else 1.0 / qi.shape[0]
-    return _TowersInBatchXent.apply(qi, ci, stack_q.flat, stack_c.flat, logq, stack_q, stack_c, scale, on_tower)
+    return _TowersInBatchXent.apply(qi, ci, stack_q.flat, stack_c.flat, logq, stack_q, stack_c, scale, on_tower,
+                                    on_dx)
 
 
 def inbatch_softmax_xent(q: torch.Tensor, c: torch.Tensor, logq: Optional[torch.Tensor] = None,

@@ -22,6 +22,7 @@ step is a single tt_dense_* launch.  Every GEMM is libtt's, on bf16x3 MFMA
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -33,6 +34,11 @@ from pkg.modelling.layers.input_layer import InputLayer
 from pkg.modelling.models.abstract_keras_model import AbstractKerasModel, TensorSpec
 
 __all__ = ["Tower", "DenseStack", "pair_compatible", "forward_acts_pair", "backward_acts_pair"]
+
+# DenseStack.backward_acts: every input gradient before any weight gradient
+# (C3 step, 3 interleaved runs each: unfused 0.535-0.541 vs 0.533-0.536 ms;
+# fused apply 0.570-0.573 vs 0.564-0.565 ms — off)
+IGRAD_FIRST = os.environ.get("TT_IGRAD_FIRST", "0") == "1"
 
 
 def _rows(p: dict) -> torch.Tensor:
@@ -165,7 +171,7 @@ class DenseStack:
                     cmask=acts[li] if li > 0 else None)
 
     def backward_acts(self, acts: List[torch.Tensor], flat: torch.Tensor, gout: torch.Tensor,
-                      gscale: Optional[torch.Tensor], need_input_grad: bool):
+                      gscale: Optional[torch.Tensor], need_input_grad: bool, on_dx=None):
         """(d x, d flat) from the saved activations.  Per layer l from the top:
         [dW_l; db_l] = [h_{l-1} | 1]^T G_l by ONE tt_mlp_wgrad straight into the
         flat gradient (the top layer's G_L = relu'(h_L) * s * gout formed inside
@@ -176,20 +182,45 @@ class DenseStack:
         width not a multiple of 4, or wider than 4096) takes its weight
         gradient from torch (the only vendor GEMM left, never at the
         reference's configurations).  Images: packed by this step's forward
-        (same flat)."""
+        (same flat).  With TT_IGRAD_FIRST=1 the input-gradient chain runs
+        before the weight gradients, and on_dx(dx), if given, is called
+        between them (the fused step's embedding update); the kernels and
+        their results are the same in either order (off by default: same step
+        time unfused, slower fused — DESIGN §9)."""
         gflat = torch.empty_like(flat)
+        if IGRAD_FIRST:
+            # the input-gradient chain first (the embedding update waits for it,
+            # the weight gradients do not), on_dx(dx) between the two
+            gs, g, dx = {}, gout, None
+            for li in range(len(self.layout) - 1, -1, -1):
+                gs[li] = g
+                if li == 0 and not need_input_grad:
+                    break
+                g = _rows(self._igrad_problem(li, acts, g, gscale))
+                if li == 0:
+                    dx = g
+            if on_dx is not None:
+                on_dx(dx)
+            for li in range(len(self.layout) - 1, -1, -1):
+                self._wgrad_layer(li, acts, gflat, gout, gs[li], gscale)
+            return dx, gflat
         g = gout
         for li in range(len(self.layout) - 1, -1, -1):
-            if self._wgrad_fits(li, g, acts):
-                p = self._wgrad_problem(li, acts, gflat, gout, g, gscale)
-                _wgrad(p)
-            else:
-                self._wgrad_torch(li, acts, gflat, g, gscale)
+            self._wgrad_layer(li, acts, gflat, gout, g, gscale)
             if li == 0 and not need_input_grad:
-                return None, gflat
+                g = None
+                break
             p = self._igrad_problem(li, acts, g, gscale)
             g = _rows(p)
+        if on_dx is not None:
+            on_dx(g)
         return g, gflat
+
+    def _wgrad_layer(self, li, acts, gflat, gout, g, gscale) -> None:
+        if self._wgrad_fits(li, g, acts):
+            _wgrad(self._wgrad_problem(li, acts, gflat, gout, g, gscale))
+        else:
+            self._wgrad_torch(li, acts, gflat, g, gscale)
 
     def __call__(self, x: torch.Tensor) -> torch.Tensor:
         if torch.is_grad_enabled() and (x.requires_grad or self.flat.requires_grad):

@@ -28,6 +28,7 @@ from pkg.modelling.losses import TOWER_C_SCOPE, InBatchSoftmaxCrossEntropy, towe
 from pkg.modelling.models.abstract_keras_model import AbstractKerasModel, TensorSpec
 from pkg.modelling import hip_ops
 from pkg.modelling.layers.input_layer import InputLayer
+from pkg.modelling.models import tower as _tower_mod
 from pkg.modelling.models.tower import Tower
 
 logger = logging.getLogger(__name__)
@@ -185,7 +186,8 @@ class TwoTowerModel(AbstractKerasModel):
         in-batch loss run as one autograd node (losses.towers_inbatch_softmax_xent)."""
         if torch.is_grad_enabled():
             return towers_inbatch_softmax_xent(qi, ci, self.query_tower.dense, self.candidate_tower.dense, logq,
-                                               self.loss.reduction, getattr(self, "_on_tower", None))
+                                               self.loss.reduction, getattr(self, "_on_tower", None),
+                                               getattr(self, "_on_dx", None))
         return self.loss(self.query_tower.dense(qi), self.candidate_tower.dense(ci), logq)
 
     def compile(self, loss=None, optimizer=None, **kwargs) -> None:
@@ -224,12 +226,17 @@ class TwoTowerModel(AbstractKerasModel):
         dense_early = (not fused and DENSE_EARLY and isinstance(self.optimizer, Adagrad)
                        and self.device.type == "cuda")
         self._dense_done = set()
+        self._sparse_done = set()
         self._on_tower = self._apply_tower if fused else (self._apply_dense_tower if dense_early else None)
+        # fused: each tower's embedding update the moment its input gradient
+        # exists (the weight gradients follow it on that tower's stream)
+        self._on_dx = self._apply_tower_sparse if (fused and _tower_mod.IGRAD_FIRST) else None
         self._in_train_step = True
         try:
             loss = self.compute_loss(data, training=True)
         finally:
             self._on_tower = None
+            self._on_dx = None
             self._in_train_step = False
         fwd_done = None
         if fused:
@@ -270,7 +277,14 @@ class TwoTowerModel(AbstractKerasModel):
         return {"loss": loss.detach()}
 
     def _apply_tower(self, i: int, input_grad: Optional[torch.Tensor], flat_grad: torch.Tensor) -> None:
+        if i in self._sparse_done:  # its embedding update ran at the input gradient
+            self.optimizer.apply_dense(self.towers[i], flat_grad)
+            return
         self.optimizer.apply_tower(self.towers[i], input_grad, flat_grad)
+
+    def _apply_tower_sparse(self, i: int, input_grad: Optional[torch.Tensor]) -> None:
+        self.optimizer.apply_tower_sparse(self.towers[i], input_grad)
+        self._sparse_done.add(i)
 
     def _apply_dense_tower(self, i: int, input_grad: Optional[torch.Tensor], flat_grad: torch.Tensor) -> None:
         self.optimizer.apply_dense(self.towers[i], flat_grad)

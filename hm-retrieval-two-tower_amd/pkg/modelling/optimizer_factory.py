@@ -123,10 +123,13 @@ class Adagrad(_Optimizer):
     def apply_tower(self, tower, input_grad: Optional[torch.Tensor], flat_grad: torch.Tensor) -> None:
         """Tower's dense Adagrad step and its tables' sparse step, on the current
         stream and workspace scope (the ones prepare_towers used for it)."""
-        lr, eps, init = self.learning_rate, self.epsilon, self.initial_accumulator_value
-        flat = tower.dense.flat
-        (acc,) = self._slot(flat, 1, init)
-        hip_ops.dense_adagrad(flat.data, acc, flat_grad, lr, eps)
+        self.apply_dense(tower, flat_grad)
+        self.apply_tower_sparse(tower, input_grad)
+
+    def apply_tower_sparse(self, tower, input_grad: Optional[torch.Tensor]) -> None:
+        """Tower's tables' sparse Adagrad step alone (apply_tower's second
+        half), on the current stream and workspace scope."""
+        lr, eps = self.learning_rate, self.epsilon
         prep = getattr(self, "_tower_prep", {}).pop(id(tower), None)
         if input_grad is None:
             return

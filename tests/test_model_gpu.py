@@ -234,6 +234,32 @@ def test_fused_optimizer_apply_bit_identical_to_unfused(cuda):
     b.optimizer.check_status(cuda)
 
 
+@pytest.mark.parametrize("fused", [False, True])
+def test_igrad_first_order_bit_identical(cuda, monkeypatch, fused):
+    """TT_IGRAD_FIRST (the default): each tower's input-gradient chain before
+    its weight gradients, and in the fused step the embedding update issued at
+    the input gradient, ahead of the weight gradients on that tower's stream —
+    the same kernels on the same operands, so losses, tables, accumulators and
+    MLP buffers stay bit-identical to the layer-by-layer order, step for step
+    at ragged batch sizes; no sparse error is recorded."""
+    from pkg.modelling.models import tower as tower_mod
+
+    a, b = _small_model(cuda, seed=12, fused=fused), _small_model(cuda, seed=12, fused=fused)
+    rng = np.random.default_rng(10)
+    for i, B in enumerate((512, 37, 256, 300)):
+        x = _batch(cuda, rng, B, True)
+        monkeypatch.setattr(tower_mod, "IGRAD_FIRST", False)
+        la = a.train_step(x)["loss"]
+        monkeypatch.setattr(tower_mod, "IGRAD_FIRST", True)
+        lb = b.train_step(x)["loss"]
+        assert torch.equal(la, lb), (i, B)
+        sa, sb = _state(a), _state(b)
+        for k in sa:
+            assert torch.equal(sa[k], sb[k]), (i, B, k)
+    a.optimizer.check_status(cuda)
+    b.optimizer.check_status(cuda)
+
+
 def test_dense_early_bit_identical_to_dense_after_join(cuda, monkeypatch):
     """The default step applies each tower's dense (MLP) Adagrad inside the
     backward on the tower's stream (TT_DENSE_EARLY); with it off the dense
