@@ -895,224 +895,6 @@ __global__ void __launch_bounds__(kSThreads) scan_kernel(const ScreenArgs a) {
   TT_STAT(0, (h == 0 ? cnt_l[ql0] + cnt_l[ql1] : 0));
 }
 
-// ---- scan, one query set per wave (TT_SCAN_ONESET) --------------------------
-// The same screen as scan_kernel with 16 waves of ONE 32-query set each (the
-// workgroup still covers 512 queries): 4 waves per SIMD instead of 2, so a
-// wave's filter work and waits overlap three partners' MFMAs rather than one.
-// Per wave: the 8 query fragments, one fragment set (read at the start of
-// each half, single-buffered), accumulators A (block (u, 0)) and B (u, 1);
-// a 64-row staging ring (a set adds <= 64 rows: the pending rows are flushed
-// first when they would not fit).  Everything else — the tile image, the
-// LDS-DMA ring and its vmcnt windows, the lists, the flush — as scan_kernel.
-constexpr int kS1Waves = 16;
-constexpr int kS1Threads = kS1Waves * kWave;  // 1024
-constexpr int kS1Rows = 64;                   // staged rows per wave
-static_assert(kS1Waves * 32 == kQPerWG, "one 32-query set per wave covers the workgroup's queries");
-
-template <int D>
-__global__ void __launch_bounds__(kS1Threads) scan1_kernel(const ScreenArgs a) {
-  using G = ScanGeo<D>;
-  constexpr int KS = D / 16;
-  constexpr int TILE_BYTES = G::TILE_BYTES;
-  constexpr int PIECES = TILE_BYTES / 1024;
-  constexpr int PPW = PIECES >= kS1Waves ? PIECES / kS1Waves : 1;
-  __shared__ __attribute__((aligned(1024))) char smem[G::RING];
-  __shared__ __attribute__((aligned(16))) float s_rows[kS1Waves * kS1Rows * kRowF];
-  __shared__ float s_tau[kQPerWG];
-  __shared__ int s_cnt[kQPerWG];
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
-  const int lane = lane_id();
-  const int h = lane >> 5, l32 = lane & 31;
-  const int split = static_cast<int>(blockIdx.x % a.S);
-  const int64_t qblk = static_cast<int64_t>(blockIdx.x / a.S) * kQPerWG;
-  const int ql0 = wave * 32 + l32;
-  const int64_t q0 = qblk + ql0;
-  const int t0 = static_cast<int>(a.row0 / kCTile);
-  const int ntiles = static_cast<int>((a.row1 + kCTile - 1) / kCTile) - t0;
-  const int per = (ntiles + a.S - 1) / a.S;
-  const int tb = t0 + split * per;
-  const int nv = max(min(ntiles - split * per, per), 0);
-  const __bf16* crow = index_rows(a.index);
-  const bool my_pieces = wave * PPW < PIECES;
-  float* const srow = s_rows + wave * kS1Rows * kRowF;
-
-  bf16x8 bq0[KS];
-#pragma unroll
-  for (int s = 0; s < KS; ++s) bq0[s] = *reinterpret_cast<const bf16x8*>(a.qb + q0 * D + 16 * s + 8 * h);
-#ifndef TT_INDEX_NOINSERT
-  const float tau0 = q0 < a.nq ? a.tau[q0] : INFINITY;
-#else
-  const float tau0 = __uint_as_float(a.cap > 0 ? 0x7f800000u : 0u);
-#endif
-  if (h == 0) {
-    s_tau[ql0] = tau0;
-    s_cnt[ql0] = 0;
-  }
-  wait_vmcnt<0>();
-
-  auto issue = [&](int tile, int stage) {
-    const int64_t base = static_cast<int64_t>(tile) * kCTile;
-#pragma unroll
-    for (int u = 0; u < PPW; ++u) {
-      const int p = wave * PPW + u;
-      if (p < PIECES) {
-        int row, ch;
-        tile_piece_src(p, lane, row, ch);
-        const __bf16* src = crow + (base + row) * D + ch * 8;
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src),
-                                         (__attribute__((address_space(3))) void*)(smem + stage * TILE_BYTES + p * 1024),
-                                         16, 0, 0);
-      }
-    }
-  };
-  const int frag_off = tile_frag_lane_off(l32, h);
-  auto load_frags = [&](bf16x8 (&f)[KS], const char* B, int t) {
-#pragma unroll
-    for (int s = 0; s < KS; ++s) f[s] = *reinterpret_cast<const bf16x8*>(B + frag_off + s * 2048 + t * 1024);
-  };
-  auto mask_pad = [&](f32x16& acc, int64_t cfirst) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int64_t c = cfirst + (r & 3) + 8 * (r >> 2);
-      if (c < a.row0 || c >= a.row1) acc[r] = -INFINITY;
-    }
-  };
-  auto edge = [&](int64_t cbase) { return cbase < a.row0 || cbase + kCTile > a.row1; };
-
-  const int dpieces = my_pieces ? PPW : 0;
-  int wa, wb, wc, da, db, dc;
-  int head = 0, tail = 0;
-  const __amdgpu_buffer_rsrc_t lists = __builtin_amdgcn_make_buffer_rsrc(
-      a.buf + qblk * a.S * static_cast<int64_t>(a.cap), 0, 0x7fffffff, 0x00020000);
-
-  // as scan_kernel's flush (rounds of one store per lane), ring of kS1Rows
-  auto flush = [&](int nrows) {
-    wsync();
-    const float* row = srow + ((tail + lane) & (kS1Rows - 1)) * kRowF;
-    const bool valid = lane < nrows;
-    f32x4 x[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) x[i] = reinterpret_cast<const f32x4*>(row)[i];
-    const f32x4 tg4 = reinterpret_cast<const f32x4*>(row)[4];
-    const unsigned pcr = __float_as_uint(tg4[0]);
-    const int ql = valid ? static_cast<int>(__float_as_uint(tg4[1])) : 0;
-    const float tr = valid ? s_tau[ql] : INFINITY;
-    unsigned hm = 0;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) hm |= (x[r >> 2][r & 3] > tr) ? (1u << r) : 0u;
-    const int n = __popc(hm);
-    int pos = 0;
-    if (n) {
-      const unsigned addr = static_cast<unsigned>(
-          reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) int*)(s_cnt + ql)));
-      asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(pos) : "v"(addr), "v"(n) : "memory");
-    }
-    const unsigned lbase = static_cast<unsigned>((ql * a.S + split) * a.cap) * 8u;
-    const int last = a.cap - 1;
-    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-    int rounds = 0;
-    while (__ballot(hm != 0u)) {
-      const int r = __builtin_ctz(hm | 0x10000u);
-      const float v = row[r];
-      const u32x2 e = {__float_as_uint(v), pcr + static_cast<unsigned>((r & 3) + 8 * (r >> 2))};
-      const unsigned off = hm != 0u ? lbase + static_cast<unsigned>(min(pos, last)) * 8u : 0x80000000u;
-      __builtin_amdgcn_raw_buffer_store_b64(e, lists, off, 0, 0);
-      pos += hm != 0u ? 1 : 0;
-      hm &= hm - 1u;
-      ++rounds;
-    }
-    wc = __builtin_amdgcn_readfirstlane(wc + rounds);
-    tail += nrows;
-    wsync();
-  };
-  // stages the rows of this block's lanes whose max beats tau; the pending
-  // rows go out first when the block's would not fit the ring
-  auto stage = [&](const f32x16& c, bool hit, unsigned pc) {
-    const uint64_t m = __ballot(hit);
-    if (m) {
-      const int n = __popcll(m);
-      if (head - tail + n > kS1Rows) flush(head - tail);
-      if (hit) {
-        const unsigned slot = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), head));
-        f32x4* d = reinterpret_cast<f32x4*>(srow + (slot & (kS1Rows - 1)) * kRowF);
-        d[0] = f32x4{c[0], c[1], c[2], c[3]};
-        d[1] = f32x4{c[4], c[5], c[6], c[7]};
-        d[2] = f32x4{c[8], c[9], c[10], c[11]};
-        d[3] = f32x4{c[12], c[13], c[14], c[15]};
-        reinterpret_cast<uint2*>(d + 4)[0] = make_uint2(pc, static_cast<unsigned>(ql0));
-      }
-      head += n;
-    }
-  };
-
-#pragma unroll
-  for (int s = 0; s < kStages - 1; ++s)
-    if (s < nv) issue(tb + s, s);
-  if (!my_pieces || nv <= 1) wait_vmcnt<0>();
-  else if (nv == 2) wait_vmcnt<PPW>();
-  else wait_vmcnt<2 * PPW>();
-  __builtin_amdgcn_s_barrier();
-  dc = 0;
-  if (3 < nv) {
-    issue(tb + 3, 3);
-    dc = dpieces;
-  }
-  da = wa = (1 < nv) ? dpieces : 0;
-  db = wb = (2 < nv) ? dpieces : 0;
-  wc = dc;
-
-  const int ue0 = (nv > 0 && edge(static_cast<int64_t>(tb) * kCTile)) ? 0 : -1;
-  const int ue1 = (nv > 0 && edge(static_cast<int64_t>(tb + nv - 1) * kCTile)) ? nv - 1 : -1;
-  auto filter = [&](f32x16& x, int u, int t) {
-    const int64_t cb = static_cast<int64_t>(tb + u) * kCTile + 32 * t;
-    if (u == ue0 || u == ue1) mask_pad(x, cb + 4 * h);
-    stage(x, max16(x) > tau0, a.index_offset + static_cast<unsigned>(cb + 4 * h));
-  };
-  auto mfmas = [&](const bf16x8 (&f)[KS], f32x16& x) {
-    x = f32x16{};
-#pragma unroll
-    for (int s = 0; s < KS; ++s) x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[s], bq0[s], x, 0, 0, 0);
-  };
-  // per tile u: F <- (u, 0), MFMAs into A; filter B = (u - 1, 1) under them;
-  // F <- (u, 1) (stage u fully read: the ring barrier, refill); MFMAs into B;
-  // filter A = (u, 0) under them
-  bf16x8 f[KS];
-  f32x16 xa = {}, xb = {};
-  for (int u = 0; u < nv; ++u) {
-    const char* B = smem + (u % kStages) * TILE_BYTES;
-    load_frags(f, B, 0);
-    mfmas(f, xa);
-    if (u > 0) filter(xb, u - 1, 1);
-    load_frags(f, B, 1);
-    if (u + 1 < nv) {
-      wait_vmcnt_atmost((wa - da) + wb + wc);
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // vmcnt(63) expcnt(7) lgkmcnt(0)
-      __builtin_amdgcn_s_barrier();
-      wa = wb;
-      da = db;
-      wb = wc;
-      db = dc;
-      dc = 0;
-      if (u + 4 < nv) {
-        issue(tb + u + 4, (u + 4) % kStages);
-        dc = dpieces;
-      }
-      wc = dc;
-    }
-    mfmas(f, xb);
-    filter(xa, u, 0);
-  }
-  if (nv > 0) filter(xb, nv - 1, 1);
-  while (head > tail) flush(min(head - tail, kWave));
-  if (h == 0) {
-    const int n0c = s_cnt[ql0];
-    a.count[q0 * a.S + split] = n0c > a.cap - 1 ? -1 : n0c;
-  }
-  TT_STAT(0, (h == 0 ? s_cnt[ql0] : 0));
-}
-
 // tau[q] = min over the splits' estimates (the lowest is the safest: more
 // entries, fewer failed certificates).
 __global__ void tau_min_kernel(const float* __restrict__ tau_split, int S, int64_t nq, float* __restrict__ tau) {
@@ -2107,11 +1889,7 @@ void launch_pass(const ScreenArgs& sa, int64_t nq_pad, bool sample, hipStream_t 
     hipLaunchKernelGGL((sample_kernel<D>), grid, block, 0, st, sa);
   } else {
     probe_begin(TT_PROBE_INDEX_SCREEN, st);
-#ifndef TT_SCAN_ONESET
-#define TT_SCAN_ONESET 0
-#endif
-    if (TT_SCAN_ONESET) hipLaunchKernelGGL((scan1_kernel<D>), grid, dim3(kS1Threads), 0, st, sa);
-    else hipLaunchKernelGGL((scan_kernel<D>), grid, block, 0, st, sa);
+    hipLaunchKernelGGL((scan_kernel<D>), grid, block, 0, st, sa);
     probe_end(TT_PROBE_INDEX_SCREEN, st);
   }
 }
