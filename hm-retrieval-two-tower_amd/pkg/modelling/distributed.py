@@ -40,6 +40,10 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+# world-1 sharded step: the route on a side stream beside the forward (1) or
+# on the compute stream ahead of it (0): 0.311 vs 0.320 ms at 2048 rows,
+# 0.584-0.586 vs 0.636-0.647 ms at 16384 (profiles/r05_step_ab.txt)
+ROUTE_SIDE = os.environ.get("TT_SHARDED_ROUTE_SIDE", "1") == "1"
 logger = logging.getLogger(__name__)
 
 __all__ = ["IndexOps", "BatchComm", "ShardedBruteForceIndex", "QueryShardedBruteForceIndex", "shard_range", "all_gather_cat",
@@ -1127,7 +1131,13 @@ class ShardedTrainStep:
         else:
             for p, a, g in jobs:
                 self.ops.dense_adagrad(p, a, g, self.lr, self.eps)
-        self._loss.copy_(loss_out)
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            # captured: the graph's own loss scalar (its pool address is fixed
+            # and every replay rewrites it) is the step's loss — no 4-byte copy
+            # node in the graph (~5 us of a memcpy node per step)
+            self._loss_graph = loss_out
+        else:
+            self._loss.copy_(loss_out)
 
     # -- one step ----------------------------------------------------------
     def _body(self) -> None:
@@ -1139,7 +1149,7 @@ class ShardedTrainStep:
         if self.tables is not None:
             lookups = [(k, ids) for k, ids, _, _ in self._lookups(self._static)]
             idx_out = self._idx_all[:len(self._idx)]
-            if self.world == 1 and idx_out.is_cuda:
+            if self.world == 1 and idx_out.is_cuda and ROUTE_SIDE:
                 # one rank: the route has no collective and the middle reads the
                 # shard by id, so the route only feeds the backward's per-request
                 # sums and the owner apply — it runs on a side stream beside the
@@ -1226,7 +1236,9 @@ class ShardedTrainStep:
             if c[0] != 0x7EADBEEF or c[2] != 0x7EADBEEF or c[1] != 0 or max(counts) > self._cap:
                 raise RuntimeError(f"ShardedTrainStep debug: call {self._calls}, canary/overflow {c}, counts {counts}, "
                                    f"cap {self._cap}, graph {self._graph is not None}")
-        return {"loss": self._loss.clone()}
+        loss = self._loss_graph if self._graph is not None and getattr(self, "_loss_graph", None) is not None \
+            else self._loss
+        return {"loss": loss.clone()}
 
     # workspaces the sharded step's sparse kernels write (EmbeddingOps.hip)
     STATUS_TAGS = ("sparse_owner", "sparse_mid")

@@ -1,0 +1,12 @@
+# Round 5: kernel timeline of the world-1 sharded train step (ShardedTrainStep,
+# one RCCL rank, the whole step one graph replay) at 2048 and 16384 rows.
+set -e
+for B in 2048 16384; do
+  OUT=$GRAFT_REPO_ROOT/gpurun_out/trace_sh$B; mkdir -p $OUT
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT -o t -- python3 $GRAFT_REPO_ROOT/bench.py --steps 30 --warmup 5 --batch $B --train-mode sharded --no-index --no-cpu-baseline --pipeline-rows 0 --no-uniform-gather --no-c5 > $OUT/line.json 2> $OUT/err.txt
+  cd $GRAFT_REPO_ROOT
+  python3 -c "import json; d=json.load(open('$OUT/line.json')); print('B=$B ms/step', round(d['ms_per_step'],4))"
+  python3 tools/step_timeline.py $OUT/t_kernel_trace.csv > $OUT/timeline.txt && cat $OUT/timeline.txt
+  rm -f $OUT/t_kernel_trace.csv
+done
