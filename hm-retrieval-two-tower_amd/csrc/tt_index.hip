@@ -712,40 +712,9 @@ __global__ void __launch_bounds__(kSThreads) scan_kernel(const ScreenArgs a) {
     wsync();
   };
   // Stages the rows of this block's lanes whose max beats their tau.
-#ifndef TT_SCAN_STAGE_ALL
-#define TT_SCAN_STAGE_ALL 0
-#endif
   auto stage = [&](const f32x16& c, bool hit, int ql, unsigned pc) {
     const uint64_t m = __ballot(hit);
-    if (TT_SCAN_STAGE_ALL) {
-      // (Probe, off: 1M x k=100 43.2 vs 41.8 ms with the branches below, 3
-      // interleaved pairs, profiles/r05_index_scan_ab.txt.)
-      // Branch-free: EVERY lane writes its row, the n hit lanes into slots
-      // head .. head + n - 1, the others after them (slots the ring does not
-      // hold yet: < 64 pending + 64 <= kStageRows), and head advances by n.
-      // The wave's five stores issue whatever the hits (as before: a block
-      // has some hit lane ~98 % of the time), with no exec-mask branches, so
-      // they schedule among the MFMAs and their count is static.  (As inline
-      // asm: the compiler, seeing these stores unconditional, put a vmcnt(0)
-      // — a wait for the whole LDS-DMA ring — before them and before the
-      // flush's reads; the rows are a separate LDS object from the ring.
-      // LDS executes a wave's operations in order, so the flush's reads see
-      // them, and any lgkmcnt wait the compiler counts stays conservative.)
-      const unsigned n = static_cast<unsigned>(__popcll(m));
-      const unsigned bh = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32),
-                                                    __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), 0u));
-      const unsigned slot = hit ? head + bh : head + n + static_cast<unsigned>(lane) - bh;
-      const unsigned addr = static_cast<unsigned>(reinterpret_cast<uintptr_t>(
-          (__attribute__((address_space(3))) float*)(srow + (slot & (kStageRows - 1)) * kRowF)));
-      const f32x4 v0 = {c[0], c[1], c[2], c[3]}, v1 = {c[4], c[5], c[6], c[7]};
-      const f32x4 v2 = {c[8], c[9], c[10], c[11]}, v3 = {c[12], c[13], c[14], c[15]};
-      const uint2 mt = make_uint2(pc, static_cast<unsigned>(ql));
-      asm volatile("ds_write_b128 %0, %1\n\tds_write_b128 %0, %2 offset:16\n\tds_write_b128 %0, %3 offset:32\n\t"
-                   "ds_write_b128 %0, %4 offset:48\n\tds_write_b64 %0, %5 offset:64"
-                   :: "v"(addr), "v"(v0), "v"(v1), "v"(v2), "v"(v3), "v"(mt) : "memory");
-      head += static_cast<int>(n);
-      if (head - tail >= kWave) flush(kWave);
-    } else if (m) {
+    if (m) {
       if (hit) {
         // slot = head + #hit lanes below this one (v_mbcnt adds head in)
         const unsigned slot = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32),
@@ -759,6 +728,36 @@ __global__ void __launch_bounds__(kSThreads) scan_kernel(const ScreenArgs a) {
       }
       head += __popcll(m);
       if (head - tail >= kWave) flush(kWave);
+    }
+  };
+#ifndef TT_SCAN_PAIR_STAGE
+#define TT_SCAN_PAIR_STAGE 1
+#endif
+  // Both query sets' rows of one block in ONE round of row stores: a lane
+  // stages its set-0 row if that hits, else its set-1 row (selected in
+  // registers); the lanes where both hit (~0.4 % of lanes) store their set-1
+  // row in a second round.  The stores' LDS issue — five instructions per
+  // round whatever the hit lanes, the filter's main cost — is then ~1.2
+  // rounds per block pair instead of ~2 (the same rows, in another order).
+  auto stage2 = [&](const f32x16& x0, const f32x16& x1, bool h0, bool h1, unsigned pc) {
+    const uint64_t m = __ballot(h0 || h1);
+    if (m) {
+      if (h0 || h1) {
+        const unsigned slot = __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), head));
+        f32x4* d = reinterpret_cast<f32x4*>(srow + (slot & (kStageRows - 1)) * kRowF);
+        f32x16 y;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) y[r] = h0 ? x0[r] : x1[r];
+        d[0] = f32x4{y[0], y[1], y[2], y[3]};
+        d[1] = f32x4{y[4], y[5], y[6], y[7]};
+        d[2] = f32x4{y[8], y[9], y[10], y[11]};
+        d[3] = f32x4{y[12], y[13], y[14], y[15]};
+        reinterpret_cast<uint2*>(d + 4)[0] = make_uint2(pc, static_cast<unsigned>(h0 ? ql0 : ql1));
+      }
+      head += __popcll(m);
+      if (head - tail >= kWave) flush(kWave);
+      stage(x1, h0 && h1, ql1, pc);
     }
   };
 
@@ -834,6 +833,8 @@ __global__ void __launch_bounds__(kSThreads) scan_kernel(const ScreenArgs a) {
       probe_acc = fmaxf(probe_acc, fmaxf(p.m0, p.m1));
     } else if (TT_SCAN_PROBE == 2) {
       probe_acc += x0[0] + x1[5];
+    } else if (TT_SCAN_PAIR_STAGE) {
+      stage2(x0, x1, p.m0 > tau0, p.m1 > tau1, p.pc);
     } else {
       stage(x0, p.m0 > tau0, ql0, p.pc);
       stage(x1, p.m1 > tau1, ql1, p.pc);
