@@ -1402,7 +1402,6 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
   bool fail = pre[kWave + 1] != 0 || ntot < K;
   const float tmax = Ls.tau[q];
   float X = -INFINITY;
-  unsigned kpfx = 0xFFFFFFFFu;  // the K-th screened score's key prefix
   // the whole list read once into LDS when it fits (the select's passes and
   // the cut then read LDS, not the lists in memory)
   const bool staged = !fail && ntot <= a.L;
@@ -1466,7 +1465,6 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
     if (!fail) {
       // certificate (below) is the only reason counted in stats[1]
       X = lb_of(order_key_float(r.prefix), m, rel);
-      kpfx = r.prefix;
       // per-row bounds: the >= K entries at or above the K-th key prefix each
       // score at least max(lb(s~), s~ - err_row) exactly, so X = the least of
       // those lower bounds has >= K candidates at or above it (and is >= the
@@ -1527,10 +1525,7 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
       const bool keepit = i < ntot && ub_of(sv, m, rel) >= X && sv + err_row(iv) >= X;
       const int p = compact_slot<NW>(keepit, n, wcnt, par);
       if constexpr (NW == 1) wsync();
-      if (keepit) {
-        sc[p] = sv;  // (s~ kept beside the id: the two-phase rescoring reads it)
-        id[p] = iv;
-      }
+      if (keepit) id[p] = iv;
       if constexpr (NW == 1) wsync();
     }
   } else if (!fail) {
@@ -1548,10 +1543,7 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
           fail = true;
           break;
         }
-        if (keepit) {
-          sc[p] = __uint_as_float(en.x);
-          id[p] = en.y;
-        }
+        if (keepit) id[p] = en.y;
       }
     }
   }
@@ -1569,74 +1561,17 @@ __global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a)
   for (int j = t; j < K; j += NT) out_s[j] = sc[j];
   return;
 #endif
-  auto exact_of = [&](unsigned idv) {
-    const int64_t row = static_cast<int64_t>(idv) - a.cand_offset;
-#ifdef TT_FINAL_NORESCORE  // timing probe only: no candidate rows read (results wrong, no ties)
-    return static_cast<float>(row);
-#else
-    return exact_score(qs, a.cand + row * a.ldc, a.dim, a.vec4 != 0) + 0.0f;
-#endif
-  };
   unsigned emin = 0xFFFFFFFFu, emax = 0u;
-#ifndef TT_INDEX_TWO_PHASE
-#define TT_INDEX_TWO_PHASE 1
+  for (int j = t; j < n; j += NT) {
+    const int64_t row = static_cast<int64_t>(id[j]) - a.cand_offset;
+#ifdef TT_FINAL_NORESCORE  // timing probe only: no candidate rows read (results wrong, no ties)
+    sc[j] = static_cast<float>(row);
+#else
+    sc[j] = exact_score(qs, a.cand + row * a.ldc, a.dim, a.vec4 != 0) + 0.0f;
 #endif
-  if (TT_INDEX_TWO_PHASE && a.floor == nullptr) {
-    // Two-phase rescoring.  (1) The entries at or above the K-th screened
-    // prefix (>= K of them, all kept by the cut) first: every one is a
-    // candidate, so Y = the least of their exact scores is a lower bound on
-    // the K-th exact score, and Y >= X (each scores >= lb(s~) >= lb(prefix)).
-    // (2) The rest are cut again at max(X, Y) — an exact-top-K member
-    // scores >= Y, so its upper bound does — and only the survivors are
-    // rescored: the window below the K-th score shrinks from ~2 screen
-    // bounds to ~1.  Marked ids (top bit) are the phase-1 entries.
-    constexpr unsigned kDone = 0x80000000u;
-    unsigned ymin = 0xFFFFFFFFu, unused = 0u;
-    for (int j = t; j < n; j += NT) {
-      if (float_order_key(sc[j]) >= kpfx) {
-        const float e = exact_of(id[j]);
-        sc[j] = e;
-        id[j] |= kDone;
-        ymin = min(ymin, float_order_key(e));
-      }
-    }
-    group_minmax<NW>(ymin, unused, wcnt);
-    const float X2 = fmaxf(X, order_key_float(ymin));
-    int n2 = 0, par2 = 0;
-    for (int i0 = 0; i0 < n; i0 += NT) {
-      const int i = i0 + t;
-      const float sv = i < n ? sc[i] : 0.0f;
-      const unsigned iv = i < n ? id[i] : 0u;
-      const bool done = i < n && (iv & kDone) != 0u;
-      const bool keepit = done || (i < n && ub_of(sv, m, rel) >= X2 && sv + err_row(iv) >= X2);
-      const int p = compact_slot<NW>(keepit, n2, wcnt, par2);
-      if constexpr (NW == 1) wsync();
-      if (keepit) {
-        sc[p] = sv;
-        id[p] = iv;
-      }
-      if constexpr (NW == 1) wsync();
-    }
-    gsync<NW>();
-    n = n2;
-    for (int j = t; j < n; j += NT) {
-      const unsigned iv = id[j];
-      if (iv & kDone) {
-        id[j] = iv & ~kDone;
-      } else {
-        sc[j] = exact_of(iv);
-      }
-      const unsigned k = float_order_key(sc[j]);
-      emin = min(emin, k);
-      emax = max(emax, k);
-    }
-  } else {
-    for (int j = t; j < n; j += NT) {
-      sc[j] = exact_of(id[j]);
-      const unsigned k = float_order_key(sc[j]);
-      emin = min(emin, k);
-      emax = max(emax, k);
-    }
+    const unsigned k = float_order_key(sc[j]);
+    emin = min(emin, k);
+    emax = max(emax, k);
   }
   group_minmax<NW>(emin, emax, wcnt);
 #if defined(TT_FINAL_STOP) && TT_FINAL_STOP == 4  // timing probe: phases up to here only
