@@ -47,6 +47,8 @@ SORT_AFTER = os.environ.get("TT_SORT_AFTER", "gather")
 # tower's stream the moment its weight gradient exists, instead of after the
 # join (the embedding update stays one call after the backward)
 DENSE_EARLY = os.environ.get("TT_DENSE_EARLY", "1") == "1"
+# fused apply: the per-tower id sorts issued right after the gather
+FUSED_SORT_EARLY = os.environ.get("TT_FUSED_SORT_EARLY", "1") == "1"
 
 
 class TwoTowerModel(AbstractKerasModel):
@@ -178,6 +180,13 @@ class TwoTowerModel(AbstractKerasModel):
                     # starts after it even when only the ids gate it
                     self.optimizer.prepare(self.towers, after=self._ids_ready)
                     self._sort_issued = True
+                if (FUSED_SORT_EARLY and getattr(self, "_in_train_step", False)
+                        and getattr(self, "_on_tower", None) == self._apply_tower):
+                    # fused apply: the per-tower id sorts captured right after the
+                    # gather (their only input), so they overlap the forward
+                    # instead of landing in front of the backward
+                    self.optimizer.prepare_towers(self.towers, ["", TOWER_C_SCOPE])
+                    self._sort_issued = True
             logq = call[1].view(-1) if call is not None else self.candidate_logq(x)
             return self.tower_loss(qi, ci, logq)
 
@@ -239,7 +248,7 @@ class TwoTowerModel(AbstractKerasModel):
             self._on_dx = None
             self._in_train_step = False
         fwd_done = None
-        if fused:
+        if fused and not getattr(self, "_sort_issued", False):
             # one id sort per tower on a side stream, before the backward needs it
             self.optimizer.prepare_towers(self.towers, ["", TOWER_C_SCOPE])
         elif hasattr(self.optimizer, "prepare") and loss.is_cuda and not getattr(self, "_sort_issued", False):
