@@ -977,10 +977,14 @@ extern "C" size_t tt_inbatch_fused_workspace_size(int64_t n, int32_t dim) {
   return cv.used();
 }
 
-extern "C" int tt_inbatch_softmax_xent(const float* q, int64_t ldq, const float* c, int64_t ldc, int64_t n,
-                                       int32_t dim, const float* logq, float* lse, float* row_loss, float* dq,
-                                       float* dc, void* workspace, size_t workspace_bytes, tt_stream_t stream) {
-  clear_error();
+namespace tt {
+namespace {
+// The fused entry's body; prepped: the bf16 copies and bias vectors are
+// already in the workspace (tt_inbatch_prep of q and of c on the same
+// workspace, ordered before this call).
+int softmax_xent(const float* q, int64_t ldq, const float* c, int64_t ldc, int64_t n, int32_t dim, const float* logq,
+                 float* lse, float* row_loss, float* dq, float* dc, void* workspace, size_t workspace_bytes,
+                 tt_stream_t stream, bool prepped) {
   int rc = check_common(q, ldq, n, c, ldc, n, dim);
   if (rc) return rc;
   TT_REQUIRE(lse && row_loss && dq && dc, "tt_inbatch_softmax_xent: NULL output");
@@ -992,7 +996,8 @@ extern "C" int tt_inbatch_softmax_xent(const float* q, int64_t ldq, const float*
                 cv.used());
   hipStream_t st = to_stream(stream);
   // one prep launch for both matrices; c's job also writes both bias vectors
-  if ((rc = prep(p.D, prep_job(q, ldq, n, dim, w.qb), prep_job(c, ldc, n, dim, w.cb, logq, w.bias_logq, w.bias_lse),
+  if (!prepped &&
+      (rc = prep(p.D, prep_job(q, ldq, n, dim, w.qb), prep_job(c, ldc, n, dim, w.cb, logq, w.bias_logq, w.bias_lse),
                  dim, p.n_pad, st)))
     return rc;
   const Plan pl{p.D, p.n_pad, p.n_pad, p.split, p.per_split};
@@ -1004,4 +1009,41 @@ extern "C" int tt_inbatch_softmax_xent(const float* q, int64_t ldq, const float*
   PassArgs ac{w.cb, w.qb, w.bias_lse, p.n_pad, p.n_pad, p.per_split, 0, nullptr, nullptr, w.part_o_cols};
   if ((rc = launch_pass<1>(pl, ac, st))) return rc;
   return combine_cols(p.D, st, w.part_o_cols, p.split, p.n_pad, q, ldq, c, ldc, lse, row_loss, logq, n, dim, 0, dc);
+}
+}  // namespace
+}  // namespace tt
+
+extern "C" int tt_inbatch_softmax_xent(const float* q, int64_t ldq, const float* c, int64_t ldc, int64_t n,
+                                       int32_t dim, const float* logq, float* lse, float* row_loss, float* dq,
+                                       float* dc, void* workspace, size_t workspace_bytes, tt_stream_t stream) {
+  using namespace tt;
+  clear_error();
+  return softmax_xent(q, ldq, c, ldc, n, dim, logq, lse, row_loss, dq, dc, workspace, workspace_bytes, stream, false);
+}
+
+extern "C" int tt_inbatch_softmax_xent_prepped(const float* q, int64_t ldq, const float* c, int64_t ldc, int64_t n,
+                                               int32_t dim, const float* logq, float* lse, float* row_loss,
+                                               float* dq, float* dc, void* workspace, size_t workspace_bytes,
+                                               tt_stream_t stream) {
+  using namespace tt;
+  clear_error();
+  return softmax_xent(q, ldq, c, ldc, n, dim, logq, lse, row_loss, dq, dc, workspace, workspace_bytes, stream, true);
+}
+
+extern "C" int tt_inbatch_prep(const float* x, int64_t ldx, int64_t n, int32_t dim, int32_t operand,
+                               const float* logq, void* workspace, size_t workspace_bytes, tt_stream_t stream) {
+  using namespace tt;
+  clear_error();
+  int rc = check_common(x, ldx, n, x, ldx, n, dim);
+  if (rc) return rc;
+  TT_REQUIRE(operand == 0 || operand == 1, "tt_inbatch_prep: operand %d is not 0 (q) or 1 (c)", operand);
+  const FusedPlan p = fused_plan(n, dim);
+  Carver cv(workspace, workspace_bytes);
+  FusedWs w = carve_fused(cv, p);
+  if (!workspace || cv.used() > workspace_bytes)
+    return fail(TT_ERR_WORKSPACE, "tt_inbatch_prep: workspace %zu < required %zu", workspace_bytes, cv.used());
+  const PrepJob none{};
+  return prep(p.D, operand == 0 ? prep_job(x, ldx, n, dim, w.qb) : prep_job(x, ldx, n, dim, w.cb, logq, w.bias_logq,
+                                                                              w.bias_lse),
+              none, dim, p.n_pad, to_stream(stream));
 }

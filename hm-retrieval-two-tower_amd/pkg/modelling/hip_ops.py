@@ -32,6 +32,8 @@ __all__ = [
     "inbatch_rows",
     "inbatch_cols",
     "inbatch_fused",
+    "inbatch_fused_workspace",
+    "inbatch_prep",
     "probe_arm",
     "probe_arm_repeat",
     "route_requests",
@@ -714,24 +716,46 @@ def inbatch_cols(q: torch.Tensor, lse: torch.Tensor, c: torch.Tensor, logq: Opti
     return dc
 
 
-def inbatch_fused(q: torch.Tensor, c: torch.Tensor, logq: Optional[torch.Tensor]):
+def inbatch_fused_workspace(B: int, E: int, device: torch.device) -> torch.Tensor:
+    """The fused entry's workspace in the current scope (fetch it before
+    forking per-tower streams so inbatch_prep on either stream and the
+    fused call share it)."""
+    return Workspace.get(lib().tt_inbatch_fused_workspace_size(B, E), device, "inbatch_fused")
+
+
+def inbatch_prep(x: torch.Tensor, operand: int, logq: Optional[torch.Tensor], ws: torch.Tensor) -> None:
+    """bf16 preparation of one operand of inbatch_fused into `ws` on the
+    current stream: operand 0 = q, 1 = c (+ the logQ bias vectors)."""
+    _req(x, "x", torch.float32, 2)
+    ld = _row_major(x, "x")
+    B, E = x.shape
+    check(lib().tt_inbatch_prep(x.data_ptr(), ld, B, E, int(operand), _opt_ptr(logq, "logq", B) if operand else None,
+                                ws.data_ptr(), ws.numel(), _stream()))
+
+
+def inbatch_fused(q: torch.Tensor, c: torch.Tensor, logq: Optional[torch.Tensor], ws: Optional[torch.Tensor] = None,
+                  prepped: bool = False):
     """Single-device loss + gradients (both passes, shared bf16 prep):
-    (lse [B], row_loss [B], dq [B,E], dc [B,E])."""
+    (lse [B], row_loss [B], dq [B,E], dc [B,E]).  prepped: both operands were
+    already prepared into `ws` by inbatch_prep (ordered before this call)."""
     _req(q, "q", torch.float32, 2)
     _req(c, "c", torch.float32, 2)
     ldq, ldc = _row_major(q, "q"), _row_major(c, "c")
     B, E = q.shape
     if tuple(c.shape) != (B, E):
         raise ValueError("q and c must both be [B, E]")
+    if prepped and ws is None:
+        raise ValueError("prepped=True needs the workspace the operands were prepared into")
     L = lib()
-    ws = Workspace.get(L.tt_inbatch_fused_workspace_size(B, E), q.device, "inbatch_fused")
+    if ws is None:
+        ws = inbatch_fused_workspace(B, E, q.device)
     lse = torch.empty(B, dtype=torch.float32, device=q.device)
     row_loss = torch.empty(B, dtype=torch.float32, device=q.device)
     dq = torch.empty(B, E, dtype=torch.float32, device=q.device)
     dc = torch.empty(B, E, dtype=torch.float32, device=q.device)
-    check(L.tt_inbatch_softmax_xent(q.data_ptr(), ldq, c.data_ptr(), ldc, B, E, _opt_ptr(logq, "logq", B),
-                                    lse.data_ptr(), row_loss.data_ptr(), dq.data_ptr(), dc.data_ptr(), ws.data_ptr(),
-                                    ws.numel(), _stream()))
+    fn = L.tt_inbatch_softmax_xent_prepped if prepped else L.tt_inbatch_softmax_xent
+    check(fn(q.data_ptr(), ldq, c.data_ptr(), ldc, B, E, _opt_ptr(logq, "logq", B), lse.data_ptr(), row_loss.data_ptr(),
+             dq.data_ptr(), dc.data_ptr(), ws.data_ptr(), ws.numel(), _stream()))
     return lse, row_loss, dq, dc
 
 

@@ -59,6 +59,9 @@ def _tower_stream(device: torch.device) -> torch.cuda.Stream:
 GLOBAL_TOWER_STREAMS = int(os.environ.get("TT_GLOBAL_TOWER_STREAMS", "4096"))
 # The single-GPU step's towers on two streams (TT_TOWER_STREAMS=0: one).
 TOWER_STREAMS = int(os.environ.get("TT_TOWER_STREAMS", "1"))
+# Each tower's bf16 loss operand prepared on that tower's stream
+# (tt_inbatch_prep) instead of one prep of both after the join.
+SPLIT_PREP = os.environ.get("TT_SPLIT_PREP", "0") == "1"
 # Both towers' layers as paired launches on one stream (tower.forward_acts_pair).
 TOWER_PAIR = int(os.environ.get("TT_TOWER_PAIR", "0"))
 
@@ -142,16 +145,23 @@ class _TowersInBatchXent(torch.autograd.Function):
             return _TowersInBatchXent._finish(ctx, qa, ca, flat_q, flat_c, logq, stack_q, stack_c, scale, on_tower)
         main = torch.cuda.current_stream()
         side = _tower_stream(qi.device) if TOWER_STREAMS else main
+        # SPLIT_PREP: each tower's bf16 copy for the loss is made on its own
+        # stream right after its MLP (the workspace is fetched before the fork)
+        ws = hip_ops.inbatch_fused_workspace(qi.shape[0], stack_q.out_dim, qi.device) if SPLIT_PREP else None
         side.wait_stream(main)
         with torch.cuda.stream(side), hip_ops.Workspace.scope(TOWER_C_SCOPE):
             ca = stack_c.forward_acts(ci, flat_c)
+            if ws is not None:
+                hip_ops.inbatch_prep(ca[-1], 1, logq, ws)
         qa = stack_q.forward_acts(qi, flat_q)
+        if ws is not None:
+            hip_ops.inbatch_prep(qa[-1], 0, None, ws)
         main.wait_stream(side)
-        return _TowersInBatchXent._finish(ctx, qa, ca, flat_q, flat_c, logq, stack_q, stack_c, scale, on_tower)
+        return _TowersInBatchXent._finish(ctx, qa, ca, flat_q, flat_c, logq, stack_q, stack_c, scale, on_tower, ws)
 
     @staticmethod
-    def _finish(ctx, qa, ca, flat_q, flat_c, logq, stack_q, stack_c, scale, on_tower):
-        _, row_loss, dq, dc = hip_ops.inbatch_fused(qa[-1], ca[-1], logq)
+    def _finish(ctx, qa, ca, flat_q, flat_c, logq, stack_q, stack_c, scale, on_tower, ws=None):
+        _, row_loss, dq, dc = hip_ops.inbatch_fused(qa[-1], ca[-1], logq, ws=ws, prepped=ws is not None)
         ctx.stacks = (stack_q, stack_c)
         ctx.nq = len(qa)
         ctx.scale = scale

@@ -409,6 +409,25 @@ int tt_inbatch_softmax_xent(const float* q, int64_t ldq, const float* c,
                             float* dq, float* dc, void* workspace,
                             size_t workspace_bytes, tt_stream_t stream);
 
+/* The same entry split at its preparation, so each tower's bf16 copy can be
+ * made on the stream that produced that tower's output (the two towers that
+ * TwoTowerModel.train_step runs, pkg/modelling/models/two_tower_model.py:
+ * 111, finish on separate streams): tt_inbatch_prep with operand 0
+ * prepares q, with operand 1 prepares c and the logQ bias vectors (logq may
+ * be NULL, as above); both must be ordered before
+ * tt_inbatch_softmax_xent_prepped on the same workspace, which then runs the
+ * passes only.  Results are bit-identical to tt_inbatch_softmax_xent. */
+int tt_inbatch_prep(const float* x, int64_t ldx, int64_t n, int32_t dim,
+                    int32_t operand, const float* logq, void* workspace,
+                    size_t workspace_bytes, tt_stream_t stream);
+int tt_inbatch_softmax_xent_prepped(const float* q, int64_t ldq,
+                                    const float* c, int64_t ldc, int64_t n,
+                                    int32_t dim, const float* logq,
+                                    float* lse, float* row_loss, float* dq,
+                                    float* dc, void* workspace,
+                                    size_t workspace_bytes,
+                                    tt_stream_t stream);
+
 /* ------------------------------------------------------------------------ *
  * K11+K12  Brute-force scoring with fused top-K.
  * Replaces BruteForceIndex.call (pkg/modelling/indices/brute_force.py:76-81):

@@ -276,6 +276,34 @@ def test_inbatch_fused_entry(cuda, B, E, use_logq, scale):
     assert _rel(dc.cpu().numpy(), ref["dc"]) <= 1e-2
 
 
+@pytest.mark.parametrize("B,E,use_logq", [(4100, 64, True), (37, 32, True), (1100, 128, False), (1, 16, True)])
+def test_inbatch_split_prep_bit_identical(cuda, B, E, use_logq):
+    """tt_inbatch_prep of c and of q (on two streams, joined) followed by
+    tt_inbatch_softmax_xent_prepped gives the one-call entry's lse, row loss,
+    dq and dc bit for bit; a bad operand selector is an error."""
+    from pkg._native import TTError
+
+    rng = np.random.default_rng(B + E)
+    q = _t(np.maximum(rng.standard_normal((B, E)) * 0.5, 0).astype(np.float32), cuda)
+    c = _t(np.maximum(rng.standard_normal((B, E)) * 0.5, 0).astype(np.float32), cuda)
+    logq = _t(np.log(rng.uniform(1e-6, 1e-2, B)).astype(np.float32), cuda) if use_logq else None
+    want = hip_ops.inbatch_fused(q, c, logq)
+    ws = torch.zeros(hip_ops.lib().tt_inbatch_fused_workspace_size(B, E), dtype=torch.uint8, device=cuda)
+    main, side = torch.cuda.current_stream(), torch.cuda.Stream(device=cuda)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        hip_ops.inbatch_prep(c, 1, logq, ws)
+    hip_ops.inbatch_prep(q, 0, None, ws)
+    main.wait_stream(side)
+    got = hip_ops.inbatch_fused(q, c, logq, ws=ws, prepped=True)
+    for w, g in zip(want, got):
+        assert torch.equal(w, g)
+    with pytest.raises(TTError, match="operand"):
+        hip_ops.inbatch_prep(q, 2, None, ws)
+    with pytest.raises(TTError, match="workspace"):
+        hip_ops.inbatch_prep(q, 0, None, ws[:16])
+
+
 def test_inbatch_row_blocks_with_offset(cuda):
     """Rows of rank r scored against all-gathered columns (global negatives)."""
     rng = np.random.default_rng(7)

@@ -309,6 +309,30 @@ def test_paired_tower_launches_bit_identical(cuda, monkeypatch, fused):
     b.optimizer.check_status(cuda)
 
 
+@pytest.mark.parametrize("fused", [False, True])
+def test_split_prep_bit_identical(cuda, monkeypatch, fused):
+    """TT_SPLIT_PREP (each tower's bf16 loss operand prepared on its own
+    stream, then tt_inbatch_softmax_xent_prepped) gives bit-identical losses,
+    tables, accumulators and MLP buffers to the one-call loss entry, unfused
+    and with the fused optimizer apply, at ragged batch sizes."""
+    from pkg.modelling import losses
+
+    a, b = _small_model(cuda, seed=23, fused=fused), _small_model(cuda, seed=23, fused=fused)
+    rng = np.random.default_rng(8)
+    for i, B in enumerate((512, 37, 256, 1)):
+        x = _batch(cuda, rng, B, True)
+        monkeypatch.setattr(losses, "SPLIT_PREP", False)
+        la = a.train_step(x)["loss"]
+        monkeypatch.setattr(losses, "SPLIT_PREP", True)
+        lb = b.train_step(x)["loss"]
+        assert torch.equal(la, lb), (i, B)
+        sa, sb = _state(a), _state(b)
+        for k in sa:
+            assert torch.equal(sa[k], sb[k]), (i, B, k)
+    a.optimizer.check_status(cuda)
+    b.optimizer.check_status(cuda)
+
+
 def test_stale_presorted_workspace_is_reported_not_applied(cuda):
     """A presorted sparse apply whose workspace holds another call's sorted
     keys applies nothing and is reported by tt_sparse_status (TTError), the
