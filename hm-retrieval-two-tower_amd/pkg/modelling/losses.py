@@ -59,6 +59,9 @@ def _tower_stream(device: torch.device) -> torch.cuda.Stream:
 GLOBAL_TOWER_STREAMS = int(os.environ.get("TT_GLOBAL_TOWER_STREAMS", "4096"))
 # The single-GPU step's towers on two streams (TT_TOWER_STREAMS=0: one).
 TOWER_STREAMS = int(os.environ.get("TT_TOWER_STREAMS", "1"))
+# The global-negatives loss at one rank through the single-device entry
+# (TT_WORLD1_FUSED=0: the rows and columns entries, as at G > 1).
+WORLD1_FUSED = os.environ.get("TT_WORLD1_FUSED", "1") == "1"
 # Each tower's bf16 loss operand prepared on that tower's stream
 # (tt_inbatch_prep) instead of one prep of both after the join.
 SPLIT_PREP = os.environ.get("TT_SPLIT_PREP", "0") == "1"
@@ -209,6 +212,11 @@ def global_inbatch_grads(q: torch.Tensor, c: torch.Tensor, logq: Optional[torch.
     all candidates; the cols pass scores all queries (with their lse) against
     the local candidates, so every gradient is summed inside one kernel in a
     fixed order (no cross-rank reduction of partial sums)."""
+    if WORLD1_FUSED and comm.world == 1 and rows is None and cols is None and not getattr(comm, "always", False):
+        # one rank: its rows are every row and its columns every column — the
+        # single-device entry (one shared preparation of q and c for both passes)
+        _, row_loss, dq, dc = hip_ops.inbatch_fused(q, c, logq)
+        return row_loss, dq, dc
     rows = rows or hip_ops.inbatch_rows
     cols = cols or hip_ops.inbatch_cols
     b = q.shape[0]
