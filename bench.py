@@ -694,21 +694,41 @@ def time_c5_sharded(device, ws: int, rank: int, steps: int = 20, rows: int = 100
 
             rows_out = torch.empty(b, D, device=device)
             side = torch.cuda.Stream(device=device)
+            # world 1: route and fetch on one stream ("serial", default; 0.128
+            # vs 0.141 ms with the route forked beside the fetch, 0.152 with
+            # the fetch captured first: the replay ran the branches one after
+            # the other anyway, plus the join — tools/runs/gpu_s05_c5_ab.sh)
+            c5_order = os.environ.get("TT_C5_ORDER", "serial")
 
             def body():
                 if ws == 1:
                     # one rank: the shard IS the owner's answer — the fetch is a
-                    # read by id (tt_gather_grouped), and the route (which then
-                    # only feeds the apply) runs beside it on a second stream,
-                    # joined from the origin stream (as ShardedTrainStep)
+                    # read by id (tt_gather_grouped); the route then only feeds
+                    # the apply
+                    # (C5_ORDER "fork": the route on a side stream beside the
+                    # fetch; "first": the same with the fetch captured first)
                     main = torch.cuda.current_stream()
-                    side.wait_stream(main)
-                    with torch.cuda.stream(side):
+                    if c5_order == "direct":  # probe: no route, the single-device sparse apply
+                        hip_ops.gather_grouped([(st.shard["big"], sid, 0)], b, rows_out)
+                        hip_ops.sparse_adagrad([dict(table=st.shard["big"], slot0=st.acc["big"], ids=[sid],
+                                                     grad_col_offset=[0])], b, grad, 0.05, 1e-7)
+                        return
+                    if c5_order == "serial":
                         rt = st.route_fixed([("big", sid)], cap)
-                    hip_ops.gather_grouped([(st.shard["big"], sid, 0)], b, rows_out)
-                    main.wait_stream(side)
-                    for t in (rt.tags, rt.rows, rt.counts, rt.idx_all, *rt.table_ids, *(rt.order or ())):
-                        t.record_stream(main)
+                        hip_ops.gather_grouped([(st.shard["big"], sid, 0)], b, rows_out)
+                    else:
+                        fork = torch.cuda.Event()
+                        fork.record(main)
+                        if c5_order == "first":
+                            hip_ops.gather_grouped([(st.shard["big"], sid, 0)], b, rows_out)
+                        side.wait_event(fork)
+                        with torch.cuda.stream(side):
+                            rt = st.route_fixed([("big", sid)], cap)
+                        if c5_order != "first":
+                            hip_ops.gather_grouped([(st.shard["big"], sid, 0)], b, rows_out)
+                        main.wait_stream(side)
+                        for t in (rt.tags, rt.rows, rt.counts, rt.idx_all, *rt.table_ids, *(rt.order or ())):
+                            t.record_stream(main)
                 else:
                     rt = st.route_fixed([("big", sid)], cap)
                     st.fetch_routed(rt)

@@ -72,6 +72,22 @@ __global__ void __launch_bounds__(256) route_keys_kernel(const RouteArgs a) {
   a.vals_in[i] = static_cast<uint32_t>(i);
 }
 
+// World-1 fixed slots written by the head / write passes themselves (no
+// route_pad launch): the one owner's requests start at slot 0, so request u
+// IS slot u (u < cap; the rest are dropped and counted).  The heads pass
+// fills every slot with (-1, -1) and the owner view with -1; the write pass
+// then overwrites the requests' slots.  send == NULL: not this mode.
+struct World1Slots {
+  int64_t cap;
+  int32_t* send;      // [cap, 2]
+  int32_t* idx;       // [total]: each lookup's slot
+  int32_t* overflow;  // optional
+  int32_t* tags;      // [cap]
+  int32_t* rows;      // [cap]
+  int32_t* tids;      // [num_tags, cap]
+  int32_t num_tags;
+};
+
 // Heads of the sorted key runs = distinct requests.  Pass 1: per block of
 // kScanThreads consecutive sorted keys (one per thread, coalesced), the
 // number of heads.  Pass 2: each block adds up the counts of the blocks
@@ -82,7 +98,7 @@ template <typename KeyT>
 __global__ void __launch_bounds__(kScanThreads) route_heads_kernel(const KeyT* keys, int64_t total,
                                                                    int32_t* block_heads, long long* counts,
                                                                    int32_t world, int32_t* grp_first, int32_t* grp_last,
-                                                                   int32_t groups) {
+                                                                   int32_t groups, const World1Slots w1) {
   // the per-owner counts route_write_kernel adds into are zeroed here, by a
   // kernel, not by a captured hipMemsetAsync: with the memset node (and the
   // counts' block recycled inside the step's graph) the overflow word picked
@@ -96,6 +112,17 @@ __global__ void __launch_bounds__(kScanThreads) route_heads_kernel(const KeyT* k
     for (int g = threadIdx.x; g < groups; g += kScanThreads) {
       grp_first[g] = 0;
       grp_last[g] = -1;
+    }
+  if (w1.send)  // world-1 slots: every slot empty until the write pass fills the requests'
+    for (int64_t t = static_cast<int64_t>(blockIdx.x) * kScanThreads + threadIdx.x; t < w1.cap;
+         t += static_cast<int64_t>(gridDim.x) * kScanThreads) {
+      w1.send[2 * t] = -1;
+      w1.send[2 * t + 1] = -1;
+      if (w1.tags) {
+        w1.tags[t] = -1;
+        w1.rows[t] = -1;
+        for (int q = 0; q < w1.num_tags; ++q) w1.tids[static_cast<int64_t>(q) * w1.cap + t] = -1;
+      }
     }
   __shared__ int wsum[kScanThreads / kWave];
   const int64_t i = static_cast<int64_t>(blockIdx.x) * kScanThreads + threadIdx.x;
@@ -116,7 +143,8 @@ __global__ void __launch_bounds__(kScanThreads) route_write_kernel(const KeyT* k
                                                                    int32_t id_bits, const int32_t* block_heads,
                                                                    int32_t* send, int32_t* idx, long long* counts,
                                                                    int32_t* num_requests, int32_t* order,
-                                                                   int32_t* grp_first, int32_t* grp_last) {
+                                                                   int32_t* grp_first, int32_t* grp_last,
+                                                                   const World1Slots w1) {
   __shared__ int wsum[kScanThreads / kWave + 1];
   __shared__ int cnt[kMaxWorld];
   __shared__ int base_s;
@@ -152,11 +180,26 @@ __global__ void __launch_bounds__(kScanThreads) route_write_kernel(const KeyT* k
     if (head) {
       const KeyT mask = (KeyT(1) << id_bits) - KeyT(1);
       const KeyT ot = k >> id_bits;
-      send[2 * static_cast<int64_t>(u)] = static_cast<int32_t>(static_cast<long long>(k & mask) - 1);
-      send[2 * static_cast<int64_t>(u) + 1] = static_cast<int32_t>(ot % num_tags);
+      const int32_t row = static_cast<int32_t>(static_cast<long long>(k & mask) - 1);
+      const int32_t tag = static_cast<int32_t>(ot % num_tags);
+      if (w1.send) {
+        if (u < w1.cap) {
+          w1.send[2 * static_cast<int64_t>(u)] = row;
+          w1.send[2 * static_cast<int64_t>(u) + 1] = tag;
+          if (w1.tags) {
+            w1.tags[u] = tag;
+            w1.rows[u] = row;
+            w1.tids[static_cast<int64_t>(tag) * w1.cap + u] = row;
+          }
+        }
+      } else {
+        send[2 * static_cast<int64_t>(u)] = row;
+        send[2 * static_cast<int64_t>(u) + 1] = tag;
+      }
       atomicAdd(&cnt[static_cast<int>(ot / num_tags)], 1);
     }
-    idx[vals[i]] = u;
+    if (w1.send) w1.idx[vals[i]] = static_cast<int32_t>(u < w1.cap ? u : w1.cap - 1);
+    else idx[vals[i]] = u;
     if (order) order[i] = static_cast<int32_t>(vals[i]);
     if (grp_first) {  // first / last sorted position of each (owner, tag) group
       const KeyT g = k >> id_bits;
@@ -167,7 +210,11 @@ __global__ void __launch_bounds__(kScanThreads) route_write_kernel(const KeyT* k
   __syncthreads();
   for (int o = threadIdx.x; o < world; o += kScanThreads)
     if (cnt[o]) atomicAdd(reinterpret_cast<unsigned long long*>(counts + o), static_cast<unsigned long long>(cnt[o]));
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *num_requests = base_s + wsum[kScanThreads / kWave];
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+    const int n = base_s + wsum[kScanThreads / kWave];
+    *num_requests = n;
+    if (w1.send && w1.overflow && n > w1.cap) atomicAdd(w1.overflow, static_cast<int32_t>(n - w1.cap));
+  }
 }
 
 __global__ void __launch_bounds__(256) route_owner_kernel(const int32_t* recv, int64_t n, int32_t world,
@@ -527,6 +574,24 @@ __global__ void __launch_bounds__(kRsThreads) route_fixed_small_kernel(const Rou
   TT_RS_STAMP(4)
 }
 
+// The route's sort configuration: rocPRIM's defaults, or (TT_ROUTE_SORT_BS >
+// 0) a merge-sort path whose block sort covers TT_ROUTE_SORT_BS x
+// TT_ROUTE_SORT_IPT keys (fewer merge launches).
+#ifndef TT_ROUTE_SORT_BS
+#define TT_ROUTE_SORT_BS 0
+#endif
+#ifndef TT_ROUTE_SORT_IPT
+#define TT_ROUTE_SORT_IPT 4
+#endif
+#if TT_ROUTE_SORT_BS > 0
+using RouteSortConfig =
+    rocprim::radix_sort_config<rocprim::default_config,
+                               rocprim::merge_sort_config<TT_ROUTE_SORT_BS, TT_ROUTE_SORT_BS, TT_ROUTE_SORT_IPT>,
+                               rocprim::default_config, TT_SORT_MERGE_LIMIT>;
+#else
+using RouteSortConfig = SortConfig;
+#endif
+
 // The route's device sort: rocPRIM's merge path below TT_SORT_MERGE_LIMIT
 // (block sort + ~6 merge launches at 65,536 keys).  Its onesweep radix path
 // (histogram + one launch per 8-bit digit) measured slower at C5: 0.19 vs
@@ -537,11 +602,11 @@ size_t route_sort_bytes(int64_t total, int end_bit) {
   hipError_t e;
   if (end_bit <= 32) {
     uint32_t* kp = nullptr;
-    e = rocprim::radix_sort_pairs<SortConfig>(nullptr, a, kp, kp, vp, vp, static_cast<unsigned>(total), 0, end_bit,
+    e = rocprim::radix_sort_pairs<RouteSortConfig>(nullptr, a, kp, kp, vp, vp, static_cast<unsigned>(total), 0, end_bit,
                                               nullptr, false);
   } else {
     unsigned long long* kp = nullptr;
-    e = rocprim::radix_sort_pairs<SortConfig>(nullptr, a, kp, kp, vp, vp, static_cast<unsigned>(total), 0, end_bit,
+    e = rocprim::radix_sort_pairs<RouteSortConfig>(nullptr, a, kp, kp, vp, vp, static_cast<unsigned>(total), 0, end_bit,
                                               nullptr, false);
   }
   return e == hipSuccess ? a : static_cast<size_t>(total) * 24 + (size_t(4) << 20);
@@ -617,12 +682,12 @@ extern "C" size_t tt_route_workspace_size(int32_t num_lookups, int64_t batch, in
   return cv.used();
 }
 
-extern "C" int tt_route_requests_ordered(const tt_route_lookup* lookups, int32_t num_lookups, int64_t batch,
-                                         int32_t world, int32_t num_tags, int32_t* send, long long* counts,
-                                         int32_t* num_requests, int32_t* idx, int32_t* order, int32_t* grp_first,
-                                         int32_t* grp_last, void* workspace, size_t workspace_bytes,
-                                         tt_stream_t stream) {
-  clear_error();
+namespace tt {
+namespace {
+int route_requests(const tt_route_lookup* lookups, int32_t num_lookups, int64_t batch, int32_t world,
+                   int32_t num_tags, int32_t* send, long long* counts, int32_t* num_requests, int32_t* idx,
+                   int32_t* order, int32_t* grp_first, int32_t* grp_last, void* workspace, size_t workspace_bytes,
+                   tt_stream_t stream, const World1Slots& w1) {
   TT_REQUIRE(lookups && send && counts && num_requests && idx, "tt_route_requests: NULL pointer");
   TT_REQUIRE((grp_first == nullptr) == (grp_last == nullptr), "tt_route_requests: grp_first / grp_last: both or neither");
   for (int l = 0; l < num_lookups && l < kMaxRouteLookups; ++l)
@@ -653,19 +718,31 @@ extern "C" int tt_route_requests_ordered(const tt_route_lookup* lookups, int32_t
                        a);
     TT_CHECK_LAUNCH();
     size_t sb = p.sort_bytes;
-    TT_CHECK_HIP(rocprim::radix_sort_pairs<SortConfig>(w.sort_tmp, sb, kin, kout, w.vals_in, w.vals,
+    TT_CHECK_HIP(rocprim::radix_sort_pairs<RouteSortConfig>(w.sort_tmp, sb, kin, kout, w.vals_in, w.vals,
                                                        static_cast<unsigned>(p.total), 0, p.end_bit, st, false));
     const unsigned nb = static_cast<unsigned>(ceil_div(p.total, kScanThreads));
     hipLaunchKernelGGL(route_heads_kernel<KeyT>, dim3(nb), dim3(kScanThreads), 0, st, kout, p.total, w.block_heads,
-                       counts, world, grp_first, grp_last, world * num_tags);
+                       counts, world, grp_first, grp_last, world * num_tags, w1);
     TT_CHECK_LAUNCH();
     hipLaunchKernelGGL(route_write_kernel<KeyT>, dim3(nb), dim3(kScanThreads), 0, st, kout, w.vals, p.total, world,
                        num_tags, p.id_bits, w.block_heads, send, idx, counts, num_requests, order, grp_first,
-                       grp_last);
+                       grp_last, w1);
     TT_CHECK_LAUNCH();
     return TT_OK;
   };
   return p.end_bit <= 32 ? run(uint32_t{}) : run(static_cast<unsigned long long>(0));
+}
+}  // namespace
+}  // namespace tt
+
+extern "C" int tt_route_requests_ordered(const tt_route_lookup* lookups, int32_t num_lookups, int64_t batch,
+                                         int32_t world, int32_t num_tags, int32_t* send, long long* counts,
+                                         int32_t* num_requests, int32_t* idx, int32_t* order, int32_t* grp_first,
+                                         int32_t* grp_last, void* workspace, size_t workspace_bytes,
+                                         tt_stream_t stream) {
+  clear_error();
+  return route_requests(lookups, num_lookups, batch, world, num_tags, send, counts, num_requests, idx, order,
+                        grp_first, grp_last, workspace, workspace_bytes, stream, World1Slots{});
 }
 
 extern "C" int tt_route_requests(const tt_route_lookup* lookups, int32_t num_lookups, int64_t batch, int32_t world,
@@ -721,6 +798,13 @@ FixedWs carve_fixed(Carver& cv, const RoutePlan& p) {
   f.idx = cv.take<int32_t>(p.total);
   f.nreq = cv.take<int32_t>(1);
   return f;
+}
+bool route_w1_slots() {  // TT_ROUTE_W1_SLOTS=0: world 1 through route_pad as well (A/B)
+  static const bool off = [] {
+    const char* e = std::getenv("TT_ROUTE_W1_SLOTS");
+    return e && e[0] == '0';
+  }();
+  return !off;
 }
 bool route_fused(const RoutePlan& p) {
   static const bool off = [] {
@@ -793,8 +877,14 @@ extern "C" int tt_route_fixed(const tt_route_lookup* lookups, int32_t num_lookup
   if (!workspace || cv.used() > workspace_bytes)
     return fail(TT_ERR_WORKSPACE, "tt_route_fixed: workspace %zu < required %zu", workspace_bytes, cv.used());
   const size_t rbytes = static_cast<size_t>(reinterpret_cast<char*>(f.send) - static_cast<char*>(workspace));
-  rc = tt_route_requests_ordered(lookups, num_lookups, batch, world, num_tags, f.send, counts, f.nreq, f.idx, order,
-                                 grp_first, grp_last, workspace, rbytes, stream);
+  if (world == 1 && route_w1_slots()) {
+    // one owner: the head / write passes lay the slots out themselves
+    const World1Slots w1{cap, send_padded, idx_padded, overflow, owner_tags, owner_rows, owner_table_ids, num_tags};
+    return route_requests(lookups, num_lookups, batch, world, num_tags, f.send, counts, f.nreq, f.idx, order,
+                          grp_first, grp_last, workspace, rbytes, stream, w1);
+  }
+  rc = route_requests(lookups, num_lookups, batch, world, num_tags, f.send, counts, f.nreq, f.idx, order, grp_first,
+                      grp_last, workspace, rbytes, stream, World1Slots{});
   if (rc) return rc;
   // tt_route_pad, with the world-1 owner view written by the same pass
   const int64_t n = std::max<int64_t>(static_cast<int64_t>(world) * cap, p.total);
