@@ -651,9 +651,10 @@ def time_c5_sharded(device, ws: int, rank: int, steps: int = 20, rows: int = 100
     per-owner slots; all_to_all of the requests), fetch (tt_gather_tagged on
     the owners + all_to_all of the rows), apply (per-request sums on the
     route's own sort, tt_sparse_routed + all_to_all of the sums +
-    tt_sparse_adagrad on the owners).  At one rank the exchanges are
-    identities: the fetch is the shard read by id with the route beside it on
-    a second stream, and the per-request sums are the Adagrad update itself.  Algorithmic HBM bytes per rank and
+    tt_sparse_adagrad on the owners).  At one rank there is nothing to
+    exchange or route: the one owner reads the rows by id and applies the
+    update keyed by the ids (ShardedTables.fetch_local / apply_local: one
+    gather, the single-device dedup + Adagrad).  Algorithmic HBM bytes per rank and
     step: lookups x (4 B id + 2 x 4D row read/write + 4D gradient read) +
     owner rows x 16D (param and accumulator read + write).  The all_to_all
     share is the three data all_to_alls of the same sizes timed alone.  At
@@ -694,11 +695,12 @@ def time_c5_sharded(device, ws: int, rank: int, steps: int = 20, rows: int = 100
 
             rows_out = torch.empty(b, D, device=device)
             side = torch.cuda.Stream(device=device)
-            # world 1: route and fetch on one stream ("serial", default; 0.128
-            # vs 0.141 ms with the route forked beside the fetch, 0.152 with
-            # the fetch captured first: the replay ran the branches one after
-            # the other anyway, plus the join — tools/runs/gpu_s05_c5_ab.sh)
-            c5_order = os.environ.get("TT_C5_ORDER", "serial")
+            # world 1 ("local", default): the one owner fetches and applies by
+            # id (ShardedTables.fetch_local / apply_local: 0.111 vs 0.125 ms for
+            # the routed form on one stream, "serial"; 0.141 with the route
+            # forked beside the fetch, "fork", 0.152 with the fetch captured
+            # first, "first" — profiles/r05_c5_ab.txt)
+            c5_order = os.environ.get("TT_C5_ORDER", "local")
 
             def body():
                 if ws == 1:
@@ -708,10 +710,9 @@ def time_c5_sharded(device, ws: int, rank: int, steps: int = 20, rows: int = 100
                     # (C5_ORDER "fork": the route on a side stream beside the
                     # fetch; "first": the same with the fetch captured first)
                     main = torch.cuda.current_stream()
-                    if c5_order == "direct":  # probe: no route, the single-device sparse apply
-                        hip_ops.gather_grouped([(st.shard["big"], sid, 0)], b, rows_out)
-                        hip_ops.sparse_adagrad([dict(table=st.shard["big"], slot0=st.acc["big"], ids=[sid],
-                                                     grad_col_offset=[0])], b, grad, 0.05, 1e-7)
+                    if c5_order == "local":  # the one owner: fetch and apply by id, no route
+                        st.fetch_local([("big", sid)], rows_out.view(1, b, D))
+                        st.apply_local([("big", sid)], [(grad, 0)], 0.05, 1e-7)
                         return
                     if c5_order == "serial":
                         rt = st.route_fixed([("big", sid)], cap)
@@ -790,7 +791,7 @@ def time_c5_sharded(device, ws: int, rank: int, steps: int = 20, rows: int = 100
                "scaling": "strong (the global batch of 65,536 ids split over the ranks)",
                "graphed": graphed, **leg(global_batch // ws),
                "note": "route + fetch + apply per step as one hipGraph replay (fixed-capacity routing, no host "
-                       "sync); uniform ids over the whole table"}
+                       "sync; at one rank fetch + apply by id, nothing to route); uniform ids over the whole table"}
         if ws > 1:
             res["weak_per_rank"] = {"scaling": "weak (65,536 ids per rank; labelled extra)", **leg(global_batch)}
         del st

@@ -910,17 +910,21 @@ __global__ void tau_min_kernel(const float* __restrict__ tau_split, int S, int64
 // Exact score: k-ordered fmaf chain over the fp32 rows (dim real columns).
 // qs is the query row in LDS (broadcast reads); the candidate row is loaded in
 // batches (16 x float4 or 16 scalars in flight) ahead of the dependent chain.
+#ifndef TT_EXACT_CHUNK
+#define TT_EXACT_CHUNK 8  // float4 loads in flight per row chunk
+#endif
 __device__ __forceinline__ float exact_score(const float* __restrict__ qs, const float* __restrict__ c, int dim,
                                              bool vec4) {
   float acc = 0.0f;
   if (vec4) {  // c 16-byte aligned, dim % 4 == 0
-    for (int e0 = 0; e0 < dim; e0 += 64) {
-      f32x4 v[16];
+    constexpr int NC = TT_EXACT_CHUNK;
+    for (int e0 = 0; e0 < dim; e0 += 4 * NC) {
+      f32x4 v[NC];
 #pragma unroll
-      for (int i = 0; i < 16; ++i)
+      for (int i = 0; i < NC; ++i)
         if (e0 + 4 * i < dim) v[i] = *reinterpret_cast<const f32x4*>(c + e0 + 4 * i);
 #pragma unroll
-      for (int i = 0; i < 16; ++i)
+      for (int i = 0; i < NC; ++i)
         if (e0 + 4 * i < dim) {
 #pragma unroll
           for (int u = 0; u < 4; ++u) acc = __builtin_fmaf(qs[e0 + 4 * i + u], v[i][u], acc);
@@ -1336,8 +1340,15 @@ __host__ __device__ inline size_t final_lds_bytes(int L, int P, int NW = 1) {
 // phase's loops over the waves (large k: long lists, many survivors, a
 // P-element sort), so a query's latency chain shrinks while its list stays
 // in LDS.
+#ifndef TT_FINAL_WPE
+#define TT_FINAL_WPE 0  // > 0: the finalize compiled for at least that many waves per SIMD
+#endif
 template <int NW>
-__global__ void __launch_bounds__(NW * kWave) finalize_kernel(const FinalArgs a) {
+__global__ void __launch_bounds__(NW * kWave)
+#if TT_FINAL_WPE > 0
+    __attribute__((amdgpu_waves_per_eu(TT_FINAL_WPE)))
+#endif
+    finalize_kernel(const FinalArgs a) {
   constexpr int NT = NW * kWave;
   extern __shared__ __attribute__((aligned(16))) char fsm[];
   float* qs = reinterpret_cast<float*>(fsm);  // query row (dim <= 128)

@@ -699,6 +699,45 @@ class ShardedTables:
         self._ctx = rt
         return self.fetch_routed(rt), rt.idx
 
+    # -- one rank: nothing to exchange --------------------------------------
+    def fetch_local(self, lookups: List[Tuple[str, torch.Tensor]], out: torch.Tensor) -> torch.Tensor:
+        """World 1 (this rank owns every row): the rows of each lookup (table
+        name, ids [B]) read from the shard by id, lookup l into out[l] ([L, B,
+        dim]) — one gather launch, no route.  The rows route_fixed +
+        fetch_routed would return, per lookup."""
+        if self.world != 1:
+            raise ValueError("fetch_local: one rank only (world %d)" % self.world)
+        B = lookups[0][1].numel()
+        self.ops.gather_multi([([(self.shard[name], ids.reshape(-1), 0)], out[l])
+                               for l, (name, ids) in enumerate(lookups)], B)
+        return out
+
+    def apply_local(self, lookups: List[Tuple[str, torch.Tensor]], grads: List[Tuple[torch.Tensor, int]],
+                    lr: float, eps: float) -> None:
+        """World 1: Adagrad on the shards from per-lookup gradients (grads[l]
+        = (gradient matrix [B, width], column) of lookup l) keyed by the ids
+        themselves — the single-device dedup + update (one sort, the block
+        sums, the update), with no route: the same update route_fixed +
+        apply_lookups makes at one rank (their world-1 form IS this
+        tt_sparse_adagrad on the same keys, bit for bit while every id is in
+        range; an out-of-range id sorts first in the route and last here,
+        which regroups the block sums within fp32 rounding —
+        tests/test_configs_gpu.py)."""
+        if self.world != 1:
+            raise ValueError("apply_local: one rank only (world %d)" % self.world)
+        if len(grads) != len(lookups):
+            raise ValueError(f"apply_local: {len(grads)} gradients for {len(lookups)} lookups")
+        B = lookups[0][1].numel()
+        specs: Dict[str, dict] = {}
+        for (name, ids), (gmat, col) in zip(lookups, grads):
+            sp = specs.setdefault(name, dict(table=self.shard[name], slot0=self.acc[name], ids=[],
+                                             grad_col_offset=[], grad=gmat))
+            if sp["grad"] is not gmat:
+                raise ValueError("apply_local: the lookups of one table must share one gradient matrix")
+            sp["ids"].append(ids.reshape(-1))
+            sp["grad_col_offset"].append(int(col))
+        self.ops.sparse_adagrad(list(specs.values()), B, None, lr, eps)
+
     # -- backward + update -------------------------------------------------
     def apply_routed(self, rt: _Route, g_req: torch.Tensor, lr: float, eps: float) -> None:
         """g_req[:R]: the per-request gradient sums of the routed requests;

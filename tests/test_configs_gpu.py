@@ -279,6 +279,64 @@ def test_c5_100m_row_table_world1(cuda):
         torch.cuda.empty_cache()
 
 
+def test_sharded_tables_local_equals_routed_world1(cuda):
+    """ShardedTables at world 1: fetch_local + apply_local (by id, no route:
+    the C5 leg's one-rank form) against route_fixed + fetch_routed +
+    apply_lookups on a copy of the same tables — the same rows per lookup and
+    bit-identical shards and accumulators after three steps of Zipf + uniform
+    ids, two tables, three lookups; then a step with an id out of range: the
+    route sorts it first, the single-device sort last, so the block sums
+    group a table's later duplicates differently — within fp32 rounding of
+    the sums (atol 1e-6 on the tables), rows still equal."""
+    import torch.distributed as dist
+
+    from pkg.modelling.distributed import ShardedTables, destroy_process_group
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device(cuda))
+    try:
+        V, D, B = {"a": 1_000_000, "b": 5000}, 128, 8192 + 37
+        g = torch.Generator(device=cuda)
+        g.manual_seed(9)
+        tabs = {n: torch.empty(v, D, device=cuda).uniform_(-0.05, 0.05, generator=g) for n, v in V.items()}
+        A = ShardedTables({n: t.clone() for n, t in tabs.items()})
+        L = ShardedTables({n: t.clone() for n, t in tabs.items()})
+        rng = np.random.default_rng(4)
+        for step in range(4):
+            ids = [((rng.zipf(1.3, B) - 1) % V["a"]).astype(np.int32), rng.integers(0, V["a"], B).astype(np.int32),
+                   ((rng.zipf(1.2, B) - 1) % V["b"]).astype(np.int32)]
+            if step == 3:
+                ids[2][5] = V["b"] + 3  # out of range: a zero row, no update
+            lookups = [("a", torch.as_tensor(ids[0], device=cuda)), ("a", torch.as_tensor(ids[1], device=cuda)),
+                       ("b", torch.as_tensor(ids[2], device=cuda))]
+            ga = torch.as_tensor(rng.standard_normal((B, 2 * D)).astype(np.float32), device=cuda)
+            gb = torch.as_tensor(rng.standard_normal((B, D)).astype(np.float32), device=cuda)
+            grads = [(ga, 0), (ga, D), (gb, 0)]
+            rt = A.route_fixed(lookups, A.route_capacity(len(lookups), B))
+            rows = A.fetch_routed(rt)
+            A.apply_lookups(rt, grads, 0.05, 1e-7)
+            out = torch.empty(3, B, D, device=cuda)
+            L.fetch_local(lookups, out)
+            L.apply_local(lookups, grads, 0.05, 1e-7)
+            torch.cuda.synchronize()
+            for l in range(3):
+                assert torch.equal(rows[rt.idx[l].long()], out[l]), (step, l)
+            for n in V:
+                if step < 3:
+                    assert torch.equal(A.shard[n], L.shard[n]), (step, n)
+                    assert torch.equal(A.acc[n], L.acc[n]), (step, n)
+                else:
+                    torch.testing.assert_close(A.shard[n], L.shard[n], rtol=0, atol=1e-6)
+                    torch.testing.assert_close(A.acc[n], L.acc[n], rtol=1e-5, atol=0)
+    finally:
+        destroy_process_group()
+        torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("B", [2048, 16384])
 def test_c3_sharded_step_world1_matches_single_gpu(cuda, B):
     """C3's schema with its H&M vocabularies (customer, postal and article

@@ -228,6 +228,12 @@ def _sharded_worker(rank, world, port, tables, lookups, grads, out):
         got = st.fetch_routed(rt)
         st.apply_lookups(rt, [(g, 16 * l) for l in range(len(lk))], lr=0.05, eps=1e-7)
         res[mode] = ([got[i.long()].numpy() for i in rt.idx], {k: st.gather_full(k).numpy() for k in tables}, 0)
+    if world == 1:  # one rank: fetch_local + apply_local (by id, no route)
+        st = ShardedTables({k: torch.from_numpy(v) for k, v in tables.items()}, 0.1, ops=_cpu_embedding_ops())
+        B = lk[0][1].numel()
+        got = st.fetch_local(lk, torch.empty(len(lk), B, st.dim))
+        st.apply_local(lk, [(g, 16 * l) for l in range(len(lk))], lr=0.05, eps=1e-7)
+        res["local"] = ([got[l].numpy() for l in range(len(lk))], {k: st.gather_full(k).numpy() for k in tables}, 0)
     out[rank] = res
     dist.destroy_process_group()
 
@@ -269,11 +275,11 @@ def test_sharded_tables_match_unsharded_adagrad(world):
         assert ff[2] == 0
         assert all(np.array_equal(x, y) for x, y in zip(ff[0], fc[0]))
         assert all(np.array_equal(ff[1][k], fc[1][k]) for k in tables)
-        for mode in ("lookups", "routed"):
+        for mode in ("lookups", "routed") + (("local",) if world == 1 else ()):
             fl = out[r][mode]
             assert all(np.array_equal(x, y) for x, y in zip(fl[0], fc[0]))
-            if mode == "routed" and world == 1:
-                # one rank: the routed op IS the owner's Adagrad (this CPU
+            if mode in ("routed", "local") and world == 1:
+                # one rank: the routed op / the local apply IS the owner's Adagrad (this CPU
                 # restatement sums in fp64 without the per-request fp32 buffer;
                 # on the GPU both are fp32 in one order: test_kernels_gpu)
                 assert all(np.allclose(fl[1][k], fc[1][k], rtol=0, atol=1e-7) for k in tables)
