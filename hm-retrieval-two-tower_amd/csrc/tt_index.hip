@@ -1766,7 +1766,7 @@ __global__ void __launch_bounds__(kFbWaves * kWave) fallback_kernel(const Fallba
 #define TT_INDEX_R_MUL 3.0
 #endif
 #ifndef TT_INDEX_R_MUL_BIG  // the same for k >= 512 (rank estimates far from the sample's tail)
-#define TT_INDEX_R_MUL_BIG 1.5
+#define TT_INDEX_R_MUL_BIG 1.2
 #endif
 #ifndef TT_INDEX_R_ADD
 #define TT_INDEX_R_ADD 100.0
@@ -1814,9 +1814,11 @@ SearchPlan plan_search(int64_t nq, int64_t n_rows, int k, int shards) {
   p.Ss = p.S;
   const int64_t nts = ceil_div(ntiles, p.S);  // tiles per split
   const double ns_cand = static_cast<double>(nts) * kCTile;
-  // 3k + 100 below k = 512; 1.5k + 100 from there (at the runner's 2048 x
-  // k = 1000: 4642 -> 2704 entries per query after the min over 32 split
-  // estimates, 0.705 -> 0.607 ms per search, no certificate failures)
+  // 3k + 100 below k = 512; 1.2k + 100 from there (at the runner's 2048 x
+  // k = 1000: 3k -> 1.5k + 100 took the lists from 4642 to 2704 entries per
+  // query after the min over 32 split estimates, 0.705 -> 0.607 ms per
+  // search; 1.5k -> 1.2k: 0.54 -> 0.46 ms, and 1.0k-1.15k no faster;
+  // bit-exact index tests green at each — profiles/r05_index_scan_ab.txt)
   const double rmul = k >= 512 ? TT_INDEX_R_MUL_BIG : TT_INDEX_R_MUL;
   const double R = (rmul * k + TT_INDEX_R_ADD) / (static_cast<double>(p.S) * (shards > 0 ? shards : 1));
   double mu;  // expected entries per (query, split)
