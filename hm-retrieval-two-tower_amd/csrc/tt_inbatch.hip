@@ -643,6 +643,37 @@ __global__ void __launch_bounds__(256) combine_rows_kernel(
 // sums holding every row but the positive i = j + pos_offset, and
 // 1 - P_pos = -expm1(-row_loss_i) (exact; from lse_i when row_loss is NULL:
 // -expm1(pos - lse_i), pos = q_i . c_j - logq_j).
+// The loss = scale * sum(row_loss) by one 256-thread block in exactly
+// tt_sum's order (its 1024 threads' strided sums and LDS tree, 4 virtual
+// threads per thread), so the value is bit-identical to a tt_sum launch.
+struct LossSum {
+  const float* x;  // NULL: no loss block
+  int64_t n;
+  float scale;
+  float* out;
+};
+
+__device__ __forceinline__ void loss_sum_block(const LossSum& L) {
+  __shared__ float red[1024];
+  for (int v = threadIdx.x; v < 1024; v += 256) {
+    float acc = 0.0f;
+    int64_t i = v;
+    for (; i + 3 * 1024 < L.n; i += 4 * 1024) {
+      const float a = L.x[i], b = L.x[i + 1024], c = L.x[i + 2048], d = L.x[i + 3072];
+      acc = ((acc + a) + b) + c;
+      acc = acc + d;
+    }
+    for (; i < L.n; i += 1024) acc += L.x[i];
+    red[v] = acc;
+  }
+  __syncthreads();
+  for (int w = 512; w > 0; w >>= 1) {
+    for (int v = threadIdx.x; v < w; v += 256) red[v] += red[v + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) L.out[0] = red[0] * L.scale;
+}
+
 template <int D>
 __global__ void __launch_bounds__(256) combine_cols_kernel(const float* __restrict__ part_o, int nsplit,
                                                            int64_t n_stat_pad, const float* __restrict__ q,
@@ -650,7 +681,12 @@ __global__ void __launch_bounds__(256) combine_cols_kernel(const float* __restri
                                                            const float* __restrict__ lse,
                                                            const float* __restrict__ row_loss,
                                                            const float* __restrict__ logq, int64_t n_cols, int dim,
-                                                           int64_t pos_offset, float* __restrict__ dc) {
+                                                           int64_t pos_offset, float* __restrict__ dc,
+                                                           const LossSum loss) {
+  if (loss.x && blockIdx.x == gridDim.x - 1) {  // the extra last block: the loss (row_loss is complete)
+    loss_sum_block(loss);
+    return;
+  }
   constexpr int LPR = D / 4;
   const int64_t j = blockIdx.x * (256ll / LPR) + threadIdx.x / LPR;
   const int sub = threadIdx.x % LPR;
@@ -813,15 +849,16 @@ int combine_rows(int D, hipStream_t st, const float* pm, const float* pl, const 
 
 int combine_cols(int D, hipStream_t st, const float* po, int nsplit, int64_t n_stat_pad, const float* q,
                  int64_t ldq, const float* c, int64_t ldc, const float* lse, const float* row_loss,
-                 const float* logq, int64_t n, int dim, int64_t pos_offset, float* dc) {
-  const dim3 grid(static_cast<unsigned>(ceil_div(n, 1024 / D)));
+                 const float* logq, int64_t n, int dim, int64_t pos_offset, float* dc,
+                 const LossSum& loss = LossSum{}) {
+  const dim3 grid(static_cast<unsigned>(ceil_div(n, 1024 / D) + (loss.x ? 1 : 0)));
   switch (D) {
     case 32: hipLaunchKernelGGL(combine_cols_kernel<32>, grid, dim3(256), 0, st, po, nsplit, n_stat_pad, q, ldq, c,
-                                ldc, lse, row_loss, logq, n, dim, pos_offset, dc); break;
+                                ldc, lse, row_loss, logq, n, dim, pos_offset, dc, loss); break;
     case 64: hipLaunchKernelGGL(combine_cols_kernel<64>, grid, dim3(256), 0, st, po, nsplit, n_stat_pad, q, ldq, c,
-                                ldc, lse, row_loss, logq, n, dim, pos_offset, dc); break;
+                                ldc, lse, row_loss, logq, n, dim, pos_offset, dc, loss); break;
     default: hipLaunchKernelGGL(combine_cols_kernel<128>, grid, dim3(256), 0, st, po, nsplit, n_stat_pad, q, ldq, c,
-                                ldc, lse, row_loss, logq, n, dim, pos_offset, dc); break;
+                                ldc, lse, row_loss, logq, n, dim, pos_offset, dc, loss); break;
   }
   TT_CHECK_LAUNCH();
   return TT_OK;
@@ -984,7 +1021,7 @@ namespace {
 // workspace, ordered before this call).
 int softmax_xent(const float* q, int64_t ldq, const float* c, int64_t ldc, int64_t n, int32_t dim, const float* logq,
                  float* lse, float* row_loss, float* dq, float* dc, void* workspace, size_t workspace_bytes,
-                 tt_stream_t stream, bool prepped) {
+                 tt_stream_t stream, bool prepped, float loss_scale = 1.0f, float* loss = nullptr) {
   int rc = check_common(q, ldq, n, c, ldc, n, dim);
   if (rc) return rc;
   TT_REQUIRE(lse && row_loss && dq && dc, "tt_inbatch_softmax_xent: NULL output");
@@ -1008,7 +1045,8 @@ int softmax_xent(const float* q, int64_t ldq, const float* c, int64_t ldc, int64
     return rc;
   PassArgs ac{w.cb, w.qb, w.bias_lse, p.n_pad, p.n_pad, p.per_split, 0, nullptr, nullptr, w.part_o_cols};
   if ((rc = launch_pass<1>(pl, ac, st))) return rc;
-  return combine_cols(p.D, st, w.part_o_cols, p.split, p.n_pad, q, ldq, c, ldc, lse, row_loss, logq, n, dim, 0, dc);
+  return combine_cols(p.D, st, w.part_o_cols, p.split, p.n_pad, q, ldq, c, ldc, lse, row_loss, logq, n, dim, 0, dc,
+                      loss ? LossSum{row_loss, n, loss_scale, loss} : LossSum{});
 }
 }  // namespace
 }  // namespace tt
@@ -1028,6 +1066,17 @@ extern "C" int tt_inbatch_softmax_xent_prepped(const float* q, int64_t ldq, cons
   using namespace tt;
   clear_error();
   return softmax_xent(q, ldq, c, ldc, n, dim, logq, lse, row_loss, dq, dc, workspace, workspace_bytes, stream, true);
+}
+
+extern "C" int tt_inbatch_softmax_xent_loss(const float* q, int64_t ldq, const float* c, int64_t ldc, int64_t n,
+                                            int32_t dim, const float* logq, float* lse, float* row_loss, float* dq,
+                                            float* dc, float loss_scale, float* loss, int32_t prepped,
+                                            void* workspace, size_t workspace_bytes, tt_stream_t stream) {
+  using namespace tt;
+  clear_error();
+  TT_REQUIRE(loss, "tt_inbatch_softmax_xent_loss: NULL loss");
+  return softmax_xent(q, ldq, c, ldc, n, dim, logq, lse, row_loss, dq, dc, workspace, workspace_bytes, stream,
+                      prepped != 0, loss_scale, loss);
 }
 
 extern "C" int tt_inbatch_prep(const float* x, int64_t ldx, int64_t n, int32_t dim, int32_t operand,

@@ -882,8 +882,10 @@ __global__ void __launch_bounds__(kSThreads) scan_kernel(const ScreenArgs a) {
     // alone holds the others at the next ring barrier).  Off by default: a
     // wave flushes when 64 rows are staged and at the end (1M x k=100: 44.7
     // vs 45.2 ms with a flush every 4 tiles; every 8: much slower)
-    if (TT_SCAN_FLUSH_TILES > 0 && u % TT_SCAN_FLUSH_TILES == TT_SCAN_FLUSH_TILES - 1)
+#if TT_SCAN_FLUSH_TILES > 0
+    if (u % TT_SCAN_FLUSH_TILES == TT_SCAN_FLUSH_TILES - 1)
       while (head > tail) flush(min(head - tail, kWave));
+#endif
   }
   if (nv > 0) stage_pair(b0, b1, prep(b0, b1, nv - 1, 1));
   if (TT_SCAN_PROBE && probe_acc == 12345.f) a.count[0] = -2;  // keeps the probe's work alive

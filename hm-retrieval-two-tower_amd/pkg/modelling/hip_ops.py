@@ -734,10 +734,12 @@ def inbatch_prep(x: torch.Tensor, operand: int, logq: Optional[torch.Tensor], ws
 
 
 def inbatch_fused(q: torch.Tensor, c: torch.Tensor, logq: Optional[torch.Tensor], ws: Optional[torch.Tensor] = None,
-                  prepped: bool = False):
+                  prepped: bool = False, loss_scale: Optional[float] = None):
     """Single-device loss + gradients (both passes, shared bf16 prep):
     (lse [B], row_loss [B], dq [B,E], dc [B,E]).  prepped: both operands were
-    already prepared into `ws` by inbatch_prep (ordered before this call)."""
+    already prepared into `ws` by inbatch_prep (ordered before this call).
+    loss_scale: also return the loss loss_scale * sum(row_loss) (a 0-d
+    tensor, computed inside the last launch, equal to loss_sum's)."""
     _req(q, "q", torch.float32, 2)
     _req(c, "c", torch.float32, 2)
     ldq, ldc = _row_major(q, "q"), _row_major(c, "c")
@@ -753,6 +755,13 @@ def inbatch_fused(q: torch.Tensor, c: torch.Tensor, logq: Optional[torch.Tensor]
     row_loss = torch.empty(B, dtype=torch.float32, device=q.device)
     dq = torch.empty(B, E, dtype=torch.float32, device=q.device)
     dc = torch.empty(B, E, dtype=torch.float32, device=q.device)
+    if loss_scale is not None:
+        loss = torch.empty((), dtype=torch.float32, device=q.device)
+        check(L.tt_inbatch_softmax_xent_loss(q.data_ptr(), ldq, c.data_ptr(), ldc, B, E, _opt_ptr(logq, "logq", B),
+                                             lse.data_ptr(), row_loss.data_ptr(), dq.data_ptr(), dc.data_ptr(),
+                                             float(loss_scale), loss.data_ptr(), int(prepped), ws.data_ptr(),
+                                             ws.numel(), _stream()))
+        return lse, row_loss, dq, dc, loss
     fn = L.tt_inbatch_softmax_xent_prepped if prepped else L.tt_inbatch_softmax_xent
     check(fn(q.data_ptr(), ldq, c.data_ptr(), ldc, B, E, _opt_ptr(logq, "logq", B), lse.data_ptr(), row_loss.data_ptr(),
              dq.data_ptr(), dc.data_ptr(), ws.data_ptr(), ws.numel(), _stream()))

@@ -59,6 +59,10 @@ def _tower_stream(device: torch.device) -> torch.cuda.Stream:
 GLOBAL_TOWER_STREAMS = int(os.environ.get("TT_GLOBAL_TOWER_STREAMS", "4096"))
 # The single-GPU step's towers on two streams (TT_TOWER_STREAMS=0: one).
 TOWER_STREAMS = int(os.environ.get("TT_TOWER_STREAMS", "1"))
+# The single-device step's loss summed by an extra workgroup of the loss
+# entry's last launch (tt_inbatch_softmax_xent_loss) instead of a tt_sum
+# launch after it (TT_LOSS_IN_COMBINE=0); the same value bit for bit.
+LOSS_IN_COMBINE = os.environ.get("TT_LOSS_IN_COMBINE", "1") == "1"
 # The global-negatives loss at one rank through the single-device entry
 # (TT_WORLD1_FUSED=0: the rows and columns entries, as at G > 1).
 WORLD1_FUSED = os.environ.get("TT_WORLD1_FUSED", "1") == "1"
@@ -164,11 +168,16 @@ class _TowersInBatchXent(torch.autograd.Function):
 
     @staticmethod
     def _finish(ctx, qa, ca, flat_q, flat_c, logq, stack_q, stack_c, scale, on_tower, ws=None):
-        _, row_loss, dq, dc = hip_ops.inbatch_fused(qa[-1], ca[-1], logq, ws=ws, prepped=ws is not None)
         ctx.stacks = (stack_q, stack_c)
         ctx.nq = len(qa)
         ctx.scale = scale
         ctx.on_tower = on_tower
+        if LOSS_IN_COMBINE:  # the loss sum inside the loss entry's last launch
+            _, _, dq, dc, loss = hip_ops.inbatch_fused(qa[-1], ca[-1], logq, ws=ws, prepped=ws is not None,
+                                                       loss_scale=scale)
+            ctx.save_for_backward(flat_q, flat_c, dq, dc, *qa, *ca)
+            return loss
+        _, row_loss, dq, dc = hip_ops.inbatch_fused(qa[-1], ca[-1], logq, ws=ws, prepped=ws is not None)
         ctx.save_for_backward(flat_q, flat_c, dq, dc, *qa, *ca)
         return hip_ops.loss_sum(row_loss, scale)
 

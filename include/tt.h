@@ -428,6 +428,20 @@ int tt_inbatch_softmax_xent_prepped(const float* q, int64_t ldq,
                                     size_t workspace_bytes,
                                     tt_stream_t stream);
 
+/* tt_inbatch_softmax_xent (prepped = 0) or tt_inbatch_softmax_xent_prepped
+ * (prepped = 1), also writing the step's loss *loss = loss_scale *
+ * sum(row_loss) (the reference's SUM reduction, two_tower_model.py:122,
+ * runner.py:78-83): one extra workgroup of the last launch sums the row
+ * losses in tt_sum's order, so the value equals a tt_sum call bit for bit
+ * without its launch. */
+int tt_inbatch_softmax_xent_loss(const float* q, int64_t ldq, const float* c,
+                                 int64_t ldc, int64_t n, int32_t dim,
+                                 const float* logq, float* lse,
+                                 float* row_loss, float* dq, float* dc,
+                                 float loss_scale, float* loss,
+                                 int32_t prepped, void* workspace,
+                                 size_t workspace_bytes, tt_stream_t stream);
+
 /* ------------------------------------------------------------------------ *
  * K11+K12  Brute-force scoring with fused top-K.
  * Replaces BruteForceIndex.call (pkg/modelling/indices/brute_force.py:76-81):

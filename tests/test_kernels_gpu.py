@@ -304,6 +304,30 @@ def test_inbatch_split_prep_bit_identical(cuda, B, E, use_logq):
         hip_ops.inbatch_prep(q, 0, None, ws[:16])
 
 
+@pytest.mark.parametrize("B,E,scale", [(16384, 128, 1.0), (4100, 64, 0.25), (37, 32, 1.0), (1, 16, 3.0),
+                                       (5000, 128, 1.0 / 5000)])
+def test_inbatch_loss_in_last_launch_equals_tt_sum(cuda, B, E, scale):
+    """tt_inbatch_softmax_xent_loss: the loss summed by an extra workgroup of
+    the columns combine equals tt_sum over the row losses bit for bit (same
+    strided order and LDS tree), with the same row losses and gradients as
+    the plain entry, prepared in one call or per operand."""
+    rng = np.random.default_rng(B * 3 + E)
+    q = _t(np.maximum(rng.standard_normal((B, E)) * 0.5, 0).astype(np.float32), cuda)
+    c = _t(np.maximum(rng.standard_normal((B, E)) * 0.5, 0).astype(np.float32), cuda)
+    logq = _t(np.log(rng.uniform(1e-6, 1e-2, B)).astype(np.float32), cuda)
+    want = hip_ops.inbatch_fused(q, c, logq)
+    want_loss = hip_ops.loss_sum(want[1], scale)
+    got = hip_ops.inbatch_fused(q, c, logq, loss_scale=scale)
+    assert torch.equal(got[4], want_loss)
+    for w, g in zip(want, got[:4]):
+        assert torch.equal(w, g)
+    ws = torch.zeros(hip_ops.lib().tt_inbatch_fused_workspace_size(B, E), dtype=torch.uint8, device=cuda)
+    hip_ops.inbatch_prep(c, 1, logq, ws)
+    hip_ops.inbatch_prep(q, 0, None, ws)
+    got_p = hip_ops.inbatch_fused(q, c, logq, ws=ws, prepped=True, loss_scale=scale)
+    assert torch.equal(got_p[4], want_loss)
+
+
 def test_inbatch_row_blocks_with_offset(cuda):
     """Rows of rank r scored against all-gathered columns (global negatives)."""
     rng = np.random.default_rng(7)
