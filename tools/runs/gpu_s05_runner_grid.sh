@@ -4,7 +4,7 @@
 set -e
 OUT=$GRAFT_REPO_ROOT/gpurun_out/s05rg; mkdir -p $OUT
 for r in 1 2; do
-  for v in new rm11 rm10; do
+  for v in rm11 rm10; do
     L=""; [ $v != new ] && L=$GRAFT_REPO_ROOT/tools/vlib/$v/libtt.so
     for lf in 0 3136 2624 2368; do
       E=""; [ $lf != 0 ] && E="TT_FINAL_LF=$lf"
