@@ -315,6 +315,7 @@ struct ScreenArgs {
   int* count;         // [nq_pad][S]; -1 = list overflowed
   float* tau_split;   // sample pass output [nq_pad][S]
   const float* tau;   // scan pass input [nq_pad]: keep s~ > tau[q]
+  float* bins;        // pooled estimate (non-NULL): the sample pass writes [nq_pad][S][64] bin maxima instead
 };
 
 // s_waitcnt with only the vector-memory counter constrained (gfx9 encoding).
@@ -508,11 +509,23 @@ __global__ void __launch_bounds__(kSThreads) sample_kernel(const ScreenArgs a) {
       }
       advance(u);
     }
-    const float tq0 = ns > 0 ? bins_select(b0a, b0b, a.jsel) : -INFINITY;
-    const float tq1 = ns > 0 ? bins_select(b1a, b1b, a.jsel) : -INFINITY;
-    if (h == 0) {
-      a.tau_split[q0 * a.S + split] = tq0;
-      a.tau_split[q1 * a.S + split] = tq1;
+    if (a.bins) {  // pooled estimate: this lane's 32 of the query's 64 bins of this split
+      float* o0 = a.bins + (q0 * a.S + split) * 64 + 32 * h;
+      float* o1 = a.bins + (q1 * a.S + split) * 64 + 32 * h;
+  #pragma unroll
+      for (int r = 0; r < 16; r += 4) {
+        *reinterpret_cast<f32x4*>(o0 + r) = f32x4{b0a[r], b0a[r + 1], b0a[r + 2], b0a[r + 3]};
+        *reinterpret_cast<f32x4*>(o0 + 16 + r) = f32x4{b0b[r], b0b[r + 1], b0b[r + 2], b0b[r + 3]};
+        *reinterpret_cast<f32x4*>(o1 + r) = f32x4{b1a[r], b1a[r + 1], b1a[r + 2], b1a[r + 3]};
+        *reinterpret_cast<f32x4*>(o1 + 16 + r) = f32x4{b1b[r], b1b[r + 1], b1b[r + 2], b1b[r + 3]};
+      }
+    } else {
+      const float tq0 = ns > 0 ? bins_select(b0a, b0b, a.jsel) : -INFINITY;
+      const float tq1 = ns > 0 ? bins_select(b1a, b1b, a.jsel) : -INFINITY;
+      if (h == 0) {
+        a.tau_split[q0 * a.S + split] = tq0;
+        a.tau_split[q1 * a.S + split] = tq1;
+      }
     }
   }
 }
@@ -906,6 +919,36 @@ __global__ void tau_min_kernel(const float* __restrict__ tau_split, int S, int64
   float t = tau_split[q * S];
   for (int s = 1; s < S; ++s) t = fminf(t, tau_split[q * S + s]);
   tau[q] = t;
+}
+
+// tau[q] = the J-th largest of the query's S x 64 bin maxima (all splits'
+// samples pooled: one estimate of the rank-R score over the whole candidate
+// set, far less noisy than the least of S per-split estimates), to a 16-bit
+// order-key prefix (rounded down); -inf if fewer than J bins.  One wave per
+// query, S <= 64.
+__global__ void __launch_bounds__(256) tau_pool_kernel(const float* __restrict__ bins, int S, int64_t nq, int J,
+                                                       float* __restrict__ tau) {
+  const int64_t q = blockIdx.x * 4ll + threadIdx.x / kWave;
+  const int lane = lane_id();
+  if (q >= nq) return;
+  const float* b = bins + q * S * 64;
+  float v[kWave];
+#pragma unroll
+  for (int s = 0; s < kWave; ++s) v[s] = s < S ? b[s * 64 + lane] : -INFINITY;
+  unsigned res = 0;
+#pragma unroll 1
+  for (int bit = 15; bit >= 0; --bit) {
+    const unsigned c = res | (1u << bit);
+    const float f = order_key_float(c << 16);  // smallest float with this prefix (NaN: none)
+    int n = 0;
+#pragma unroll
+    for (int s = 0; s < kWave; ++s) n += v[s] >= f ? 1 : 0;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) n += __shfl_xor(n, m, kWave);
+    if (n >= J) res = c;
+  }
+  const float t = order_key_float(res << 16);
+  if (lane == 0) tau[q] = (t > -INFINITY) ? t : -INFINITY;
 }
 
 // ---- finalize ------------------------------------------------------------
@@ -1770,11 +1813,16 @@ __global__ void __launch_bounds__(kFbWaves * kWave) fallback_kernel(const Fallba
 #ifndef TT_INDEX_R_MUL_BIG  // the same for k >= 512 (rank estimates far from the sample's tail)
 #define TT_INDEX_R_MUL_BIG 1.2
 #endif
+#ifndef TT_INDEX_POOL  // 1: the pooled rank estimate when the sample pass splits the candidates (k < 512)
+#define TT_INDEX_POOL 1
+#endif
 #ifndef TT_INDEX_R_ADD
 #define TT_INDEX_R_ADD 100.0
 #endif
 struct SearchPlan {
   int S, NS, jsel, cap, L, LF, P, k, parts;
+  int pool;  // pooled estimate (> 1 sample splits): tau = the J-th largest of a query's Ss x 64 bins
+  int J;
   int Ss;  // sample-pass splits (<= S): their estimates give one tau per query
   int NW;  // waves per finalize workgroup (one query each)
   int64_t chunk;
@@ -1840,6 +1888,18 @@ SearchPlan plan_search(int64_t nq, int64_t n_rows, int k, int shards) {
     int j = static_cast<int>(std::lround(64.0 * pbin));
     p.jsel = j < 1 ? 1 : (j > 64 ? 64 : j);
     mu = R;
+    // pooled: every split's 64 bins estimate the same global rank (R per
+    // split x Ss splits), so the J-th largest of all Ss x 64 estimates it
+    // once — lists near their target instead of above it (2048 x k = 100:
+    // 0.31 -> 0.20 ms per search).  Not for k >= 512: there the rank sits
+    // deep in the bins (pbin near 1) and the pooled estimate lands high
+    // enough to fail certificates (runner point 0.46 -> 1.7 ms at 1.3k + 100,
+    // no gain at 1.5k + 100; profiles/r05_index_scan_ab.txt)
+    if (TT_INDEX_POOL && p.Ss > 1 && p.Ss <= 64 && k < 512) {
+      const int64_t jj = std::llround(64.0 * p.Ss * pbin);
+      p.pool = 1;
+      p.J = static_cast<int>(jj < 1 ? 1 : (jj > 64 * p.Ss ? 64 * p.Ss : jj));
+    }
   }
   if (p.NS > 0) {
     // the scan needs only the per-query tau (the min over the sample
@@ -1870,6 +1930,7 @@ struct SearchWs {
   int* count;
   float* tau_split;
   float* tau;
+  float* bins;      // pooled estimate: [nq_pad][Ss][64] bin maxima
   int* fail_count;  // [0] failures, then the fallback's ctrl words
   int* fail_list;
   uint2* fb_scratch;
@@ -1888,6 +1949,7 @@ SearchWs carve_search(Carver& cv, int D, const SearchPlan& p, bool lists, bool f
     w.count = cv.take<int>(nq_pad * p.S);
     w.tau_split = cv.take<float>(nq_pad * p.Ss);
     w.tau = cv.take<float>(nq_pad);
+    if (p.pool) w.bins = cv.take<float>(nq_pad * p.Ss * 64);
   }
   if (finalize) {
     w.fail_count = cv.take<int>(2 + kFbSlots);
@@ -1933,9 +1995,13 @@ int run_prep(const float* q, int64_t ldq, int64_t nq, int dim, int D, const void
 int run_estimate(int D, const void* index, int64_t row0, int64_t row1, int64_t nq, const SearchPlan& p,
                  const SearchWs& w, float* tau, hipStream_t st) {
   const int64_t nq_pad = round_up(nq, kQPerWG);
-  ScreenArgs sa{index, w.qb, nq, row0, row1, p.Ss, p.NS, p.jsel, p.cap, 0u, nullptr, nullptr, w.tau_split, nullptr};
+  ScreenArgs sa{index, w.qb, nq, row0, row1, p.Ss, p.NS, p.jsel, p.cap, 0u, nullptr, nullptr, w.tau_split, nullptr,
+                p.pool ? w.bins : nullptr};
   if (int rc = run_pass(D, sa, nq_pad, true, st)) return rc;
-  hipLaunchKernelGGL(tau_min_kernel, dim3(ceil_div(nq, 256)), dim3(256), 0, st, w.tau_split, p.Ss, nq, tau);
+  if (p.pool)
+    hipLaunchKernelGGL(tau_pool_kernel, dim3(ceil_div(nq, 4)), dim3(256), 0, st, w.bins, p.Ss, nq, p.J, tau);
+  else
+    hipLaunchKernelGGL(tau_min_kernel, dim3(ceil_div(nq, 256)), dim3(256), 0, st, w.tau_split, p.Ss, nq, tau);
   TT_CHECK_LAUNCH();
   return TT_OK;
 }
