@@ -559,8 +559,18 @@ __global__ void __launch_bounds__(kWgThreads) mlp_wgrad_pair_kernel(const WgradA
 // float4 of the output; group g of 16 adds splits [g S/16, (g+1) S/16) in
 // order (their loads all in flight), then the 16 group sums are added in
 // group order.  len % 4 == 0.
+// Optional Adagrad on the summed gradient (tt_mlp_wgrad_adagrad): the layer's
+// parameters and accumulator, the same per-element arithmetic as
+// tt_dense_adagrad.
+struct PartsAdagrad {
+  float* param;  // NULL: none
+  float* accum;
+  float lr, eps;
+};
+
 __device__ __forceinline__ void mlp_sum_parts_block(const float* __restrict__ parts, int S, int64_t len,
-                                                    float* __restrict__ out, const int64_t bid, f32x4 (*red)[64]) {
+                                                    float* __restrict__ out, const int64_t bid, f32x4 (*red)[64],
+                                                    const PartsAdagrad& ad = PartsAdagrad{}) {
   const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int64_t e4 = (bid * 64 + lane) * 4;
   const int per = (S + 15) / 16;
@@ -590,13 +600,26 @@ __device__ __forceinline__ void mlp_sum_parts_block(const float* __restrict__ pa
       for (int q = 0; q < 4; ++q) t[q] += r[q];
     }
     *reinterpret_cast<f32x4*>(out + e4) = t;
+    if (ad.param) {
+      f32x4 pa = *reinterpret_cast<const f32x4*>(ad.param + e4);
+      f32x4 ac = *reinterpret_cast<const f32x4*>(ad.accum + e4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float gi = t[q];
+        const float a = ac[q] + gi * gi;
+        ac[q] = a;
+        pa[q] = pa[q] - (gi * ad.lr) / (sqrtf(a) + ad.eps);
+      }
+      *reinterpret_cast<f32x4*>(ad.accum + e4) = ac;
+      *reinterpret_cast<f32x4*>(ad.param + e4) = pa;
+    }
   }
 }
 
 __global__ void __launch_bounds__(1024) mlp_sum_parts_kernel(const float* __restrict__ parts, int S, int64_t len,
-                                                             float* __restrict__ out) {
+                                                             float* __restrict__ out, const PartsAdagrad ad) {
   __shared__ f32x4 red[16][64];
-  mlp_sum_parts_block(parts, S, len, out, blockIdx.x, red);
+  mlp_sum_parts_block(parts, S, len, out, blockIdx.x, red, ad);
 }
 
 // Both problems' partial sums in one launch: blocks [0, split) are the first's.
@@ -921,23 +944,44 @@ static void launch_wgrad(const WgradArgs& a, hipStream_t st) {
   else hipLaunchKernelGGL((mlp_wgrad_kernel<false>), grid, dim3(kWgThreads), 0, st, a);
 }
 
-extern "C" int tt_mlp_wgrad(const float* A, int64_t lda, const float* G, int64_t ldg, const float* gmask,
-                            int64_t ldgm, const float* scale, int64_t M, int32_t Ka, int32_t N, float* dwb,
-                            void* workspace, size_t workspace_bytes, tt_stream_t stream) {
-  clear_error();
+namespace {
+int wgrad_one(const char* fn, const float* A, int64_t lda, const float* G, int64_t ldg, const float* gmask,
+              int64_t ldgm, const float* scale, int64_t M, int32_t Ka, int32_t N, float* dwb, void* workspace,
+              size_t workspace_bytes, tt_stream_t stream, const PartsAdagrad& ad) {
   WgradArgs a;
-  const int rc = wgrad_setup("tt_mlp_wgrad", A, lda, G, ldg, gmask, ldgm, scale, M, Ka, N, dwb, a);
+  const int rc = wgrad_setup(fn, A, lda, G, ldg, gmask, ldgm, scale, M, Ka, N, dwb, a);
   if (rc != TT_OK) return rc;
-  TT_REQUIRE(workspace && workspace_bytes >= tt_mlp_wgrad_workspace_size(M, Ka, N),
-             "tt_mlp_wgrad: workspace %zu < %zu", workspace_bytes, tt_mlp_wgrad_workspace_size(M, Ka, N));
+  TT_REQUIRE(workspace && workspace_bytes >= tt_mlp_wgrad_workspace_size(M, Ka, N), "%s: workspace %zu < %zu", fn,
+             workspace_bytes, tt_mlp_wgrad_workspace_size(M, Ka, N));
   a.parts = static_cast<float*>(workspace);
   hipStream_t st = to_stream(stream);
   launch_wgrad(a, st);
   TT_CHECK_LAUNCH();
   const int64_t len = static_cast<int64_t>(Ka + 1) * N;
-  hipLaunchKernelGGL(mlp_sum_parts_kernel, dim3(ceil_div(len, 256)), dim3(1024), 0, st, a.parts, a.S, len, dwb);
+  hipLaunchKernelGGL(mlp_sum_parts_kernel, dim3(ceil_div(len, 256)), dim3(1024), 0, st, a.parts, a.S, len, dwb, ad);
   TT_CHECK_LAUNCH();
   return TT_OK;
+}
+}  // namespace
+
+extern "C" int tt_mlp_wgrad(const float* A, int64_t lda, const float* G, int64_t ldg, const float* gmask,
+                            int64_t ldgm, const float* scale, int64_t M, int32_t Ka, int32_t N, float* dwb,
+                            void* workspace, size_t workspace_bytes, tt_stream_t stream) {
+  clear_error();
+  return wgrad_one("tt_mlp_wgrad", A, lda, G, ldg, gmask, ldgm, scale, M, Ka, N, dwb, workspace, workspace_bytes,
+                   stream, PartsAdagrad{});
+}
+
+extern "C" int tt_mlp_wgrad_adagrad(const float* A, int64_t lda, const float* G, int64_t ldg, const float* gmask,
+                                    int64_t ldgm, const float* scale, int64_t M, int32_t Ka, int32_t N, float* dwb,
+                                    float* param, float* accum, float lr, float epsilon, void* workspace,
+                                    size_t workspace_bytes, tt_stream_t stream) {
+  clear_error();
+  TT_REQUIRE(param && accum, "tt_mlp_wgrad_adagrad: NULL param / accum");
+  TT_REQUIRE(reinterpret_cast<uintptr_t>(param) % 16 == 0 && reinterpret_cast<uintptr_t>(accum) % 16 == 0,
+             "tt_mlp_wgrad_adagrad: param / accum must be 16-B aligned");
+  return wgrad_one("tt_mlp_wgrad_adagrad", A, lda, G, ldg, gmask, ldgm, scale, M, Ka, N, dwb, workspace,
+                   workspace_bytes, stream, PartsAdagrad{param, accum, lr, epsilon});
 }
 
 // the second problem's partials start 256-B aligned after the first's

@@ -312,6 +312,10 @@ _PROTOS = {
         c_int32,
         [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int32, c_int32, c_void_p,
          c_void_p, c_size_t, c_void_p]),
+    "tt_mlp_wgrad_adagrad": (
+        c_int32,
+        [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int32, c_int32, c_void_p,
+         c_void_p, c_void_p, c_float, c_float, c_void_p, c_size_t, c_void_p]),
     "tt_mlp_rows_pair": (c_int32, [c_void_p, c_void_p]),
     "tt_mlp_wgrad_pair_workspace_size": (c_size_t, [c_void_p]),
     "tt_mlp_wgrad_pair": (c_int32, [c_void_p, c_void_p, c_size_t, c_void_p]),

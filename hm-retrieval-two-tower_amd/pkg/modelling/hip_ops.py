@@ -1092,14 +1092,26 @@ def _check_wgrad(a, g, dwb, gmask) -> Tuple[int, int, int]:
 
 
 def mlp_wgrad(a: torch.Tensor, g: torch.Tensor, dwb: torch.Tensor, *, gmask: Optional[torch.Tensor] = None,
-              scale: Optional[torch.Tensor] = None) -> torch.Tensor:
+              scale: Optional[torch.Tensor] = None, adagrad: Optional[tuple] = None) -> torch.Tensor:
     """dwb [Ka + 1, N] = [a | 1]^T . Gm (weight gradient rows then the bias
-    gradient row), Gm = g or (gmask > 0) ? g * scale : 0 (tt_mlp_wgrad)."""
+    gradient row), Gm = g or (gmask > 0) ? g * scale : 0 (tt_mlp_wgrad).
+    adagrad = (param, accum, lr, eps): also the layer's Adagrad step on
+    param / accum (contiguous, dwb's shape) from the summed gradient
+    (tt_mlp_wgrad_adagrad: dense_adagrad's arithmetic inside the sum launch)."""
     M, Ka, N = _check_wgrad(a, g, dwb, gmask)
     ws = Workspace.get(lib().tt_mlp_wgrad_workspace_size(M, Ka, N), a.device, "mlp_wgrad")
-    check(lib().tt_mlp_wgrad(a.data_ptr(), _row_major(a, "a"), g.data_ptr(), _row_major(g, "g"), _ptr(gmask),
-                             _row_major(gmask, "gmask") if gmask is not None else 0,
-                             _ptr(scale), M, Ka, N, dwb.data_ptr(), ws.data_ptr(), ws.numel(), _stream()))
+    args = (a.data_ptr(), _row_major(a, "a"), g.data_ptr(), _row_major(g, "g"), _ptr(gmask),
+            _row_major(gmask, "gmask") if gmask is not None else 0, _ptr(scale), M, Ka, N, dwb.data_ptr())
+    if adagrad is not None:
+        param, accum, lr, eps = adagrad
+        for t, n in ((param, "param"), (accum, "accum")):
+            _req(t, n, torch.float32)
+            if t.numel() != dwb.numel() or not t.is_contiguous():
+                raise ValueError(f"{n} must be contiguous with dwb's {dwb.numel()} elements")
+        check(lib().tt_mlp_wgrad_adagrad(*args, param.data_ptr(), accum.data_ptr(), float(lr), float(eps),
+                                         ws.data_ptr(), ws.numel(), _stream()))
+        return dwb
+    check(lib().tt_mlp_wgrad(*args, ws.data_ptr(), ws.numel(), _stream()))
     return dwb
 
 

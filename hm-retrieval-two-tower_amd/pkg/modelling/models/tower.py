@@ -89,6 +89,11 @@ class DenseStack:
             flat[w_off:w_off + fi * fo] = w.reshape(-1)
         self.flat = flat.to(device).requires_grad_(True)
         self.out_dim = fan_in
+        # (accumulator of flat, lr, eps) while a train step applies this
+        # stack's Adagrad inside its weight-gradient launches (TwoTowerModel:
+        # FUSED_DENSE_WGRAD); the layers it was applied to in this backward
+        self.fused_adagrad = None
+        self.fused_applied: set = set()
 
     def params(self, flat: Optional[torch.Tensor] = None):
         f = self.flat if flat is None else flat
@@ -218,7 +223,14 @@ class DenseStack:
 
     def _wgrad_layer(self, li, acts, gflat, gout, g, gscale) -> None:
         if self._wgrad_fits(li, g, acts):
-            _wgrad(self._wgrad_problem(li, acts, gflat, gout, g, gscale))
+            p = self._wgrad_problem(li, acts, gflat, gout, g, gscale)
+            if self.fused_adagrad is not None:  # this layer's Adagrad step in the same launches
+                acc, lr, eps = self.fused_adagrad
+                w_off, fi, fo, _ = self.layout[li]
+                n = (fi + 1) * fo
+                p["adagrad"] = (self.flat.data[w_off:w_off + n], acc[w_off:w_off + n], lr, eps)
+                self.fused_applied.add(li)
+            _wgrad(p)
         else:
             self._wgrad_torch(li, acts, gflat, g, gscale)
 

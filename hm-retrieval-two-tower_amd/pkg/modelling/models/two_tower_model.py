@@ -49,6 +49,10 @@ SORT_AFTER = os.environ.get("TT_SORT_AFTER", "gather")
 DENSE_EARLY = os.environ.get("TT_DENSE_EARLY", "1") == "1"
 # fused apply: the per-tower id sorts issued right after the gather
 FUSED_SORT_EARLY = os.environ.get("TT_FUSED_SORT_EARLY", "1") == "1"
+# with DENSE_EARLY: each layer's Adagrad step applied by its weight-gradient
+# launches (tt_mlp_wgrad_adagrad: the partial-sum launch updates the layer)
+# instead of one dense_adagrad launch per tower after its backward
+FUSED_DENSE_WGRAD = os.environ.get("TT_FUSED_DENSE_WGRAD", "1") == "1"
 
 
 class TwoTowerModel(AbstractKerasModel):
@@ -236,6 +240,13 @@ class TwoTowerModel(AbstractKerasModel):
                        and self.device.type == "cuda")
         self._dense_done = set()
         self._sparse_done = set()
+        for t in self.towers:
+            t.dense.fused_applied = set()
+            t.dense.fused_adagrad = None
+            if dense_early and FUSED_DENSE_WGRAD:
+                opt = self.optimizer
+                (acc,) = opt._slot(t.dense.flat, 1, opt.initial_accumulator_value)
+                t.dense.fused_adagrad = (acc, opt.learning_rate, opt.epsilon)
         self._on_tower = self._apply_tower if fused else (self._apply_dense_tower if dense_early else None)
         # fused: each tower's embedding update the moment its input gradient
         # exists (the weight gradients follow it on that tower's stream)
@@ -266,7 +277,11 @@ class TwoTowerModel(AbstractKerasModel):
             t.dense.flat.grad = None
         if getattr(self, "_one", None) is None or self._one.device != loss.device:
             self._one = torch.ones((), dtype=loss.dtype, device=loss.device)
-        loss.backward(self._one)  # a persistent seed: no ones-fill launch per step
+        try:
+            loss.backward(self._one)  # a persistent seed: no ones-fill launch per step
+        finally:
+            for t in self.towers:
+                t.dense.fused_adagrad = None
         if fused:
             self.optimizer.iterations += 1
             # the update is applied: a later apply_gradients must not apply it again
@@ -296,7 +311,17 @@ class TwoTowerModel(AbstractKerasModel):
         self._sparse_done.add(i)
 
     def _apply_dense_tower(self, i: int, input_grad: Optional[torch.Tensor], flat_grad: torch.Tensor) -> None:
-        self.optimizer.apply_dense(self.towers[i], flat_grad)
+        st = self.towers[i].dense
+        if st.fused_applied:  # the weight-gradient launches applied those layers' step
+            for li, (w_off, fi, fo, _) in enumerate(st.layout):
+                if li not in st.fused_applied:  # a layer outside tt_mlp_wgrad's contract
+                    n = (fi + 1) * fo
+                    (acc,) = self.optimizer._slot(st.flat, 1, self.optimizer.initial_accumulator_value)
+                    hip_ops.dense_adagrad(st.flat.data[w_off:w_off + n], acc[w_off:w_off + n],
+                                          flat_grad[w_off:w_off + n], self.optimizer.learning_rate,
+                                          self.optimizer.epsilon)
+        else:
+            self.optimizer.apply_dense(self.towers[i], flat_grad)
         self._dense_done.add(i)
 
     def fit(self, dataset: Iterable[Dict[str, Any]], epochs: int = 1, callbacks=None,

@@ -603,6 +603,14 @@ size_t tt_mlp_wgrad_workspace_size(int64_t M, int32_t Ka, int32_t N);
 int tt_mlp_wgrad(const float* A, int64_t lda, const float* G, int64_t ldg, const float* gmask, int64_t ldgm,
                  const float* scale, int64_t M, int32_t Ka, int32_t N, float* dwb, void* workspace,
                  size_t workspace_bytes, tt_stream_t stream);
+/* tt_mlp_wgrad plus the layer's Adagrad step (ResourceApplyAdagradV2 on
+ * param / accum, the layer's [Ka + 1, N] region of the flat buffer and its
+ * accumulator, 16-B aligned) applied by the partial-sum launch to the summed
+ * gradient — tt_dense_adagrad's arithmetic, without its launch. */
+int tt_mlp_wgrad_adagrad(const float* A, int64_t lda, const float* G, int64_t ldg, const float* gmask,
+                         int64_t ldgm, const float* scale, int64_t M, int32_t Ka, int32_t N, float* dwb,
+                         float* param, float* accum, float lr, float epsilon, void* workspace,
+                         size_t workspace_bytes, tt_stream_t stream);
 
 /* The two towers' layers as ONE launch each (the query and the candidate
  * tower are independent chains of the same shape of work: one stream, no

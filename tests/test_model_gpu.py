@@ -309,6 +309,34 @@ def test_paired_tower_launches_bit_identical(cuda, monkeypatch, fused):
     b.optimizer.check_status(cuda)
 
 
+@pytest.mark.parametrize("pair", [0, 1])
+def test_fused_dense_wgrad_bit_identical(cuda, monkeypatch, pair):
+    """TT_FUSED_DENSE_WGRAD: each layer's Adagrad step applied by its
+    weight-gradient launches (tt_mlp_wgrad_adagrad) instead of one
+    dense_adagrad launch per tower gives bit-identical losses, tables,
+    accumulators and MLP buffers at ragged batch sizes (and, with paired
+    tower launches, falls back to the dense launch)."""
+    from pkg.modelling import losses
+    from pkg.modelling.models import two_tower_model as ttm
+
+    monkeypatch.setattr(losses, "TOWER_PAIR", pair)
+    a, b = _small_model(cuda, seed=41), _small_model(cuda, seed=41)
+    rng = np.random.default_rng(14)
+    for i, B in enumerate((512, 37, 256, 1)):
+        x = _batch(cuda, rng, B, True)
+        monkeypatch.setattr(ttm, "FUSED_DENSE_WGRAD", False)
+        la = a.train_step(x)["loss"]
+        monkeypatch.setattr(ttm, "FUSED_DENSE_WGRAD", True)
+        lb = b.train_step(x)["loss"]
+        assert all(bool(t.dense.fused_applied) == (pair == 0) for t in b.towers)
+        assert torch.equal(la, lb), (i, B)
+        sa, sb = _state(a), _state(b)
+        for k in sa:
+            assert torch.equal(sa[k], sb[k]), (i, B, k)
+    a.optimizer.check_status(cuda)
+    b.optimizer.check_status(cuda)
+
+
 @pytest.mark.parametrize("fused", [False, True])
 def test_split_prep_bit_identical(cuda, monkeypatch, fused):
     """TT_SPLIT_PREP (each tower's bf16 loss operand prepared on its own
