@@ -198,7 +198,9 @@ __global__ void __launch_bounds__(kScanThreads) route_write_kernel(const KeyT* k
       }
       atomicAdd(&cnt[static_cast<int>(ot / num_tags)], 1);
     }
-    if (w1.send) w1.idx[vals[i]] = static_cast<int32_t>(u < w1.cap ? u : w1.cap - 1);
+    // a dropped request's lookups get the sentinel -1 - owner (owner 0 here):
+    // gathers read a zero row for them, the sparse sums skip them
+    if (w1.send) w1.idx[vals[i]] = static_cast<int32_t>(u < w1.cap ? u : -1);
     else idx[vals[i]] = u;
     if (order) order[i] = static_cast<int32_t>(vals[i]);
     if (grp_first) {  // first / last sorted position of each (owner, tag) group
@@ -278,9 +280,10 @@ __global__ void __launch_bounds__(256) route_pad_kernel(const int32_t* send, con
       const int mid = (lo + hi + 1) >> 1;
       if (start[mid] <= u) lo = mid; else hi = mid - 1;
     }
-    long long j = u - start[lo];
-    if (j >= cap) j = cap - 1;  // dropped request (counted in *overflow): a defined slot
-    idx_padded[t] = static_cast<int32_t>(static_cast<int64_t>(lo) * cap + j);
+    const long long j = u - start[lo];
+    // dropped request (counted in *overflow): the sentinel -1 - owner (no slot;
+    // a gather reads a zero row, the sparse sums skip it)
+    idx_padded[t] = j < cap ? static_cast<int32_t>(static_cast<int64_t>(lo) * cap + j) : -1 - lo;
   }
 }
 
@@ -534,8 +537,8 @@ __global__ void __launch_bounds__(kRsThreads) route_fixed_small_kernel(const Rou
     const int o = static_cast<int>(g / static_cast<uint32_t>(T));
     const int tag = static_cast<int>(g - static_cast<uint32_t>(o * T));
     const int64_t j = u - start[o];
-    const int64_t slot = static_cast<int64_t>(o) * a.cap + (j < a.cap ? j : a.cap - 1);
-    a.idx_padded[pos] = static_cast<int32_t>(slot);
+    const int64_t slot = static_cast<int64_t>(o) * a.cap + j;
+    a.idx_padded[pos] = j < a.cap ? static_cast<int32_t>(slot) : -1 - o;  // dropped: sentinel -1 - owner
     if (a.order) a.order[p] = pos;
     if (a.grp_first) {
       if (p == 0 || (kp >> a.id_bits) != g) a.grp_first[g] = p;

@@ -1419,11 +1419,17 @@ __global__ void __launch_bounds__(kRoutedThreads) routed_keys_kernel(const Job j
     const int lk = r.order[i];
     const int l = static_cast<int>(lk / j.batch);
     const int b = static_cast<int>(lk - static_cast<int64_t>(l) * j.batch);
+    // a request dropped by a small route capacity carries the slot sentinel
+    // -1 - owner: its lookups keep their place in the (owner, tag) group and
+    // take the invalid key with no gradient (like an out-of-range id: never
+    // applied, never written — an invalid run may sit mid-region; block_sum
+    // and join only need equal keys contiguous)
     const int s = r.slot[lk];
-    const int g = static_cast<int>(s / r.cap) * T + r.lk_tag[l];
+    const int o = s >= 0 ? static_cast<int>(s / r.cap) : -1 - s;
+    const int g = o * T + r.lk_tag[l];
     const int dst = r.lk_base[l] + pre[g] + static_cast<int>(i - r.grp_first[g]);
-    uint32_t id = static_cast<uint32_t>(s);
-    if (r.slot_row) {
+    uint32_t id = s >= 0 ? static_cast<uint32_t>(s) : invalid;
+    if (r.slot_row && s >= 0) {
       const int32_t row = r.slot_row[s];
       id = row >= 0 ? static_cast<uint32_t>(row) : invalid;
     }

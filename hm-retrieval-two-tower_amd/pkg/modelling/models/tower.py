@@ -47,6 +47,17 @@ def _rows(p: dict) -> torch.Tensor:
     return hip_ops.mlp_rows(q.pop("a"), q.pop("img"), q.pop("k"), q.pop("n"), q.pop("out"), **q)
 
 
+def _aligned(t: torch.Tensor, width: Optional[int] = None) -> torch.Tensor:
+    """t itself when its rows are 16-B aligned and it has `width` columns
+    (default: its own), else a copy with 16-B rows, zero-padded to `width`."""
+    width = t.shape[1] if width is None else width
+    if t.stride(1) == 1 and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0 and t.shape[1] == width:
+        return t
+    out = torch.zeros(t.shape[0], (width + 3) // 4 * 4, dtype=t.dtype, device=t.device)
+    out[:, :t.shape[1]] = t
+    return out[:, :width]
+
+
 def _wgrad(p: dict) -> torch.Tensor:
     q = dict(p)
     return hip_ops.mlp_wgrad(q.pop("a"), q.pop("g"), q.pop("dwb"), **q)
@@ -79,6 +90,10 @@ class DenseStack:
         off = 0
         fan_in = in_dim
         for u in units:
+            if not 1 <= u <= 384 or fan_in > 384:
+                # tt_mlp_rows' output width (the forward's units, the input
+                # gradient's fan-in) is at most 384: no fallback GEMM
+                raise ValueError(f"Dense layer {fan_in} -> {u}: widths must be in 1..384 (tt_mlp_rows)")
             self.layout.append((off, fan_in, u, off + fan_in * u))
             off += fan_in * u + u
             fan_in = u
@@ -126,8 +141,12 @@ class DenseStack:
 
     def _fwd_problem(self, li: int, h: torch.Tensor, flat: torch.Tensor, imgs) -> dict:
         w, b = self.params(flat)[li]
-        out = torch.empty(h.shape[0], w.shape[1], dtype=torch.float32, device=h.device)
-        return dict(a=h, img=imgs[("f", li)], k=w.shape[0], n=w.shape[1], out=out, bias=b, relu=True)
+        n = w.shape[1]
+        # hidden layers: 16-B output rows (the next layer's A operand); the top
+        # layer's output (the joint embedding) stays contiguous
+        ld = n if li == len(self.layout) - 1 else (n + 3) // 4 * 4
+        out = torch.empty(h.shape[0], ld, dtype=torch.float32, device=h.device)[:, :n]
+        return dict(a=h, img=imgs[("f", li)], k=w.shape[0], n=n, out=out, bias=b, relu=True)
 
     def forward_acts(self, x: torch.Tensor, flat: torch.Tensor) -> List[torch.Tensor]:
         """[x, h_1, ..., h_L] with h_l = relu(h_{l-1} W_l + b_l) (tt_mlp_rows)."""
@@ -139,8 +158,9 @@ class DenseStack:
         return acts
 
     def _wgrad_fits(self, li: int, g: torch.Tensor, acts: List[torch.Tensor]) -> bool:
-        """tt_mlp_wgrad's contract for layer li: N % 4 == 0, N and K <= 4096,
-        16-B aligned rows of its activations, gradient and mask operands."""
+        """tt_mlp_wgrad's alignment contract for layer li: N % 4 == 0 and
+        16-B aligned rows of its activations, gradient and mask operands
+        (widths over 384 are refused when the stack is built)."""
         _, fi, fo, _ = self.layout[li]
         for t in (g, acts[li], acts[-1]):
             if t.stride(1) != 1 or t.stride(0) % 4 or t.data_ptr() % 16:
@@ -156,13 +176,27 @@ class DenseStack:
             return dict(a=acts[li], g=gout, dwb=dwb, gmask=acts[-1], scale=gscale)
         return dict(a=acts[li], g=g, dwb=dwb)
 
-    def _wgrad_torch(self, li: int, acts, gflat, g, gscale) -> None:
-        """The weight gradient outside tt_mlp_wgrad's contract (torch)."""
+    def _wgrad_padded(self, li: int, acts, gflat, g, gscale) -> None:
+        """The weight gradient outside tt_mlp_wgrad's alignment contract (an
+        output width that is not a multiple of 4, or unaligned operand rows):
+        the same tt_mlp_wgrad on zero-padded copies — operands with 16-B rows
+        of width ceil4(N) (the padding columns of G are zero, so their
+        gradient columns are zero and dropped) — then the [K + 1, N] block
+        copied into the flat gradient.  The same sums in the same order as an
+        aligned layer's (no vendor GEMM)."""
         w_off, fi, fo, _ = self.layout[li]
         dwb = gflat[w_off:w_off + (fi + 1) * fo].view(fi + 1, fo)
-        gm = g * (acts[-1] > 0) * (gscale if gscale is not None else 1.0) if li == len(self.layout) - 1 else g
-        torch.mm(acts[li].t(), gm, out=dwb[:fi])
-        torch.sum(gm, 0, out=dwb[fi])
+        top = li == len(self.layout) - 1
+        n4 = (fo + 3) // 4 * 4
+
+        a = _aligned(acts[li])
+        gp = _aligned(g, n4)
+        out = torch.empty(fi + 1, n4, dtype=torch.float32, device=g.device)
+        if top:
+            hip_ops.mlp_wgrad(a, gp, out, gmask=_aligned(acts[-1], n4), scale=gscale)
+        else:
+            hip_ops.mlp_wgrad(a, gp, out)
+        dwb.copy_(out[:, :fo])
 
     def _igrad_problem(self, li: int, acts, g, gscale) -> dict:
         """G_{l-1} = (G_l W_l^T) * relu'(h_{l-1}) (the top layer's relu mask and
@@ -171,8 +205,11 @@ class DenseStack:
         top = li == len(self.layout) - 1
         ld = (fi + 3) // 4 * 4  # 16-B rows for the kernel's vector stores
         out = torch.empty(g.shape[0], ld, dtype=torch.float32, device=g.device)[:, :fi]
+        amask = acts[-1] if top else None
+        if top and fo % 4:  # the joint embedding's rows are not 16-B: aligned copies
+            g, amask = _aligned(g), _aligned(amask)
         return dict(a=g, img=self.__dict__["_images"][("t", li)], k=fo, n=fi, out=out,
-                    amask=acts[-1] if top else None, scale=gscale if top else None,
+                    amask=amask, scale=gscale if top else None,
                     cmask=acts[li] if li > 0 else None)
 
     def backward_acts(self, acts: List[torch.Tensor], flat: torch.Tensor, gout: torch.Tensor,
@@ -183,10 +220,9 @@ class DenseStack:
         its loads), then ONE tt_mlp_rows for the layer below:
         G_{l-1} = (G_l W_l^T) * relu'(h_{l-1}) (the top layer's relu mask and
         scale applied to its A loads), or the input gradient dx = G_1 W_1^T.
-        gout is not modified.  A layer outside tt_mlp_wgrad's contract (output
-        width not a multiple of 4, or wider than 4096) takes its weight
-        gradient from torch (the only vendor GEMM left, never at the
-        reference's configurations).  Images: packed by this step's forward
+        gout is not modified.  A layer outside tt_mlp_wgrad's alignment
+        contract (output width not a multiple of 4) runs it on zero-padded
+        copies (_wgrad_padded).  Images: packed by this step's forward
         (same flat).  With TT_IGRAD_FIRST=1 the input-gradient chain runs
         before the weight gradients, and on_dx(dx), if given, is called
         between them (the fused step's embedding update); the kernels and
@@ -232,7 +268,7 @@ class DenseStack:
                 self.fused_applied.add(li)
             _wgrad(p)
         else:
-            self._wgrad_torch(li, acts, gflat, g, gscale)
+            self._wgrad_padded(li, acts, gflat, g, gscale)
 
     def __call__(self, x: torch.Tensor) -> torch.Tensor:
         if torch.is_grad_enabled() and (x.requires_grad or self.flat.requires_grad):
@@ -281,7 +317,7 @@ def backward_acts_pair(stacks, acts, flats, gouts, gscale, need_input_grad):
                     p = st._wgrad_problem(li, acts[t], gflats[t], gouts[t], gs[t], gscale)
                     _wgrad(p)
                 else:
-                    st._wgrad_torch(li, acts[t], gflats[t], gs[t], gscale)
+                    st._wgrad_padded(li, acts[t], gflats[t], gs[t], gscale)
         want = [li > 0 or need_input_grad[t] for t in range(2)]
         probs = [st._igrad_problem(li, a, g, gscale) if w else None
                  for st, a, g, w in zip(stacks, acts, gs, want)]

@@ -119,13 +119,10 @@ class TwoTowerModel(AbstractKerasModel):
         (hip_ops.score_matrix, bf16x3 MFMA: fp32-faithful); with gradients
         enabled it is hip_ops.ScoreMatrix, whose backward GEMMs (dQ = G.C,
         dC = G^T.Q) run on the same kernel, so a caller can differentiate
-        through it (the reference's tf.matmul semantics).  Host tensors
-        (no GPU) take torch.matmul."""
+        through it (the reference's tf.matmul semantics)."""
         q, c = self._split(x)
         with torch.set_grad_enabled(training and torch.is_grad_enabled()):
             qe, ce = self.query_tower.call(q), self.candidate_tower.call(c)
-            if not qe.is_cuda:
-                return torch.matmul(qe, ce.t())
             if torch.is_grad_enabled():
                 return hip_ops.ScoreMatrix.apply(qe, ce)
             return hip_ops.score_matrix(qe, ce)

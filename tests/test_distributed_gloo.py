@@ -198,9 +198,14 @@ def _cpu_embedding_ops(routed: bool = False):
         if op == "sum":
             return scatter_sum(specs, batch, grad)
         rows = route["slot_row"]
-        return sparse_adagrad([dict(sp, ids=[rows[i.long()] for i in sp["ids"]]) for sp in specs], batch, grad, lr, eps)
+        # a dropped request's lookups carry the sentinel -1 - owner: no row
+        key = lambda i: torch.where(i >= 0, rows[i.long().clamp(min=0)], torch.full_like(i, -1))
+        return sparse_adagrad([dict(sp, ids=[key(i) for i in sp["ids"]]) for sp in specs], batch, grad, lr, eps)
+
+    from torch_route import torch_route_owner, torch_route_pad, torch_route_requests
 
     return EmbeddingOps(gather_multi, gather_tagged, scatter_sum, sparse_adagrad, dense_adagrad,
+                        torch_route_requests, torch_route_owner, torch_route_pad,
                         sparse_routed=sparse_routed if routed else None)
 
 
@@ -217,7 +222,8 @@ def _sharded_worker(rank, world, port, tables, lookups, grads, out):
         st = ShardedTables({k: torch.from_numpy(v) for k, v in tables.items()}, 0.1, ops=_cpu_embedding_ops())
         ov = torch.zeros(1, dtype=torch.int32)
         got, idx = st.fetch(lk, capacity=cap, overflow=ov)
-        fwd = [got[i.long()].numpy() for i in idx]
+        # a dropped request's lookups carry the slot sentinel -1 - owner: zero rows
+        fwd = [torch.where((i >= 0)[:, None], got[i.long().clamp(min=0)], torch.zeros(())).numpy() for i in idx]
         st.apply([(g, [(idx[l], 16 * l) for l in range(len(lk))])], lr=0.05, eps=1e-7)
         res[mode] = (fwd, {k: st.gather_full(k).numpy() for k in tables}, int(ov.item()))
     # route_fixed + fetch_routed + apply_lookups (per-lookup gradients): the
@@ -295,6 +301,33 @@ def test_sharded_tables_match_unsharded_adagrad(world):
                 reqs[key] = (int(v) % world) if 0 <= v < n else world - 1
         per_owner = np.bincount(list(reqs.values()), minlength=world)
         assert out[r]["small"][2] == int(np.maximum(per_owner - 5, 0).sum()) > 0
+    # ... and the dropped requests' lookups read zero rows and add no gradient,
+    # while the kept requests (per owner the first 5 in the route's (tag, row)
+    # order, an invalid id first) and every untouched row stay exact
+    names = list(tables)
+    kept_g = {k: np.zeros_like(v) for k, v in ref.items()}
+    for r in range(world):
+        per = {}
+        for name, idsl in lookups:
+            n = tables[name].shape[0]
+            for v in np.unique(idsl[r]):
+                ok = 0 <= v < n
+                o = int(v) % world if ok else world - 1
+                per.setdefault(o, set()).add((names.index(name), int(v) + 1 if ok else 0))
+        kept = {(names[t], rp - 1) for o in per for t, rp in sorted(per[o])[:5]}
+        for l, (name, idsl) in enumerate(lookups):
+            ok = np.array([(name, int(v)) in kept for v in idsl[r]]) & (idsl[r] >= 0)
+            exp = np.zeros((B, D), np.float32)
+            exp[ok] = tables[name][idsl[r][ok]]
+            assert np.array_equal(out[r]["small"][0][l], exp)
+            np.add.at(kept_g[name], idsl[r][ok], grads[r][ok, 16 * l:16 * l + D])
+    for k in tables:
+        touched = np.abs(kept_g[k]).sum(1) > 0
+        a = 0.1 + kept_g[k] ** 2
+        exp = np.where(touched[:, None], tables[k] - 0.05 * kept_g[k] / (np.sqrt(a) + 1e-7), tables[k])
+        for r in range(world):
+            np.testing.assert_allclose(out[r]["small"][1][k], exp, rtol=0, atol=2e-6)
+            assert np.array_equal(out[r]["small"][1][k][~touched], tables[k][~touched])
 
 
 def _global_loss_worker(rank, world, port, q, c, logq, out):

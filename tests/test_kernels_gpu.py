@@ -507,10 +507,10 @@ def test_recall_hits(cuda):
 @pytest.mark.parametrize("world", [1, 3, 8])
 def test_route_requests_match_torch_restatement(cuda, world):
     """tt_route_requests / tt_route_owner equal the torch restatement
-    (distributed.torch_route_requests) element for element: owner-major
+    (tests/torch_route.py) element for element: owner-major
     deduplicated requests (tag, then row ascending; invalid ids as row -1 on
     rank world-1), per-owner counts and each lookup's request position."""
-    from pkg.modelling.distributed import torch_route_owner, torch_route_requests
+    from torch_route import torch_route_owner, torch_route_requests
 
     rng = np.random.default_rng(world)
     B = 3000
@@ -721,10 +721,10 @@ def test_mlp_wgrad_pair_equals_single(cuda, shapes, masked):
 @pytest.mark.parametrize("world,cap_frac", [(1, None), (3, None), (8, None), (8, 0.1)])
 def test_route_pad_matches_torch_restatement(cuda, world, cap_frac):
     """tt_route_pad: the compact requests laid into fixed per-owner slots
-    equal distributed.torch_route_pad (slots, padding, each lookup's slot and
+    equal torch_route.torch_route_pad (slots, padding, each lookup's slot and
     the overflow count), at the never-overflowing capacity (every lookup
     distinct) and at one that drops requests."""
-    from pkg.modelling.distributed import torch_route_pad
+    from torch_route import torch_route_pad
 
     rng = np.random.default_rng(10 + world)
     B = 2048
@@ -812,11 +812,12 @@ def test_sparse_adagrad_rows_equals_sorted_apply_on_distinct_rows(cuda, dim):
         assert torch.equal(x, y)
 
 
-def _routed_case(cuda, world, B, seed, invalid=False):
+def _routed_case(cuda, world, B, seed, invalid=False, cap=None):
     """Three sharded tables, five lookups (two tables with two sources each,
     Zipf ids with long duplicate runs), routed with tt_route_requests_ordered
-    + tt_route_pad at `world`: the lookups, the route tensors and per table
-    its (lookup, source) list."""
+    + tt_route_pad at `world` (cap: slots per owner, default never
+    overflowing): the lookups, the route tensors and per table its (lookup,
+    source) list."""
     rng = np.random.default_rng(seed)
     rows = [5000, 1371980, 700]
     tags = [0, 1, 1, 2, 0]
@@ -826,7 +827,7 @@ def _routed_case(cuda, world, B, seed, invalid=False):
         ids[3][::71] = 700 + 5
     lookups = [(_t(x, cuda), rows[t], t) for x, t in zip(ids, tags)]
     send, counts, _, idx, order = hip_ops.route_requests(lookups, world, 3, ordered=True)
-    cap = len(tags) * B
+    cap = len(tags) * B if cap is None else cap
     sp, ip = hip_ops.route_pad(send, counts, idx, world, cap)
     _, rws, _ = hip_ops.route_owner(sp, world, 3)
     tab_of_tag = {0: 0, 1: 1, 2: 2}
@@ -867,13 +868,63 @@ def test_sparse_routed_sum_equals_scatter_sum(cuda, world):
     assert (g1 != 7.0).any()
 
 
-@pytest.mark.parametrize("B", [512, 16384])
-def test_sparse_routed_adagrad_world1_equals_sparse_adagrad(cuda, B):
+@pytest.mark.parametrize("world", [1, 3, 8])
+def test_sparse_routed_sum_under_overflow(cuda, world):
+    """A route capacity too small for the batch: the dropped requests'
+    lookups carry the slot sentinel -1 - owner, add nothing anywhere, and
+    every kept slot holds exactly its own lookups' sum (fp64 reference,
+    within the fp32 summation bound) — tt_sparse_routed and
+    tt_sparse_scatter_sum alike; unreferenced slots stay untouched."""
+    B, D = 4096, 64
+    cap = max(64, 5 * B // (8 * world))
+    rows, tags, ids, ip, _, route, src = _routed_case(cuda, world, B, 60 + world, invalid=True, cap=cap)
+    ipn = ip.cpu().numpy()
+    assert (ipn < 0).any() and (ipn >= 0).any()
+    own = np.where(ipn >= 0, ipn // cap, -1 - ipn)
+    assert ((own >= 0) & (own < world)).all()
+    rng = np.random.default_rng(world + 100)
+    grads = [torch.as_tensor(rng.standard_normal((B, 3 * D)).astype(np.float32), device=cuda) for _ in range(3)]
+    slots = world * cap
+    exp = np.zeros((slots, D))
+    absum = np.zeros((slots, D))
+    hit = np.zeros(slots, bool)
+    for t in range(3):
+        g = grads[t].cpu().numpy().astype(np.float64)
+        for l in src[t]:
+            ok = ipn[l] >= 0
+            np.add.at(exp, ipn[l][ok], g[ok, D * (l % 3):D * (l % 3) + D])
+            np.add.at(absum, ipn[l][ok], np.abs(g[ok, D * (l % 3):D * (l % 3) + D]))
+            hit[ipn[l][ok]] = True
+
+    def specs(g_req):
+        return [dict(table=g_req, ids=[ip[l] for l in src[t]], grad_col_offset=[D * (l % 3) for l in src[t]],
+                     grad=grads[t]) for t in range(3)]
+
+    for run in ("routed", "scatter"):
+        g = torch.full((slots, D), 7.0, device=cuda)
+        if run == "routed":
+            hip_ops.sparse_routed(specs(g), B, None, route, "sum")
+        else:
+            hip_ops.sparse_scatter_sum(specs(g), B, grads[0])
+        got = g.cpu().numpy()
+        assert (got[~hit] == 7.0).all(), run
+        bound = 2 * B * 2.0 ** -24 * absum[hit] + 1e-30
+        assert (np.abs(got[hit] - exp[hit]) <= bound).all(), run
+
+
+@pytest.mark.parametrize("B,small", [(512, False), (16384, False), (16384, True)])
+def test_sparse_routed_adagrad_world1_equals_sparse_adagrad(cuda, B, small):
     """At world 1 tt_sparse_routed (op Adagrad, keys = the owner's local rows
     per slot) is the single-GPU tt_sparse_adagrad on the raw ids: tables and
-    accumulators bit-identical, two sources per table included."""
+    accumulators bit-identical, two sources per table included.  small: a
+    capacity that drops requests — their lookups (slot sentinel -1) update
+    nothing, as if their ids were invalid; rows nobody kept stay untouched."""
     D = 128
-    rows, tags, ids, ip, rws, route, src = _routed_case(cuda, 1, B, B)
+    rows, tags, ids, ip, rws, route, src = _routed_case(cuda, 1, B, B, cap=B if small else None)
+    if small:
+        ipn = ip.cpu().numpy()
+        assert (ipn < 0).any() and (ipn == -1).sum() == (ipn < 0).sum()
+        ids = [np.where(ipn[l] >= 0, ids[l], -1).astype(np.int32) for l in range(len(ids))]
     route["slot_row"] = rws
     rng = np.random.default_rng(B + 1)
     grads = [torch.as_tensor(rng.standard_normal((B, 2 * D)).astype(np.float32), device=cuda) for _ in range(3)]
@@ -892,6 +943,12 @@ def test_sparse_routed_adagrad_world1_equals_sparse_adagrad(cuda, B):
     for x, y in zip(t1 + a1, t2 + a2):
         assert torch.equal(x, y)
     assert not torch.equal(t1[1], tabs[1])
+    if small:  # rows no kept lookup names are bit-for-bit untouched
+        for t in range(3):
+            named = np.zeros(rows[t], bool)
+            for l in src[t]:
+                named[ids[l][ids[l] >= 0]] = True
+            assert torch.equal(t1[t][torch.as_tensor(~named, device=cuda)], tabs[t][torch.as_tensor(~named, device=cuda)])
 
 
 @pytest.mark.parametrize("world,B", [(1, 2048), (3, 2048), (8, 1024), (1, 16384), (2, 16384)])
@@ -952,3 +1009,42 @@ def test_scatter_sum_presorted_equals_one_call(cuda):
     torch.cuda.synchronize()
     assert torch.equal(a0, b0) and torch.equal(a1, b1)
     assert (a0 != 0).any() and (a1 != 0).any()
+
+
+@pytest.mark.parametrize("in_dim,units,top_grad", [(37, [66, 130], True), (258, [256, 130], True),
+                                                   (42, [6, 3], False)])
+def test_dense_stack_odd_widths_vs_torch_fp64(cuda, in_dim, units, top_grad):
+    """DenseStack layers whose widths are not multiples of 4 (e.g.
+    joint_embedding_size=130 through the public API) stay on libtt: hidden
+    outputs with 16-B rows, the weight gradient on zero-padded operands
+    (no vendor GEMM).  Forward, every weight / bias gradient and the input
+    gradient against torch fp64 autograd, fp32-faithful bound 2e-5."""
+    from pkg.modelling.models.tower import DenseStack
+
+    gen = torch.Generator()
+    gen.manual_seed(in_dim + sum(units))
+    st = DenseStack(in_dim, units, cuda, gen)
+    M = 3000
+    x = torch.randn(M, (in_dim + 3) // 4 * 4, device=cuda)[:, :in_dim]
+    flat = st.flat.detach()
+    acts = st.forward_acts(x, flat)
+    gout = torch.randn(M, units[-1], device=cuda)
+    s = torch.full((1,), 0.5, device=cuda) if top_grad else None
+    dx, gflat = st.backward_acts(acts, flat, gout.contiguous(), s, True)
+    # torch fp64 reference
+    fd = flat.double().clone().requires_grad_(True)
+    xd = x.double().clone().requires_grad_(True)
+    h = xd
+    for w_off, fi, fo, b_off in st.layout:
+        h = torch.relu(h @ fd[w_off:w_off + fi * fo].view(fi, fo) + fd[b_off:b_off + fo])
+    assert float((acts[-1].double() - h).norm() / h.norm()) < 2e-5
+    (h * gout.double() * (0.5 if top_grad else 1.0)).sum().backward()
+    assert float((gflat.double() - fd.grad).norm() / fd.grad.norm()) < 2e-5
+    assert float((dx.double() - xd.grad).norm() / xd.grad.norm()) < 2e-5
+
+
+def test_dense_stack_refuses_widths_over_384(cuda):
+    from pkg.modelling.models.tower import DenseStack
+
+    with pytest.raises(ValueError, match="384"):
+        DenseStack(128, [512, 128], cuda, torch.Generator())
