@@ -286,7 +286,17 @@ def time_inbatch_kernel(model, data, device, B: int, reps: int = 20):
     ms_rows_b = sum(a.elapsed_time(b) for a, b in rb) / (calls * burst)
     ms_cols_b = sum(a.elapsed_time(b) for a, b in cb) / (calls * burst)
     flops = 4.0 * B * B * E  # S (2 B^2 E) + P.C (2 B^2 E) per pass
-    return flops, (ms_rows_b, ms_rows), (ms_cols_b, ms_cols), ms_entry
+    # the opt-in fp32-faithful entry (bf16x3 scores, TT_INBATCH_X3=1): its cost
+    for _ in range(3):
+        hip_ops.inbatch_fused(q, c, logq, x3=True)
+    e0, e1 = ev(), ev()
+    e0.record(stream)
+    for _ in range(reps):
+        hip_ops.inbatch_fused(q, c, logq, x3=True)
+    e1.record(stream)
+    e1.synchronize()
+    ms_x3 = e0.elapsed_time(e1) / reps
+    return flops, (ms_rows_b, ms_rows), (ms_cols_b, ms_cols), ms_entry, ms_x3
 
 
 def pmc_traffic(kernel: str):
@@ -300,10 +310,19 @@ def pmc_traffic(kernel: str):
         return None
     with open(files[-1]) as f:
         d = json.load(f)
-    for k, v in d.items():
-        if kernel in k and isinstance(v, dict):
-            return {"bytes_per_launch": v["hbm_bytes_per_launch"], "source": os.path.relpath(files[-1], ROOT)}
+    for name in _name_variants(kernel):
+        for k, v in d.items():
+            if name in k and isinstance(v, dict):
+                return {"bytes_per_launch": v["hbm_bytes_per_launch"], "source": os.path.relpath(files[-1], ROOT)}
     return None
+
+
+def _name_variants(kernel: str):
+    """The in-batch pass's rocprof name with the round-6 X3 template flag
+    (`<128, 0, false>`), then as older profiles hold it (`<128, 0>`)."""
+    if kernel.startswith("inbatch_pass_kernel<") and kernel.endswith(">") and kernel.count(",") == 1:
+        return [kernel[:-1] + ", false>", kernel]
+    return [kernel]
 
 
 def _graph_time(fn, reps: int) -> float:
@@ -360,7 +379,8 @@ def time_gather_uniform(model, device, B: int, reps: int = 50, c5_rows: int = 10
     gbs = nbytes / (ms * 1e-3) / 1e9
     out = {"kernel": "gather_grouped_kernel, C3 step shapes, uniform ids", "bound": "hbm", "achieved": gbs,
            "peak": MI355X_HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / MI355X_HBM_PEAK_GBS,
-           "algorithmic_bytes_per_launch": nbytes, "ms_per_launch": ms}
+           "algorithmic_bytes_per_launch": nbytes, "ms_per_launch": ms,
+           "copy_floor": copy_floor(device, nbytes, ms, reps)}
     if c5_rows:
         table = torch.empty(c5_rows, 128, device=device)  # 51.2 GB; contents irrelevant to the rate
         ids = torch.randint(0, c5_rows, (c5_batch,), generator=g, device=device, dtype=torch.int32)
@@ -377,6 +397,24 @@ def time_gather_uniform(model, device, B: int, reps: int = 50, c5_rows: int = 10
     return out
 
 
+def copy_floor(device, nbytes: int, gather_ms: float, reps: int = 50) -> dict:
+    """The launch-size floor of an HBM-bound kernel moving `nbytes`: a plain
+    device copy of nbytes / 2 read + nbytes / 2 written (torch's vectorised
+    copy kernel; no index loads, fully coalesced, HBM-resident source of
+    nbytes / 2 > L2), timed like the gather (one hipGraph of `reps` launches).
+    What the gather's launch of the same bytes can at best approach:
+    frac_of_copy = copy ms / gather ms."""
+    n = nbytes // 8
+    src = torch.rand(n, device=device)
+    dst = torch.empty_like(src)
+    # twelve rotating sources (30 MB each, 365 MB with dst > the 256 MB Infinity Cache): HBM reads
+    srcs = [src] + [torch.rand(n, device=device) for _ in range(11)]
+    it = iter(range(1 << 30))
+    ms = _graph_time(lambda: dst.copy_(srcs[next(it) % 12]), reps)
+    return {"kernel": "torch device copy (the same bytes, half read, half written)", "ms_per_launch": ms,
+            "achieved": nbytes / (ms * 1e-3) / 1e9, "unit": "GB/s", "frac_of_copy": ms / gather_ms}
+
+
 def rocprof_avg_ms(kernel: str):
     """Average duration (ms) of `kernel` in the newest committed rocprofv3
     --stats summary (profiles/*_bench_kernel_stats.csv), or None."""
@@ -387,8 +425,10 @@ def rocprof_avg_ms(kernel: str):
     if not files:
         return None
     with open(files[-1]) as f:
-        for r in csv.DictReader(f):
-            if kernel in r["Name"]:
+        rows = list(csv.DictReader(f))
+    for name in _name_variants(kernel):
+        for r in rows:
+            if name in r["Name"]:
                 return {"ms": float(r["AverageNs"]) * 1e-6, "calls": int(r["Calls"]),
                         "source": os.path.relpath(files[-1], ROOT)}
     return None
@@ -973,7 +1013,7 @@ def main():
     model, data = build_model(device, rank, args.fused_apply)
     B = args.batch
     # kernel-level timings on the unsharded model, before the train step takes its tables
-    flops, ms_rows, ms_cols, ms_entry = time_inbatch_kernel(model, data, device, B)
+    flops, ms_rows, ms_cols, ms_entry, ms_x3 = time_inbatch_kernel(model, data, device, B)
     gather = time_gather(model, data, device, B)
     if ws == 1 and not args.no_uniform_gather:
         gather["uniform_ids"] = time_gather_uniform(model, device, B)
@@ -1027,6 +1067,7 @@ def main():
                           "ms_per_launch_one_event_pair_each": ms_cols_1,
                           "achieved": flops / (ms_cols * 1e-3) / 1e12},
             "ms_fused_entry": ms_entry,
+            "ms_fused_entry_x3": ms_x3,
             "algorithmic_flops_per_launch": flops,
         },
         "gather_roofline": gather,

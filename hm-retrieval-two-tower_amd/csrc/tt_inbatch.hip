@@ -100,6 +100,7 @@ struct PrepJob {
   float* bias;
   float* bias2;
   int vec;  // src 16-B aligned, ld % 4 == 0, dim % 4 == 0: float4 loads
+  __bf16* dst_lo;  // x3 mode: also the residual plane bf16(x - bf16(x)) (NULL: none)
 };
 
 template <int D>
@@ -130,6 +131,17 @@ __global__ void __launch_bounds__(256) prep_kernel(PrepJob j0, PrepJob j1, int d
     v.z = pack_bf16x2(x[4], x[5]);
     v.w = pack_bf16x2(x[6], x[7]);
     *reinterpret_cast<u32x4*>(j.dst + r * D + c8) = v;
+    if (j.dst_lo) {  // x = hi + lo + O(2^-16 |x|): the bf16x3 products' operands
+      float e[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) e[u] = x[u] - static_cast<float>(static_cast<__bf16>(x[u]));
+      u32x4 w;
+      w.x = pack_bf16x2(e[0], e[1]);
+      w.y = pack_bf16x2(e[2], e[3]);
+      w.z = pack_bf16x2(e[4], e[5]);
+      w.w = pack_bf16x2(e[6], e[7]);
+      *reinterpret_cast<u32x4*>(j.dst_lo + r * D + c8) = w;
+    }
   }
   if (j.bias && threadIdx.x < 32) {
     const int64_t r = r0 + threadIdx.x;
@@ -149,6 +161,8 @@ struct PassArgs {
   float* part_m;          // [S, n_stat_pad]   (rows pass; log2 units, integer valued)
   float* part_l;          // [S, n_stat_pad]   (rows pass)
   float* part_o;          // [S, n_stat_pad, D]
+  const __bf16* stat_lo;  // x3 mode: residual planes of the stationary / streamed rows
+  const __bf16* strm_lo;
 };
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -214,9 +228,18 @@ __device__ __forceinline__ void wait_vmcnt() {
 // Two workgroups per CU (<= 256 registers per lane): the second hides the
 // first's barrier and DMA waits.  At one per CU (the mask_diag of the
 // contract commit in its 64-bit form needed 302) the passes ran 25 % slower.
-template <int D, int MODE>
-__global__ void __launch_bounds__(kThreads, 2) inbatch_pass_kernel(const PassArgs a) {
+//
+// X3 (opt-in, tt_inbatch_softmax_xent_x3): fp32-faithful products — S and
+// P.V both from bf16x3 products hi.hi + hi.lo + lo.hi of split operands (x =
+// hi + lo, both bf16; P split the same way in registers), three MFMAs where
+// the default issues one; the streamed rows' lo image has a ring of its own
+// (LDS 129 KB at D = 128: one workgroup per CU).
+template <int D, int MODE, bool X3 = false>
+__global__ void __launch_bounds__(kThreads, X3 ? 1 : 2) inbatch_pass_kernel(const PassArgs a) {
   using G = Geo<D>;
+  constexpr int IMG = X3 ? 2 : 1;                           // bf16 images per streamed tile
+  constexpr int LO_OFF = kRingStages * G::A_BYTES;          // the lo ring (X3)
+  constexpr int BIAS_OFF = IMG * kRingStages * G::A_BYTES;
   extern __shared__ __attribute__((aligned(16))) char ring[];
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) / kWave);
   const int lane = lane_id();
@@ -233,12 +256,19 @@ __global__ void __launch_bounds__(kThreads, 2) inbatch_pass_kernel(const PassArg
 #pragma unroll
   for (int s = 0; s < G::KS; ++s)
     bfrag[s] = *reinterpret_cast<const bf16x8*>(a.stat + stat_row * D + 16 * s + 8 * h);
+  bf16x8 bfrag_lo[X3 ? G::KS : 1];
+  if constexpr (X3) {
+#pragma unroll
+    for (int s = 0; s < G::KS; ++s)
+      bfrag_lo[s] = *reinterpret_cast<const bf16x8*>(a.stat_lo + stat_row * D + 16 * s + 8 * h);
+  }
 
   // DMA plan: every wave moves PPW 1 KiB pieces of each tile image, wave 0
   // also the 64 biases.  Per-lane source offsets are tile-invariant (the
   // swizzle is applied on the source so pieces land lane-linear).
   const i32x4 desc = buffer_desc(a.strm, static_cast<unsigned>(a.n_strm_pad * D * 2));
   const i32x4 bdesc = buffer_desc(a.bias, static_cast<unsigned>(a.n_strm_pad * 4));
+  const i32x4 ldesc = buffer_desc(X3 ? a.strm_lo : a.strm, static_cast<unsigned>(a.n_strm_pad * D * 2));
   unsigned voff[G::PPW];
 #pragma unroll
   for (int u = 0; u < G::PPW; ++u) {
@@ -255,17 +285,22 @@ __global__ void __launch_bounds__(kThreads, 2) inbatch_pass_kernel(const PassArg
     const unsigned st = ring_lds + stage * G::A_BYTES;
 #pragma unroll
     for (int u = 0; u < G::PPW; ++u) dma_b128(desc, voff[u], row0 * (D * 2), st + (wave * G::PPW + u) * 1024);
-    if (wave == 0) dma_b32(bdesc, lane * 4, row0 * 4, ring_lds + G::BIAS_OFF + stage * (kTile * 4));
+    if constexpr (X3) {
+#pragma unroll
+      for (int u = 0; u < G::PPW; ++u)
+        dma_b128(ldesc, voff[u], row0 * (D * 2), st + LO_OFF + (wave * G::PPW + u) * 1024);
+    }
+    if (wave == 0) dma_b32(bdesc, lane * 4, row0 * 4, ring_lds + BIAS_OFF + stage * (kTile * 4));
   };
   // Wait until at most `ahead` issued tiles of this wave are still in flight.
   auto wait_tiles = [&](int ahead) {
     if (wave == 0) {
-      if (ahead >= 2) wait_vmcnt<2 * (G::PPW + 1)>();
-      else if (ahead == 1) wait_vmcnt<G::PPW + 1>();
+      if (ahead >= 2) wait_vmcnt<2 * (IMG * G::PPW + 1)>();
+      else if (ahead == 1) wait_vmcnt<IMG * G::PPW + 1>();
       else wait_vmcnt<0>();
     } else {
-      if (ahead >= 2) wait_vmcnt<2 * G::PPW>();
-      else if (ahead == 1) wait_vmcnt<G::PPW>();
+      if (ahead >= 2) wait_vmcnt<2 * IMG * G::PPW>();
+      else if (ahead == 1) wait_vmcnt<IMG * G::PPW>();
       else wait_vmcnt<0>();
     }
   };
@@ -300,6 +335,10 @@ __global__ void __launch_bounds__(kThreads, 2) inbatch_pass_kernel(const PassArg
   auto rd_a = [&](int stage, int i) {
     return *reinterpret_cast<const bf16x8*>(ring + rbase[i >> 1] + (stage * G::A_BYTES + (i & 1) * 32 * 2 * D));
   };
+  auto rd_a_lo = [&](int stage, int i) {  // X3: the same fragment of the lo image
+    return *reinterpret_cast<const bf16x8*>(ring + rbase[i >> 1] +
+                                            (LO_OFF + stage * G::A_BYTES + (i & 1) * 32 * 2 * D));
+  };
   auto rd_t = [&](int stage, int j) {
     const int dt = j % G::DT, g = j / G::DT;  // g = 2t + s2
     typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
@@ -308,8 +347,16 @@ __global__ void __launch_bounds__(kThreads, 2) inbatch_pass_kernel(const PassArg
     const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(ring + tbase[dt][1] + roff));
     return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   };
+  auto rd_t_lo = [&](int stage, int j) {  // X3: the same transposed read of the lo image
+    const int dt = j % G::DT, g = j / G::DT;
+    typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+    const int roff = LO_OFF + stage * G::A_BYTES + 16 * g * 2 * D;
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(ring + tbase[dt][0] + roff));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(ring + tbase[dt][1] + roff));
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
   auto rd_bias = [&](int stage, f32x16* sacc) {
-    const float* bias = reinterpret_cast<const float*>(ring + G::BIAS_OFF + stage * (kTile * 4)) + 4 * h;
+    const float* bias = reinterpret_cast<const float*>(ring + BIAS_OFF + stage * (kTile * 4)) + 4 * h;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -323,8 +370,14 @@ __global__ void __launch_bounds__(kThreads, 2) inbatch_pass_kernel(const PassArg
   auto scores_plain = [&](f32x16* sacc) {  // prologue: tile 0, stage 0
     rd_bias(0, sacc);
 #pragma unroll
-    for (int i = 0; i < 2 * G::KS; ++i)
-      sacc[i & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rd_a(0, i), bfrag[i >> 1], sacc[i & 1], 0, 0, 0);
+    for (int i = 0; i < 2 * G::KS; ++i) {
+      const bf16x8 ah = rd_a(0, i);
+      sacc[i & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bfrag[i >> 1], sacc[i & 1], 0, 0, 0);
+      if constexpr (X3) {
+        sacc[i & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bfrag_lo[i >> 1], sacc[i & 1], 0, 0, 0);
+        sacc[i & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(rd_a_lo(0, i), bfrag[i >> 1], sacc[i & 1], 0, 0, 0);
+      }
+    }
   };
   auto half_max = [&](const f32x16* sacc) {
     float m = -INFINITY;
@@ -371,7 +424,8 @@ __global__ void __launch_bounds__(kThreads, 2) inbatch_pass_kernel(const PassArg
     if constexpr (MODE == 0) mx = half_max(sa);
   }
 
-  constexpr int NS = 2 * G::KS;  // score MFMAs per tile
+  constexpr int NS = 2 * G::KS;  // score steps per tile (one MFMA each; three in X3)
+  constexpr int NSR = IMG * NS;  // score fragment reads per tile (X3: hi and lo)
   constexpr int NP = 4 * G::DT;  // P.V MFMAs per tile
 #ifndef TT_IB_AHEAD
 #define TT_IB_AHEAD 3
@@ -407,23 +461,36 @@ __global__ void __launch_bounds__(kThreads, 2) inbatch_pass_kernel(const PassArg
       __builtin_amdgcn_s_barrier();
     }
     // (after the last tile the look-ahead reads a stale stage: harmless, unused)
-    bf16x8 fr[AHEAD + 1];
-    auto prefetch = [&](int idx) {  // idx over the tile's NS + NP fragment reads
-      if (idx < NS) fr[idx % (AHEAD + 1)] = rd_a(NXT, idx);
-      else if (idx < NS + NP) fr[idx % (AHEAD + 1)] = rd_t(STG, idx - NS);
+    constexpr int FR = AHEAD + IMG;  // fragment ring: X3 consumes two reads per score step
+    bf16x8 fr[FR];
+    auto prefetch = [&](int idx) {  // idx over the tile's NSR + IMG * NP fragment reads
+      if (idx < NSR) {
+        if constexpr (X3) fr[idx % FR] = (idx & 1) ? rd_a_lo(NXT, idx >> 1) : rd_a(NXT, idx >> 1);
+        else fr[idx % FR] = rd_a(NXT, idx);
+      } else if (idx < NSR + IMG * NP) {
+        const int k = idx - NSR;
+        if constexpr (X3) fr[idx % FR] = (k & 1) ? rd_t_lo(STG, k >> 1) : rd_t(STG, k >> 1);
+        else fr[idx % FR] = rd_t(STG, k);
+      }
     };
     rd_bias(NXT, sn);
 #pragma unroll
     for (int i = 0; i < AHEAD; ++i) prefetch(i);
     const float mb = (MODE == 0) ? m_run : 0.0f;
     bf16x8 pf[4];
+    bf16x8 pf_lo[X3 ? 4 : 1];  // X3: P's residual plane (P.V as bf16x3 too)
     __builtin_amdgcn_sched_barrier(0);
 
     // Region A: S(tile+1) MFMAs || p = exp2(s log2e - m log2e), bf16 pack.
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
-      prefetch(i + AHEAD);
-      sn[i & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[i % (AHEAD + 1)], bfrag[i >> 1], sn[i & 1], 0, 0, 0);
+      prefetch(IMG * i + AHEAD);
+      if constexpr (X3) prefetch(IMG * i + 1 + AHEAD);
+      sn[i & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[(IMG * i) % FR], bfrag[i >> 1], sn[i & 1], 0, 0, 0);
+      if constexpr (X3) {
+        sn[i & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[(IMG * i) % FR], bfrag_lo[i >> 1], sn[i & 1], 0, 0, 0);
+        sn[i & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[(IMG * i + 1) % FR], bfrag[i >> 1], sn[i & 1], 0, 0, 0);
+      }
 #pragma unroll
       for (int k = i * EPS; k < (i + 1) * EPS; ++k) {
         sc[k >> 4][k & 15] = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[k >> 4][k & 15], kLog2e, -mb));
@@ -435,6 +502,17 @@ __global__ void __launch_bounds__(kThreads, 2) inbatch_pass_kernel(const PassArg
           pk.z = pack_bf16x2(sc[t][b + 4], sc[t][b + 5]);
           pk.w = pack_bf16x2(sc[t][b + 6], sc[t][b + 7]);
           pf[g] = __builtin_bit_cast(bf16x8, pk);
+          if constexpr (X3) {
+            float e[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) e[u] = sc[t][b + u] - static_cast<float>(static_cast<__bf16>(sc[t][b + u]));
+            u32x4 pl;
+            pl.x = pack_bf16x2(e[0], e[1]);
+            pl.y = pack_bf16x2(e[2], e[3]);
+            pl.z = pack_bf16x2(e[4], e[5]);
+            pl.w = pack_bf16x2(e[6], e[7]);
+            pf_lo[g] = __builtin_bit_cast(bf16x8, pl);
+          }
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -444,9 +522,16 @@ __global__ void __launch_bounds__(kThreads, 2) inbatch_pass_kernel(const PassArg
     float mxa = -INFINITY;
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-      prefetch(NS + j + AHEAD);
-      o[j % G::DT] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[(NS + j) % (AHEAD + 1)], pf[j / G::DT], o[j % G::DT],
+      prefetch(NSR + IMG * j + AHEAD);
+      if constexpr (X3) prefetch(NSR + IMG * j + 1 + AHEAD);
+      o[j % G::DT] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[(NSR + IMG * j) % FR], pf[j / G::DT], o[j % G::DT],
                                                               0, 0, 0);
+      if constexpr (X3) {
+        o[j % G::DT] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[(NSR + IMG * j) % FR], pf_lo[j / G::DT],
+                                                                o[j % G::DT], 0, 0, 0);
+        o[j % G::DT] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[(NSR + IMG * j + 1) % FR], pf[j / G::DT],
+                                                                o[j % G::DT], 0, 0, 0);
+      }
       // S(tile+1)'s positives out, half way through: its MFMAs have landed
       // by now (masked right after region A the wave waited for them: +4 %
       // per pass), and the next max below reads them after
@@ -864,33 +949,34 @@ int combine_cols(int D, hipStream_t st, const float* po, int nsplit, int64_t n_s
   return TT_OK;
 }
 
-template <int D, int MODE>
+template <int D, int MODE, bool X3>
 int launch_pass_d(dim3 grid, const PassArgs& a, hipStream_t st) {
-  constexpr int shm = Geo<D>::LDS_BYTES;
+  constexpr int shm = Geo<D>::LDS_BYTES + (X3 ? kRingStages * Geo<D>::A_BYTES : 0);
   if (shm > 65536) {
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(inbatch_pass_kernel<D, MODE>),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, shm);
+    static const hipError_t attr = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(inbatch_pass_kernel<D, MODE, X3>), hipFuncAttributeMaxDynamicSharedMemorySize, shm);
     TT_CHECK_HIP(attr);
   }
   const int probe = MODE == 0 ? TT_PROBE_INBATCH_ROWS : TT_PROBE_INBATCH_COLS;
   const int reps = probe_reps(probe);  // > 1 only for a repeat probe (the pass is idempotent)
   probe_begin(probe, st);
-  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((inbatch_pass_kernel<D, MODE>), grid, dim3(kThreads), shm, st, a);
+  for (int r = 0; r < reps; ++r)
+    hipLaunchKernelGGL((inbatch_pass_kernel<D, MODE, X3>), grid, dim3(kThreads), shm, st, a);
   probe_end(MODE == 0 ? TT_PROBE_INBATCH_ROWS : TT_PROBE_INBATCH_COLS, st);
   TT_CHECK_LAUNCH();
   return TT_OK;
 }
 
-template <int MODE>
+template <int MODE, bool X3 = false>
 int launch_pass(const Plan& p, const PassArgs& a, hipStream_t st) {
   // buffer descriptors address the bf16 images with 32-bit byte offsets
   if (p.strm_pad * p.D * 2 >= (1ll << 31))
     return fail(TT_ERR_UNSUPPORTED, "inbatch: %lld x %d streamed batch too large", (long long)p.strm_pad, p.D);
   dim3 grid(static_cast<unsigned>(p.stat_pad / kRowsPerWG), static_cast<unsigned>(p.split));
   switch (p.D) {
-    case 32: return launch_pass_d<32, MODE>(grid, a, st);
-    case 64: return launch_pass_d<64, MODE>(grid, a, st);
-    default: return launch_pass_d<128, MODE>(grid, a, st);
+    case 32: return launch_pass_d<32, MODE, X3>(grid, a, st);
+    case 64: return launch_pass_d<64, MODE, X3>(grid, a, st);
+    default: return launch_pass_d<128, MODE, X3>(grid, a, st);
   }
 }
 
@@ -975,6 +1061,7 @@ namespace tt {
 namespace {
 struct FusedWs {
   __bf16 *qb, *cb;
+  __bf16 *qb_lo, *cb_lo;  // x3 mode only
   float *bias_logq, *bias_lse;
   float *part_m, *part_l, *part_o_rows, *part_o_cols;
 };
@@ -992,10 +1079,12 @@ FusedPlan fused_plan(int64_t n, int dim) {
   p.per_split = round_up(ceil_div(p.n_pad, p.split), kTile);
   return p;
 }
-FusedWs carve_fused(Carver& cv, const FusedPlan& p) {
+FusedWs carve_fused(Carver& cv, const FusedPlan& p, bool x3 = false) {
   FusedWs w;
   w.qb = cv.take<__bf16>(p.n_pad * p.D);
   w.cb = cv.take<__bf16>(p.n_pad * p.D);
+  w.qb_lo = x3 ? cv.take<__bf16>(p.n_pad * p.D) : nullptr;
+  w.cb_lo = x3 ? cv.take<__bf16>(p.n_pad * p.D) : nullptr;
   w.bias_logq = cv.take<float>(p.n_pad);
   w.bias_lse = cv.take<float>(p.n_pad);
   w.part_m = cv.take<float>(int64_t(p.split) * p.n_pad);
@@ -1021,30 +1110,32 @@ namespace {
 // workspace, ordered before this call).
 int softmax_xent(const float* q, int64_t ldq, const float* c, int64_t ldc, int64_t n, int32_t dim, const float* logq,
                  float* lse, float* row_loss, float* dq, float* dc, void* workspace, size_t workspace_bytes,
-                 tt_stream_t stream, bool prepped, float loss_scale = 1.0f, float* loss = nullptr) {
+                 tt_stream_t stream, bool prepped, float loss_scale = 1.0f, float* loss = nullptr, bool x3 = false) {
   int rc = check_common(q, ldq, n, c, ldc, n, dim);
   if (rc) return rc;
   TT_REQUIRE(lse && row_loss && dq && dc, "tt_inbatch_softmax_xent: NULL output");
   const FusedPlan p = fused_plan(n, dim);
   Carver cv(workspace, workspace_bytes);
-  FusedWs w = carve_fused(cv, p);
+  FusedWs w = carve_fused(cv, p, x3);
   if (!workspace || cv.used() > workspace_bytes)
     return fail(TT_ERR_WORKSPACE, "tt_inbatch_softmax_xent: workspace %zu < required %zu", workspace_bytes,
                 cv.used());
   hipStream_t st = to_stream(stream);
   // one prep launch for both matrices; c's job also writes both bias vectors
-  if (!prepped &&
-      (rc = prep(p.D, prep_job(q, ldq, n, dim, w.qb), prep_job(c, ldc, n, dim, w.cb, logq, w.bias_logq, w.bias_lse),
-                 dim, p.n_pad, st)))
-    return rc;
+  PrepJob jq = prep_job(q, ldq, n, dim, w.qb), jc = prep_job(c, ldc, n, dim, w.cb, logq, w.bias_logq, w.bias_lse);
+  jq.dst_lo = w.qb_lo;
+  jc.dst_lo = w.cb_lo;
+  if (!prepped && (rc = prep(p.D, jq, jc, dim, p.n_pad, st))) return rc;
   const Plan pl{p.D, p.n_pad, p.n_pad, p.split, p.per_split};
-  PassArgs ar{w.qb, w.cb, w.bias_logq, p.n_pad, p.n_pad, p.per_split, 0, w.part_m, w.part_l, w.part_o_rows};
-  if ((rc = launch_pass<0>(pl, ar, st))) return rc;
+  PassArgs ar{w.qb, w.cb, w.bias_logq, p.n_pad, p.n_pad, p.per_split, 0, w.part_m, w.part_l, w.part_o_rows,
+              w.qb_lo, w.cb_lo};
+  if ((rc = x3 ? launch_pass<0, true>(pl, ar, st) : launch_pass<0>(pl, ar, st))) return rc;
   if ((rc = combine_rows(p.D, st, w.part_m, w.part_l, w.part_o_rows, p.split, p.n_pad, q, ldq, c, ldc, logq, n, dim,
                          0, lse, row_loss, dq, w.bias_lse)))
     return rc;
-  PassArgs ac{w.cb, w.qb, w.bias_lse, p.n_pad, p.n_pad, p.per_split, 0, nullptr, nullptr, w.part_o_cols};
-  if ((rc = launch_pass<1>(pl, ac, st))) return rc;
+  PassArgs ac{w.cb, w.qb, w.bias_lse, p.n_pad, p.n_pad, p.per_split, 0, nullptr, nullptr, w.part_o_cols,
+              w.cb_lo, w.qb_lo};
+  if ((rc = x3 ? launch_pass<1, true>(pl, ac, st) : launch_pass<1>(pl, ac, st))) return rc;
   return combine_cols(p.D, st, w.part_o_cols, p.split, p.n_pad, q, ldq, c, ldc, lse, row_loss, logq, n, dim, 0, dc,
                       loss ? LossSum{row_loss, n, loss_scale, loss} : LossSum{});
 }
@@ -1095,4 +1186,27 @@ extern "C" int tt_inbatch_prep(const float* x, int64_t ldx, int64_t n, int32_t d
   return prep(p.D, operand == 0 ? prep_job(x, ldx, n, dim, w.qb) : prep_job(x, ldx, n, dim, w.cb, logq, w.bias_logq,
                                                                               w.bias_lse),
               none, dim, p.n_pad, to_stream(stream));
+}
+
+// Opt-in fp32-faithful products (X3): the fused loss with S = Q.C^T and the
+// softmax-weighted sums P.V both from bf16x3 products (hi.hi + hi.lo + lo.hi
+// of split operands) in both passes — the reference's fp32 logits and
+// gradients to ~2^-16 relative, so softmax weights at trained score
+// magnitudes (|S| ~ 100) keep their fp32 values.  Three MFMAs where the
+// default issues one, one workgroup per CU: ~3x the passes' time.
+extern "C" size_t tt_inbatch_fused_x3_workspace_size(int64_t n, int32_t dim) {
+  if (n < 1 || pick_dpad(dim) == 0) return 0;
+  Carver cv(nullptr, 0);
+  carve_fused(cv, fused_plan(n, dim), true);
+  return cv.used();
+}
+
+extern "C" int tt_inbatch_softmax_xent_x3(const float* q, int64_t ldq, const float* c, int64_t ldc, int64_t n,
+                                          int32_t dim, const float* logq, float* lse, float* row_loss, float* dq,
+                                          float* dc, float loss_scale, float* loss, void* workspace,
+                                          size_t workspace_bytes, tt_stream_t stream) {
+  using namespace tt;
+  clear_error();
+  return softmax_xent(q, ldq, c, ldc, n, dim, logq, lse, row_loss, dq, dc, workspace, workspace_bytes, stream, false,
+                      loss_scale, loss, true);
 }

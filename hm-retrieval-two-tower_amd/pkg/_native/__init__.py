@@ -273,6 +273,12 @@ _PROTOS = {
         [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          c_float, c_void_p, c_int32, c_void_p, c_size_t, c_void_p],
     ),
+    "tt_inbatch_fused_x3_workspace_size": (c_size_t, [c_int64, c_int32]),
+    "tt_inbatch_softmax_xent_x3": (
+        c_int32,
+        [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_float, c_void_p, c_void_p, c_size_t, c_void_p],
+    ),
     "tt_bruteforce_index_bytes": (c_size_t, [c_int64, c_int32]),
     "tt_bruteforce_build": (c_int32, [c_void_p, c_int64, c_int64, c_int32, c_void_p, c_size_t, c_void_p]),
     "tt_bruteforce_workspace_size": (c_size_t, [c_int64, c_int64, c_int32, c_int32]),

@@ -382,8 +382,9 @@ class EmbeddingOps:
                                                                            presorted=True))
 
 
-def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits: List[int], in_splits: List[int], group) -> torch.Tensor:
-    if dist.get_world_size(group) == 1:  # one rank: the exchange is the identity
+def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits: List[int], in_splits: List[int], group,
+         force: bool = False) -> torch.Tensor:
+    if dist.get_world_size(group) == 1 and not force:  # one rank: the exchange is the identity
         if out.numel():
             out.copy_(inp)
         return out
@@ -396,8 +397,8 @@ def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits: List[int], in_splits:
     return out
 
 
-def _all_reduce_sum(t: torch.Tensor, group) -> None:
-    if dist.get_world_size(group) == 1:  # one rank: the sum is the tensor
+def _all_reduce_sum(t: torch.Tensor, group, force: bool = False) -> None:
+    if dist.get_world_size(group) == 1 and not force:  # one rank: the sum is the tensor
         return
     if _staged(group) and t.is_cuda:
         h = t.cpu()
@@ -474,13 +475,19 @@ class ShardedTables:
     """
 
     def __init__(self, tables: Dict[str, torch.Tensor], init_accumulator: float = 0.1, group=None,
-                 ops: Optional[EmbeddingOps] = None, full_tables: bool = True):
+                 ops: Optional[EmbeddingOps] = None, full_tables: bool = True, always: bool = False):
         """tables: name -> full [rows, dim] table (full_tables=True, the shard is
         sliced out) or this rank's shard with a "__rows__" entry giving the
-        global row counts (full_tables=False, for tables too big to build)."""
+        global row counts (full_tables=False, for tables too big to build).
+        always: take the multi-rank path at world 1 too — the request, row and
+        gradient all_to_alls run as real one-rank collectives instead of being
+        skipped (tests: the N > 1 step's exchanges inside a captured graph on
+        one GPU, as BatchComm(always=True) does for the global negatives)."""
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        self.always = bool(always)
+        self.exchange = self.world > 1 or self.always  # the exchanges run (else: identities, skipped)
         self.ops = ops or EmbeddingOps.hip()
         self.names = [n for n in tables if n != "__rows__"]
         dims = {tables[n].shape[1] for n in self.names}
@@ -570,7 +577,7 @@ class ShardedTables:
         ordered = self.ops.sparse_routed is not None  # keep the route's sort for apply_lookups
         if self.ops.route_fixed is not None:  # one call (one launch for small batches)
             send_p, idx_p, counts, order, own = self.ops.route_fixed(tagged, W, T, cap, overflow, ordered=ordered,
-                                                                     owner=W == 1, idx_out=idx_out)
+                                                                     owner=not self.exchange, idx_out=idx_out)
         else:
             if ordered:
                 send, counts, _, idx, order = self.ops.need("route_requests")(tagged, W, T, ordered=True)
@@ -582,9 +589,9 @@ class ShardedTables:
                 idx_p = idx_out
         split = [cap] * W
         recv = send_p  # world 1: the exchange is the identity
-        if W > 1:
+        if self.exchange:
             recv = torch.empty(W * cap, 2, dtype=torch.int32, device=dev)
-            _a2a(recv, send_p, split, split, group)
+            _a2a(recv, send_p, split, split, group, self.always)
         tags, rows, tids = own if own is not None else self.ops.need("route_owner")(recv, W, T)
         return _Route(s_split=split, r_split=split, R=W * cap, n_recv=W * cap, tags=tags, rows=rows,
                       table_ids=list(tids.unbind(0)), idx=list(idx_p.unbind(0)), idx_all=idx_p, dev=dev,
@@ -594,12 +601,12 @@ class ShardedTables:
     def fetch_routed(self, rt: _Route, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Rows of the routed requests, [R, dim] (into out[:R] when given)."""
         got = out[:rt.R] if out is not None else torch.empty(rt.R, self.dim, dtype=torch.float32, device=rt.dev)
-        if self.world == 1:  # the owner's answer IS the fetched rows
+        if not self.exchange:  # one rank: the owner's answer IS the fetched rows
             self.ops.gather_tagged([self.shard[n] for n in self.names], rt.tags, rt.rows, got)
             return got
         reply = torch.empty(rt.n_recv, self.dim, dtype=torch.float32, device=rt.dev)
         self.ops.gather_tagged([self.shard[n] for n in self.names], rt.tags, rt.rows, reply)
-        _a2a(got, reply, rt.s_split, rt.r_split, self.group)
+        _a2a(got, reply, rt.s_split, rt.r_split, self.group, self.always)
         return got
 
     def fetch(self, lookups: List[Tuple[str, torch.Tensor]], capacity: Optional[int] = None,
@@ -661,7 +668,7 @@ class ShardedTables:
     def apply_routed(self, rt: _Route, g_req: torch.Tensor, lr: float, eps: float) -> None:
         """g_req[:R]: the per-request gradient sums of the routed requests;
         returns them to the owners, which apply Adagrad to their shards."""
-        if self.world == 1:  # the per-request sums are already the owner's
+        if not self.exchange:  # one rank: the per-request sums are already the owner's
             recv = g_req[:rt.R]
             if self.ops.sparse_adagrad_rows is not None:
                 # one rank's requests are distinct (tag, row) pairs: no sort, no sums
@@ -670,7 +677,7 @@ class ShardedTables:
                 return
         else:
             recv = torch.empty(rt.n_recv, self.dim, dtype=torch.float32, device=rt.dev)
-            _a2a(recv, g_req[:rt.R], rt.r_split, rt.s_split, self.group)
+            _a2a(recv, g_req[:rt.R], rt.r_split, rt.s_split, self.group, self.always)
         specs = [dict(table=self.shard[name], slot0=self.acc[name], ids=[rt.table_ids[ti]], grad_col_offset=[0])
                  for ti, name in enumerate(self.names)]
         if recv.shape[0] > 0:
@@ -703,7 +710,7 @@ class ShardedTables:
             sp["ids"].append(rt.idx[l])
             sp["grad_col_offset"].append(int(col))
         routed = self.ops.sparse_routed is not None and getattr(rt, "order", None) is not None
-        if g_req is None and not (self.world == 1 and routed):
+        if g_req is None and not (not self.exchange and routed):
             g_req = torch.zeros(rt.R, self.dim, dtype=torch.float32, device=rt.dev)
         if not routed:
             for sp in specs:
@@ -714,7 +721,7 @@ class ShardedTables:
         route = dict(order=rt.order[0], grp_first=rt.order[1], grp_last=rt.order[2], slot=rt.idx_all, cap=rt.cap,
                      world=self.world, num_tags=len(self.names), lookup_tag=rt.lookup_tags, lookup_table=lk_table,
                      lookup_source=lk_source)
-        if self.world == 1:  # the owner is this rank: Adagrad on the shard, keyed by local row
+        if not self.exchange:  # the owner is this rank: Adagrad on the shard, keyed by local row
             route["slot_row"] = rt.rows
             for sp in specs:
                 name = self.names[sp["tag"]]
@@ -828,7 +835,11 @@ class ShardedTrainStep:
 
     def __init__(self, model, shard_min_rows: int = 100_000, group=None, ops: Optional[EmbeddingOps] = None,
                  use_graph: bool = True, global_negatives: bool = True, comm: Optional[BatchComm] = None,
-                 route_capacity: Optional[int] = None):
+                 route_capacity: Optional[int] = None, always_exchange: bool = False):
+        """always_exchange: the multi-rank structure at world 1 too (the
+        sharded tables' all_to_alls and the bucket's all_reduce as real
+        one-rank collectives, ShardedTables(always=True)) — how one GPU runs
+        the N > 1 step's graph over RCCL (tests)."""
         from pkg.modelling.optimizer_factory import Adagrad
 
         opt = model.optimizer
@@ -848,7 +859,9 @@ class ShardedTrainStep:
         # step eagerly); over gloo, whose host staging synchronises, the step
         # runs eagerly.  At world 1 every exchange is skipped.
         self.route_capacity = None if route_capacity is None else int(route_capacity)
-        collectives = self.world > 1 or (self.global_negatives and self.comm.always)
+        self.always = bool(always_exchange)
+        self.exchange = self.world > 1 or self.always
+        collectives = self.exchange or (self.global_negatives and self.comm.always)
         self.use_graph = use_graph and os.environ.get("TT_SHARDED_EAGER") != "1" and not (
             collectives and _staged(group))
         big: Dict[str, torch.Tensor] = {}
@@ -861,7 +874,7 @@ class ShardedTrainStep:
                     t._shard_key = f"{len(big) - 1}:{name}"
                 else:
                     self.small[key] = t
-        self.tables = ShardedTables(big, self.init, group, self.ops) if big else None
+        self.tables = ShardedTables(big, self.init, group, self.ops, always=self.always) if big else None
         for tower in model.towers:  # drop the full copies of sharded tables
             for t in tower.input_layer.embedding_layers.values():
                 if hasattr(t, "_shard_key"):
@@ -951,7 +964,7 @@ class ShardedTrainStep:
         slots = self.world * self._cap
         dim = self.tables.dim if self.tables is not None else 1
         # the fetched rows (world 1: unused, the middle reads the shard)
-        self._got = torch.zeros(slots if self.world > 1 else 1, dim, dtype=torch.float32, device=dev)
+        self._got = torch.zeros(slots if self.exchange else 1, dim, dtype=torch.float32, device=dev)
         self._g_req = torch.zeros(slots, dim, dtype=torch.float32, device=dev)
         # dropped requests (capacity); TT_SHARDED_DEBUG=1: between two canary words
         self._canary = torch.full((3,), 0x7EADBEEF, dtype=torch.int32, device=dev)
@@ -991,7 +1004,7 @@ class ShardedTrainStep:
             for f, off in zip(layer.categorical_features, layer.column_offsets()):
                 t = layer.embedding_layers[f.name]
                 if hasattr(t, "_shard_key"):
-                    if self.world == 1:  # one rank: the shard IS the fetched rows, read by id directly
+                    if not self.exchange:  # one rank: the shard IS the fetched rows, read by id directly
                         segs.append((self.tables.shard[t._shard_key], layer._ids(xx[f.name]), off))
                     else:
                         segs.append((self._got, self._idx[j], off))
@@ -1068,12 +1081,12 @@ class ShardedTrainStep:
         flat small-table buffer, and the loss into its static scalar — fixed
         shapes, captured into the step's hipGraph."""
         m = self.model
-        if self.world == 1:
+        if not self.exchange:
             grads, small, loss_out = [g.view_as(t.dense.flat) for g, t in zip(flat_grads, m.towers)], \
                 self._small_grad, loss.reshape(())
         else:
             torch.cat([g.reshape(-1) for g in flat_grads] + [self._small_grad, loss.reshape(1)], out=self._bucket)
-            _all_reduce_sum(self._bucket, self.group)
+            _all_reduce_sum(self._bucket, self.group, self.always)
             grads, off = [], 0
             for t in m.towers:
                 n = t.dense.flat.numel()
@@ -1107,7 +1120,7 @@ class ShardedTrainStep:
         if self.tables is not None:
             lookups = [(k, ids) for k, ids, _, _ in self._lookups(self._static)]
             idx_out = self._idx_all[:len(self._idx)]
-            if self.world == 1 and idx_out.is_cuda and ROUTE_SIDE:
+            if not self.exchange and idx_out.is_cuda and ROUTE_SIDE:
                 # one rank: the route has no collective and the middle reads the
                 # shard by id, so the route only feeds the backward's per-request
                 # sums and the owner apply — it runs on a side stream beside the
@@ -1126,7 +1139,7 @@ class ShardedTrainStep:
             else:
                 rt = self.tables.route_fixed(lookups, self._cap, overflow=self._overflow, idx_out=idx_out)
                 self._route_joined(rt)
-                if self.world > 1:
+                if self.exchange:
                     self.tables.fetch_routed(rt, out=self._got)  # rt.idx_all IS self._idx_all[:L]
         self._middle()
         if rt is not None:

@@ -47,6 +47,9 @@ __all__ = [
     "topk_merge",
     "recall_hits",
     "Workspace",
+    "capture_guard",
+    "CaptureTopology",
+    "NestedJoinError",
 ]
 
 
@@ -72,6 +75,60 @@ def _row_major(t: torch.Tensor, name: str) -> int:
     return max(t.stride(0), t.shape[1])
 
 
+class NestedJoinError(RuntimeError):
+    """A captured stream waited on a side branch without being the capture's
+    origin stream (CaptureTopology)."""
+
+
+class CaptureTopology:
+    """The fork / join structure of one hipGraph capture, checked as it is
+    issued.  ROCm 7.2's hipStreamEndCapture segfaults when a captured side
+    branch waits on another side branch — the branch that forked it
+    (tools/graph_fork_probe.py nested_join, profiles/r03_graph_fork_probe.txt)
+    or a sibling (the round-5 embedding update on the id-sort stream) — so
+    here only the capture's origin stream may wait on a branch; a stream
+    entering the capture may wait on any captured stream (a fork) and a
+    branch may wait on the origin again.  The origin is the stream of the first event
+    recorded while capturing (nothing else is in the capture yet).  On a
+    violating wait the wait is NOT issued: every branch is joined into the
+    origin instead (so the capture can end cleanly) and NestedJoinError is
+    raised."""
+
+    def __init__(self):
+        self.active = True
+        self.depth = 0  # > 0 inside a checked Stream.wait_event (its Event.wait is the same wait)
+        self.origin = None
+        self.branches: Dict[int, object] = {}  # stream id -> stream (streams that joined by waiting)
+        self.source: Dict[int, object] = {}    # id(event) -> stream it was recorded on
+
+    def recorded(self, event, stream) -> None:
+        if not self.active:
+            return
+        if self.origin is None:
+            if not torch.cuda.is_current_stream_capturing():
+                return
+            self.origin = stream
+        self.source[id(event)] = stream
+
+    def waiting(self, stream, event) -> None:
+        src = self.source.get(id(event)) if self.active else None
+        if src is None or self.origin is None or src == stream:
+            return
+        if stream != self.origin and stream.cuda_stream not in self.branches:
+            # a stream entering the capture: a fork (from the origin or from a
+            # branch: legal, tools/graph_fork_probe.py origin_join)
+            self.branches[stream.cuda_stream] = stream
+            return
+        if src != self.origin and stream != self.origin:
+            origin, branches = self.origin, list(self.branches.values())
+            self.active = False  # the repair below is not itself checked, nor anything after it
+            for b in branches:
+                origin.wait_stream(b)
+            raise NestedJoinError(
+                f"captured stream {stream} waits on side branch {src}: only the capture's origin stream "
+                f"({origin}) may join a branch (ROCm's hipStreamEndCapture crashes on nested joins)")
+
+
 @contextlib.contextmanager
 def capture_guard(keep: Optional[list] = None):
     """Around a hipGraph capture on this thread: Python's garbage collector
@@ -80,15 +137,41 @@ def capture_guard(keep: Optional[list] = None):
     runtime refuses during capture and the process aborts — and every HIP
     event created during the capture appended to `keep`, so the caller holds
     them for the graph's lifetime (a captured cross-stream wait whose event
-    was destroyed after the capture crashed a later replay)."""
+    was destroyed after the capture crashed a later replay).  Every event
+    record / wait is checked against the nested-join pattern
+    (CaptureTopology: raises NestedJoinError instead of reaching a crash in
+    hipStreamEndCapture)."""
     import torch.cuda.streams as _streams
 
     gc.collect()
     was = gc.isenabled()
     gc.disable()
     orig = (torch.cuda.Event, _streams.Event)
+    base = orig[0]
+    topo = CaptureTopology()
+    methods = (base.record, base.wait, _streams.Stream.wait_event)
+
+    def record(ev, stream=None):
+        stream = torch.cuda.current_stream() if stream is None else stream
+        methods[0](ev, stream)
+        topo.recorded(ev, stream)
+
+    def wait(ev, stream=None):
+        stream = torch.cuda.current_stream() if stream is None else stream
+        if topo.depth == 0:
+            topo.waiting(stream, ev)
+        methods[1](ev, stream)
+
+    def wait_event(stream, ev):
+        topo.waiting(stream, ev)
+        topo.depth += 1
+        try:
+            methods[2](stream, ev)  # torch implements it as ev.wait(stream): checked once, here
+        finally:
+            topo.depth -= 1
+
+    base.record, base.wait, _streams.Stream.wait_event = record, wait, wait_event
     if keep is not None:
-        base = orig[0]
 
         class _Kept(base):
             def __new__(cls, *a, **k):
@@ -102,6 +185,7 @@ def capture_guard(keep: Optional[list] = None):
         yield
     finally:
         torch.cuda.Event, _streams.Event = orig
+        base.record, base.wait, _streams.Stream.wait_event = methods
         if was:
             gc.enable()
 
@@ -734,12 +818,14 @@ def inbatch_prep(x: torch.Tensor, operand: int, logq: Optional[torch.Tensor], ws
 
 
 def inbatch_fused(q: torch.Tensor, c: torch.Tensor, logq: Optional[torch.Tensor], ws: Optional[torch.Tensor] = None,
-                  prepped: bool = False, loss_scale: Optional[float] = None):
+                  prepped: bool = False, loss_scale: Optional[float] = None, x3: bool = False):
     """Single-device loss + gradients (both passes, shared bf16 prep):
     (lse [B], row_loss [B], dq [B,E], dc [B,E]).  prepped: both operands were
     already prepared into `ws` by inbatch_prep (ordered before this call).
     loss_scale: also return the loss loss_scale * sum(row_loss) (a 0-d
-    tensor, computed inside the last launch, equal to loss_sum's)."""
+    tensor, computed inside the last launch, equal to loss_sum's).
+    x3: fp32-faithful products (tt_inbatch_softmax_xent_x3: S and P.V as
+    bf16x3 products, ~3x the passes' time; not with prepped)."""
     _req(q, "q", torch.float32, 2)
     _req(c, "c", torch.float32, 2)
     ldq, ldc = _row_major(q, "q"), _row_major(c, "c")
@@ -749,12 +835,24 @@ def inbatch_fused(q: torch.Tensor, c: torch.Tensor, logq: Optional[torch.Tensor]
     if prepped and ws is None:
         raise ValueError("prepped=True needs the workspace the operands were prepared into")
     L = lib()
+    if x3:
+        if prepped:
+            raise ValueError("x3: the fp32-faithful entry prepares its operands itself (prepped=False)")
+        ws = Workspace.get(L.tt_inbatch_fused_x3_workspace_size(B, E), q.device, "inbatch_fused_x3")
     if ws is None:
         ws = inbatch_fused_workspace(B, E, q.device)
     lse = torch.empty(B, dtype=torch.float32, device=q.device)
     row_loss = torch.empty(B, dtype=torch.float32, device=q.device)
     dq = torch.empty(B, E, dtype=torch.float32, device=q.device)
     dc = torch.empty(B, E, dtype=torch.float32, device=q.device)
+    if x3:
+        loss = torch.empty((), dtype=torch.float32, device=q.device) if loss_scale is not None else None
+        check(L.tt_inbatch_softmax_xent_x3(q.data_ptr(), ldq, c.data_ptr(), ldc, B, E, _opt_ptr(logq, "logq", B),
+                                           lse.data_ptr(), row_loss.data_ptr(), dq.data_ptr(), dc.data_ptr(),
+                                           float(loss_scale if loss_scale is not None else 1.0),
+                                           loss.data_ptr() if loss is not None else None, ws.data_ptr(), ws.numel(),
+                                           _stream()))
+        return (lse, row_loss, dq, dc, loss) if loss is not None else (lse, row_loss, dq, dc)
     if loss_scale is not None:
         loss = torch.empty((), dtype=torch.float32, device=q.device)
         check(L.tt_inbatch_softmax_xent_loss(q.data_ptr(), ldq, c.data_ptr(), ldc, B, E, _opt_ptr(logq, "logq", B),

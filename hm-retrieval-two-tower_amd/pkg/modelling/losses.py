@@ -23,10 +23,20 @@ __all__ = ["InBatchSoftmaxCrossEntropy", "inbatch_softmax_xent", "towers_inbatch
            "global_inbatch_grads", "global_towers_inbatch_softmax_xent", "TOWER_C_SCOPE"]
 
 
+def x3_scores() -> bool:
+    """TT_INBATCH_X3=1 (read at each call): the single-device in-batch loss
+    with fp32-faithful products (hip_ops.inbatch_fused(x3=True): S and P.V
+    as bf16x3 products) — the reference's fp32 logits and gradients to
+    ~2^-16, dQ / dC within 1e-3 of fp64 at trained score magnitudes; ~3x the
+    passes' time.  The
+    default is the bf16-operand contract (include/tt.h K5-K7)."""
+    return os.environ.get("TT_INBATCH_X3", "0") == "1"
+
+
 class _InBatchXent(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, c, logq, scale):
-        lse, row_loss, dq, dc = hip_ops.inbatch_fused(q, c, logq)
+        lse, row_loss, dq, dc = hip_ops.inbatch_fused(q, c, logq, x3=x3_scores())
         ctx.scale = scale
         ctx.save_for_backward(dq, dc)
         return hip_ops.loss_sum(row_loss, scale)
@@ -172,6 +182,10 @@ class _TowersInBatchXent(torch.autograd.Function):
         ctx.nq = len(qa)
         ctx.scale = scale
         ctx.on_tower = on_tower
+        if x3_scores():  # fp32-faithful scores (its own preparation and workspace)
+            _, _, dq, dc, loss = hip_ops.inbatch_fused(qa[-1], ca[-1], logq, loss_scale=scale, x3=True)
+            ctx.save_for_backward(flat_q, flat_c, dq, dc, *qa, *ca)
+            return loss
         if LOSS_IN_COMBINE:  # the loss sum inside the loss entry's last launch
             _, _, dq, dc, loss = hip_ops.inbatch_fused(qa[-1], ca[-1], logq, ws=ws, prepped=ws is not None,
                                                        loss_scale=scale)

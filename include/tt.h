@@ -187,6 +187,22 @@ int tt_route_fixed(const tt_route_lookup* lookups, int32_t num_lookups, int64_t 
                    int32_t* owner_tags, int32_t* owner_rows, int32_t* owner_table_ids,
                    void* workspace, size_t workspace_bytes, tt_stream_t stream);
 
+/* Opt-in fp32-faithful products: tt_inbatch_softmax_xent_loss's contract
+ * (prepped = 0; loss may be NULL) with every score S_ij AND the softmax-
+ * weighted sums P.V from bf16x3 products (x = hi + lo, both bf16: hi.hi +
+ * hi.lo + lo.hi, fp32 accumulation — the reference's fp32 logits and
+ * gradients, two_tower_model.py:92,124, to ~2^-16 relative) in both passes.
+ * At trained score magnitudes (|S| ~ 100) this holds dQ and dC to the fp64
+ * gradients within 1e-3 where the default bf16 operands do not.
+ * Three MFMAs where the default issues one, one workgroup per CU. */
+size_t tt_inbatch_fused_x3_workspace_size(int64_t n, int32_t dim);
+int tt_inbatch_softmax_xent_x3(const float* q, int64_t ldq, const float* c,
+                               int64_t ldc, int64_t n, int32_t dim,
+                               const float* logq, float* lse, float* row_loss,
+                               float* dq, float* dc, float loss_scale,
+                               float* loss, void* workspace,
+                               size_t workspace_bytes, tt_stream_t stream);
+
 /* ------------------------------------------------------------------------ *
  * K8+K9  Sparse optimizer step on embedding tables.
  * Replaces the legacy Keras optimizer's sparse path reached from

@@ -72,7 +72,7 @@ def _mirror(m, inbatch="bf16"):
     return ref
 
 
-def _train_steps_vs_cpu(cuda, emb, joint, B, steps, loss_rtol, upd_rtol):
+def _train_steps_vs_cpu(cuda, emb, joint, B, steps, loss_rtol, upd_rtol, inbatch="bf16"):
     """`steps` full train steps of the main.py schema at (emb, joint, towers
     [256]) and batch B, each vs oracle.CpuTwoTower started from the model's
     state before that step: the loss within loss_rtol of the fp32 (exact
@@ -108,7 +108,7 @@ def _train_steps_vs_cpu(cuda, emb, joint, B, steps, loss_rtol, upd_rtol):
         # the oracle restarts from the GPU model's state each step, so every
         # step is checked as a function of its inputs (the trajectories of two
         # sum-reduced runs at lr 0.05 drift apart by compounding, not by error)
-        ref = _mirror(m)
+        ref = _mirror(m, inbatch)
         b = data.batch(B)
         lq = m.candidate_logq(b).cpu().numpy()
         rows = {**touched(m.query_tower.input_layer, b), **touched(m.candidate_tower.input_layer, b)}
@@ -202,6 +202,17 @@ def test_c3_train_steps_match_cpu_restatement(cuda):
     """configs[2], the headline train config: the main.py schema at D = E =
     128, H&M vocabularies, towers [256] -> 128, logQ, Adagrad, B = 16384."""
     _train_steps_vs_cpu(cuda, 128, 128, 16384, 3, 1e-3, 2e-3)
+
+
+def test_c3_train_steps_x3_match_fp32_restatement(cuda, monkeypatch):
+    """The opt-in fp32-faithful in-batch loss (TT_INBATCH_X3=1: bf16x3 S and
+    P.V) in the C3 train step: every step's gradients and updates within 1e-3
+    of the plain fp32 restatement (oracle.CpuTwoTower, inbatch="fp32") — the
+    reference's arithmetic, not the bf16 contract's — through the scores'
+    growth to O(100)."""
+    monkeypatch.setenv("TT_INBATCH_X3", "1")
+    errs = _train_steps_vs_cpu(cuda, 128, 128, 16384, 3, 1e-4, 1e-3, inbatch="fp32")
+    assert max(v for k, v in errs.items() if k[0] == "loss") <= 1e-4
 
 
 def _c4_data(cuda, Q, seed=2):
@@ -383,3 +394,64 @@ def test_c3_sharded_step_world1_matches_single_gpu(cuda, B):
     finally:
         destroy_process_group()
         torch.cuda.empty_cache()
+
+
+def _fp64_inbatch(q, c, logq, block=2048):
+    """torch fp64 reference of the in-batch loss and its gradients (the
+    reference's fp32 semantics, evaluated exactly): row_loss [B], dq, dc."""
+    qd, cd, ld = q.double(), c.double(), logq.double()
+    B = qd.shape[0]
+    dq = torch.empty_like(qd)
+    dc = torch.zeros_like(cd)
+    rl = torch.empty(B, dtype=torch.float64, device=q.device)
+    for s in range(0, B, block):
+        S = qd[s:s + block] @ cd.T - ld[None, :]
+        lse = torch.logsumexp(S, 1)
+        r = torch.arange(s, min(s + block, B), device=q.device)
+        rl[s:s + block] = lse - S[r - s, r]
+        P = torch.exp(S - lse[:, None])
+        P[r - s, r] -= 1.0
+        dq[s:s + block] = P @ cd
+        dc += P.T @ qd[s:s + block]
+    return rl, dq, dc
+
+
+def test_c3_inbatch_grads_vs_fp64_after_training(cuda):
+    """The fused in-batch loss's dQ / dC at C3 (B = 16384, E = 128) against a
+    torch fp64 evaluation of the reference's loss (two_tower_model.py:113-124)
+    on the model's OWN tower outputs after 1 and 4 Adagrad steps, where the
+    scores have grown to O(100) — no input scaling.  The default bf16-operand
+    scores drift from fp64 as the scores grow (dC ~8e-3 at |S| ~ 100: bf16
+    rounding of q, c moves each logit by ~1e-2); the opt-in fp32-faithful
+    entry (x3: bf16x3 score products, TT_INBATCH_X3=1) holds dQ and dC within
+    1e-3 of fp64 at every step.  Measured errors: DESIGN §6."""
+    from pkg.modelling import hip_ops
+
+    schema = bench.main_schema(emb_big=128, joint=128, hidden=(256,))
+    data = bench.SyntheticHM(cuda, seed=11)
+    schema.set_candidate_prob_lookup(data.prob_lookup())
+    m = TwoTowerModel.create_from_schema(schema, "article_id", device=cuda, seed=0)
+    m.compile(optimizer=OptimizerFactory.get_optimizer("adagrad", {"learning_rate": 0.05}))
+    res = {}
+    for step in range(5):
+        if step in (0, 1, 4):
+            b = data.batch(16384)
+            with torch.no_grad():
+                q, c = (t.dense.forward_acts(t.input_layer({f.name: b[f.name] for f in
+                                                            t.input_layer.categorical_features}), t.dense.flat)[-1]
+                        for t in m.towers)
+                logq = m.candidate_logq(b)
+                rl, dq_ref, dc_ref = _fp64_inbatch(q, c, logq)
+                smax = float((q.double() @ c.double()[:256].T).abs().max())
+                res[step] = dict(score_max=smax)
+                for tag, x3 in (("", False), ("x3_", True)):
+                    _, row_loss, dq, dc = hip_ops.inbatch_fused(q.contiguous(), c.contiguous(), logq, x3=x3)
+                    res[step][tag + "dq"] = float((dq.double() - dq_ref).norm() / dq_ref.norm())
+                    res[step][tag + "dc"] = float((dc.double() - dc_ref).norm() / dc_ref.norm())
+                    res[step][tag + "loss"] = abs(float(row_loss.double().sum()) - float(rl.sum())) / float(rl.sum())
+        m.train_step(data.batch(16384))
+    print({k: {a: f"{v:.3g}" for a, v in d.items()} for k, d in res.items()})
+    for k, d in res.items():
+        assert d["loss"] <= 1e-3 and d["x3_loss"] <= 1e-4, (k, d)
+        assert d["dq"] <= 5e-2 and d["dc"] <= 5e-2, (k, d)  # the bf16 contract: recorded, loosely held
+        assert d["x3_dq"] <= 1e-3 and d["x3_dc"] <= 1e-3, (k, d)  # fp32-faithful: the north-star tolerance

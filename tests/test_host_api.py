@@ -196,3 +196,50 @@ def test_workspace_scopes_nest_and_empty_scope_is_root():
             assert Workspace._scope == ""
         assert Workspace._scope == TOWER_C_SCOPE + "/"
     assert Workspace._scope == ""
+
+
+def test_capture_topology_rules():
+    """hip_ops.CaptureTopology (the capture guard's fork / join check) on
+    stand-in streams: forks from the origin or from a branch and joins into
+    the origin pass; a branch joining another branch raises NestedJoinError
+    after joining every branch into the origin (the capture can still end)."""
+    from pkg.modelling import hip_ops
+
+    class S:
+        def __init__(self, n):
+            self.cuda_stream = n
+            self.waited = []
+
+        def __eq__(self, o):
+            return isinstance(o, S) and o.cuda_stream == self.cuda_stream
+
+        def __hash__(self):
+            return self.cuda_stream
+
+        def wait_stream(self, o):
+            self.waited.append(o.cuda_stream)
+
+    origin, s1, s2, s3 = S(0), S(1), S(2), S(3)
+    t = hip_ops.CaptureTopology()
+    t.origin = origin
+    ev = {}
+
+    def rec(name, stream, topo=None):
+        ev[name] = object()
+        (topo or t).source[id(ev[name])] = stream
+        return ev[name]
+
+    t.waiting(s1, rec("a", origin))      # fork from the origin
+    t.waiting(s2, rec("b", s1))          # fork from a branch
+    t.waiting(origin, rec("c", s2))      # the origin joins a branch
+    t.waiting(s1, rec("d", origin))      # a branch waits on the origin again
+    t.waiting(s3, rec("e", origin))
+    with pytest.raises(hip_ops.NestedJoinError, match="origin"):
+        t.waiting(s1, rec("f", s3))      # a branch joining a sibling branch
+    assert sorted(origin.waited) == [1, 2, 3]  # every branch joined into the origin
+    t2 = hip_ops.CaptureTopology()
+    t2.origin = origin
+    t2.waiting(s1, rec("g", origin, t2))
+    t2.waiting(s2, rec("h", s1, t2))
+    with pytest.raises(hip_ops.NestedJoinError):
+        t2.waiting(s1, rec("i", s2, t2))     # tools/graph_fork_probe.py nested_join

@@ -589,6 +589,57 @@ def test_global_negatives_step_captures_rccl_collectives(cuda, monkeypatch, B):
         destroy_process_group()  # the captured step graphs first, then the group
 
 
+@pytest.mark.parametrize("B", [2048, 16384])
+def test_sharded_step_routed_exchanges_captured_on_rccl(cuda, monkeypatch, B):
+    """The N > 1 step's structure on one GPU over RCCL: ShardedTrainStep(
+    global_negatives=True, always_exchange=True) on a one-rank RCCL group runs
+    the routed exchanges — the requests', rows' and per-request gradients'
+    all_to_alls and the bucket's all_reduce — as real collectives inside the
+    step's captured hipGraph (at world 1 they are otherwise skipped).  For 5
+    steps (call 1 eager, then replays) it trains bit-identically to the
+    world-1 shortcut step and to the single-GPU GraphedTrainStep; the status
+    words and the overflow canary stay clean."""
+    import socket
+
+    import torch.distributed as dist
+
+    from pkg.modelling.distributed import ShardedTrainStep, destroy_process_group
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device(cuda))
+    monkeypatch.setenv("TT_SHARDED_KEEP", "0")  # no pinned route buffers: the graph's pool as it is
+    try:
+        a, b, c = (_small_model(cuda, seed=8) for _ in range(3))
+        xchg = ShardedTrainStep(a, shard_min_rows=300, global_negatives=True, always_exchange=True)
+        short = ShardedTrainStep(b, shard_min_rows=300, global_negatives=True)
+        assert xchg.use_graph and xchg.exchange and not short.exchange and xchg.tables is not None
+        rng = np.random.default_rng(B)
+        batches = [_batch(cuda, rng, B) for _ in range(5)]
+        single = GraphedTrainStep(c, batches[0], warmup=1)  # its warm-up step trains on batch 0
+        for i, batch in enumerate(batches):
+            la, lb = xchg(batch)["loss"], short(batch)["loss"]
+            lc = single.warmup_out["loss"] if i == 0 else single(batch)["loss"]
+            assert torch.equal(la, lb) and torch.equal(la, lc), (i, la, lb, lc)
+        assert xchg._graph is not None and short._graph is not None
+        torch.cuda.synchronize()
+        assert xchg._canary.tolist() == [0x7EADBEEF, 0, 0x7EADBEEF]
+        for ta, tb, tc in zip(a.towers, b.towers, c.towers):
+            assert torch.equal(ta.dense.flat, tb.dense.flat) and torch.equal(ta.dense.flat, tc.dense.flat)
+            for name, t in tc.input_layer.embedding_layers.items():
+                ma, mb = ta.input_layer.embedding_layers[name], tb.input_layer.embedding_layers[name]
+                ga = xchg.tables.gather_full(ma._shard_key) if hasattr(ma, "_shard_key") else ma.weight
+                gb = short.tables.gather_full(mb._shard_key) if hasattr(mb, "_shard_key") else mb.weight
+                assert torch.equal(ga, gb) and torch.equal(ga, t.weight), name
+        xchg.check_status()
+        short.check_status()
+    finally:
+        destroy_process_group()  # the captured step graphs first, then the group
+
+
 def test_sharded_step_status_reports_stale_owner_keys(cuda):
     """ShardedTrainStep.check_status reads the workspaces the sharded step's
     sparse kernels write ("sparse_owner": the owners' Adagrad apply,
@@ -708,3 +759,54 @@ def test_model_call_with_gradients_on_libtt(cuda):
         assert torch.isfinite(g).all()
         err = ((g - f.grad).norm() / f.grad.norm()).item()
         assert err <= 1e-4, err
+
+
+@pytest.mark.parametrize("variant", ["nested_join", "sibling_join", "origin_join"])
+def test_capture_guard_refuses_nested_joins(cuda, variant):
+    """hip_ops.capture_guard checks the capture's fork / join structure as it
+    is issued: a side branch waiting on the sub-branch it forked
+    (tools/graph_fork_probe.py nested_join, which crashes ROCm 7.2's
+    hipStreamEndCapture) or on a sibling branch raises NestedJoinError before
+    that wait is issued, and the capture still ends cleanly; the origin
+    joining every branch (origin_join) captures and replays correctly."""
+    x = torch.arange(1 << 16, dtype=torch.float32, device=cuda)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    out = {}
+
+    def body():
+        cur = torch.cuda.current_stream()
+        s1.wait_stream(cur)
+        if variant == "sibling_join":
+            s2.wait_stream(cur)
+        with torch.cuda.stream(s1):
+            y = x * 2
+            if variant != "sibling_join":
+                s2.wait_stream(s1)  # a fork from a branch: legal
+        with torch.cuda.stream(s2):
+            z = (y if variant != "sibling_join" else x) + 1
+        if variant == "origin_join":
+            cur.wait_stream(s1)
+            cur.wait_stream(s2)
+            out["w"] = y * 3 + z
+        else:
+            s1.wait_stream(s2)  # a branch joining a branch: refused
+            with torch.cuda.stream(s1):
+                w = z * 3
+            cur.wait_stream(s1)
+            out["w"] = w
+
+    body()  # eager: any order is fine outside a capture
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    if variant == "origin_join":
+        with hip_ops.capture_guard([]), torch.cuda.graph(g, capture_error_mode="thread_local"):
+            body()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out["w"], x * 2 * 3 + x * 2 + 1)
+    else:
+        with pytest.raises(hip_ops.NestedJoinError, match="origin"):
+            with hip_ops.capture_guard([]), torch.cuda.graph(g, capture_error_mode="thread_local"):
+                body()
+        torch.cuda.synchronize()  # the refused capture ended cleanly: the device is usable
+        assert torch.equal(x * 2, torch.arange(1 << 16, dtype=torch.float32, device=cuda) * 2)
