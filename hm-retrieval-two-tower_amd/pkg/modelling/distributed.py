@@ -1070,7 +1070,12 @@ class ShardedTrainStep:
         for key, (li, srcs) in small_srcs.items():
             specs.append((dict(table=self._small_views[key][1], ids=[s[0] for s in srcs],
                                grad_col_offset=[s[1] for s in srcs]), li))
-        self._sspecs = specs
+        # cached only while every id tensor is a view of the static buffers
+        # (the batch's int32 rows, the route's slots): a categorical column
+        # staged as floats makes _ids return a fresh copy per call
+        static = {t.untyped_storage().data_ptr() for t in (self._ibuf, self._idx_all)}
+        if all(ids.untyped_storage().data_ptr() in static for sp, _ in specs for ids in sp["ids"]):
+            self._sspecs = specs
         return specs
 
     def _dense_update(self, flat_grads: List[torch.Tensor], loss: torch.Tensor) -> None:
@@ -1158,7 +1163,7 @@ class ShardedTrainStep:
         self._route_joined(rt)
 
     def _route_joined(self, rt: _Route) -> None:
-        if os.environ.get("TT_SHARDED_KEEP", "1") == "1":
+        if os.environ.get("TT_SHARDED_DEBUG") == "2":  # the per-owner counts, for the status report
             self._last_counts = rt.counts
         if os.environ.get("TT_SHARDED_DEBUG") == "2":  # running max of the per-owner counts, in the graph
             if getattr(self, "_cmax", None) is None:
@@ -1190,7 +1195,7 @@ class ShardedTrainStep:
                         g, capture_error_mode="thread_local"):
                     self._body()
                 self._graph = g
-                hip_ops.Workspace.snapshot()  # its workspaces are never freed from now on
+                hip_ops.Workspace.snapshot(owner=g)  # its workspaces live as long as the graph
             except Exception as e:  # keep training eagerly (still the HIP kernels)
                 logger.warning(f"ShardedTrainStep: graph capture failed ({e!r}); running eagerly")
                 self.use_graph = False
@@ -1203,7 +1208,7 @@ class ShardedTrainStep:
         if os.environ.get("TT_SHARDED_DEBUG") == "1" and self.tables is not None:
             torch.cuda.synchronize()
             c = self._canary.tolist()
-            counts = self._last_counts.tolist()
+            counts = self._last_counts.tolist() if getattr(self, "_last_counts", None) is not None else [0]
             if c[0] != 0x7EADBEEF or c[2] != 0x7EADBEEF or c[1] != 0 or max(counts) > self._cap:
                 raise RuntimeError(f"ShardedTrainStep debug: call {self._calls}, canary/overflow {c}, counts {counts}, "
                                    f"cap {self._cap}, graph {self._graph is not None}")

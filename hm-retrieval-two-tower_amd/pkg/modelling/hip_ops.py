@@ -201,17 +201,30 @@ class Workspace:
 
     _bufs: Dict[Tuple[int, str], torch.Tensor] = {}
     _scope = ""
-    # device addresses a captured graph may hold (snapshot()), and the buffers
-    # a regrowth replaced while a graph could still address them: never freed
-    _captured: set = set()
+    # device addresses each live captured graph may hold (snapshot(owner)), and
+    # the buffers a regrowth replaced while such a graph could still address
+    # them: kept until no live graph holds their address (the owner's
+    # finalizer releases its hold)
+    _holds: Dict[int, set] = {}
+    _next_hold = 0
     _retired: List[torch.Tensor] = []
+
+    @classmethod
+    def _captured(cls) -> set:
+        return set().union(*cls._holds.values()) if cls._holds else set()
+
+    @classmethod
+    def _release(cls, token: int) -> None:
+        cls._holds.pop(token, None)
+        live = cls._captured()
+        cls._retired = [b for b in cls._retired if b.data_ptr() in live]
 
     @classmethod
     def get(cls, nbytes: int, device: torch.device, tag: str) -> torch.Tensor:
         key = (device.index if device.index is not None else torch.cuda.current_device(), cls._scope + tag)
         buf = cls._bufs.get(key)
         if buf is None or buf.numel() < nbytes:
-            if buf is not None and buf.data_ptr() in cls._captured:
+            if buf is not None and buf.data_ptr() in cls._captured():
                 cls._retired.append(buf)  # a live graph may replay into it
             # zeroed once (a fresh sparse workspace carries no recorded error)
             buf = torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=device)
@@ -234,18 +247,31 @@ class Workspace:
     @classmethod
     def clear(cls) -> None:
         """Forget every buffer (those a captured graph may address stay alive)."""
-        cls._retired.extend(b for b in cls._bufs.values() if b.data_ptr() in cls._captured)
+        live = cls._captured()
+        cls._retired.extend(b for b in cls._bufs.values() if b.data_ptr() in live)
         cls._bufs.clear()
 
     @classmethod
-    def snapshot(cls) -> Dict[Tuple[int, str], int]:
+    def snapshot(cls, owner=None) -> Dict[Tuple[int, str], int]:
         """{key: device address} of every buffer now allocated.  A captured
-        hipGraph holds these addresses: they are never freed from now on
-        (a regrowth retires the old buffer instead), and the graph should be
-        replayed only while `unchanged(snapshot)` — the host-side readers
-        (sparse_status) look at the current buffers."""
+        hipGraph holds these addresses: while `owner` (the graph object) is
+        alive they are never freed (a regrowth retires the old buffer
+        instead); once it is collected its hold is released and retired
+        buffers no live graph addresses are freed (owner=None: held for the
+        process's lifetime).  Replay the graph only while
+        `unchanged(snapshot)` — the host-side readers (sparse_status) look at
+        the current buffers."""
+        import weakref
+
         snap = {k: v.data_ptr() for k, v in cls._bufs.items()}
-        cls._captured.update(snap.values())
+        token = cls._next_hold
+        cls._next_hold += 1
+        cls._holds[token] = set(snap.values())
+        if owner is not None:
+            try:
+                weakref.finalize(owner, cls._release, token)
+            except TypeError:  # not weak-referenceable: held for good
+                pass
         return snap
 
     @classmethod

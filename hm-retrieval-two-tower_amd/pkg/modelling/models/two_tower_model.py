@@ -501,7 +501,7 @@ class GraphedTrainStep:
             self.out = self._step()
         # what the captured pointers refer to (see reusable)
         self.optimizer = model.optimizer
-        self.ws_snapshot = hip_ops.Workspace.snapshot()
+        self.ws_snapshot = hip_ops.Workspace.snapshot(owner=self.graph)
 
     def reusable(self, model: "TwoTowerModel", source=None) -> bool:
         """True while a replay still trains `model` from `source` through the

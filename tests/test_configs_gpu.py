@@ -238,6 +238,30 @@ def test_c4_index_full_candidates_bitexact(cuda, Q, k):
     assert np.array_equal(s.cpu().numpy(), rs)
 
 
+def test_c4_index_pipelined_chunks_bitexact(cuda):
+    """A search of more queries than one chunk (k = 100: 131,072 queries per
+    chunk; here 3 chunks) runs its chunks pipelined — the finalize of chunk c
+    on the auxiliary stream beside the scan of chunk c + 1, two alternating
+    state sets — and equals the chunk-by-chunk searches (each one chunk: no
+    pipelining) bit for bit; rows of every chunk against the fp32 oracle."""
+    from pkg.modelling import hip_ops
+
+    k = 100
+    C, Qm = _c4_data(cuda, 300_000)
+    image = hip_ops.bruteforce_build(C)
+    chunk = int(hip_ops.lib().tt_bruteforce_shard_chunk(Qm.shape[0], C.shape[0], C.shape[1], k))
+    assert Qm.shape[0] > 2 * chunk  # three chunks: both state sets reused
+    s, i = hip_ops.bruteforce_search(image, C, Qm, k)
+    for q0 in range(0, Qm.shape[0], chunk):
+        sc, ic = hip_ops.bruteforce_search(image, C, Qm[q0:q0 + chunk].contiguous(), k)
+        assert torch.equal(sc, s[q0:q0 + chunk]) and torch.equal(ic, i[q0:q0 + chunk]), q0
+    rows = np.concatenate([np.arange(0, 40), np.arange(chunk - 20, chunk + 20), np.arange(2 * chunk, 2 * chunk + 20),
+                           np.arange(Qm.shape[0] - 20, Qm.shape[0])])
+    rs, ri, _ = oracle.bruteforce_topk(Qm[rows].cpu().numpy(), C.cpu().numpy(), k)
+    assert np.array_equal(i[rows].cpu().numpy(), ri)
+    assert np.array_equal(s[rows].cpu().numpy(), rs)
+
+
 def test_c5_100m_row_table_world1(cuda):
     """A 100M x 128 table (BASELINE configs[4]) through ShardedTables at world
     1: fetch = the exact rows; one apply = oracle Adagrad on the touched rows

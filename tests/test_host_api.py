@@ -243,3 +243,33 @@ def test_capture_topology_rules():
     t2.waiting(s2, rec("h", s1, t2))
     with pytest.raises(hip_ops.NestedJoinError):
         t2.waiting(s1, rec("i", s2, t2))     # tools/graph_fork_probe.py nested_join
+
+
+def test_workspace_retired_buffers_follow_graph_lifetime():
+    """hip_ops.Workspace: a buffer a live graph's snapshot holds is retired
+    (kept) when it regrows, and freed once that graph (the snapshot's owner)
+    is gone — no leak across captures (host logic, CPU tensors)."""
+    import gc
+
+    from pkg.modelling import hip_ops
+
+    W = hip_ops.Workspace
+    dev = torch.device("cpu", 0)
+    with W.scope("t_lifetime"):
+        a = W.get(1024, dev, "buf")
+
+        class Graph:  # stands in for torch.cuda.CUDAGraph
+            pass
+
+        g = Graph()
+        snap = W.snapshot(owner=g)
+        assert W.unchanged(snap)
+        b = W.get(4096, dev, "buf")  # regrowth while g may replay into `a`
+        assert b.data_ptr() != a.data_ptr() and not W.unchanged(snap)
+        assert any(r.data_ptr() == a.data_ptr() for r in W._retired)
+        del g
+        gc.collect()
+        assert not any(r.data_ptr() == a.data_ptr() for r in W._retired)
+        c = W.get(8192, dev, "buf")  # no live graph holds `b`: not retired
+        assert not any(r.data_ptr() == b.data_ptr() for r in W._retired) and c.numel() >= 8192
+    W._bufs = {k: v for k, v in W._bufs.items() if "t_lifetime" not in k[1]}

@@ -611,7 +611,6 @@ def test_sharded_step_routed_exchanges_captured_on_rccl(cuda, monkeypatch, B):
     s.close()
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                             device_id=torch.device(cuda))
-    monkeypatch.setenv("TT_SHARDED_KEEP", "0")  # no pinned route buffers: the graph's pool as it is
     try:
         a, b, c = (_small_model(cuda, seed=8) for _ in range(3))
         xchg = ShardedTrainStep(a, shard_min_rows=300, global_negatives=True, always_exchange=True)
