@@ -49,7 +49,6 @@
 //  answer (indices 0..k-1 by the tie rule) is written directly.
 #include <cmath>
 #include <cstdlib>
-#include <mutex>
 
 #include "tt_common.h"
 
@@ -2085,54 +2084,11 @@ extern "C" int tt_bruteforce_build(const float* cand, int64_t ldc, int64_t n_can
   return TT_OK;
 }
 
-namespace tt {
-namespace {
-// Chunk pipelining (searches of more than one query chunk): every chunk's
-// query state, lists and finalize state in one of two alternating sets, the
-// finalize of chunk c on an auxiliary stream beside the prep / estimate /
-// scan of chunk c + 1 on the caller's stream.  The scan's workgroup leaves
-// ~12 KB of a CU's LDS and ~96 registers per SIMD free: one finalize
-// workgroup fits beside it, and the finalize's row reads (memory latency)
-// overlap the scan's MFMA / LDS work.  TT_INDEX_PIPE=0: one set, one stream.
-bool pipe_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("TT_INDEX_PIPE");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-bool pipelined(const SearchPlan& p, int64_t n_queries) { return pipe_enabled() && n_queries > p.chunk; }
-
-struct AuxStream {  // one per device: the finalize stream and the cross-stream events
-  hipStream_t st = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr, scan[2] = {nullptr, nullptr}, fin[2] = {nullptr, nullptr};
-  std::mutex mu;  // one pipelined search at a time per device (the events are shared)
-};
-int aux_stream(AuxStream** out) {
-  static AuxStream aux[64];
-  static std::mutex init_mu;
-  int dev = 0;
-  TT_CHECK_HIP(hipGetDevice(&dev));
-  TT_REQUIRE(dev >= 0 && dev < 64, "tt_bruteforce_search: device %d out of range", dev);
-  std::lock_guard<std::mutex> g(init_mu);
-  AuxStream& a = aux[dev];
-  if (!a.st) {
-    TT_CHECK_HIP(hipStreamCreateWithFlags(&a.st, hipStreamNonBlocking));
-    for (hipEvent_t* e : {&a.fork, &a.join, &a.scan[0], &a.scan[1], &a.fin[0], &a.fin[1]})
-      TT_CHECK_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
-  }
-  *out = &a;
-  return TT_OK;
-}
-}  // namespace
-}  // namespace tt
-
 extern "C" size_t tt_bruteforce_workspace_size(int64_t n_queries, int64_t n_cand, int32_t dim, int32_t k) {
   if (n_queries < 1 || n_cand < 1 || k < 1 || pick_dpad(dim) == 0) return 0;
   const SearchPlan p = plan_search(n_queries, n_cand, k, 1);
   Carver cv(nullptr, 0);
   carve_search(cv, pick_dpad(dim), p, true, true);
-  if (pipelined(p, n_queries)) carve_search(cv, pick_dpad(dim), p, true, true);  // the second set
   return cv.used();
 }
 
@@ -2154,32 +2110,15 @@ extern "C" int tt_bruteforce_search(const void* index, const float* cand, int64_
   TT_REQUIRE(queries && out_scores && out_idx, "tt_bruteforce_search: NULL queries/outputs");
   const int D = pick_dpad(dim);
   const SearchPlan p = plan_search(n_queries, n_cand, k, 1);
-  const bool pipe = pipelined(p, n_queries);
   Carver cv(workspace, workspace_bytes);
-  SearchWs ws[2];
-  ws[0] = carve_search(cv, D, p, true, true);
-  ws[1] = pipe ? carve_search(cv, D, p, true, true) : ws[0];
+  SearchWs w = carve_search(cv, D, p, true, true);
   if (!workspace || cv.used() > workspace_bytes)
     return fail(TT_ERR_WORKSPACE, "tt_bruteforce_search: workspace %zu < required %zu", workspace_bytes, cv.used());
   hipStream_t st = to_stream(stream);
-  AuxStream* aux = nullptr;
-  std::unique_lock<std::mutex> lock;
-  if (pipe) {
-    if (int rc = aux_stream(&aux)) return rc;
-    lock = std::unique_lock<std::mutex>(aux->mu);
-    // the aux stream joins the caller's (a fork: also what brings it into a capture)
-    TT_CHECK_HIP(hipEventRecord(aux->fork, st));
-    TT_CHECK_HIP(hipStreamWaitEvent(aux->st, aux->fork, 0));
-  }
   const int vec4 = is_vec4(cand, ldc, dim) ? 1 : 0;
-  int c = 0;
-  for (int64_t q0 = 0; q0 < n_queries; q0 += p.chunk, ++c) {
+  for (int64_t q0 = 0; q0 < n_queries; q0 += p.chunk) {
     const int64_t nq = (n_queries - q0 < p.chunk) ? n_queries - q0 : p.chunk;
     const float* qc = queries + q0 * ldq;
-    const int set = pipe ? (c & 1) : 0;
-    const SearchWs& w = ws[set];
-    // this set's previous chunk (c - 2) must be finalized before its state is reused
-    if (pipe && c >= 2) TT_CHECK_HIP(hipStreamWaitEvent(st, aux->fin[set], 0));
     TT_CHECK_HIP(hipMemsetAsync(w.fail_count, 0, (2 + kFbSlots) * sizeof(int), st));
     if (int rc = run_prep(qc, ldq, nq, dim, D, index, w, true, st)) return rc;
     if (int rc = run_estimate(D, index, 0, n_cand, nq, p, w, w.tau, st)) return rc;
@@ -2192,18 +2131,7 @@ extern "C" int tt_bruteforce_search(const void* index, const float* cand, int64_
     FallbackArgs fb{qc, ldq, cand, ldc, n_cand, index_offset, dim, k, p.L, p.P, p.parts, vec4,
                     w.fail_count, w.fail_list, w.fail_count + 1, w.fb_scratch, w.fb_scratch_n,
                     out_scores + q0 * k, out_idx + q0 * k};
-    if (pipe) {  // the finalize of this chunk on the aux stream, beside the next chunk's scan
-      TT_CHECK_HIP(hipEventRecord(aux->scan[set], st));
-      TT_CHECK_HIP(hipStreamWaitEvent(aux->st, aux->scan[set], 0));
-      if (int rc = run_finalize(fa, fb, nq, p, aux->st)) return rc;
-      TT_CHECK_HIP(hipEventRecord(aux->fin[set], aux->st));
-    } else if (int rc = run_finalize(fa, fb, nq, p, st)) {
-      return rc;
-    }
-  }
-  if (pipe) {  // the caller's stream joins the aux stream (every finalize done)
-    TT_CHECK_HIP(hipEventRecord(aux->join, aux->st));
-    TT_CHECK_HIP(hipStreamWaitEvent(st, aux->join, 0));
+    if (int rc = run_finalize(fa, fb, nq, p, st)) return rc;
   }
   return TT_OK;
 }

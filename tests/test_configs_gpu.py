@@ -238,12 +238,11 @@ def test_c4_index_full_candidates_bitexact(cuda, Q, k):
     assert np.array_equal(s.cpu().numpy(), rs)
 
 
-def test_c4_index_pipelined_chunks_bitexact(cuda):
+def test_c4_index_multi_chunk_bitexact(cuda):
     """A search of more queries than one chunk (k = 100: 131,072 queries per
-    chunk; here 3 chunks) runs its chunks pipelined — the finalize of chunk c
-    on the auxiliary stream beside the scan of chunk c + 1, two alternating
-    state sets — and equals the chunk-by-chunk searches (each one chunk: no
-    pipelining) bit for bit; rows of every chunk against the fp32 oracle."""
+    chunk; here 3 chunks, the workspace's list state reused chunk after
+    chunk) equals the chunk-by-chunk searches bit for bit; rows of every
+    chunk against the fp32 oracle."""
     from pkg.modelling import hip_ops
 
     k = 100
