@@ -10,6 +10,7 @@
 // lanes.  tt_gather_multi puts several calls (both towers) in one launch.
 // The op is HBM-bound (algorithmic bytes per row: 2*dim*4 + 4).
 #include "tt_common.h"
+#include "tt_mlp_pack.h"
 
 namespace tt {
 namespace {
@@ -108,7 +109,16 @@ __device__ __forceinline__ void gather_segment(const GatherArgs& a, const Gather
   }
 }
 
-__global__ void __launch_bounds__(kGatherThreads) gather_grouped_kernel(const GatherArgs a) {
+// Blocks [0, gather_blocks) gather; the rest (tt_gather_multi_pack) pack the
+// towers' MLP weight images for the step's forward (independent work in the
+// same launch: no pack launch, no cross-queue fork in front of the forward).
+__global__ void __launch_bounds__(kGatherThreads) gather_grouped_kernel(const GatherArgs a, const pack::PackJobs pj,
+                                                                        int64_t pack_total, int32_t gather_blocks) {
+  if (static_cast<int32_t>(blockIdx.x) >= gather_blocks) {
+    const int64_t t = static_cast<int64_t>(blockIdx.x - gather_blocks) * kGatherThreads + threadIdx.x;
+    if (t < pack_total) pack::pack_many_thread(pj, t);
+    return;
+  }
   // Locate this block's segment (<= 32 segments; scalar loop).
   int si = 0;
 #pragma unroll 1
@@ -212,8 +222,13 @@ int add_call(GatherArgs& a, int32_t& blocks, const tt_gather_segment* segs, int3
   return TT_OK;
 }
 
-int launch(const GatherArgs& a, int32_t blocks, tt_stream_t stream) {
-  hipLaunchKernelGGL(gather_grouped_kernel, dim3(blocks), dim3(kGatherThreads), 0, to_stream(stream), a);
+int launch(const GatherArgs& a, int32_t blocks, tt_stream_t stream, const pack::PackJobs* pj = nullptr,
+           int64_t pack_total = 0) {
+  static_assert(kGatherThreads == 256, "the pack blocks are 256-thread blocks");
+  const int64_t pack_blocks = pj ? ceil_div(pack_total, kGatherThreads) : 0;
+  const pack::PackJobs none{};
+  hipLaunchKernelGGL(gather_grouped_kernel, dim3(static_cast<unsigned>(blocks + pack_blocks)), dim3(kGatherThreads), 0,
+                     to_stream(stream), a, pj ? *pj : none, pj ? pack_total : int64_t(0), blocks);
   TT_CHECK_LAUNCH();
   return TT_OK;
 }
@@ -253,6 +268,25 @@ extern "C" int tt_gather_multi(const tt_gather_call* calls, int32_t num_calls, i
     if (rc) return rc;
   }
   return launch(a, blocks, stream);
+}
+
+extern "C" int tt_gather_multi_pack(const tt_gather_call* calls, int32_t num_calls, int64_t batch,
+                                    const tt_mlp_pack_job* jobs, int32_t num_jobs, tt_stream_t stream) {
+  using namespace tt;
+  clear_error();
+  TT_REQUIRE(calls != nullptr && num_calls >= 1, "tt_gather_multi_pack: no calls");
+  TT_REQUIRE(batch >= 1, "tt_gather_multi_pack: batch must be >= 1");
+  pack::PackJobs pj;
+  int64_t total = 0;
+  if (int rc = pack::make_pack_jobs(jobs, num_jobs, &pj, &total, "tt_gather_multi_pack")) return rc;
+  GatherArgs a{};
+  a.batch = batch;
+  int32_t blocks = 0;
+  for (int c = 0; c < num_calls; ++c) {
+    int rc = add_call(a, blocks, calls[c].segs, calls[c].num_segs, calls[c].out, calls[c].out_stride);
+    if (rc) return rc;
+  }
+  return launch(a, blocks, stream, &pj, total);
 }
 
 extern "C" int tt_gather_tagged(const tt_row_table* tables, int32_t num_tables, int32_t dim, const int32_t* tags,

@@ -30,6 +30,7 @@
 #include <cstdlib>
 
 #include "tt_common.h"
+#include "tt_mlp_pack.h"
 
 namespace tt {
 namespace {
@@ -78,10 +79,14 @@ __device__ __forceinline__ f32x4 mlp_load4s(__amdgpu_buffer_rsrc_t d, unsigned v
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(d, voff, soff, 0));
 }
 
-__device__ __forceinline__ unsigned bf16_bits(float v) {
-  return static_cast<unsigned>(__builtin_bit_cast(unsigned short, static_cast<__bf16>(v)));
-}
-__device__ __forceinline__ float bf16_val(unsigned bits) { return __uint_as_float(bits << 16); }
+using pack::bf16_bits;
+using pack::bf16_val;
+using pack::pack_fragment;
+using pack::PackJob;
+using pack::PackJobs;
+using pack::kMaxPackJobs;
+using pack::mlp_ks;
+using pack::mlp_nb;
 
 // LDS A tile: plane p, row r (0..63), 16-B chunk c (0..7) of the 64-deep stage
 // at byte (p * 64 + r) * 128 + ((c ^ ((r >> 1) & 7)) << 4): the 16 lanes of
@@ -633,39 +638,6 @@ __global__ void __launch_bounds__(1024) mlp_sum_parts_pair_kernel(const float* _
   else mlp_sum_parts_block(p1, S1, len1, o1, b - split, red);
 }
 
-// One thread per (k-step, column block, lane): 8 hi + 8 lo bf16 of
-// B[k = 16 ks + 8 (lane >> 5) + j][n = 32 cb + (lane & 31)], j < 8, zero padded.
-// trans: B = W^T with W [N, K] row-major (B[k][n] = W[n * ldw + k]).
-// One lane's 8 consecutive k of column n, as bf16 hi and lo, into the image
-// (fragment (ks, cb) of the B image, planes hi / lo).  All 8 loads are issued
-// before any is used (branch-free: out-of-range elements read w[0], become 0).
-__device__ __forceinline__ void pack_fragment(const float* __restrict__ w, int64_t ldw, int K, int N, int trans,
-                                              int ks, int cb, int NB, int lane, __bf16* __restrict__ img) {
-  const int n = 32 * cb + (lane & 31);
-  float x[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int k = 16 * ks + 8 * (lane >> 5) + j;
-    const bool ok = k < K && n < N;
-    const int64_t at = trans ? static_cast<int64_t>(n) * ldw + k : static_cast<int64_t>(k) * ldw + n;
-    x[j] = w[ok ? at : 0];
-  }
-  unsigned hb[8], lb[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int k = 16 * ks + 8 * (lane >> 5) + j;
-    const float v = (k < K && n < N) ? x[j] : 0.0f;
-    hb[j] = bf16_bits(v);
-    lb[j] = bf16_bits(v - bf16_val(hb[j]));
-  }
-  u32x4 hv, lv;
-  hv.x = hb[0] | (hb[1] << 16); hv.y = hb[2] | (hb[3] << 16); hv.z = hb[4] | (hb[5] << 16); hv.w = hb[6] | (hb[7] << 16);
-  lv.x = lb[0] | (lb[1] << 16); lv.y = lb[2] | (lb[3] << 16); lv.z = lb[4] | (lb[5] << 16); lv.w = lb[6] | (lb[7] << 16);
-  const int64_t base = ((static_cast<int64_t>(ks) * NB + cb) * 2) * 64 + lane;
-  reinterpret_cast<u32x4*>(img)[base] = hv;        // plane 0: hi
-  reinterpret_cast<u32x4*>(img)[base + 64] = lv;   // plane 1: lo
-}
-
 __global__ void __launch_bounds__(256) mlp_pack_kernel(const float* __restrict__ w, int64_t ldw, int K, int N,
                                                        int trans, int KS, int NB, __bf16* __restrict__ img) {
   const int64_t t = blockIdx.x * 256ll + threadIdx.x;
@@ -674,37 +646,13 @@ __global__ void __launch_bounds__(256) mlp_pack_kernel(const float* __restrict__
   pack_fragment(w, ldw, K, N, trans, static_cast<int>((t >> 6) / NB), static_cast<int>((t >> 6) % NB), NB, lane, img);
 }
 
-// image k-steps padded to whole 64-deep stages, column blocks to 4 per wave row
-struct PackJob {
-  const float* w;
-  int64_t ldw;
-  int K, N, trans, KS, NB;
-  __bf16* img;
-  int64_t first;  // first thread of this job
-};
-constexpr int kMaxPackJobs = 8;
-struct PackJobs {
-  PackJob j[kMaxPackJobs];
-  int n;
-};
-
 __global__ void __launch_bounds__(256) mlp_pack_many_kernel(const PackJobs jobs, int64_t total) {
   const int64_t t = blockIdx.x * 256ll + threadIdx.x;
   if (t >= total) return;
-  // jobs start on multiples of 64 threads: the job is wave-uniform (scalar search)
-  const int64_t tw = (static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(t >> 6)))) << 6;
-  int q = 0;
-  while (q + 1 < jobs.n && tw >= jobs.j[q + 1].first) ++q;
-  const PackJob& J = jobs.j[q];
-  const int64_t u = t - J.first;
-  const int lane = static_cast<int>(u & 63);
-  const int cb = static_cast<int>((u >> 6) % J.NB);
-  const int ks = static_cast<int>((u >> 6) / J.NB);
-  pack_fragment(J.w, J.ldw, J.K, J.N, J.trans, ks, cb, J.NB, lane, J.img);
+  pack::pack_many_thread(jobs, t);
 }
 
-inline int mlp_ks(int K) { return (K + 63) / 64 * 4; }
-inline int mlp_nb(int N) { return (N + 127) / 128 * 4; }
+
 
 }  // namespace
 }  // namespace tt
@@ -733,27 +681,9 @@ extern "C" int tt_mlp_pack(const float* w, int64_t ldw, int32_t K, int32_t N, in
 
 extern "C" int tt_mlp_pack_many(const tt_mlp_pack_job* jobs, int32_t num_jobs, tt_stream_t stream) {
   clear_error();
-  TT_REQUIRE(jobs && num_jobs >= 1 && num_jobs <= kMaxPackJobs, "tt_mlp_pack_many: 1..%d jobs", kMaxPackJobs);
-  PackJobs pj{};
-  pj.n = num_jobs;
+  PackJobs pj;
   int64_t total = 0;
-  for (int i = 0; i < num_jobs; ++i) {
-    const tt_mlp_pack_job& j = jobs[i];
-    TT_REQUIRE(j.w && j.img && j.K >= 1 && j.N >= 1, "tt_mlp_pack_many: job %d: bad w/img/K/N", i);
-    TT_REQUIRE(j.ldw >= (j.trans ? j.K : j.N), "tt_mlp_pack_many: job %d: ldw too small", i);
-    TT_REQUIRE(j.img_bytes >= tt_mlp_pack_bytes(j.K, j.N), "tt_mlp_pack_many: job %d: image too small", i);
-    PackJob& J = pj.j[i];
-    J.w = j.w;
-    J.ldw = j.ldw;
-    J.K = j.K;
-    J.N = j.N;
-    J.trans = j.trans ? 1 : 0;
-    J.KS = mlp_ks(j.K);
-    J.NB = mlp_nb(j.N);
-    J.img = static_cast<__bf16*>(j.img);
-    J.first = total;
-    total += static_cast<int64_t>(J.KS) * J.NB * 64;
-  }
+  if (int rc = pack::make_pack_jobs(jobs, num_jobs, &pj, &total, "tt_mlp_pack_many")) return rc;
   hipLaunchKernelGGL(mlp_pack_many_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, to_stream(stream), pj, total);
   TT_CHECK_LAUNCH();
   return TT_OK;

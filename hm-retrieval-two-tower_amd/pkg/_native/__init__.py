@@ -185,6 +185,7 @@ _PROTOS = {
     "tt_probe_arm_repeat": (c_int32, [c_int32, c_void_p, c_void_p, c_int32]),
     "tt_gather_grouped": (c_int32, [POINTER(GatherSegment), c_int32, c_int64, c_void_p, c_int64, c_void_p]),
     "tt_gather_multi": (c_int32, [POINTER(GatherCall), c_int32, c_int64, c_void_p]),
+    "tt_gather_multi_pack": (c_int32, [POINTER(GatherCall), c_int32, c_int64, c_void_p, c_int32, c_void_p]),
     "tt_gather_tagged": (c_int32, [POINTER(RowTable), c_int32, c_int32, c_void_p, c_void_p, c_int64, c_void_p, c_int64,
                                    c_void_p]),
     "tt_sparse_workspace_size": (c_size_t, [POINTER(SparseTable), c_int32, c_int64]),

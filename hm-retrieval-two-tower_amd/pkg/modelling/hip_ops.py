@@ -334,8 +334,10 @@ def gather_grouped(
 
 
 def gather_multi(calls: Sequence[Tuple[Sequence[Tuple[torch.Tensor, Optional[torch.Tensor], int]], torch.Tensor]],
-                 batch: int) -> None:
-    """Several gather_grouped calls of one batch (e.g. both towers) in one launch."""
+                 batch: int, pack_jobs: Optional[Sequence[Tuple[torch.Tensor, bool, torch.Tensor]]] = None) -> None:
+    """Several gather_grouped calls of one batch (e.g. both towers) in one
+    launch; pack_jobs (mlp_pack_many's jobs): the weight images packed by the
+    same launch (tt_gather_multi_pack)."""
     if sum(len(segs) for segs, _ in calls) > _native.MAX_SEGMENTS:
         raise ValueError(f"at most {_native.MAX_SEGMENTS} segments per launch")
     keep = []
@@ -349,7 +351,12 @@ def gather_multi(calls: Sequence[Tuple[Sequence[Tuple[torch.Tensor, Optional[tor
         arr[i].num_segs = len(segs)
         arr[i].out = out.data_ptr()
         arr[i].out_stride = ld
+    if pack_jobs:
+        check(lib().tt_gather_multi_pack(arr, len(calls), batch, _pack_job_array(pack_jobs), len(pack_jobs),
+                                         _stream()))
+        return
     check(lib().tt_gather_multi(arr, len(calls), batch, _stream()))
+
 
 def _sparse_tables(tables: Sequence[dict], batch: int, adam: bool, slots: bool = True):
     arr = (SparseTable * len(tables))()
@@ -1121,15 +1128,19 @@ class ScoreMatrix(torch.autograd.Function):
         return dq, dc
 
 
-def mlp_pack_many(jobs: Sequence[Tuple[torch.Tensor, bool, torch.Tensor]]) -> None:
-    """Several mlp_pack images in one launch: jobs of (w, trans, image buffer)."""
+def _pack_job_array(jobs: Sequence[Tuple[torch.Tensor, bool, torch.Tensor]]):
     arr = (_native.MlpPackJob * len(jobs))()
     for i, (w, trans, img) in enumerate(jobs):
         _req(w, "w", torch.float32, 2)
         K, N = (w.shape[1], w.shape[0]) if trans else (w.shape[0], w.shape[1])
         arr[i].w, arr[i].ldw, arr[i].K, arr[i].N = w.data_ptr(), _row_major(w, "w"), K, N
         arr[i].trans, arr[i].img, arr[i].img_bytes = int(bool(trans)), img.data_ptr(), img.numel()
-    check(lib().tt_mlp_pack_many(arr, len(jobs), _stream()))
+    return arr
+
+
+def mlp_pack_many(jobs: Sequence[Tuple[torch.Tensor, bool, torch.Tensor]]) -> None:
+    """Several mlp_pack images in one launch: jobs of (w, trans, image buffer)."""
+    check(lib().tt_mlp_pack_many(_pack_job_array(jobs), len(jobs), _stream()))
 
 
 def _check_rows(a, k, n, out, amask, cmask, bias) -> int:

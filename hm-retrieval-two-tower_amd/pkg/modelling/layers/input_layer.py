@@ -64,9 +64,9 @@ class _MultiGatherFn(torch.autograd.Function):
     """Several InputLayers of one batch gathered by one tt_gather_multi launch."""
 
     @staticmethod
-    def forward(ctx, layers, seglists, batch, extra, *anchors):
+    def forward(ctx, layers, seglists, batch, extra, pack_jobs, *anchors):
         outs = [torch.empty(batch, l.row_stride, dtype=torch.float32, device=l.device) for l in layers]
-        hip_ops.gather_multi(list(zip(seglists, outs)) + list(extra), batch)
+        hip_ops.gather_multi(list(zip(seglists, outs)) + list(extra), batch, pack_jobs=pack_jobs)
         ctx.layers = layers
         return tuple(o[:, : l.output_dim] for o, l in zip(outs, layers))
 
@@ -76,7 +76,7 @@ class _MultiGatherFn(torch.autograd.Function):
             if g is not None and g.stride(1) != 1:
                 g = g.contiguous()
             layer.last_grad = g
-        return (None, None, None, None) + (None,) * len(ctx.layers)
+        return (None, None, None, None, None) + (None,) * len(ctx.layers)
 
 
 class InputLayer:
@@ -186,11 +186,12 @@ class InputLayer:
 
     @staticmethod
     def gather_many(layers: Sequence["InputLayer"], xs: Sequence[Dict[str, torch.Tensor]],
-                    extra: Sequence = ()) -> List[torch.Tensor]:
+                    extra: Sequence = (), pack_jobs: Optional[Sequence] = None) -> List[torch.Tensor]:
         """The outputs of several InputLayers on one batch from ONE gather launch
         (the query and candidate towers of a train step).  `extra`: further
         (segments, out) calls of the same batch riding in that launch without
-        gradients (the logQ lookup)."""
+        gradients (the logQ lookup); `pack_jobs`: the towers' MLP weight
+        images packed by the same launch (hip_ops.gather_multi)."""
         prepared = [l._segments(x) for l, x in zip(layers, xs)]
         batches = {b for _, b in prepared}
         if len(batches) != 1:
@@ -200,9 +201,11 @@ class InputLayer:
             b = batches.pop()
             for segs, out in extra:
                 hip_ops.gather_grouped(segs, b, out)
+            if pack_jobs:
+                hip_ops.mlp_pack_many(pack_jobs)
             return [_GatherFn.apply(l._anchor, l, segs, bb) for l, (segs, bb) in zip(layers, prepared)]
         return list(_MultiGatherFn.apply(list(layers), [segs for segs, _ in prepared], batches.pop(), list(extra),
-                                         *[l._anchor for l in layers]))
+                                         pack_jobs or None, *[l._anchor for l in layers]))
 
     def sparse_sources(self) -> List[dict]:
         """Per table: its lookups of the last call as (ids, grad column) sources."""

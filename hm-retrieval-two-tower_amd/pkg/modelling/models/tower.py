@@ -129,6 +129,22 @@ class DenseStack:
                 jobs.append((w, trans, buf))
         return imgs, jobs
 
+    def prepack_jobs(self, flat: torch.Tensor) -> list:
+        """The pack jobs of this stack's images for a forward on `flat`, to be
+        run by another launch (the train step's gather: hip_ops.gather_multi
+        with pack_jobs); the next forward_acts on the same flat then uses the
+        images as they are (once)."""
+        imgs, jobs = self._pack_jobs(flat)
+        self.__dict__["_prepacked"] = flat.data_ptr()
+        return jobs
+
+    def _images_for(self, flat: torch.Tensor) -> Dict[Tuple[str, int], torch.Tensor]:
+        """This forward's images: prepacked by the gather launch, or packed now."""
+        if self.__dict__.get("_prepacked") == flat.data_ptr():
+            self.__dict__["_prepacked"] = None
+            return self.__dict__["_images"]
+        return self._pack_images(flat)
+
     def _pack_images(self, flat: torch.Tensor) -> Dict[Tuple[str, int], torch.Tensor]:
         """Every layer's packed bf16 hi/lo weight images, forward ("f": B = W)
         and transposed ("t": B = W^T, the input-gradient GEMMs), in ONE
@@ -150,7 +166,7 @@ class DenseStack:
 
     def forward_acts(self, x: torch.Tensor, flat: torch.Tensor) -> List[torch.Tensor]:
         """[x, h_1, ..., h_L] with h_l = relu(h_{l-1} W_l + b_l) (tt_mlp_rows)."""
-        imgs = self._pack_images(flat)
+        imgs = self._images_for(flat)
         acts = [x]
         for li in range(len(self.layout)):
             p = self._fwd_problem(li, acts[-1], flat, imgs)
@@ -285,8 +301,12 @@ def forward_acts_pair(stacks, xs, flats) -> List[List[torch.Tensor]]:
     """DenseStack.forward_acts of the two towers on ONE stream with every
     launch shared: one tt_mlp_pack_many for both towers' images (8 jobs at
     one hidden layer), then one tt_mlp_rows_pair per layer."""
+    pre = [st.__dict__.get("_prepacked") == f.data_ptr() for st, f in zip(stacks, flats)]
     packed = [st._pack_jobs(f) for st, f in zip(stacks, flats)]
-    jobs = packed[0][1] + packed[1][1]
+    jobs = [j for p, (_, js) in zip(pre, packed) if not p for j in js]
+    for st, p in zip(stacks, pre):
+        if p:
+            st.__dict__["_prepacked"] = None
     for i in range(0, len(jobs), 8):
         hip_ops.mlp_pack_many(jobs[i:i + 8])
     acts = [[xs[0]], [xs[1]]]

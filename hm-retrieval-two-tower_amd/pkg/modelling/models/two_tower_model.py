@@ -53,6 +53,10 @@ FUSED_SORT_EARLY = os.environ.get("TT_FUSED_SORT_EARLY", "1") == "1"
 # launches (tt_mlp_wgrad_adagrad: the partial-sum launch updates the layer)
 # instead of one dense_adagrad launch per tower after its backward
 FUSED_DENSE_WGRAD = os.environ.get("TT_FUSED_DENSE_WGRAD", "1") == "1"
+# The towers' MLP weight images packed by the train step's gather launch
+# (tt_gather_multi_pack) instead of one pack launch per tower at the start of
+# each tower's forward (TT_PACK_WITH_GATHER=0).
+PACK_WITH_GATHER = os.environ.get("TT_PACK_WITH_GATHER", "1") == "1"
 
 
 class TwoTowerModel(AbstractKerasModel):
@@ -166,8 +170,16 @@ class TwoTowerModel(AbstractKerasModel):
         q, c = self._split(x)
         with torch.set_grad_enabled(training):
             call = self._logq_call(x)  # rides in the towers' gather launch
+            # ... and so do the towers' MLP weight images of this forward (at most 8 jobs)
+            pack = []
+            if training and PACK_WITH_GATHER and torch.is_grad_enabled() and self.device.type == "cuda":
+                pack = [j for t in self.towers for j in t.dense.prepack_jobs(t.dense.flat.detach())]
+                if len(pack) > 8:
+                    for t in self.towers:
+                        t.dense.__dict__["_prepacked"] = None
+                    pack = []
             qi, ci = InputLayer.gather_many([self.query_tower.input_layer, self.candidate_tower.input_layer], [q, c],
-                                            extra=[call] if call is not None else ())
+                                            extra=[call] if call is not None else (), pack_jobs=pack or None)
             self._sort_issued = False
             if training and qi.is_cuda:
                 # the embedding update's id sort needs only these ids

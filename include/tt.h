@@ -600,6 +600,12 @@ typedef struct {
   size_t img_bytes;
 } tt_mlp_pack_job;
 int tt_mlp_pack_many(const tt_mlp_pack_job* jobs, int32_t num_jobs, tt_stream_t stream);
+/* tt_gather_multi and tt_mlp_pack_many in ONE launch (independent work: the
+ * towers' input gather and the weight images their forward reads), so the
+ * train step's forward starts with no pack launch and no fork in front of
+ * it.  Results identical to the two calls.  batch >= 1, 1..8 jobs. */
+int tt_gather_multi_pack(const tt_gather_call* calls, int32_t num_calls, int64_t batch,
+                         const tt_mlp_pack_job* jobs, int32_t num_jobs, tt_stream_t stream);
 /* colsum != NULL: also colsum[n] = sum_m C[m][n] (the bias gradient of the
  * layer below, BiasAddGrad): per-workgroup partial sums in the epilogue, then
  * one small launch adds them in workgroup order (deterministic); needs a

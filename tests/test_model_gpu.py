@@ -75,6 +75,10 @@ def test_index_recall_with_gpu_index(cuda):
     assert all(isinstance(v, np.float64) for v in rec.metric.values())
 
 
+def _t(x, cuda):
+    return torch.as_tensor(x, device=cuda)
+
+
 def _small_model(cuda, seed=0, logq=True, fused=False):
     V = [str(i) for i in range(300)]
     qf = [Feature("cust", dtypes.string, FeatureFamily.QUERY, embedding_size=16, vocab=V),
@@ -335,6 +339,69 @@ def test_fused_dense_wgrad_bit_identical(cuda, monkeypatch, pair):
             assert torch.equal(sa[k], sb[k]), (i, B, k)
     a.optimizer.check_status(cuda)
     b.optimizer.check_status(cuda)
+
+
+@pytest.mark.parametrize("pair", [0, 1])
+def test_pack_with_gather_bit_identical(cuda, monkeypatch, pair):
+    """TT_PACK_WITH_GATHER: the towers' MLP weight images packed by the train
+    step's gather launch (tt_gather_multi_pack) instead of one pack launch
+    per tower: bit-identical losses, tables, accumulators and MLP buffers at
+    ragged batch sizes, eager and graphed (and with paired tower launches)."""
+    from pkg.modelling import losses
+    from pkg.modelling.models import two_tower_model as ttm
+
+    monkeypatch.setattr(losses, "TOWER_PAIR", pair)
+    a, b = _small_model(cuda, seed=43), _small_model(cuda, seed=43)
+    rng = np.random.default_rng(15)
+    for i, B in enumerate((512, 37, 256, 1)):
+        x = _batch(cuda, rng, B, True)
+        monkeypatch.setattr(ttm, "PACK_WITH_GATHER", False)
+        la = a.train_step(x)["loss"]
+        monkeypatch.setattr(ttm, "PACK_WITH_GATHER", True)
+        lb = b.train_step(x)["loss"]
+        assert all(t.dense.__dict__.get("_prepacked") is None for t in b.towers)  # consumed by the forward
+        assert torch.equal(la, lb), (i, B)
+        sa, sb = _state(a), _state(b)
+        for k in sa:
+            assert torch.equal(sa[k], sb[k]), (i, B, k)
+    batches = [_batch(cuda, rng, 256, True) for _ in range(4)]
+    ga = GraphedTrainStep(a, batches[0], warmup=1)
+    monkeypatch.setattr(ttm, "PACK_WITH_GATHER", False)
+    gb = GraphedTrainStep(b, batches[0], warmup=1)
+    for x in batches[1:]:
+        assert torch.equal(ga(x)["loss"], gb(x)["loss"])
+    torch.cuda.synchronize()
+    sa, sb = _state(a), _state(b)
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
+
+
+def test_gather_multi_pack_equals_two_launches(cuda):
+    """tt_gather_multi_pack: the gather and the weight images of one launch
+    equal tt_gather_multi + tt_mlp_pack_many, byte for byte."""
+    from pkg.modelling.models.tower import DenseStack
+
+    g = torch.Generator()
+    g.manual_seed(3)
+    st = DenseStack(37, [66, 128], cuda, g)
+    rng = np.random.default_rng(8)
+    B = 1000
+    tab = torch.as_tensor(rng.standard_normal((500, 32)).astype(np.float32), device=cuda)
+    ids = _t(rng.integers(-2, 505, B).astype(np.int32), cuda)
+    num = torch.as_tensor(rng.standard_normal(B).astype(np.float32), device=cuda)
+    outs = [torch.full((B, 36), 7.0, device=cuda) for _ in range(2)]
+    flat = st.flat.detach()
+    jobs = st.prepack_jobs(flat)
+    hip_ops.gather_multi([([(num, None, 0), (tab, ids, 1)], outs[0])], B, pack_jobs=jobs)
+    imgs1 = {k: v.clone() for k, v in st.__dict__["_images"].items()}
+    for v in st.__dict__["_images"].values():
+        v.zero_()
+    hip_ops.gather_multi([([(num, None, 0), (tab, ids, 1)], outs[1])], B)
+    hip_ops.mlp_pack_many(jobs)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    for k, v in st.__dict__["_images"].items():
+        assert torch.equal(v, imgs1[k]), k
 
 
 @pytest.mark.parametrize("fused", [False, True])
