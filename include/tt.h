@@ -162,8 +162,9 @@ int tt_route_owner(const int32_t* recv, int64_t n, int32_t world,
  * [num_lookups] = each lookup's slot.  Every exchange of the step then has
  * the split sizes [cap]*world.  cap = num_lookups never overflows; a smaller
  * cap drops an owner's requests past it, adds their number to *overflow
- * (optional, zero it first) and points their lookups at the owner's last
- * slot. */
+ * (optional, zero it first) and marks their lookups idx_padded = -1 - owner:
+ * the lookup reads a zero row and contributes no gradient (the step reports
+ * the overflow and the sharded trainer raises on it). */
 int tt_route_pad(const int32_t* send, const long long* counts, const int32_t* idx,
                  int64_t num_lookups, int32_t world, int64_t cap,
                  int32_t* send_padded, int32_t* idx_padded, int32_t* overflow,
