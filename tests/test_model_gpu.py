@@ -376,6 +376,81 @@ def test_pack_with_gather_bit_identical(cuda, monkeypatch, pair):
         assert torch.equal(sa[k], sb[k]), k
 
 
+@pytest.mark.parametrize("fused", [False, True])
+def test_fused_backward_layer_bit_identical(cuda, monkeypatch, fused):
+    """TT_FUSED_BWD: each layer's weight-gradient partials, the layer below's
+    input gradient and the upper layer's partial sums + Adagrad in ONE launch
+    (tt_mlp_backward_layer) instead of three: bit-identical losses, tables,
+    accumulators and MLP buffers at ragged batch sizes, eager and graphed,
+    unfused and with the fused optimizer apply."""
+    from pkg.modelling.models import tower as tower_mod
+
+    a, b = _small_model(cuda, seed=47, fused=fused), _small_model(cuda, seed=47, fused=fused)
+    rng = np.random.default_rng(16)
+    for i, B in enumerate((512, 37, 256, 1)):
+        x = _batch(cuda, rng, B, True)
+        monkeypatch.setattr(tower_mod, "FUSED_BWD", False)
+        la = a.train_step(x)["loss"]
+        monkeypatch.setattr(tower_mod, "FUSED_BWD", True)
+        lb = b.train_step(x)["loss"]
+        assert torch.equal(la, lb), (i, B)
+        sa, sb = _state(a), _state(b)
+        for k in sa:
+            assert torch.equal(sa[k], sb[k]), (i, B, k)
+    batches = [_batch(cuda, rng, 256, True) for _ in range(4)]
+    monkeypatch.setattr(tower_mod, "FUSED_BWD", False)
+    ga = GraphedTrainStep(a, batches[0], warmup=1)
+    monkeypatch.setattr(tower_mod, "FUSED_BWD", True)
+    gb = GraphedTrainStep(b, batches[0], warmup=1)
+    for x in batches[1:]:
+        assert torch.equal(ga(x)["loss"], gb(x)["loss"])
+    torch.cuda.synchronize()
+    sa, sb = _state(a), _state(b)
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
+    a.optimizer.check_status(cuda)
+    b.optimizer.check_status(cuda)
+
+
+@pytest.mark.parametrize("units,need_dx", [([256, 128], True), ([256, 128], False), ([96, 66, 128], True),
+                                           ([128], True), ([64, 32, 16, 128], False)])
+def test_dense_stack_fused_backward_equals_per_layer(cuda, monkeypatch, units, need_dx):
+    """DenseStack.backward_acts with TT_FUSED_BWD equals the per-layer launches
+    bit for bit (input gradient and flat gradient), with and without the
+    fused Adagrad step, including a layer outside tt_mlp_wgrad's contract
+    (width 66: the chain finishes the pending sums, runs that layer on the
+    padded path, then resumes)."""
+    from pkg.modelling.models import tower as tower_mod
+    from pkg.modelling.models.tower import DenseStack
+
+    rng = np.random.default_rng(5)
+    M, in_dim = 3000, 132
+    x = torch.as_tensor(rng.standard_normal((M, in_dim)).astype(np.float32), device=cuda)
+    gout = torch.as_tensor(rng.standard_normal((M, units[-1])).astype(np.float32), device=cuda)
+    s = torch.tensor([0.5], device=cuda)
+    res = {}
+    for fb in (False, True):
+        for adagrad in (False, True):
+            g = torch.Generator()
+            g.manual_seed(9)
+            st = DenseStack(in_dim, units, cuda, g)
+            acc = torch.full_like(st.flat.detach(), 0.1)
+            st.fused_adagrad = (acc, 0.05, 1e-7) if adagrad else None
+            flat = st.flat.detach()
+            acts = st.forward_acts(x, flat)
+            monkeypatch.setattr(tower_mod, "FUSED_BWD", fb)
+            dx, gflat = st.backward_acts(acts, flat, gout, s, need_dx)
+            torch.cuda.synchronize()
+            res[(fb, adagrad)] = (dx, gflat, st.flat.detach().clone(), acc.clone())
+    for adagrad in (False, True):
+        r0, r1 = res[(False, adagrad)], res[(True, adagrad)]
+        assert (r0[0] is None) == (r1[0] is None) == (not need_dx)
+        if need_dx:
+            assert torch.equal(r0[0], r1[0])
+        for t0, t1 in zip(r0[1:], r1[1:]):
+            assert torch.equal(t0, t1)
+
+
 def test_gather_multi_pack_equals_two_launches(cuda):
     """tt_gather_multi_pack: the gather and the weight images of one launch
     equal tt_gather_multi + tt_mlp_pack_many, byte for byte."""
