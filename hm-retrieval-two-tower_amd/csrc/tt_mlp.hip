@@ -638,102 +638,6 @@ __global__ void __launch_bounds__(1024) mlp_sum_parts_pair_kernel(const float* _
   else mlp_sum_parts_block(p1, S1, len1, o1, b - split, red);
 }
 
-// 256-thread form of mlp_sum_parts_block for launches whose other block
-// roles are 256 threads: the same 16 split groups, each summed from 0 in
-// split order, then the 16 group sums added in group order — bit-identical;
-// each thread adds 4 of the groups (one after the other).
-__device__ __forceinline__ void mlp_sum_parts_block256(const float* __restrict__ parts, int S, int64_t len,
-                                                       float* __restrict__ out, const int64_t bid, f32x4 (*red)[64],
-                                                       const PartsAdagrad& ad) {
-  const int lane = threadIdx.x & 63, q4 = threadIdx.x >> 6;
-  const int64_t e4 = (bid * 64 + lane) * 4;
-  const int per = (S + 15) / 16;
-#pragma unroll 1
-  for (int gg = 0; gg < 4; ++gg) {
-    const int grp = 4 * q4 + gg;
-    const int s0 = grp * per, s1 = min(S, s0 + per);
-    f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (e4 < len) {
-      f32x4 v[8];
-      for (int sb = s0; sb < s1; sb += 8) {
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (sb + u < s1) v[u] = *reinterpret_cast<const f32x4*>(parts + (sb + u) * len + e4);
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (sb + u < s1) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) acc[q] += v[u][q];
-          }
-      }
-    }
-    red[grp][lane] = acc;
-  }
-  __syncthreads();
-  if (q4 == 0 && e4 < len) {
-    f32x4 t = red[0][lane];
-    for (int g = 1; g < 16; ++g) {
-      const f32x4 r = red[g][lane];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) t[q] += r[q];
-    }
-    *reinterpret_cast<f32x4*>(out + e4) = t;
-    if (ad.param) {
-      f32x4 pa = *reinterpret_cast<const f32x4*>(ad.param + e4);
-      f32x4 ac = *reinterpret_cast<const f32x4*>(ad.accum + e4);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float gi = t[q];
-        const float a = ac[q] + gi * gi;
-        ac[q] = a;
-        pa[q] = pa[q] - (gi * ad.lr) / (sqrtf(a) + ad.eps);
-      }
-      *reinterpret_cast<f32x4*>(ad.accum + e4) = ac;
-      *reinterpret_cast<f32x4*>(ad.param + e4) = pa;
-    }
-  }
-}
-
-// A layer's pending partial sums (+ its Adagrad step): the sum launch of
-// tt_mlp_wgrad(_adagrad) as a block role of another launch.
-struct SumJob {
-  const float* parts;
-  int S;
-  int64_t len;
-  float* out;
-  PartsAdagrad ad;
-};
-
-// One Dense layer's backward as ONE launch of independent block roles:
-// [0, nw) the layer's weight-gradient split partials (mlp_wgrad_block),
-// [nw, nw + nr) the input-gradient GEMM of the layer below (mlp_rows_block;
-// NCB = 0: none), then the previous (upper) layer's partial sums + Adagrad
-// (sum blocks; none when the grid ends before them).  No data flows between
-// the roles inside the launch: the input-gradient GEMM reads the packed
-// weight image, not the parameters the sum role updates.
-template <bool WMASK, int NCB, bool RMASK>
-__global__ void __launch_bounds__(kWgThreads) mlp_bwd_layer_kernel(const WgradArgs w, const int nw, const MlpArgs r,
-                                                                   const int nr, const SumJob sj) {
-  static_assert(kWgThreads == kMlpThreads, "one block size for every role");
-  constexpr int WB = 2 * kWgStageB, RB = NCB > 0 ? MlpSmem<NCB>::BYTES : 0, SB = 16 * 64 * 16;
-  constexpr int BYTES = WB > RB ? (WB > SB ? WB : SB) : (RB > SB ? RB : SB);
-  __shared__ __attribute__((aligned(16))) char smem[BYTES];
-  int b = blockIdx.x;
-  if (b < nw) {
-    mlp_wgrad_block<WMASK>(w, b, smem);
-    return;
-  }
-  b -= nw;
-  if constexpr (NCB > 0) {
-    if (b < nr) {
-      mlp_rows_block<NCB, RMASK>(r, b, smem);
-      return;
-    }
-    b -= nr;
-  }
-  mlp_sum_parts_block256(sj.parts, sj.S, sj.len, sj.out, b, reinterpret_cast<f32x4(*)[64]>(smem), sj.ad);
-}
-
 __global__ void __launch_bounds__(256) mlp_pack_kernel(const float* __restrict__ w, int64_t ldw, int K, int N,
                                                        int trans, int KS, int NB, __bf16* __restrict__ img) {
   const int64_t t = blockIdx.x * 256ll + threadIdx.x;
@@ -1050,97 +954,6 @@ extern "C" int tt_mlp_wgrad_pair(const tt_mlp_wgrad_problem* p, void* workspace,
   const int sb0 = static_cast<int>(ceil_div(len0, 256));
   hipLaunchKernelGGL(mlp_sum_parts_pair_kernel, dim3(static_cast<unsigned>(sb0 + ceil_div(len1, 256))), dim3(1024), 0,
                      st, a[0].parts, a[0].S, len0, p[0].dwb, a[1].parts, a[1].S, len1, p[1].dwb, sb0);
-  TT_CHECK_LAUNCH();
-  return TT_OK;
-}
-
-// ---- one Dense layer's backward in one launch ------------------------------
-namespace {
-
-// One weight-gradient job into its kernel arguments and its sum role.
-int wgrad_job_setup(const char* fn, const tt_mlp_wgrad_job* j, WgradArgs& a, SumJob& s) {
-  const tt_mlp_wgrad_problem& q = j->p;
-  if (int rc = wgrad_setup(fn, q.A, q.lda, q.G, q.ldg, q.gmask, q.ldgm, q.scale, q.M, q.Ka, q.N, q.dwb, a)) return rc;
-  const size_t need = tt_mlp_wgrad_workspace_size(q.M, q.Ka, q.N);
-  TT_REQUIRE(j->parts && j->parts_bytes >= need, "%s: partials buffer %zu < %zu bytes", fn, j->parts_bytes, need);
-  TT_REQUIRE(reinterpret_cast<uintptr_t>(q.dwb) % 16 == 0 && reinterpret_cast<uintptr_t>(j->parts) % 16 == 0,
-             "%s: dwb / parts must be 16-B aligned", fn);
-  TT_REQUIRE(!j->param || (j->accum && reinterpret_cast<uintptr_t>(j->param) % 16 == 0 &&
-                           reinterpret_cast<uintptr_t>(j->accum) % 16 == 0),
-             "%s: Adagrad param / accum must both be set and 16-B aligned", fn);
-  a.parts = static_cast<float*>(j->parts);
-  s = SumJob{a.parts, a.S, static_cast<int64_t>(q.Ka + 1) * q.N, q.dwb,
-             PartsAdagrad{j->param, j->param ? j->accum : nullptr, j->lr, j->eps}};
-  return TT_OK;
-}
-
-template <bool WM, int NCB>
-void launch_bwd2(bool rm, const WgradArgs& w, int nw, const MlpArgs& r, int nr, const SumJob& s, dim3 grid,
-                 hipStream_t st) {
-  if (rm) hipLaunchKernelGGL((mlp_bwd_layer_kernel<WM, NCB, true>), grid, dim3(kWgThreads), 0, st, w, nw, r, nr, s);
-  else hipLaunchKernelGGL((mlp_bwd_layer_kernel<WM, NCB, false>), grid, dim3(kWgThreads), 0, st, w, nw, r, nr, s);
-}
-
-template <bool WM>
-void launch_bwd1(int ncb, bool rm, const WgradArgs& w, int nw, const MlpArgs& r, int nr, const SumJob& s, dim3 grid,
-                 hipStream_t st) {
-  switch (ncb) {
-    case 0: launch_bwd2<WM, 0>(rm, w, nw, r, nr, s, grid, st); break;
-    case 1: launch_bwd2<WM, 1>(rm, w, nw, r, nr, s, grid, st); break;
-    case 2: launch_bwd2<WM, 2>(rm, w, nw, r, nr, s, grid, st); break;
-    default: launch_bwd2<WM, 3>(rm, w, nw, r, nr, s, grid, st); break;
-  }
-}
-
-}  // namespace
-
-extern "C" int tt_mlp_backward_layer(const tt_mlp_wgrad_job* w, const tt_mlp_rows_problem* r,
-                                     const tt_mlp_wgrad_job* prev, tt_stream_t stream) {
-  clear_error();
-  const char* fn = "tt_mlp_backward_layer";
-  TT_REQUIRE(w, "%s: NULL weight-gradient job", fn);
-  WgradArgs wa;
-  SumJob cur;
-  if (int rc = wgrad_job_setup(fn, w, wa, cur)) return rc;
-  MlpArgs ra{};
-  int ncb = 0;
-  const bool has_r = r != nullptr && r->M > 0;
-  if (has_r) {
-    if (int rc = rows_setup(fn, r->A, r->lda, r->amask, r->ldam, r->scale, r->M, r->K, r->img, r->N, r->bias, r->relu,
-                            r->cmask, r->ldcm, r->C, r->ldc, ra, ncb))
-      return rc;
-  }
-  SumJob ps{};
-  int64_t ns = 0;
-  if (prev) {
-    WgradArgs pa;
-    if (int rc = wgrad_job_setup(fn, prev, pa, ps)) return rc;
-    // the previous layer's partials are read while this layer's are written
-    const char *p0 = static_cast<const char*>(prev->parts), *w0 = static_cast<const char*>(w->parts);
-    const size_t pn = tt_mlp_wgrad_workspace_size(prev->p.M, prev->p.Ka, prev->p.N),
-                 wn = tt_mlp_wgrad_workspace_size(w->p.M, w->p.Ka, w->p.N);
-    TT_REQUIRE(p0 + pn <= w0 || w0 + wn <= p0, "%s: the previous layer's partials overlap this layer's", fn);
-    ns = ceil_div(ps.len, 256);
-  }
-  const int nw = wa.S * wa.TI * wa.TJ;
-  const int nr = has_r ? static_cast<int>(ceil_div(ra.M, kMlpBM)) : 0;
-  const dim3 grid(static_cast<unsigned>(nw + nr + ns));
-  hipStream_t st = to_stream(stream);
-  const bool rm = has_r && ra.amask != nullptr;
-  if (wa.gmask) launch_bwd1<true>(has_r ? ncb : 0, rm, wa, nw, ra, nr, ps, grid, st);
-  else launch_bwd1<false>(has_r ? ncb : 0, rm, wa, nw, ra, nr, ps, grid, st);
-  TT_CHECK_LAUNCH();
-  return TT_OK;
-}
-
-extern "C" int tt_mlp_wgrad_finish(const tt_mlp_wgrad_job* w, tt_stream_t stream) {
-  clear_error();
-  TT_REQUIRE(w, "tt_mlp_wgrad_finish: NULL job");
-  WgradArgs wa;
-  SumJob s;
-  if (int rc = wgrad_job_setup("tt_mlp_wgrad_finish", w, wa, s)) return rc;
-  hipLaunchKernelGGL(mlp_sum_parts_kernel, dim3(static_cast<unsigned>(ceil_div(s.len, 256))), dim3(1024), 0,
-                     to_stream(stream), s.parts, s.S, s.len, s.out, s.ad);
   TT_CHECK_LAUNCH();
   return TT_OK;
 }

@@ -838,8 +838,11 @@ __global__ void __launch_bounds__(kThreads) block_sum_kernel(const Job j, const 
     }
   }
   float* pc = j.pieces + T.piece_off + static_cast<int64_t>(blk) * 2 * T.dim;
-  // segment sums of one column, left in v[r] at each segment's last row
-  auto seg_sums = [&](float (&v)[kBlock], int col) {
+  for (int col = lane % P; col < T.dim; col += P) {
+    float v[kBlock];
+#pragma unroll
+    for (int r = 0; r < kBlock; ++r) v[r] = off[r] != 0xFFFFFFFFu ? grad[off[r] + col] : 0.0f;
+    // segment sums, left in v[r] at each segment's last row
     float acc = 0.0f;
     int seg_begin = 0;
 #pragma unroll
@@ -853,84 +856,26 @@ __global__ void __launch_bounds__(kThreads) block_sum_kernel(const Job j, const 
         seg_begin = r + 1;
       }
     }
-  };
-  auto write_sums = [&](const float (&v)[kBlock], int col) {  // kWriteSum
-    int sb = 0;
-#pragma unroll
-    for (int r = 0; r < kBlock; ++r) {
-      if (apply >> r & 1u) j.dense_out[static_cast<int64_t>(b0 + sb) * j.dense_dim + col] = ieee_op<'+'>(0.0f, v[r]);
-      if (ends >> r & 1u) sb = r + 1;
-    }
-  };
-  auto load_states = [&](RowState (&st)[kBlock], int col) {
-#pragma unroll
-    for (int r = 0; r < kBlock; ++r)
-      if (apply >> r & 1u) st[r] = load_row<OP>(T, static_cast<int64_t>(key[r] & id_mask) * T.dim + col);
-  };
-  auto store_states = [&](const float (&v)[kBlock], const RowState (&st)[kBlock], int col) {
-#pragma unroll
-    for (int r = 0; r < kBlock; ++r)
-      if (apply >> r & 1u)
-        store_row<OP>(T, ap, static_cast<int64_t>(key[r] & id_mask) * T.dim + col, st[r], ieee_op<'+'>(0.0f, v[r]));
-  };
-  const int c0 = lane % P;
-  if (T.dim <= 2 * P) {
-    // at most two columns per lane (every table of dim <= 128): both columns'
-    // gradient rows AND the applied rows' optimizer state in flight in one
-    // round trip — the block is latency-bound (keys -> loads -> stores), not
-    // bandwidth-bound, so one wait instead of two per column
-    const int c1 = c0 + P;
-    const bool h0 = c0 < T.dim, h1 = c1 < T.dim;
-    float v0[kBlock], v1[kBlock];
-#pragma unroll
-    for (int r = 0; r < kBlock; ++r) {
-      v0[r] = (off[r] != 0xFFFFFFFFu && h0) ? grad[off[r] + c0] : 0.0f;
-      v1[r] = (off[r] != 0xFFFFFFFFu && h1) ? grad[off[r] + c1] : 0.0f;
-    }
     if (OP == kWriteSum) {
-      if (h0) {
-        seg_sums(v0, c0);
-        write_sums(v0, c0);
-      }
-      if (h1) {
-        seg_sums(v1, c1);
-        write_sums(v1, c1);
+      int sb = 0;
+#pragma unroll
+      for (int r = 0; r < kBlock; ++r) {
+        if (apply >> r & 1u) j.dense_out[static_cast<int64_t>(b0 + sb) * j.dense_dim + col] = ieee_op<'+'>(0.0f, v[r]);
+        if (ends >> r & 1u) sb = r + 1;
       }
     } else {
-      // column 1's state is loaded once column 0's is consumed (both at once
-      // would take 256 VGPRs: one wave per SIMD)
-      RowState s0[kBlock];
-      if (h0) load_states(s0, c0);
-      // one wait for every load: the state loads sit under branches, so the
+      RowState st[kBlock];
+#pragma unroll
+      for (int r = 0; r < kBlock; ++r)
+        if (apply >> r & 1u) st[r] = load_row<OP>(T, static_cast<int64_t>(key[r] & id_mask) * T.dim + col);
+      // one wait for every row's state: the loads sit under branches, so the
       // compiler cannot count them and would otherwise drain the queue (the
       // stores included) before each row's stores
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
-      if (h0) {
-        seg_sums(v0, c0);
-        store_states(v0, s0, c0);
-      }
-      if (h1) {
-        RowState s1[kBlock];
-        load_states(s1, c1);
-        seg_sums(v1, c1);
-        __builtin_amdgcn_s_waitcnt(0x0F70);
-        store_states(v1, s1, c1);
-      }
-    }
-    return;
-  }
-  for (int col = c0; col < T.dim; col += P) {
-    float v[kBlock];
 #pragma unroll
-    for (int r = 0; r < kBlock; ++r) v[r] = off[r] != 0xFFFFFFFFu ? grad[off[r] + col] : 0.0f;
-    seg_sums(v, col);
-    if (OP == kWriteSum) {
-      write_sums(v, col);
-    } else {
-      RowState st[kBlock];
-      load_states(st, col);
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
-      store_states(v, st, col);
+      for (int r = 0; r < kBlock; ++r)
+        if (apply >> r & 1u)
+          store_row<OP>(T, ap, static_cast<int64_t>(key[r] & id_mask) * T.dim + col, st[r], ieee_op<'+'>(0.0f, v[r]));
     }
   }
 }

@@ -23,7 +23,6 @@ __all__ = [
     "MlpPackJob",
     "MlpRowsProblem",
     "MlpWgradProblem",
-    "MlpWgradJob",
     "MAX_SEGMENTS",
     "MAX_SOURCES",
     "lib",
@@ -131,20 +130,6 @@ class MlpWgradProblem(ctypes.Structure):
         ("Ka", c_int32),
         ("N", c_int32),
         ("dwb", c_void_p),
-    ]
-
-
-class MlpWgradJob(ctypes.Structure):
-    """tt_mlp_wgrad_job: a weight-gradient problem, its partials buffer and
-    its optional Adagrad step (tt_mlp_backward_layer / tt_mlp_wgrad_finish)."""
-    _fields_ = [
-        ("p", MlpWgradProblem),
-        ("parts", c_void_p),
-        ("parts_bytes", c_size_t),
-        ("param", c_void_p),
-        ("accum", c_void_p),
-        ("lr", ctypes.c_float),
-        ("eps", ctypes.c_float),
     ]
 
 
@@ -341,8 +326,6 @@ _PROTOS = {
     "tt_mlp_rows_pair": (c_int32, [c_void_p, c_void_p]),
     "tt_mlp_wgrad_pair_workspace_size": (c_size_t, [c_void_p]),
     "tt_mlp_wgrad_pair": (c_int32, [c_void_p, c_void_p, c_size_t, c_void_p]),
-    "tt_mlp_backward_layer": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p]),
-    "tt_mlp_wgrad_finish": (c_int32, [c_void_p, c_void_p]),
     "tt_batch_take": (
         c_int32,
         [c_void_p, c_int64, c_int32, c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_int64, c_void_p,

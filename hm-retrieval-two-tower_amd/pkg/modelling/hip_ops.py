@@ -1198,21 +1198,17 @@ def mlp_rows_pair(problems: Sequence[dict]) -> None:
         raise ValueError("mlp_rows_pair takes exactly 2 problems")
     arr = (_native.MlpRowsProblem * 2)()
     for i, p in enumerate(problems):
-        _fill_rows_problem(arr[i], p)
+        a, img, k, n, out = p["a"], p["img"], p["k"], p["n"], p["out"]
+        amask, cmask, bias = p.get("amask"), p.get("cmask"), p.get("bias")
+        M = _check_rows(a, k, n, out, amask, cmask, bias)
+        q = arr[i]
+        q.A, q.lda, q.amask = a.data_ptr(), _row_major(a, "a"), _ptr(amask)
+        q.ldam = _row_major(amask, "amask") if amask is not None else 0
+        q.scale, q.M, q.K, q.img, q.N = _ptr(p.get("scale")), M, k, img.data_ptr(), n
+        q.bias, q.relu, q.cmask = _ptr(bias), int(bool(p.get("relu", False))), _ptr(cmask)
+        q.ldcm = _row_major(cmask, "cmask") if cmask is not None else 0
+        q.C, q.ldc = out.data_ptr(), _row_major(out, "out")
     check(lib().tt_mlp_rows_pair(arr, _stream()))
-
-
-def _fill_rows_problem(q, p: dict) -> None:
-    """A tt_mlp_rows_problem from a dict of mlp_rows' arguments (no colsum)."""
-    a, img, k, n, out = p["a"], p["img"], p["k"], p["n"], p["out"]
-    amask, cmask, bias = p.get("amask"), p.get("cmask"), p.get("bias")
-    M = _check_rows(a, k, n, out, amask, cmask, bias)
-    q.A, q.lda, q.amask = a.data_ptr(), _row_major(a, "a"), _ptr(amask)
-    q.ldam = _row_major(amask, "amask") if amask is not None else 0
-    q.scale, q.M, q.K, q.img, q.N = _ptr(p.get("scale")), M, k, img.data_ptr(), n
-    q.bias, q.relu, q.cmask = _ptr(bias), int(bool(p.get("relu", False))), _ptr(cmask)
-    q.ldcm = _row_major(cmask, "cmask") if cmask is not None else 0
-    q.C, q.ldc = out.data_ptr(), _row_major(out, "out")
 
 
 def _check_wgrad(a, g, dwb, gmask) -> Tuple[int, int, int]:
@@ -1242,58 +1238,16 @@ def mlp_wgrad(a: torch.Tensor, g: torch.Tensor, dwb: torch.Tensor, *, gmask: Opt
     args = (a.data_ptr(), _row_major(a, "a"), g.data_ptr(), _row_major(g, "g"), _ptr(gmask),
             _row_major(gmask, "gmask") if gmask is not None else 0, _ptr(scale), M, Ka, N, dwb.data_ptr())
     if adagrad is not None:
-        check(lib().tt_mlp_wgrad_adagrad(*args, *_adagrad_args(adagrad, dwb), ws.data_ptr(), ws.numel(), _stream()))
+        param, accum, lr, eps = adagrad
+        for t, n in ((param, "param"), (accum, "accum")):
+            _req(t, n, torch.float32)
+            if t.numel() != dwb.numel() or not t.is_contiguous():
+                raise ValueError(f"{n} must be contiguous with dwb's {dwb.numel()} elements")
+        check(lib().tt_mlp_wgrad_adagrad(*args, param.data_ptr(), accum.data_ptr(), float(lr), float(eps),
+                                         ws.data_ptr(), ws.numel(), _stream()))
         return dwb
     check(lib().tt_mlp_wgrad(*args, ws.data_ptr(), ws.numel(), _stream()))
     return dwb
-
-
-def _adagrad_args(adagrad, dwb: torch.Tensor):
-    param, accum, lr, eps = adagrad
-    for t, n in ((param, "param"), (accum, "accum")):
-        _req(t, n, torch.float32)
-        if t.numel() != dwb.numel() or not t.is_contiguous():
-            raise ValueError(f"{n} must be contiguous with dwb's {dwb.numel()} elements")
-    return param.data_ptr(), accum.data_ptr(), float(lr), float(eps)
-
-
-def mlp_wgrad_job(a: torch.Tensor, g: torch.Tensor, dwb: torch.Tensor, *, gmask: Optional[torch.Tensor] = None,
-                  scale: Optional[torch.Tensor] = None, adagrad: Optional[tuple] = None,
-                  tag: str = "mlp_wgrad_job"):
-    """mlp_wgrad's problem (and optional Adagrad step) as a tt_mlp_wgrad_job
-    for mlp_backward_layer / mlp_wgrad_finish; its split partials live in
-    the workspace `tag` (consecutive layers of one chain need different
-    tags: a job's partials are summed by the NEXT launch)."""
-    M, Ka, N = _check_wgrad(a, g, dwb, gmask)
-    ws = Workspace.get(lib().tt_mlp_wgrad_workspace_size(M, Ka, N), a.device, tag)
-    j = _native.MlpWgradJob()
-    q = j.p
-    q.A, q.lda, q.G, q.ldg = a.data_ptr(), _row_major(a, "a"), g.data_ptr(), _row_major(g, "g")
-    q.gmask, q.ldgm = _ptr(gmask), _row_major(gmask, "gmask") if gmask is not None else 0
-    q.scale, q.M, q.Ka, q.N, q.dwb = _ptr(scale), M, Ka, N, dwb.data_ptr()
-    j.parts, j.parts_bytes = ws.data_ptr(), ws.numel()
-    if adagrad is not None:
-        j.param, j.accum, j.lr, j.eps = _adagrad_args(adagrad, dwb)
-    return j
-
-
-def mlp_backward_layer(job, rows: Optional[dict] = None, prev=None) -> Optional[torch.Tensor]:
-    """One Dense layer's backward in ONE launch (tt_mlp_backward_layer): the
-    weight-gradient partials of `job`, the input-gradient GEMM `rows` (a dict
-    of mlp_rows' arguments, no colsum; None: none) and the partial sums (+
-    Adagrad) of the previous layer's job `prev`.  Returns rows["out"]."""
-    r = None
-    if rows is not None:
-        r = _native.MlpRowsProblem()
-        _fill_rows_problem(r, rows)
-    check(lib().tt_mlp_backward_layer(ctypes.byref(job), ctypes.byref(r) if r is not None else None,
-                                      ctypes.byref(prev) if prev is not None else None, _stream()))
-    return rows["out"] if rows is not None else None
-
-
-def mlp_wgrad_finish(job) -> None:
-    """The partial sums (+ Adagrad) of the last job of a backward chain."""
-    check(lib().tt_mlp_wgrad_finish(ctypes.byref(job), _stream()))
 
 
 def mlp_wgrad_pair(problems: Sequence[dict]) -> None:

@@ -39,10 +39,6 @@ __all__ = ["Tower", "DenseStack", "pair_compatible", "forward_acts_pair", "backw
 # (C3 step, 3 interleaved runs each: unfused 0.535-0.541 vs 0.533-0.536 ms;
 # fused apply 0.570-0.573 vs 0.564-0.565 ms — off)
 IGRAD_FIRST = os.environ.get("TT_IGRAD_FIRST", "0") == "1"
-# DenseStack.backward_acts: each layer's weight gradient, the layer below's
-# input gradient and the upper layer's partial sums + Adagrad as ONE launch
-# (tt_mlp_backward_layer) instead of three in a row; bit-identical
-FUSED_BWD = os.environ.get("TT_FUSED_BWD", "0") == "1"
 
 
 def _rows(p: dict) -> torch.Tensor:
@@ -266,55 +262,39 @@ class DenseStack:
                 self._wgrad_layer(li, acts, gflat, gout, gs[li], gscale)
             return dx, gflat
         g = gout
-        prev = None  # FUSED_BWD: the job whose partial sums the next launch adds
         for li in range(len(self.layout) - 1, -1, -1):
-            want_rows = li > 0 or need_input_grad
-            if FUSED_BWD and self._wgrad_fits(li, g, acts):
-                # one launch: this layer's weight-gradient partials, the layer
-                # below's input gradient and the upper layer's sums + Adagrad
-                job = self._wgrad_job(li, acts, gflat, gout, g, gscale)
-                rows = self._igrad_problem(li, acts, g, gscale) if want_rows else None
-                hip_ops.mlp_backward_layer(job, rows, prev)
-                prev = job
-                g = rows["out"] if rows is not None else None
-            else:
-                if prev is not None:
-                    hip_ops.mlp_wgrad_finish(prev)
-                    prev = None
-                self._wgrad_layer(li, acts, gflat, gout, g, gscale)
-                g = _rows(self._igrad_problem(li, acts, g, gscale)) if want_rows else None
-            if not want_rows:
+            self._wgrad_layer(li, acts, gflat, gout, g, gscale)
+            if li == 0 and not need_input_grad:
+                g = None
                 break
-        if prev is not None:
-            hip_ops.mlp_wgrad_finish(prev)
+            p = self._igrad_problem(li, acts, g, gscale)
+            g = _rows(p)
         if on_dx is not None:
             on_dx(g)
         return g, gflat
 
-    def _wgrad_job(self, li, acts, gflat, gout, g, gscale):
-        """Layer li's weight gradient (+ its fused Adagrad step) as a
-        tt_mlp_wgrad_job; the partials alternate between two workspaces by
-        layer parity (a job's partials are summed by the next launch)."""
-        p = self._wgrad_problem(li, acts, gflat, gout, g, gscale)
-        ad = None
-        if self.fused_adagrad is not None:
-            acc, lr, eps = self.fused_adagrad
-            w_off, fi, fo, _ = self.layout[li]
-            n = (fi + 1) * fo
-            ad = (self.flat.data[w_off:w_off + n], acc[w_off:w_off + n], lr, eps)
-            self.fused_applied.add(li)
-        return hip_ops.mlp_wgrad_job(p["a"], p["g"], p["dwb"], gmask=p.get("gmask"), scale=p.get("scale"),
-                                     adagrad=ad, tag=f"mlp_wgrad_l{li % 2}")
+    def _layer_adagrad(self, li: int):
+        """(param, accum, lr, eps) of layer li for its weight-gradient launches
+        to apply (marked in fused_applied), or None: no fused step, or the
+        layer's region of the flat buffer is not 16-B aligned (a layer after
+        one whose width is not a multiple of 4: the dense step applies it)."""
+        if self.fused_adagrad is None:
+            return None
+        acc, lr, eps = self.fused_adagrad
+        w_off, fi, fo, _ = self.layout[li]
+        n = (fi + 1) * fo
+        param, accum = self.flat.data[w_off:w_off + n], acc[w_off:w_off + n]
+        if param.data_ptr() % 16 or accum.data_ptr() % 16:
+            return None
+        self.fused_applied.add(li)
+        return param, accum, lr, eps
 
     def _wgrad_layer(self, li, acts, gflat, gout, g, gscale) -> None:
         if self._wgrad_fits(li, g, acts):
             p = self._wgrad_problem(li, acts, gflat, gout, g, gscale)
-            if self.fused_adagrad is not None:  # this layer's Adagrad step in the same launches
-                acc, lr, eps = self.fused_adagrad
-                w_off, fi, fo, _ = self.layout[li]
-                n = (fi + 1) * fo
-                p["adagrad"] = (self.flat.data[w_off:w_off + n], acc[w_off:w_off + n], lr, eps)
-                self.fused_applied.add(li)
+            ad = self._layer_adagrad(li)
+            if ad is not None:  # this layer's Adagrad step in the same launches
+                p["adagrad"] = ad
             _wgrad(p)
         else:
             self._wgrad_padded(li, acts, gflat, g, gscale)

@@ -674,32 +674,6 @@ typedef struct {
 size_t tt_mlp_wgrad_pair_workspace_size(const tt_mlp_wgrad_problem* p);
 int tt_mlp_wgrad_pair(const tt_mlp_wgrad_problem* p, void* workspace, size_t workspace_bytes, tt_stream_t stream);
 
-/* One Dense layer's backward (tower.py:41-49, the tape's MatMul /
- * BiasAddGrad / ReluGrad of one layer) in ONE launch of three independent
- * block roles: the layer's weight-gradient split partials (job w), the
- * input-gradient GEMM of the layer below (r: tt_mlp_rows' problem, no colsum;
- * NULL or M == 0: none) and the PREVIOUS (upper) layer's partial sums plus
- * its optional Adagrad step (prev: the job passed as w to the previous call;
- * NULL: none).  The chain of a tower's backward is then one launch per layer
- * plus tt_mlp_wgrad_finish(last job) — where tt_mlp_wgrad(_adagrad) +
- * tt_mlp_rows took three per layer, one after another.  Results equal those
- * calls bit for bit.  A job's partials (parts, tt_mlp_wgrad_workspace_size
- * bytes) must stay untouched until its sums ran, so consecutive layers use
- * different partial buffers. */
-typedef struct {
-  tt_mlp_wgrad_problem p;
-  void* parts;
-  size_t parts_bytes;
-  float* param; /* optional Adagrad on the summed gradient (NULL: none) */
-  float* accum;
-  float lr, eps;
-} tt_mlp_wgrad_job;
-int tt_mlp_backward_layer(const tt_mlp_wgrad_job* w, const tt_mlp_rows_problem* r, const tt_mlp_wgrad_job* prev,
-                          tt_stream_t stream);
-/* The partial sums (+ Adagrad) of one job on their own (the last layer of a
- * chain). */
-int tt_mlp_wgrad_finish(const tt_mlp_wgrad_job* w, tt_stream_t stream);
-
 #ifdef __cplusplus
 }
 #endif

@@ -79,7 +79,7 @@ def _t(x, cuda):
     return torch.as_tensor(x, device=cuda)
 
 
-def _small_model(cuda, seed=0, logq=True, fused=False):
+def _small_model(cuda, seed=0, logq=True, fused=False, hidden=(64,)):
     V = [str(i) for i in range(300)]
     qf = [Feature("cust", dtypes.string, FeatureFamily.QUERY, embedding_size=16, vocab=V),
           Feature("post", dtypes.string, FeatureFamily.QUERY, embedding_size=8, vocab=V[:50])]
@@ -88,7 +88,8 @@ def _small_model(cuda, seed=0, logq=True, fused=False):
           Feature("ptn", dtypes.string, FeatureFamily.CANDIDATE, embedding_size=4, vocab=V[:20])]
     rng = np.random.default_rng(seed)
     probs = {str(i): float(p) for i, p in enumerate(rng.dirichlet(np.ones(300)))} if logq else None
-    m = TwoTowerModel(qf, cf, "art", 32, [64], [64], probs, device=cuda, seed=seed, fused_optimizer_apply=fused)
+    m = TwoTowerModel(qf, cf, "art", 32, list(hidden), list(hidden), probs, device=cuda, seed=seed,
+                      fused_optimizer_apply=fused)
     m.compile(optimizer=OptimizerFactory.get_optimizer("adagrad", {"learning_rate": 0.05}))
     return m
 
@@ -376,79 +377,34 @@ def test_pack_with_gather_bit_identical(cuda, monkeypatch, pair):
         assert torch.equal(sa[k], sb[k]), k
 
 
-@pytest.mark.parametrize("fused", [False, True])
-def test_fused_backward_layer_bit_identical(cuda, monkeypatch, fused):
-    """TT_FUSED_BWD: each layer's weight-gradient partials, the layer below's
-    input gradient and the upper layer's partial sums + Adagrad in ONE launch
-    (tt_mlp_backward_layer) instead of three: bit-identical losses, tables,
-    accumulators and MLP buffers at ragged batch sizes, eager and graphed,
-    unfused and with the fused optimizer apply."""
-    from pkg.modelling.models import tower as tower_mod
+def test_fused_dense_wgrad_odd_hidden_width_bit_identical(cuda, monkeypatch):
+    """A hidden width that is not a multiple of 4 (towers [68, 66] -> 32: the
+    66-wide layer runs tt_mlp_wgrad on padded copies) leaves the next layer's
+    region of the flat buffer 8-B aligned: TT_FUSED_DENSE_WGRAD applies the
+    aligned layers' Adagrad in their weight-gradient launches and leaves that
+    layer to the dense step (DenseStack._layer_adagrad) — losses, tables,
+    accumulators and MLP buffers bit-identical to the dense step for every
+    layer, at ragged batch sizes (tt_mlp_wgrad_adagrad used to refuse the
+    unaligned region and fail the step)."""
+    from pkg.modelling.models import two_tower_model as ttm
 
-    a, b = _small_model(cuda, seed=47, fused=fused), _small_model(cuda, seed=47, fused=fused)
-    rng = np.random.default_rng(16)
+    a, b = _small_model(cuda, seed=49, hidden=(68, 66)), _small_model(cuda, seed=49, hidden=(68, 66))
+    rng = np.random.default_rng(17)
     for i, B in enumerate((512, 37, 256, 1)):
         x = _batch(cuda, rng, B, True)
-        monkeypatch.setattr(tower_mod, "FUSED_BWD", False)
+        monkeypatch.setattr(ttm, "FUSED_DENSE_WGRAD", False)
         la = a.train_step(x)["loss"]
-        monkeypatch.setattr(tower_mod, "FUSED_BWD", True)
+        monkeypatch.setattr(ttm, "FUSED_DENSE_WGRAD", True)
         lb = b.train_step(x)["loss"]
+        # layer 0 applied by its weight-gradient launch; layer 1 (width 66, padded path) and
+        # layer 2 (its region 8-B aligned) by the dense step
+        assert all(t.dense.fused_applied == {0} for t in b.towers)
         assert torch.equal(la, lb), (i, B)
         sa, sb = _state(a), _state(b)
         for k in sa:
             assert torch.equal(sa[k], sb[k]), (i, B, k)
-    batches = [_batch(cuda, rng, 256, True) for _ in range(4)]
-    monkeypatch.setattr(tower_mod, "FUSED_BWD", False)
-    ga = GraphedTrainStep(a, batches[0], warmup=1)
-    monkeypatch.setattr(tower_mod, "FUSED_BWD", True)
-    gb = GraphedTrainStep(b, batches[0], warmup=1)
-    for x in batches[1:]:
-        assert torch.equal(ga(x)["loss"], gb(x)["loss"])
-    torch.cuda.synchronize()
-    sa, sb = _state(a), _state(b)
-    for k in sa:
-        assert torch.equal(sa[k], sb[k]), k
     a.optimizer.check_status(cuda)
     b.optimizer.check_status(cuda)
-
-
-@pytest.mark.parametrize("units,need_dx", [([256, 128], True), ([256, 128], False), ([96, 66, 128], True),
-                                           ([128], True), ([64, 32, 16, 128], False)])
-def test_dense_stack_fused_backward_equals_per_layer(cuda, monkeypatch, units, need_dx):
-    """DenseStack.backward_acts with TT_FUSED_BWD equals the per-layer launches
-    bit for bit (input gradient and flat gradient), with and without the
-    fused Adagrad step, including a layer outside tt_mlp_wgrad's contract
-    (width 66: the chain finishes the pending sums, runs that layer on the
-    padded path, then resumes)."""
-    from pkg.modelling.models import tower as tower_mod
-    from pkg.modelling.models.tower import DenseStack
-
-    rng = np.random.default_rng(5)
-    M, in_dim = 3000, 132
-    x = torch.as_tensor(rng.standard_normal((M, in_dim)).astype(np.float32), device=cuda)
-    gout = torch.as_tensor(rng.standard_normal((M, units[-1])).astype(np.float32), device=cuda)
-    s = torch.tensor([0.5], device=cuda)
-    res = {}
-    for fb in (False, True):
-        for adagrad in (False, True):
-            g = torch.Generator()
-            g.manual_seed(9)
-            st = DenseStack(in_dim, units, cuda, g)
-            acc = torch.full_like(st.flat.detach(), 0.1)
-            st.fused_adagrad = (acc, 0.05, 1e-7) if adagrad else None
-            flat = st.flat.detach()
-            acts = st.forward_acts(x, flat)
-            monkeypatch.setattr(tower_mod, "FUSED_BWD", fb)
-            dx, gflat = st.backward_acts(acts, flat, gout, s, need_dx)
-            torch.cuda.synchronize()
-            res[(fb, adagrad)] = (dx, gflat, st.flat.detach().clone(), acc.clone())
-    for adagrad in (False, True):
-        r0, r1 = res[(False, adagrad)], res[(True, adagrad)]
-        assert (r0[0] is None) == (r1[0] is None) == (not need_dx)
-        if need_dx:
-            assert torch.equal(r0[0], r1[0])
-        for t0, t1 in zip(r0[1:], r1[1:]):
-            assert torch.equal(t0, t1)
 
 
 def test_gather_multi_pack_equals_two_launches(cuda):
