@@ -244,23 +244,14 @@ class DenseStack:
         between them (the fused step's embedding update); the kernels and
         their results are the same in either order (off by default: same step
         time unfused, slower fused — DESIGN §9)."""
-        gflat = torch.empty_like(flat)
         if IGRAD_FIRST:
             # the input-gradient chain first (the embedding update waits for it,
             # the weight gradients do not), on_dx(dx) between the two
-            gs, g, dx = {}, gout, None
-            for li in range(len(self.layout) - 1, -1, -1):
-                gs[li] = g
-                if li == 0 and not need_input_grad:
-                    break
-                g = _rows(self._igrad_problem(li, acts, g, gscale))
-                if li == 0:
-                    dx = g
+            dx, finish = self.backward_split(acts, flat, gout, gscale, need_input_grad)
             if on_dx is not None:
                 on_dx(dx)
-            for li in range(len(self.layout) - 1, -1, -1):
-                self._wgrad_layer(li, acts, gflat, gout, gs[li], gscale)
-            return dx, gflat
+            return dx, finish()
+        gflat = torch.empty_like(flat)
         g = gout
         for li in range(len(self.layout) - 1, -1, -1):
             self._wgrad_layer(li, acts, gflat, gout, g, gscale)
@@ -272,6 +263,36 @@ class DenseStack:
         if on_dx is not None:
             on_dx(g)
         return g, gflat
+
+    def backward_split(self, acts: List[torch.Tensor], flat: torch.Tensor, gout: torch.Tensor,
+                       gscale: Optional[torch.Tensor], need_input_grad: bool):
+        """backward_acts in two phases: the input-gradient chain now (returns
+        dx, None without need_input_grad) and the weight gradients when the
+        returned finish() is called (returns the flat gradient) — the same
+        kernels on the same operands as backward_acts, in IGRAD_FIRST order;
+        finish() applies the fused Adagrad step that was set at the split,
+        whenever it runs."""
+        gs, g, dx = {}, gout, None
+        for li in range(len(self.layout) - 1, -1, -1):
+            gs[li] = g
+            if li == 0 and not need_input_grad:
+                break
+            g = _rows(self._igrad_problem(li, acts, g, gscale))
+            if li == 0:
+                dx = g
+        fused_adagrad = self.fused_adagrad
+
+        def finish() -> torch.Tensor:
+            gflat = torch.empty_like(flat)
+            prev, self.fused_adagrad = self.fused_adagrad, fused_adagrad
+            try:
+                for li in range(len(self.layout) - 1, -1, -1):
+                    self._wgrad_layer(li, acts, gflat, gout, gs[li], gscale)
+            finally:
+                self.fused_adagrad = prev
+            return gflat
+
+        return dx, finish
 
     def _layer_adagrad(self, li: int):
         """(param, accum, lr, eps) of layer li for its weight-gradient launches
